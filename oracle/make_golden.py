@@ -1,0 +1,329 @@
+"""Golden-vector generator: runs the REFERENCE (``/root/reference``) in this build
+container and writes small ``.npz`` fixtures under ``tests/golden/``.
+
+Test infrastructure only -- never shipped, never run on the GPU box (the
+reference does not exist there).  The committed fixtures are data: seeded
+inputs and the reference's outputs.
+
+How the reference is made importable:
+  * ``gym`` -> ``oracle/_stubs/gym`` (first on sys.path);
+  * ``ray`` absent -> the reference's own fallback (``multiagent_env.py:13-17``);
+  * ``five_zone_rom_env.load_data`` is monkeypatched: the exogenous CSV is a
+    missing blob, and the state-space pickle is NOT unpickled -- the model is
+    rebuilt from ``powergridworld_amd/data/state_space_model.json`` (decoded
+    from the pickle's opcodes by ``tools/import_reference_data.py``);
+  * OpenDSS is absent: multi-agent fixtures use ``OraclePowerFlowSolver``
+    (``oracle/pf_oracle.py``) behind the reference's ``PowerFlowSolver`` ABC,
+    so every non-PF output is pinned by the reference and the voltages fed
+    in are recorded in the fixture.
+  * the battery's ``print`` on every obs (``energy_storage_env.py:172``) is
+    sent to /dev/null.
+
+Usage:  python oracle/make_golden.py [--only NAME]
+"""
+import argparse
+import contextlib
+import copy
+import io
+import json
+import os
+import sys
+
+import numpy as np
+import pandas as pd
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(HERE, "_stubs"))
+sys.path.insert(1, "/root/reference")
+sys.path.insert(2, REPO)
+
+from oracle.exogenous import synthetic_exogenous_frame  # noqa: E402
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+EXO = synthetic_exogenous_frame()
+
+
+def _ss_models():
+    with open(os.path.join(REPO, "powergridworld_amd", "data",
+                           "state_space_model.json")) as f:
+        zones = json.load(f)["zones"]
+    models = []
+    for z in zones:
+        models.append({
+            "ss_A": np.array([z["ss_A"]], dtype=np.float64),
+            "ss_B": np.array([z["ss_B"]], dtype=np.float64),
+            "ss_C": np.array([z["ss_C"]], dtype=np.int64),
+            "ss_D": np.array([z["ss_D"]], dtype=np.int64),
+            "ss_K": np.array([z["ss_K"]], dtype=np.float64),
+            "input_sel_list": np.array([z["input_sel_list"]], dtype=np.int64),
+            "mean_inputs": np.array([z["mean_inputs"]], dtype=np.int64),
+            "mean_output": np.array([z["mean_output"]], dtype=np.float64),
+            "neighbors": list(z["neighbors"]),
+            "x_k": np.array([z["x_k"]], dtype=np.float64),
+        })
+    return models
+
+
+def _patched_load_data(start_time=None, end_time=None):
+    """Stand-in for five_zone_rom_env.load_data (five_zone_rom_env.py:30-52)
+    with the synthetic frame and the opcode-decoded state-space model."""
+    df = EXO
+    start_time = pd.Timestamp(start_time) if start_time else df.index[0]
+    end_time = pd.Timestamp(end_time) if end_time else df.index[-1]
+    _df = df.loc[start_time:end_time]
+    if _df is None or len(_df) == 0:
+        raise ValueError("empty exogenous range")
+    return _df, _ss_models()
+
+
+import gridworld  # noqa: E402
+from gridworld import MultiComponentEnv, MultiAgentEnv  # noqa: E402
+from gridworld.agents.buildings import five_zone_rom_env  # noqa: E402
+five_zone_rom_env.load_data = _patched_load_data
+from gridworld.agents.buildings import FiveZoneROMThermalEnergyEnv  # noqa: E402
+from gridworld.agents.pv import PVEnv  # noqa: E402
+from gridworld.agents.energy_storage import EnergyStorageEnv  # noqa: E402
+from gridworld.agents.vehicles import EVChargingEnv  # noqa: E402
+import logging  # noqa: E402
+logging.getLogger("default").setLevel(logging.ERROR)
+
+
+@contextlib.contextmanager
+def quiet():
+    with contextlib.redirect_stdout(io.StringIO()):
+        yield
+
+
+def _save(name, **arrays):
+    os.makedirs(GOLDEN, exist_ok=True)
+    path = os.path.join(GOLDEN, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: np.shape(v) for k, v in arrays.items()})
+
+
+def _actions(rng, T, K, dim, lo=-1.0, hi=1.0, overshoot=0.0):
+    """Seeded actions; a few entries pushed past the box to exercise to_raw's clip."""
+    a = rng.uniform(lo, hi, size=(T, K, dim))
+    if overshoot > 0:
+        mask = rng.random((T, K, dim)) < 0.05
+        a[mask] *= (1.0 + overshoot)
+    return a
+
+
+# --------------------------------------------------------------------------
+# Battery (energy_storage_env.py)
+# --------------------------------------------------------------------------
+def gen_battery():
+    rng = np.random.default_rng(101)
+    cases = {
+        "default": dict(),
+        "norescale": dict(rescale_spaces=False),
+        "big": dict(storage_range=(3.0, 250.0), max_power=20.0,
+                    charge_efficiency=0.9, discharge_efficiency=0.85),
+    }
+    for cname, cfg in cases.items():
+        K, T = 8, 300
+        init = np.concatenate([[3.0, 50.0, 1.0, 400.0],
+                               rng.uniform(3.0, 50.0, K - 4)])
+        acts = _actions(rng, T, K, 1, overshoot=0.3)
+        if not cfg.get("rescale_spaces", True):
+            acts = np.clip(acts, -1, 1)
+        acts[:20, 0, 0] = 1.0     # drive env 0 to the discharge clamp
+        acts[:20, 1, 0] = -1.0    # env 1 to the charge clamp
+        obs = np.zeros((T + 1, K, 1)); rp = np.zeros((T, K)); rew = np.zeros((T, K))
+        done = np.zeros((T, K), bool); soc = np.zeros((T + 1, K))
+        envs = [EnergyStorageEnv(name="storage", **cfg) for _ in range(K)]
+        with quiet():
+            for k, e in enumerate(envs):
+                o, _ = e.reset(init_storage=init[k])
+                obs[0, k] = o; soc[0, k] = e.current_storage
+            for t in range(T):
+                for k, e in enumerate(envs):
+                    o, r, d, _ = e.step(acts[t, k])
+                    obs[t + 1, k] = o; rp[t, k] = e.real_power; rew[t, k] = r
+                    done[t, k] = d; soc[t + 1, k] = e.current_storage
+        _save("battery_" + cname, config=json.dumps(cfg), init_storage=init,
+              actions=acts, obs=obs, real_power=rp, reward=rew, done=done, soc=soc)
+
+
+# --------------------------------------------------------------------------
+# PV (pv_profile_env.py)
+# --------------------------------------------------------------------------
+def gen_pv():
+    rng = np.random.default_rng(202)
+    cases = {
+        "default": dict(profile_csv="pv_profile.csv", scaling_factor=40.0),
+        "norescale": dict(profile_csv="pv_profile.csv", scaling_factor=10.0,
+                          rescale_spaces=False),
+        "offpeak_short": dict(profile_csv="off-peak.csv", scaling_factor=40.0,
+                              max_episode_steps=100),
+    }
+    for cname, cfg in cases.items():
+        K, T = 4, 286 if "max_episode_steps" not in cfg else 99
+        acts = _actions(rng, T, K, 1, overshoot=0.2)
+        if not cfg.get("rescale_spaces", True):
+            acts = rng.uniform(0, 1, size=(T, K, 1))
+        envs = [PVEnv(name="pv", **cfg) for _ in range(K)]
+        obs = np.zeros((T, K, 1)); rp = np.zeros((T, K)); done = np.zeros((T, K), bool)
+        rew = np.zeros((T, K))
+        for e in envs:
+            assert e.reset() is None
+        for t in range(T):
+            for k, e in enumerate(envs):
+                o, r, d, _ = e.step(acts[t, k])
+                obs[t, k] = o; rp[t, k] = e.real_power; done[t, k] = d; rew[t, k] = r
+        _save("pv_" + cname, config=json.dumps(cfg), actions=acts, obs=obs,
+              real_power=rp, reward=rew, done=done)
+
+
+# --------------------------------------------------------------------------
+# Building (five_zone_rom_env.py) -- standalone, lagged reward
+# --------------------------------------------------------------------------
+def gen_building():
+    rng = np.random.default_rng(303)
+    cases = {
+        "default": dict(start_time="08-12-2020 00:00:00", end_time="08-13-2020 00:00:00"),
+        "tests_obs": dict(start_time="08-12-2020 00:00:00", end_time="08-13-2020 00:00:00",
+                          rescale_spaces=False,
+                          obs_config={"zone_temp": (18, 34), "p_consumed": (-100, 100)}),
+        "allobs": dict(start_time="08-12-2020 06:00:00", end_time="08-12-2020 12:00:00",
+                       obs_config={"zone_temp": (16., 40.), "zone_upper_viol": (-10., 10.),
+                                   "zone_lower_viol": (-10., 10.), "comfort_lower": (20., 23.),
+                                   "comfort_upper": (23., 29.), "outdoor_temp": (0., 56.),
+                                   "p_setpoint": (0., 200.), "p_consumed": (0., 200.),
+                                   "time_of_day": (0., 1.), "bus_voltage": (0.9, 1.1),
+                                   "min_voltage": (0.9, 1.1), "max_voltage": (0.9, 1.1)}),
+    }
+    for cname, cfg in cases.items():
+        K = 4
+        envs = [FiveZoneROMThermalEnergyEnv(name="building", **cfg) for _ in range(K)]
+        T1 = envs[0].max_episode_steps - 1     # steps until done
+        T2 = 20                                # second episode (x_k carry-over)
+        odim = envs[0].observation_space.shape[0]
+        for ep, T in enumerate([T1, T2]):
+            acts = _actions(rng, T, K, 6, overshoot=0.2)
+            if not cfg.get("rescale_spaces", True):
+                lo, hi = envs[0]._action_space.low, envs[0]._action_space.high
+                acts = rng.uniform(lo, hi, size=(T, K, 6))
+            obs = np.zeros((T + 1, K, odim)); rew = np.zeros((T, K)); rp = np.zeros((T, K))
+            done = np.zeros((T, K), bool); xk = np.zeros((T + 1, K, 5))
+            for k, e in enumerate(envs):
+                obs[0, k] = e.reset()
+                xk[0, k] = [float(np.squeeze(m["x_k"])) for m in e.models]
+            for t in range(T):
+                for k, e in enumerate(envs):
+                    o, r, d, _ = e.step(acts[t, k])
+                    obs[t + 1, k] = o; rew[t, k] = r; rp[t, k] = e.real_power
+                    done[t, k] = d
+                    xk[t + 1, k] = [float(np.squeeze(m["x_k"])) for m in e.models]
+            _save("building_%s_ep%d" % (cname, ep), config=json.dumps(cfg),
+                  actions=acts, obs=obs, reward=rew, real_power=rp, done=done,
+                  x_k=xk, max_episode_steps=envs[0].max_episode_steps)
+
+
+# --------------------------------------------------------------------------
+# EV charging (ev_charging_env.py)
+# --------------------------------------------------------------------------
+EV_NB_CONFIG = dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7.,
+                    peak_threshold=250., vehicle_multiplier=5., rescale_spaces=False)
+
+
+def gen_ev():
+    rng = np.random.default_rng(404)
+    cases = {
+        "notebook": dict(EV_NB_CONFIG),
+        "rescaled": dict(EV_NB_CONFIG, rescale_spaces=True),
+        "hetero25": dict(num_vehicles=25, minutes_per_step=5, max_charge_rate_kw=7.,
+                         peak_threshold=200., vehicle_multiplier=40., rescale_spaces=True),
+    }
+    for cname, cfg in cases.items():
+        K = 4
+        envs = [EVChargingEnv(**cfg) for _ in range(K)]
+        T = int(envs[0].max_episode_steps) - 2
+        if cfg["rescale_spaces"]:
+            acts = _actions(rng, T, K, 1, overshoot=0.2)
+        else:
+            acts = rng.uniform(0, 1, size=(T, K, 1))
+            acts[:, 0, 0] = 1.0   # the notebook's "high" policy in env 0
+            acts[:, 1, 0] = 0.0   # "low" in env 1
+        obs = np.zeros((T + 1, K, 6)); rew = np.zeros((T, K)); rp = np.zeros((T, K))
+        done = np.zeros((T, K), bool)
+        for k, e in enumerate(envs):
+            obs[0, k], _ = e.reset()
+        for t in range(T):
+            for k, e in enumerate(envs):
+                o, r, d, _ = e.step(acts[t, k])
+                obs[t + 1, k] = o; rew[t, k] = r; rp[t, k] = e.real_power; done[t, k] = d
+        assert done[-1].all() and not done[:-1].any()
+        _save("ev_" + cname, config=json.dumps(cfg), actions=acts, obs=obs,
+              reward=rew, real_power=rp, done=done)
+
+
+# --------------------------------------------------------------------------
+# MultiComponentEnv C3: building + PV + battery + EV (base.py:74-182)
+# --------------------------------------------------------------------------
+def c3_components():
+    return [
+        {"name": "building", "cls": FiveZoneROMThermalEnergyEnv, "config": {}},
+        {"name": "pv", "cls": PVEnv,
+         "config": {"profile_csv": "pv_profile.csv", "scaling_factor": 40.}},
+        {"name": "storage", "cls": EnergyStorageEnv, "config": {}},
+        {"name": "ev", "cls": EVChargingEnv,
+         "config": dict(EV_NB_CONFIG, rescale_spaces=True)},
+    ]
+
+
+def gen_mc():
+    rng = np.random.default_rng(505)
+    K = 3
+    envs = [MultiComponentEnv(name="mc", components=c3_components()) for _ in range(K)]
+    names = [e.name for e in envs[0].envs]
+    dims = {e.name: e.observation_space.shape[0] for e in envs[0].envs}
+    adims = {e.name: e.action_space.shape[0] for e in envs[0].envs}
+    T = 285
+    init = np.zeros(K)
+    acts = {n: _actions(rng, T, K, adims[n], overshoot=0.1) for n in names}
+    obs = {n: np.zeros((T + 1, K, dims[n])) for n in names}
+    rew = np.zeros((T, K)); rp = np.zeros((T, K)); done = np.zeros((T, K), bool)
+    with quiet():
+        for k, e in enumerate(envs):
+            # MC.reset forwards kwargs to every component and the EV step_reward
+            # rejects them (base.py:110, ev_charging_env.py:163,259), so the SoC
+            # drawn by the reference's global RNG is recorded and injected instead.
+            o, _ = e.reset()
+            init[k] = e.env_dict["storage"].current_storage
+            for n in names:
+                obs[n][0, k] = o[n]
+        for t in range(T):
+            for k, e in enumerate(envs):
+                o, r, d, _ = e.step({n: acts[n][t, k] for n in names})
+                for n in names:
+                    obs[n][t + 1, k] = o[n]
+                rew[t, k] = r; rp[t, k] = e.real_power; done[t, k] = d
+    arrays = dict(init_storage=init, reward=rew, real_power=rp, done=done,
+                  names=np.array(names))
+    for n in names:
+        arrays["act_" + n] = acts[n]
+        arrays["obs_" + n] = obs[n]
+    _save("mc_c3", **arrays)
+
+
+GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
+              "ev": gen_ev, "mc": gen_mc}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    np.random.seed(0)
+    EXO.to_csv(os.path.join(GOLDEN, "exogenous_synthetic.csv.gz"))
+    for name, fn in GENERATORS.items():
+        if args.only and name != args.only:
+            continue
+        fn()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,436 @@
+"""CPU oracle: batched NumPy fp64 restatement of the PowerGridworld step path.
+
+TEST INFRASTRUCTURE.  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import this module, and only as the
+checker / the timed CPU baseline -- the product package never imports it.
+
+Each class restates one reference component over K independent env copies
+(arrays carry a leading env axis).  Arithmetic follows the reference's
+operation order so results agree with it to ~1e-15 relative; the residual is
+summation order (Python ``set`` iteration in the EV step, numpy pairwise sums
+in ``np.mean``, BLAS dot order in the building's ``np.matmul``).
+
+Pinned against the reference's own outputs: ``tests/golden/*.npz`` (written by
+``oracle/make_golden.py``) and the EV known-answer totals from
+``examples/envs/ev-charging.ipynb:130,161,192``.
+"""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+
+DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    "powergridworld_amd", "data")
+
+
+# ---------------------------------------------------------------- utils.py
+def to_scaled(x, low, high):
+    """gridworld/utils.py:9-24"""
+    x = np.clip(x, low, high)
+    return (2 * x - (low + high)) / (high - low)
+
+
+def to_raw(y, low, high):
+    """gridworld/utils.py:27-43 (the out-of-bounds warning is not restated)."""
+    y = np.clip(y, -1.0, 1.0)
+    return (y * (high - low) + (high + low)) / 2.
+
+
+# ------------------------------------------------------------ battery
+class BatteryOracle:
+    """gridworld/agents/energy_storage/energy_storage_env.py:11-181"""
+
+    def __init__(self, K, storage_range=(3.0, 50.0), initial_storage_mean=30.0,
+                 initial_storage_std=5.0, charge_efficiency=0.95,
+                 discharge_efficiency=0.9, max_power=15.0, max_episode_steps=288,
+                 control_timedelta=pd.Timedelta(300, "s"), rescale_spaces=True, **kw):
+        self.K = K
+        self.lo, self.hi = float(storage_range[0]), float(storage_range[1])
+        self.eta_c, self.eta_d = charge_efficiency, discharge_efficiency
+        self.max_power = max_power
+        self.max_episode_steps = max_episode_steps
+        self.dt = control_timedelta.seconds / 3600.0            # :49
+        self.rescale = rescale_spaces
+        self.soc = np.zeros(K)
+        self.step_count = 0
+        self.real_power = np.zeros(K)
+
+    def obs(self):                                              # :166-178
+        raw = self.soc[:, None].copy()
+        if self.rescale:
+            return to_scaled(raw, np.array([self.lo]), np.array([self.hi]))
+        return raw
+
+    def reset(self, init_storage):                              # :72-97
+        self.step_count = 0
+        self.soc = np.clip(np.asarray(init_storage, dtype=np.float64), self.lo, self.hi)
+        return self.obs()
+
+    def step(self, action):                                     # :131-157
+        a = np.asarray(action, dtype=np.float64)[:, 0]
+        if self.rescale:
+            a = to_raw(a, -1.0, 1.0)
+        p = a * self.max_power
+        soc = self.soc
+        # validate_power :100-128 (clamps omit the efficiencies)
+        dis = (p > 0) & (soc - p * self.dt / self.eta_d < self.lo)
+        p = np.where(dis, np.maximum(soc - self.lo, 0.0) / self.dt, p)
+        chg = (p < 0) & (soc - self.eta_c * p * self.dt > self.hi)
+        p = np.where(chg, -np.maximum(self.hi - soc, 0.0) / self.dt, p)
+        # :141-147
+        soc_c = np.minimum(soc - self.eta_c * p * self.dt, self.hi)
+        soc_d = np.maximum(soc - p * self.dt / self.eta_d, self.lo)
+        self.soc = np.where(p < 0.0, soc_c, np.where(p > 0.0, soc_d, soc))
+        self.real_power = -p                                    # :150
+        obs = self.obs()
+        self.step_count += 1
+        done = self.step_count + 1 == self.max_episode_steps    # :180-181
+        return obs, np.zeros(self.K), np.full(self.K, done), {}
+
+    def step_reward(self):
+        return np.zeros(self.K)
+
+
+# ------------------------------------------------------------ PV
+def load_pv_profile(profile_csv):
+    name = os.path.splitext(os.path.basename(profile_csv))[0]
+    with np.load(os.path.join(DATA, "pv_profiles.npz")) as z:
+        return z[name].copy()
+
+
+class PVOracle:
+    """gridworld/agents/pv/pv_profile_env.py:15-148"""
+
+    def __init__(self, K, profile_csv, scaling_factor=1., rescale_spaces=True,
+                 grid_aware=False, max_episode_steps=None, profile=None, **kw):
+        self.K = K
+        data = load_pv_profile(profile_csv) if profile is None else np.asarray(profile, float).copy()
+        data *= scaling_factor                                  # :69
+        self.data = data
+        self.episode_length = len(data)
+        if max_episode_steps is not None:
+            self.episode_length = min(max_episode_steps, self.episode_length)
+        self.rescale = rescale_spaces
+        self.grid_aware = grid_aware
+        self.obs_low = np.array([-np.max(data)] + ([0.9] if grid_aware else []))
+        self.obs_high = np.array([0.] + ([1.1] if grid_aware else []))
+        self.index = 0
+        self.real_power = np.zeros(K)
+
+    def obs(self, min_voltage=None):                            # :102-114
+        raw = np.full((self.K, 1), -self.data[self.index])
+        if self.grid_aware:
+            raw = np.concatenate([raw, np.asarray(min_voltage, float).reshape(self.K, 1)], 1)
+        return to_scaled(raw, self.obs_low, self.obs_high) if self.rescale else raw
+
+    def reset(self):                                            # :127-130 (returns None)
+        self.index = 0
+        return None
+
+    def step(self, action, min_voltage=None):                   # :133-148
+        a = np.asarray(action, dtype=np.float64)[:, 0]
+        if self.rescale:
+            a = to_raw(a, np.array([0.]), np.array([1.]))
+        obs = self.obs(min_voltage)
+        self.real_power = a * (-self.data[self.index])
+        self.index += 1
+        done = self.index == self.episode_length - 1
+        return obs, np.zeros(self.K), np.full(self.K, done), {}
+
+    def step_reward(self):
+        return np.zeros(self.K)
+
+
+# ------------------------------------------------------------ building
+BUILDING_OBS_ORDER = ["zone_temp", "zone_upper_viol", "zone_lower_viol", "comfort_lower",
+                      "comfort_upper", "outdoor_temp", "p_setpoint", "p_consumed",
+                      "time_of_day", "bus_voltage", "min_voltage", "max_voltage"]
+MULTIZONE = ["zone_temp", "zone_upper_viol", "zone_lower_viol"]
+DEFAULT_BUILDING_OBS = {"zone_upper_viol": (-10., 10.), "zone_lower_viol": (-10., 10.),
+                        "comfort_lower": (20., 25.), "comfort_upper": (25., 30),
+                        "outdoor_temp": (0., 56.), "p_consumed": (0., 100.),
+                        "time_of_day": (0., 1.)}                # defaults.py:2-10
+
+
+def load_ss_model():
+    with open(os.path.join(DATA, "state_space_model.json")) as f:
+        return json.load(f)["zones"]
+
+
+class BuildingOracle:
+    """FiveZoneROMThermalEnergyEnv: five_zone_rom_env.py:60-335 and
+    five_zone_rom_dynamics.py:12-114.  ``lagged_reward`` selects the standalone
+    behaviour where step() returns the reward of the PREVIOUS state
+    (five_zone_rom_env.py:215)."""
+
+    act_low = np.array([.22, .22, .22, .22, .32, 10.0])        # :22-26
+    act_high = np.array([2.2, 2.2, 2.2, 2.2, 3.2, 16.0])
+
+    def __init__(self, K, exo, obs_config=None, start_time=None, end_time=None,
+                 comfort_bounds=None, zone_temp_init=None, max_episode_steps=None,
+                 rescale_spaces=True, **kw):
+        self.K = K
+        start = pd.Timestamp(start_time) if start_time else exo.index[0]
+        end = pd.Timestamp(end_time) if end_time else exo.index[-1]
+        df = exo.loc[start:end]
+        if len(df) == 0:
+            raise ValueError("empty exogenous range")
+        cols = list(df.columns)
+        pick = lambda pre: df[[c for c in cols if c.startswith(pre)]].values
+        self.T_oa = pick("T_oa")[:, 0]
+        self.q_solar, self.q_cool, self.q_int = pick("Q_solar"), pick("Q_cool_"), pick("Q_int")
+        max_steps = len(df) - 3                                 # :97
+        self.max_episode_steps = max_steps if max_episode_steps is None else min(max_episode_steps, max_steps)
+        cb = comfort_bounds if comfort_bounds is not None else (22., 28.)
+        self.cb = np.zeros((len(df), 2))
+        if isinstance(cb, tuple):
+            self.cb[:, 0], self.cb[:, 1] = cb
+        else:
+            self.cb[:] = np.asarray(cb)[:len(df), :2]
+        zones = load_ss_model()
+        self.A = np.array([z["ss_A"][0] for z in zones])
+        self.B32 = np.array([z["ss_B"] for z in zones]).astype(np.float32).astype(np.float64)
+        self.Kf = np.array([z["ss_K"][0] for z in zones])
+        self.C = np.array([z["ss_C"][0] for z in zones], dtype=np.float64)
+        self.mean = np.array([z["mean_output"][0] for z in zones])
+        self.nbrs = [z["neighbors"] for z in zones]
+        self.sel = [z["input_sel_list"] for z in zones]
+        self.x = np.tile(np.array([z["x_k"][0] for z in zones]), (K, 1))
+        self.T_init = np.full(5, 27.) if zone_temp_init is None else np.asarray(zone_temp_init, float)
+        self.rescale = rescale_spaces
+        cfg = obs_config if obs_config is not None else DEFAULT_BUILDING_OBS
+        # make_obs_space (obs_space.py:66-101): bounds in DEFAULT_OBS_CONFIG order.
+        self.labels, lo, hi = [], [], []
+        for key in [k for k in BUILDING_OBS_ORDER if k in cfg]:
+            n = 5 if key in MULTIZONE else 1
+            self.labels += ["%s_%d" % (key, i) for i in range(5)] if n == 5 else [key]
+            lo += [cfg[key][0]] * n
+            hi += [cfg[key][1]] * n
+        self.obs_low, self.obs_high = np.array(lo, float), np.array(hi, float)
+        self.t = 0
+        self.p = np.zeros(K)
+        self.state = None
+
+    # --- dynamics (five_zone_rom_dynamics.py)
+    def _u(self, T, t, action):                                 # :12-41
+        K = T.shape[0]
+        u = np.zeros((K, 5, 4))
+        for z in range(5):
+            upos = np.zeros((K, 8))
+            upos[:, 0] = self.T_oa[t] - T[:, z]
+            upos[:, 1] = self.q_solar[t, z]
+            upos[:, 2] = self.q_int[t, z]
+            for i, y in enumerate(self.nbrs[z]):
+                upos[:, 3 + i] = T[:, y] - T[:, z]
+            upos[:, 7] = self.q_cool[t, z] if action is None else action[:, z] * (action[:, 5] - T[:, z])
+            for j, s in enumerate(self.sel[z]):
+                u[:, z, j] = upos[:, s - 1]
+        return u
+
+    def _state_update(self, u):                                 # :44-55
+        bu = (((self.B32[:, 0] * u[:, :, 0] + self.B32[:, 1] * u[:, :, 1])
+               + self.B32[:, 2] * u[:, :, 2]) + self.B32[:, 3] * u[:, :, 3])
+        self.x = self.A * self.x + bu
+
+    def _temps(self):                                           # :75-85
+        return self.C * self.x + self.mean
+
+    def reset(self):                                            # five_zone_rom_env.py:147-180
+        self.t = 0
+        self.p = np.zeros(self.K)
+        T = np.tile(self.T_init, (self.K, 1))
+        u = self._u(T, 0, None)
+        for _ in range(2):                                      # filter_update x2 (:58-72)
+            self._state_update(u)
+            yhat = self.C * self.x
+            self.x = self.x + self.Kf * ((T - self.mean) - yhat)
+        self.T = self._temps()
+        return self.get_obs()
+
+    def p_consumed(self, a, t):                                 # dynamics.py:106-114
+        s = (((a[:, 0] + a[:, 1]) + a[:, 2]) + a[:, 3]) + a[:, 4]
+        return (0.0076 * s ** 3 + 4.8865) + np.maximum(0., s * (self.T_oa[t] - a[:, 5]))
+
+    def step(self, action, lagged_reward=True, **obs_kwargs):   # :183-225
+        a = np.asarray(action, dtype=np.float64)
+        if self.rescale:
+            a = to_raw(a, self.act_low, self.act_high)
+        u = self._u(self.T, self.t, a)
+        self._state_update(u)
+        self.T = self._temps()
+        self.p = self.p_consumed(a, self.t)
+        stale = self.step_reward()
+        self.t += 1
+        obs = self.get_obs(**obs_kwargs)
+        done = self.t == self.max_episode_steps - 1
+        rew = stale if lagged_reward else self.step_reward()
+        return obs, rew, np.full(self.K, done), {}
+
+    def get_obs(self, **kw):                                    # :228-283
+        lb, ub = self.cb[self.t, 0], self.cb[self.t, 1]
+        K = self.K
+        st = {}
+        for z in range(5):
+            st["zone_temp_%d" % z] = self.T[:, z]
+        for z in range(5):
+            st["zone_upper_viol_%d" % z] = self.T[:, z] - ub
+        for z in range(5):
+            st["zone_lower_viol_%d" % z] = lb - self.T[:, z]
+        bv = kw.get("bus_voltage")
+        ps = kw.get("p_setpoint")
+        st.update({"comfort_lower": np.full(K, lb), "comfort_upper": np.full(K, ub),
+                   "outdoor_temp": np.full(K, self.T_oa[self.t]), "p_consumed": self.p,
+                   "time_of_day": np.full(K, 1. * self.t / self.max_episode_steps),
+                   "bus_voltage": bv if bv is not None else np.full(K, 1.0),
+                   "min_voltage": bv if bv is not None else np.full(K, 1.0),
+                   "max_voltage": bv if bv is not None else np.full(K, 1.0),
+                   "p_setpoint": ps if ps is not None else np.full(K, np.inf)})
+        st.update(kw)
+        self.state = st
+        obs = np.stack([np.broadcast_to(v, (K,)) for k, v in st.items() if k in self.labels], 1)
+        obs = np.clip(obs, self.obs_low, self.obs_high)
+        return to_scaled(obs, self.obs_low, self.obs_high) if self.rescale else obs
+
+    def step_reward(self):                                      # :315-335
+        alpha = 0.2
+        e = -self.state["p_consumed"] / 12.0
+        c = 0
+        for i in range(5):
+            x = np.maximum(np.maximum(self.state["zone_upper_viol_%d" % i],
+                                      self.state["zone_lower_viol_%d" % i]), 0.0)
+            c = c + x ** 2
+        c = -c
+        return alpha * e * 0.5 + (1. - alpha) * c
+
+    @property
+    def real_power(self):                                       # :305-308
+        return self.state["p_consumed"]
+
+
+# ------------------------------------------------------------ EV
+def load_vehicles():
+    with np.load(os.path.join(DATA, "vehicles.npz")) as z:
+        return {k: z[k].copy() for k in z.files}
+
+
+class EVOracle:
+    """gridworld/agents/vehicles/ev_charging_env.py:17-275"""
+
+    def __init__(self, K, num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7.0,
+                 max_episode_steps=None, unserved_penalty=1., peak_penalty=1.,
+                 peak_threshold=10., reward_scale=1e5, vehicle_multiplier=1,
+                 rescale_spaces=True, **kw):
+        self.K, self.V = K, num_vehicles
+        self.rate, self.mps = max_charge_rate_kw, minutes_per_step
+        self.mult = vehicle_multiplier
+        self.rescale = rescale_spaces
+        self.u_pen, self.p_pen, self.thr, self.scale = unserved_penalty, peak_penalty, peak_threshold, reward_scale
+        mes = max_episode_steps if max_episode_steps is not None else np.inf
+        self.max_episode_steps = min(mes, 24 * 60 / minutes_per_step)        # :54-55
+        self.sim_times = np.arange(0, self.max_episode_steps * minutes_per_step, minutes_per_step)
+        veh = load_vehicles()
+        req_all = veh["energy_required_kwh"] * self.mult                     # :72
+        rnd = lambda x: x - x % minutes_per_step                             # :273-275
+        self.start = np.floor(rnd(veh["start_time_min"])[:self.V])
+        self.endp_int = rnd(veh["end_time_park_min"])[:self.V]
+        self.endp = np.floor(self.endp_int)
+        self.req0 = req_all[:self.V].copy()
+        emax = req_all.max()
+        self.obs_low = np.zeros(6)
+        self.obs_high = np.array([self.sim_times[-1], self.V, self.V * self.rate,
+                                  self.V * emax, emax / (self.mps / 60.), emax])   # :79-91
+        self.state = np.zeros((K, 6))
+        self.real_power = np.zeros(K)
+
+    def obs(self):
+        return to_scaled(self.state, self.obs_low, self.obs_high) if self.rescale else self.state.copy()
+
+    def reset(self):                                           # :145-168
+        self.ti = 0
+        self.time = self.sim_times[0]
+        self.charging = np.zeros((self.K, self.V), bool)
+        self.req = np.tile(self.req0, (self.K, 1))
+        self.real_power = np.zeros(self.K)
+        self.step(None)
+        return self.obs()
+
+    def step(self, action):                                    # :171-264
+        if action is None:
+            a = np.zeros(self.K)                                # _action_space.low
+        else:
+            a = np.asarray(action, dtype=np.float64)[:, 0]
+        if self.rescale:
+            a = to_raw(a, np.array([0.]), np.array([1.]))
+        kwh = a * self.rate * (self.mps / 60.)
+        t = self.time
+        charging = (t >= self.start) & (t <= self.endp) & (self.req > 0.)
+        departed = self.charging & ~charging
+        demand = np.zeros(self.K); consumed = np.zeros(self.K)
+        dsum = np.zeros(self.K); dcnt = np.zeros(self.K, int)
+        for i in range(self.V):                                 # ascending index order
+            m = charging[:, i]
+            if not m.any():
+                continue
+            req = self.req[:, i]
+            demand = np.where(m, demand + req, demand)
+            tl = (self.endp_int[i] - t) / 60.
+            if tl <= 0:
+                continue
+            deficit = np.maximum(0, self.rate - req / tl)
+            dsum = np.where(m, dsum + deficit, dsum); dcnt += m
+            ch = np.minimum(kwh, req)
+            self.req[:, i] = np.where(m, req - ch, req)
+            consumed = np.where(m, consumed + ch, consumed)
+        self.ti += 1
+        self.time = self.sim_times[self.ti]
+        self.charging = charging
+        unserved = (self.req * departed).sum(1)
+        mean_def = np.where(dcnt > 0, dsum / np.maximum(dcnt, 1), 0.)
+        self.state = np.stack([np.full(self.K, self.time), self.mult * charging.sum(1),
+                               self.mult * consumed, self.mult * demand, mean_def, unserved], 1)
+        self.real_power = self.mult * consumed
+        return self.obs(), self.step_reward(), np.full(self.K, self.ti == self.max_episode_steps - 1), {}
+
+    def step_reward(self):                                     # :135-142
+        ur = -self.u_pen * self.state[:, 5] ** 2
+        pr = -self.p_pen * np.maximum(0, self.state[:, 2] - self.thr) ** 2
+        return (ur + pr) / self.scale
+
+
+# ------------------------------------------------------------ MultiComponentEnv
+class MCOracle:
+    """gridworld/base.py:74-182: components stepped in order, real power summed,
+    reward recomputed from every component AFTER all steps (fresh)."""
+
+    def __init__(self, comps):
+        self.comps = comps        # list of (name, oracle)
+        self.real_power = None
+
+    def reset(self, init_storage=None):
+        obs = {}
+        for n, c in self.comps:
+            if isinstance(c, BatteryOracle):
+                c.reset(init_storage)
+            else:
+                c.reset()
+        for n, c in self.comps:
+            obs[n] = c.obs() if not isinstance(c, BuildingOracle) else c.get_obs()
+        return obs
+
+    def step(self, action):
+        obs, dones = {}, []
+        rp = 0.
+        for n, c in self.comps:
+            if isinstance(c, BuildingOracle):
+                o, _, d, _ = c.step(action[n], lagged_reward=True)
+            else:
+                o, _, d, _ = c.step(action[n])
+            obs[n] = o
+            dones.append(d)
+            rp = rp + c.real_power
+        self.real_power = rp
+        rew = 0.
+        for n, c in self.comps:
+            rew = rew + c.step_reward()
+        return obs, rew, np.any(dones, 0), {}
