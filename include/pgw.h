@@ -1,0 +1,341 @@
+/*
+ * pgw.h -- C ABI of libpgw, the MI355X (gfx950) step engine for
+ * PowerGridworld-style environments.
+ *
+ * Boundary rules:
+ *   - every array argument is a DEVICE pointer owned by the caller (PyTorch-ROCm
+ *     tensors); the library never allocates on the step path;
+ *   - state is struct-of-arrays, env index fastest: field f of env e lives at
+ *     ptr[f * n + e];
+ *   - small per-call parameters are passed as HOST pointers to POD structs and
+ *     copied by value into the kernel arguments (so calls are hipGraph-capturable
+ *     and reentrant: the library holds no device state);
+ *   - calls are asynchronous on `stream` (a hipStream_t, NULL = default stream);
+ *   - return 0 on success, < 0 on error (pgw_last_error() gives the message);
+ *     no C++ exception crosses the ABI.
+ *
+ * Each entry point cites the reference interface it replaces
+ * (paths relative to lmchion/PowerGridworld).
+ */
+#ifndef PGW_H_
+#define PGW_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGW_ABI_VERSION 1
+
+#define PGW_OK 0
+#define PGW_ERR_ARG (-1)
+#define PGW_ERR_HIP (-2)
+
+/* Version of this header the library was built from. */
+int32_t pgw_abi_version(void);
+/* Message of the last error on the calling thread ("" if none). */
+const char* pgw_last_error(void);
+
+/* sizeof() of every ABI struct, in the order pgw_mat, battery_params, pv_params,
+ * building_params, building_exo, building_ext, ev_params, ev_step_info,
+ * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
+ * coord_step_info -- lets a binding verify its layouts.  Writes min(n, 15)
+ * values, returns 15. */
+int32_t pgw_struct_sizes(int64_t* out, int32_t n);
+
+/* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
+ * ptr[e * s_env + j * s_dim].  Used for actions (read) and observations
+ * (written), so callers can hand over row-major [N, dim] policy tensors or
+ * env-minor [dim, N] buffers without a copy. */
+typedef struct pgw_mat {
+  double* ptr;
+  int64_t s_env;
+  int64_t s_dim;
+} pgw_mat;
+
+/* ------------------------------------------------------------------------
+ * Energy storage.  Replaces EnergyStorageEnv.reset/step/get_obs
+ * (gridworld/agents/energy_storage/energy_storage_env.py:72-178).
+ * ---------------------------------------------------------------------- */
+typedef struct pgw_battery_params {
+  double soc_min, soc_max;   /* storage_range            (:23)  */
+  double eta_c, eta_d;       /* charge/discharge eff.    (:26-27) */
+  double max_power;          /* kW                       (:28)  */
+  double dt_h;               /* control_timedelta in h   (:49)  */
+  int32_t rescale;           /* rescale_spaces           (:31)  */
+  int32_t pad_;
+} pgw_battery_params;
+
+/* soc[e] = clip(init_soc[e], soc_min, soc_max); obs = SoC (scaled). (:72-97) */
+int32_t pgw_battery_reset(const pgw_battery_params* p, int64_t n, const double* init_soc,
+                          double* soc, pgw_mat obs, void* stream);
+/* One control step: to_raw, validate_power, SoC update, real_power = -power.
+ * Reward is identically 0 (:159-164).  (:100-157) */
+int32_t pgw_battery_step(const pgw_battery_params* p, int64_t n, pgw_mat action,
+                         double* soc, pgw_mat obs, double* real_power, void* stream);
+
+/* ------------------------------------------------------------------------
+ * PV curtailment.  Replaces PVEnv.get_obs/step
+ * (gridworld/agents/pv/pv_profile_env.py:102-148).
+ * ---------------------------------------------------------------------- */
+typedef struct pgw_pv_params {
+  double obs_low, obs_high;     /* (-max(data), 0)           (:86-96) */
+  double vmin_low, vmin_high;   /* (0.9, 1.1) when grid_aware */
+  int32_t rescale, grid_aware;
+} pgw_pv_params;
+
+/* obs only (PVEnv.get_obs at the current index); `pmax` = data[index]. */
+int32_t pgw_pv_obs(const pgw_pv_params* p, int64_t n, double pmax, const double* min_voltage,
+                   pgw_mat obs, void* stream);
+/* obs (pre-advance, :143) and real_power = to_raw(a,0,1) * (-pmax) (:144). */
+int32_t pgw_pv_step(const pgw_pv_params* p, int64_t n, double pmax, pgw_mat action,
+                    const double* min_voltage, pgw_mat obs, double* real_power, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Five-zone reduced-order building.  Replaces FiveZoneROMEnv.reset/step_/get_obs
+ * and FiveZoneROMThermalEnergyEnv.step_reward
+ * (gridworld/agents/buildings/five_zone_rom_env.py:147-335,
+ *  five_zone_rom_dynamics.py:12-114).
+ * ---------------------------------------------------------------------- */
+#define PGW_BLD_MAX_OBS 24   /* 15 zone values + 9 scalars */
+
+/* observation variable ids, in the reference's state-dict order (:230-246) */
+enum {
+  PGW_BV_ZONE_TEMP = 0,        /* + zone (0..4) */
+  PGW_BV_UPPER_VIOL = 5,       /* + zone */
+  PGW_BV_LOWER_VIOL = 10,      /* + zone */
+  PGW_BV_COMFORT_LOWER = 15,
+  PGW_BV_COMFORT_UPPER = 16,
+  PGW_BV_OUTDOOR_TEMP = 17,
+  PGW_BV_P_CONSUMED = 18,
+  PGW_BV_TIME_OF_DAY = 19,
+  PGW_BV_BUS_VOLTAGE = 20,
+  PGW_BV_MIN_VOLTAGE = 21,
+  PGW_BV_MAX_VOLTAGE = 22,
+  PGW_BV_P_SETPOINT = 23
+};
+
+typedef struct pgw_building_params {
+  double A[5];           /* ss_A                                   */
+  double B[5][4];        /* ss_B rounded to float32 (dynamics.py:51) */
+  double K[5];           /* ss_K (filter gain)                     */
+  double C[5];           /* ss_C                                   */
+  double mean[5];        /* mean_output                            */
+  double act_low[6], act_high[6];   /* (:22-26)                    */
+  double T_init[5];      /* zone_temp_init (:91)                   */
+  double obs_low[PGW_BLD_MAX_OBS], obs_high[PGW_BLD_MAX_OBS];  /* make_obs_space order */
+  double alpha;          /* 0.2 (:318)                             */
+  int32_t sel[5][4];     /* input_sel_list - 1 (index into u_pos)  */
+  int32_t nbr[5][4];     /* neighbors                              */
+  int32_t obs_var[PGW_BLD_MAX_OBS];   /* PGW_BV_* per obs slot, state-dict order */
+  int32_t n_obs;
+  int32_t rescale;
+} pgw_building_params;
+
+/* Exogenous row (shared by all envs, host values) + the obs-time scalars. */
+typedef struct pgw_building_exo {
+  double T_oa;
+  double q_solar[5], q_int[5], q_cool[5];
+  double comfort_lb, comfort_ub;
+  double time_of_day;    /* time_index / max_episode_steps */
+  double pad_;
+} pgw_building_exo;
+
+/* External obs inputs (device [n] arrays); NULL selects the reference default
+ * (bus/min/max voltage 1.0 -- or bus_voltage when given --, p_setpoint +inf). */
+typedef struct pgw_building_ext {
+  const double* bus_voltage;
+  const double* min_voltage;
+  const double* max_voltage;
+  const double* p_setpoint;
+} pgw_building_ext;
+
+/* reset: u from q_cool at row 0, two filter updates, obs at row 0.  x (5 x n,
+ * zone-major) is updated IN PLACE: the Kalman state persists across resets as in
+ * the reference (:147-180).  p_consumed := 0; reward_state := reward of the reset
+ * state (what the first standalone step returns). */
+int32_t pgw_building_reset(const pgw_building_params* p, const pgw_building_exo* ex0, int64_t n,
+                           double* x, double* p_consumed, double* reward_state,
+                           pgw_building_ext ext, pgw_mat obs, void* stream);
+/* step: to_raw, dynamics with row `ex_t`, p_consumed, advance, obs with row
+ * `ex_next`.  reward_out gets the PREVIOUS state's reward when lagged != 0
+ * (standalone env, :215) or the fresh reward otherwise (MultiComponentEnv,
+ * base.py:137); reward_state always ends holding the fresh reward. */
+int32_t pgw_building_step(const pgw_building_params* p, const pgw_building_exo* ex_t,
+                          const pgw_building_exo* ex_next, int64_t n, pgw_mat action, double* x,
+                          double* p_consumed, double* reward_out, double* reward_state,
+                          int32_t lagged, pgw_building_ext ext, pgw_mat obs, void* stream);
+
+/* ------------------------------------------------------------------------
+ * EV charging station.  Replaces EVChargingEnv.reset/step/step_reward
+ * (gridworld/agents/vehicles/ev_charging_env.py:135-264).
+ * ---------------------------------------------------------------------- */
+#define PGW_EV_MAX_WORDS 16   /* up to 1024 vehicles */
+
+typedef struct pgw_ev_params {
+  double rate;           /* max_charge_rate_kw       */
+  double hours_per_step; /* minutes_per_step / 60.   */
+  double mult;           /* vehicle_multiplier       */
+  double u_pen, p_pen, thr, reward_scale;
+  double obs_low[6], obs_high[6];
+  int32_t n_vehicles, rescale;
+} pgw_ev_params;
+
+/* Per-step schedule, shared by all envs (time is lockstep): bit v of `window`
+ * = vehicle v parked (start <= time <= end_park), of `scan` = parked now or at the
+ * previous step. */
+typedef struct pgw_ev_step_info {
+  double time;           /* minutes, before the step's advance        */
+  double next_time;      /* simulation_times[time_index + 1]          */
+  double action_default; /* raw action used when action.ptr == NULL (reset step) */
+  int32_t n_words, pad_;
+  uint64_t window[PGW_EV_MAX_WORDS];
+  uint64_t scan[PGW_EV_MAX_WORDS];
+} pgw_ev_step_info;
+
+/* req (V x n) := req0 (V) broadcast; charging bits := 0. */
+int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, double* req,
+                     uint64_t* charging, void* stream);
+/* One step (reset's action-less step when action.ptr == NULL).  endp = rounded
+ * end_time_park_min (V).  Writes obs (6), real_power, reward. */
+int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
+                    const double* endp, double* req, uint64_t* charging, pgw_mat obs,
+                    double* real_power, double* reward, void* stream);
+
+/* ------------------------------------------------------------------------
+ * MultiComponentEnv reduction (gridworld/base.py:125-156): real_power and
+ * reward summed in component order starting from 0.
+ * ---------------------------------------------------------------------- */
+#define PGW_MAX_COMP 8
+typedef struct pgw_reduce_args {
+  const double* real_power[PGW_MAX_COMP];  /* NULL = contributes 0 */
+  const double* reward[PGW_MAX_COMP];      /* NULL = contributes 0 */
+  int32_t n_comp, pad_;
+} pgw_reduce_args;
+int32_t pgw_agent_reduce(const pgw_reduce_args* a, int64_t n, double* real_power, double* reward,
+                         void* stream);
+
+/* ------------------------------------------------------------------------
+ * Distribution power flow.  Replaces OpenDSSSolver.calculate_power_flow +
+ * get_bus_voltages (gridworld/distribution_system/opendss.py:80-165); the
+ * per-env snap solve is a fixed-point current-injection iteration on the
+ * load-element voltages  U = U0 + W f(U)  (see DESIGN.md).
+ * ---------------------------------------------------------------------- */
+#define PGW_PF_MAX_M 16     /* load phase elements (IEEE-13: 14) */
+#define PGW_PF_MAX_CTRL 8   /* controllable loads     */
+
+typedef struct pgw_pf_params {
+  double vbase[PGW_PF_MAX_M];       /* element base voltage (V)               */
+  double vmin[PGW_PF_MAX_M], vmax[PGW_PF_MAX_M], vlow[PGW_PF_MAX_M];  /* pu   */
+  double nph[PGW_PF_MAX_M];          /* phases of the element's load           */
+  double base_kw[PGW_PF_MAX_M];     /* the element's LOAD total kW this step  */
+  double base_kvar[PGW_PF_MAX_M];   /*   (loadshape x base x rescale)         */
+  double tol;                       /* max |dU|/vbase convergence tolerance   */
+  int32_t elem_ctrl[PGW_PF_MAX_M];  /* controllable-load slot of the element, -1 none */
+  int32_t m, n_ctrl, n_out, max_iter;
+} pgw_pf_params;
+
+/* Device tables built once by pgw_feeder_build / pgw_pf_reduce. */
+typedef struct pgw_pf_tables {
+  const double* W;      /* m x m complex (re,im interleaved), row-major */
+  const double* U0;     /* m complex                                    */
+  const double* G;      /* n_out x m complex: node voltage response     */
+  const double* V0;     /* n_out complex: no-load node voltages         */
+  const double* inv_vbase_out;  /* n_out: 1 / (kV_LN * 1000)           */
+} pgw_pf_tables;
+
+/* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)
+ * (opendss.py:107-129 then OpenDSS's per-phase WNominal).
+ * ctrl_p / ctrl_q: n_ctrl x n (kW / kvar, NULL = 0).  v_out: n_out x n (pu).
+ * iters: n (int32, nullable) iteration count per env. */
+int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
+                     const double* ctrl_p, const double* ctrl_q, double* v_out,
+                     int32_t* iters, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Host-side feeder construction (C++, no GPU): the native stand-in for the
+ * OpenDSS model build behind opendss.py:36-51.
+ * ---------------------------------------------------------------------- */
+enum { PGW_ELEM_LINE = 1, PGW_ELEM_XFMR = 2, PGW_ELEM_VSOURCE = 3 };
+
+typedef struct pgw_feeder_elem {
+  int32_t kind;          /* PGW_ELEM_*                                     */
+  int32_t nphases;
+  int32_t node1[3];      /* terminal-1 node per phase (-1 = ground)        */
+  int32_t node2[3];      /* terminal-2 node per phase (-1 = ground)        */
+  int32_t conn1, conn2;  /* transformer winding connection: 0 wye, 1 delta */
+  double r[9], x[9], c[9];  /* line: R, X (ohm/unit), C (nF/unit), row-major nphases^2 */
+  double length;         /* line: length in the matrices' unit            */
+  double freq;           /* Hz                                            */
+  double kv1, kv2, kva, pct_r1, pct_r2, xhl;       /* transformer          */
+  double basekv, pu, angle, mvasc3, mvasc1, x1r1, x0r0;  /* vsource        */
+} pgw_feeder_elem;
+
+/* Assemble the nodal admittance Y (n_nodes^2, complex interleaved, loads
+ * excluded), Z = Y^-1, the source current injection and the no-load voltages
+ * V0 = Z I_src.  Any output pointer may be NULL.  Host memory. */
+int32_t pgw_feeder_build(const pgw_feeder_elem* elems, int32_t n_elems, int32_t n_nodes,
+                         double* Y, double* Z, double* I_src, double* V0);
+/* Reduce to the m load elements (element k spans node p[k] -> q[k], q = -1
+ * ground): W = -C Z C^T, U0 = C V0, and for the n_out nodes in out_nodes:
+ * G = -(Z C^T)[out_nodes], V0_out = V0[out_nodes].  Host memory. */
+int32_t pgw_pf_reduce(int32_t n_nodes, const double* Z, const double* V0, int32_t m,
+                      const int32_t* elem_p, const int32_t* elem_q, int32_t n_out,
+                      const int32_t* out_nodes, double* W, double* U0, double* G,
+                      double* V0_out);
+
+/* ------------------------------------------------------------------------
+ * Fused coordinated multi-building step (the BASELINE C4 hot path):
+ * MultiAgentEnv.step (gridworld/multiagent_env.py:151-212) over n_agents
+ * MultiComponentEnv agents of [building, pv, storage] (gridworld/scenarios/
+ * buildings.py:11-72) + the power flow + CoordinatedMultiBuildingControlEnv.
+ * reward_transform (examples/marl/openai/train.py:51-88), one thread per env.
+ * ---------------------------------------------------------------------- */
+#define PGW_MAX_AGENTS 8
+
+typedef struct pgw_coord_params {
+  pgw_building_params bld;
+  pgw_pv_params pv;
+  pgw_battery_params bat;
+  double vv_lo, vv_hi, vv_penalty;   /* VOLTAGE_LIMITS, VV_UNIT_PENALTY         */
+  int32_t n_agents;
+  int32_t act_dim, obs_dim;          /* per agent                               */
+  int32_t act_bld, act_pv, act_bat;  /* component action offsets (-1 = absent)  */
+  int32_t obs_bld, obs_pv, obs_bat;  /* component obs offsets                   */
+  int32_t comp_order[3];             /* 0 building, 1 pv, 2 storage             */
+  int32_t n_comp;
+  int32_t agent_ctrl[PGW_MAX_AGENTS];/* PF controllable slot of each agent's bus */
+  int32_t coordinated;               /* apply the voltage-violation transform   */
+  int32_t vv_row;                    /* PF output row of the common-bus voltage */
+} pgw_coord_params;
+
+/* Per-env buffers.  action: agent a's block at action.ptr + a * act_stride_agent;
+ * obs likewise.  x: n_agents x 5 x n;  soc: n_agents x n;  reward, agent_power:
+ * n_agents x n;  v_out: pf n_out x n;  vv: n (nullable). */
+typedef struct pgw_coord_buffers {
+  pgw_mat action; int64_t act_stride_agent;
+  pgw_mat obs;    int64_t obs_stride_agent;
+  double* x;
+  double* soc;
+  double* reward;
+  double* agent_power;
+  double* v_out;
+  double* vv;
+  int32_t* iters;
+} pgw_coord_buffers;
+
+typedef struct pgw_coord_step_info {
+  pgw_building_exo ex_t, ex_next;
+  double pv_pmax;        /* PV data[index] before the advance */
+} pgw_coord_step_info;
+
+int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf,
+                       const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                       pgw_coord_buffers b, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PGW_H_ */

@@ -309,8 +309,101 @@ def gen_mc():
     _save("mc_c3", **arrays)
 
 
+# --------------------------------------------------------------------------
+# C4: 5 coordinated buildings + power flow (multiagent_env.py + train.py:37-88)
+# --------------------------------------------------------------------------
+from gridworld.distribution_system.powerflow import PowerFlowSolver  # noqa: E402
+from gridworld.scenarios.buildings import make_env_config  # noqa: E402
+from oracle.pf_oracle import BatchedPF  # noqa: E402
+
+
+class OraclePowerFlowSolver(PowerFlowSolver):
+    """The oracle PF behind the reference's PowerFlowSolver ABC (OpenDSS is absent)."""
+
+    def __init__(self, system_load_rescale_factor=1.0, **kwargs):
+        self.pf = BatchedPF(system_load_rescale_factor=system_load_rescale_factor)
+        self.bus_voltages = {}
+        self.trace = []
+
+    def calculate_power_flow(self, p_controllable_consumed=None, q_controllable_consumed=None,
+                             current_time=None):
+        pu = self.pf.calculate(current_time, p_controllable_consumed, q_controllable_consumed, K=1)[0]
+        self.bus_voltages = dict(zip(self.pf.feeder.node_names, pu))
+        self.trace.append(pu.copy())
+
+    def get_bus_voltages(self):
+        return self.bus_voltages
+
+    def get_bus_voltage_by_name(self, bus_name):
+        PHASE_MAP = {'a': '.1', 'b': '.2', 'c': '.3'}
+        if bus_name[-1] in PHASE_MAP.keys():
+            return self.bus_voltages[bus_name.replace(bus_name[-1], PHASE_MAP[bus_name[-1]])]
+        return [self.bus_voltages[x] for x in [bus_name + p for p in PHASE_MAP.values()]]
+
+
+class CoordinatedEnv(MultiAgentEnv):
+    """Restates CoordinatedMultiBuildingControlEnv (examples/marl/openai/train.py:37-88),
+    whose module cannot be imported here (tensorflow/maddpg)."""
+    VOLTAGE_LIMITS = [0.95, 1.05]
+    VV_UNIT_PENALTY = 1e4
+
+    def reward_transform(self, rew_dict):
+        vv = self.get_voltage_violation()
+        for key in rew_dict.keys():
+            rew_dict[key] -= (vv * self.VV_UNIT_PENALTY / len(rew_dict))
+        return rew_dict
+
+    def meta_transform(self, meta):
+        meta.update({'voltage_violation': self.get_voltage_violation()})
+        return meta
+
+    def get_voltage_violation(self):
+        bus_id = list(set(self.agent_name_bus_map.values()))[0]
+        v = self.pf_solver.get_bus_voltage_by_name(bus_id)
+        return max([0.0, self.VOLTAGE_LIMITS[0] - v, v - self.VOLTAGE_LIMITS[1]])
+
+
+def gen_c4():
+    rng = np.random.default_rng(606)
+    K, NA = 2, 5
+    T = 286
+    cfg = make_env_config(building_config={},
+                          pv_config={"profile_csv": "pv_profile.csv", "scaling_factor": 40.},
+                          storage_config={"max_power": 15., "storage_range": (3., 50.)},
+                          system_load_rescale_factor=1.2, num_buildings=NA)
+    cfg["pf_config"] = {"cls": OraclePowerFlowSolver, "config": {"system_load_rescale_factor": 1.2}}
+    acts = rng.uniform(-1, 1, size=(T, NA, K, 8))
+    mask = rng.random(acts.shape) < 0.03
+    acts[mask] *= 1.2
+    obs = np.zeros((T + 1, NA, K, 17)); rew = np.zeros((T, NA, K)); vv = np.zeros((T, K))
+    done = np.zeros((T, K), bool); soc0 = np.zeros((NA, K)); v675 = np.zeros((T + 1, K))
+    for k in range(K):
+        env = CoordinatedEnv(**copy.deepcopy(cfg))
+        names = [a.name for a in env.agents]
+        with quiet():
+            o = env.reset()
+        for a, nm in enumerate(names):
+            soc0[a, k] = env.agent_dict[nm].env_dict["storage"].current_storage
+            obs[0, a, k] = np.concatenate([o[nm]["building"], o[nm]["pv"], o[nm]["storage"]])
+        v675[0, k] = env.pf_solver.get_bus_voltage_by_name("675c")
+        for t in range(T):
+            action = {nm: {"building": acts[t, a, k, :6], "pv": acts[t, a, k, 6:7],
+                           "storage": acts[t, a, k, 7:8]} for a, nm in enumerate(names)}
+            with quiet():
+                o, r, d, m = env.step(action)
+            for a, nm in enumerate(names):
+                obs[t + 1, a, k] = np.concatenate([o[nm]["building"], o[nm]["pv"], o[nm]["storage"]])
+                rew[t, a, k] = r[nm]
+            vv[t, k] = m["voltage_violation"]
+            done[t, k] = d["__all__"]
+            v675[t + 1, k] = env.pf_solver.get_bus_voltage_by_name("675c")
+    assert done[-1].all() and not done[:-1].any()
+    _save("c4_coordinated", actions=acts, obs=obs, reward=rew, voltage_violation=vv, done=done,
+          init_storage=soc0, v675=v675)
+
+
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "mc": gen_mc}
+              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4}
 
 
 def main():
@@ -318,7 +411,9 @@ def main():
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
     np.random.seed(0)
-    EXO.to_csv(os.path.join(GOLDEN, "exogenous_synthetic.csv.gz"))
+    np.savez_compressed(os.path.join(GOLDEN, "exogenous_synthetic.npz"),
+                        index_ns=EXO.index.values.astype("datetime64[ns]").astype(np.int64),
+                        columns=np.array(list(EXO.columns)), values=EXO.values)
     for name, fn in GENERATORS.items():
         if args.only and name != args.only:
             continue

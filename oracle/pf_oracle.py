@@ -1,0 +1,314 @@
+"""CPU oracle for the distribution power flow (TEST INFRASTRUCTURE; see
+``oracle/pgw_oracle.py`` header for the import rule).
+
+The reference delegates the solve to the third-party OpenDSS engine through
+``OpenDSSDirect.py==0.6.1`` (``requirements.txt:6``), which is absent from this
+image: PF parity is UNPINNED.  This module restates, in NumPy
+fp64 and independently of the product's C++/HIP code, the published OpenDSS
+models the reference's call sites rely on:
+
+* ``OpenDSSSolver.calculate_power_flow`` (``opendss.py:80-135``): load =
+  loadshape[hour_of_year] * base(kW,kvar) * rescale, plus controllable P/Q
+  looked up by LOAD NAME; snap solve; per-node |V| in pu (``:156-165``);
+* ``get_bus_voltage_by_name`` (``opendss.py:173-186``): 'xxxc' -> 'xxx.3';
+* OpenDSS element models: Vsource (Thevenin from MVAsc3/MVAsc1, X1/R1=4,
+  X0/R0=3), 2-winding transformers (leakage %r1+%r2 + jXHL, wye/delta),
+  lines (R/X/C matrices x length, C split half/half), PQ loads (model 1:
+  constant PQ inside [Vminpu, Vmaxpu], constant Z outside, Vlowpu floor).
+
+Solve: nodal admittance Y (no loads) -> Z = Y^-1, no-load voltages V0 =
+Z I_src; the load-element voltages U obey U = U0 + W f(U) with W = -C Z C^T
+(C: element incidence) and f the PQ-load current law, iterated to
+``max |dU| / Vbase < tol``.  The product kernel uses the same algorithm.
+"""
+import json
+import math
+import os
+from datetime import datetime
+
+import numpy as np
+import pandas as pd
+
+DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    "powergridworld_amd", "data")
+
+_TO_MI = {"mi": 1.0, "kft": 1000.0 / 5280.0, "ft": 1.0 / 5280.0, "km": 1.0 / 1.609344,
+          "m": 1.0 / 1609.344, "none": 1.0}
+
+
+def load_ieee13():
+    with open(os.path.join(DATA, "ieee13.json")) as f:
+        return json.load(f)
+
+
+def _bus(spec, default):
+    parts = spec.split(".")
+    return parts[0].lower(), ([int(p) for p in parts[1:]] if len(parts) > 1 else list(default))
+
+
+class Feeder:
+    """Nodal model of a parsed feeder spec (see powergridworld_amd/distribution_system/dss.py)."""
+
+    def __init__(self, spec):
+        self.spec = spec
+        self.bus_nodes = {}           # bus -> ordered node numbers
+        self.buses = []
+
+        def touch(bus, nodes):
+            if bus not in self.bus_nodes:
+                self.bus_nodes[bus] = []
+                self.buses.append(bus)
+            for nd in nodes:
+                if nd != 0 and nd not in self.bus_nodes[bus]:
+                    self.bus_nodes[bus].append(nd)
+
+        src = spec["source"]
+        touch(src["bus"], [1, 2, 3])
+        for t in spec["transformers"]:
+            for w in t["windings"]:
+                b, nds = _bus(w["bus"], [1, 2, 3][:t["phases"]])
+                touch(b, nds)
+        for ld in spec["loads"]:
+            b, nds = _bus(ld["bus1"], [1, 2, 3][:ld["phases"]])
+            touch(b, nds)
+        for ln in spec["lines"]:
+            for key in ("bus1", "bus2"):
+                b, nds = _bus(ln[key], [1, 2, 3][:ln["phases"]])
+                touch(b, nds)
+        self.node_names = ["%s.%d" % (b, nd) for b in self.buses for nd in self.bus_nodes[b]]
+        self.idx = {n: i for i, n in enumerate(self.node_names)}
+        self.n = len(self.node_names)
+        self._build_y()
+        self._assign_bases()
+        self._build_loads()
+
+    def node(self, bus, nd):
+        return -1 if nd == 0 else self.idx["%s.%d" % (bus, nd)]
+
+    def _stamp(self, nodes, yprim):
+        for a, na in enumerate(nodes):
+            if na < 0:
+                continue
+            for b, nb in enumerate(nodes):
+                if nb < 0:
+                    continue
+                self.Y[na, nb] += yprim[a, b]
+
+    def _build_y(self):
+        spec = self.spec
+        f = spec.get("base_frequency", 60.0)
+        w = 2 * math.pi * f
+        self.Y = np.zeros((self.n, self.n), complex)
+        self.I_src = np.zeros(self.n, complex)
+        # --- Vsource (Thevenin -> Norton)
+        s = spec["source"]
+        kv = s["basekv"]
+        z1mag = kv * kv / s["mvasc3"]
+        x1 = z1mag * s["x1r1"] / math.sqrt(1 + s["x1r1"] ** 2)
+        r1 = x1 / s["x1r1"]
+        zs_mag = 3.0 * kv * kv / s["mvasc1"]        # |2 Z1 + Z0|
+        a = 1 + s["x0r0"] ** 2
+        b = 4 * (r1 + x1 * s["x0r0"])
+        c = 4 * (r1 * r1 + x1 * x1) - zs_mag ** 2
+        r0 = (-b + math.sqrt(b * b - 4 * a * c)) / (2 * a)
+        x0 = r0 * s["x0r0"]
+        Z1, Z0 = complex(r1, x1), complex(r0, x0)
+        zself, zmut = (2 * Z1 + Z0) / 3, (Z0 - Z1) / 3
+        Zs = np.full((3, 3), zmut) + np.eye(3) * (zself - zmut)
+        Ys = np.linalg.inv(Zs)
+        vln = s["pu"] * kv * 1000 / math.sqrt(3)
+        ang = np.deg2rad(s["angle"] + np.array([0.0, -120.0, 120.0]))
+        E = vln * np.exp(1j * ang)
+        nodes = [self.node(s["bus"], k) for k in (1, 2, 3)]
+        self._stamp(nodes, Ys)
+        self.I_src[nodes] += Ys @ E
+        # --- transformers
+        for t in spec["transformers"]:
+            ph = t["phases"]
+            w1, w2 = t["windings"]
+            b1, n1 = _bus(w1["bus"], [1, 2, 3][:ph])
+            b2, n2 = _bus(w2["bus"], [1, 2, 3][:ph])
+            vw1 = w1["kv"] * 1000 / (math.sqrt(3) if (w1["conn"] == "wye" and ph == 3) else 1.0)
+            vw2 = w2["kv"] * 1000 / (math.sqrt(3) if (w2["conn"] == "wye" and ph == 3) else 1.0)
+            kva_ph = w1["kva"] * 1000 / ph
+            zpu = complex((w1["pct_r"] + w2["pct_r"]) / 100.0, t["xhl"] / 100.0)
+            y = 1.0 / (zpu * vw1 * vw1 / kva_ph)
+            nr = vw1 / vw2
+            yw = y * np.array([[1, -nr], [-nr, nr * nr]])
+            for p in range(ph):
+                inc = np.zeros((2, self.n), complex)
+                for k, (bb, nn, conn) in enumerate(((b1, n1, w1["conn"]), (b2, n2, w2["conn"]))):
+                    hi = self.node(bb, nn[p])
+                    inc[k, hi] += 1
+                    if conn == "delta":
+                        lo = self.node(bb, nn[(p + 1) % ph])
+                        inc[k, lo] -= 1
+                self.Y += inc.T @ yw @ inc
+        # --- lines
+        for ln in spec["lines"]:
+            ph = ln["phases"]
+            if ln.get("sequence") is not None or ln["linecode"] is None:
+                sq = ln.get("sequence") or {}
+                Z1 = complex(sq.get("r1", 0.058), sq.get("x1", 0.1206))
+                Z0 = complex(sq.get("r0", 0.1784), sq.get("x0", 0.4047))
+                C1, C0 = sq.get("c1", 3.4), sq.get("c0", 1.6)
+                Zm = np.full((ph, ph), (Z0 - Z1) / 3) + np.eye(ph) * ((2 * Z1 + Z0) / 3 - (Z0 - Z1) / 3)
+                Cm = np.full((ph, ph), (C0 - C1) / 3) + np.eye(ph) * ((2 * C1 + C0) / 3 - (C0 - C1) / 3)
+                scale = ln["length"] * (1.0 if ln["units"] == "none" else _TO_MI[ln["units"]])
+            else:
+                lc = spec["linecodes"][ln["linecode"]]
+                Zm = np.array(lc["rmatrix"]) + 1j * np.array(lc["xmatrix"])
+                if lc.get("cmatrix") is not None:
+                    Cm = np.array(lc["cmatrix"], float)
+                else:
+                    C1, C0 = lc["c1"], lc["c0"]
+                    Cm = np.full((ph, ph), (C0 - C1) / 3) + np.eye(ph) * ((2 * C1 + C0) / 3 - (C0 - C1) / 3)
+                unit = lc["units"] if ln["units"] == "none" else ln["units"]
+                scale = ln["length"] * (_TO_MI[ln["units"]] / _TO_MI[lc["units"]]
+                                        if ln["units"] != "none" and lc["units"] != "none" else 1.0)
+            Zt = Zm * scale
+            Yc = 1j * w * Cm * 1e-9 * scale
+            Yser = np.linalg.inv(Zt)
+            b1, n1 = _bus(ln["bus1"], [1, 2, 3][:ph])
+            b2, n2 = _bus(ln["bus2"], [1, 2, 3][:ph])
+            nodes = [self.node(b1, k) for k in n1] + [self.node(b2, k) for k in n2]
+            yp = np.block([[Yser + Yc / 2, -Yser], [-Yser, Yser + Yc / 2]])
+            self._stamp(nodes, yp)
+        self.Z = np.linalg.inv(self.Y)
+        self.V0 = self.Z @ self.I_src
+
+    def _assign_bases(self):
+        """'Set Voltagebases' + 'calcv': nearest base (kV LL) to each bus's no-load voltage."""
+        bases = np.array(self.spec["voltagebases"], float)
+        self.kv_ln = np.zeros(self.n)
+        for b in self.buses:
+            ids = [self.idx["%s.%d" % (b, nd)] for nd in self.bus_nodes[b]]
+            vll = np.abs(self.V0[ids]).mean() * math.sqrt(3) / 1000.0
+            base = bases[np.argmin(np.abs(bases - vll))]
+            self.kv_ln[ids] = base / math.sqrt(3)
+
+    def _build_loads(self):
+        """PQ load phase elements: (p node, q node, Vbase, load index)."""
+        self.load_names = [ld["name"] for ld in self.spec["loads"]]
+        self.elem_p, self.elem_q, self.elem_vbase, self.elem_load, self.elem_nph = [], [], [], [], []
+        self.load_vmin, self.load_vmax, self.load_vlow = [], [], []
+        for li, ld in enumerate(self.spec["loads"]):
+            ph = ld["phases"]
+            b, nds = _bus(ld["bus1"], [1, 2, 3][:ph])
+            for p in range(ph):
+                hi = self.node(b, nds[p])
+                if ld["conn"] == "delta":
+                    lo = self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])
+                    vb = ld["kv"] * 1000
+                else:
+                    lo = -1
+                    vb = ld["kv"] * 1000 / (math.sqrt(3) if ph == 3 else 1.0)
+                self.elem_p.append(hi); self.elem_q.append(lo); self.elem_vbase.append(vb)
+                self.elem_load.append(li); self.elem_nph.append(ph)
+            self.load_vmin.append(ld.get("vminpu", 0.95)); self.load_vmax.append(ld.get("vmaxpu", 1.05))
+            self.load_vlow.append(ld.get("vlowpu", 0.5))
+        m = len(self.elem_p)
+        C = np.zeros((m, self.n))
+        for k in range(m):
+            C[k, self.elem_p[k]] = 1
+            if self.elem_q[k] >= 0:
+                C[k, self.elem_q[k]] = -1
+        self.Cinc = C
+        self.W = -C @ self.Z @ C.T
+        self.U0 = C @ self.V0
+        self.G = -self.Z @ C.T
+        self.elem_vbase = np.array(self.elem_vbase)
+        self.elem_load = np.array(self.elem_load)
+        self.elem_nph = np.array(self.elem_nph)
+        self.base_kw = np.array([ld["kw"] for ld in self.spec["loads"]], float)
+        self.base_kvar = np.array([ld["kvar"] for ld in self.spec["loads"]], float)
+
+    # ------------------------------------------------------------------ solve
+    def load_currents(self, U, W_ph, var_ph):
+        """OpenDSS Load.DoConstantPQLoad, per element (K, m) complex."""
+        vb = self.elem_vbase
+        vmin = np.array(self.load_vmin)[self.elem_load]
+        vmax = np.array(self.load_vmax)[self.elem_load]
+        vlow = np.array(self.load_vlow)[self.elem_load]
+        S = W_ph + 1j * var_ph
+        yeq = np.conj(S) / (vb * vb)
+        mag = np.abs(U)
+        i_pq = np.conj(S) / np.conj(np.where(mag > 0, U, 1.0))
+        I = np.where(mag <= vlow * vb, yeq * U,
+            np.where(mag <= vmin * vb, (yeq / (vmin * vmin)) * U,
+            np.where(mag > vmax * vb, (yeq / (vmax * vmax)) * U, i_pq)))
+        return I
+
+    def solve(self, load_kw, load_kvar, tol=1e-10, max_iter=100):
+        """load_kw/kvar: (K, n_loads) total per load.  Returns (V nodes (K,n), iters (K,)).
+        Each env iterates until ITS OWN max |dU|/Vbase < tol (as the kernel does)."""
+        load_kw = np.atleast_2d(load_kw)
+        load_kvar = np.atleast_2d(load_kvar)
+        K = load_kw.shape[0]
+        W_ph = load_kw[:, self.elem_load] * 1000.0 / self.elem_nph
+        var_ph = load_kvar[:, self.elem_load] * 1000.0 / self.elem_nph
+        U = np.tile(self.U0, (K, 1))
+        iters = np.zeros(K, int)
+        active = np.ones(K, bool)
+        for it in range(1, max_iter + 1):
+            idx = np.nonzero(active)[0]
+            I = self.load_currents(U[idx], W_ph[idx], var_ph[idx])
+            Un = self.U0 + I @ self.W.T
+            err = np.max(np.abs(Un - U[idx]) / self.elem_vbase, axis=1)
+            U[idx] = Un
+            iters[idx] = it
+            active[idx[err < tol]] = False
+            if not active.any():
+                break
+        I = self.load_currents(U, W_ph, var_ph)
+        V = self.V0 + I @ self.G.T
+        return V, iters
+
+    def pu(self, V):
+        return np.abs(V) / (self.kv_ln * 1000.0)
+
+
+def hour_of_year(ts):
+    """opendss.py:98-103"""
+    ts = pd.Timestamp(ts)
+    return int((ts - datetime(ts.year, 1, 1)).total_seconds() // 3600)
+
+
+def load_loadshape():
+    return np.load(os.path.join(DATA, "loadshape_8760.npy"))
+
+
+class BatchedPF:
+    """Batched restatement of OpenDSSSolver.calculate_power_flow for K envs."""
+
+    def __init__(self, spec=None, system_load_rescale_factor=1.0, tol=1e-10):
+        self.feeder = Feeder(spec if spec is not None else load_ieee13())
+        self.rescale = system_load_rescale_factor
+        self.shape = load_loadshape()
+        self.tol = tol
+
+    def base_loads(self, current_time):
+        coef = self.shape[hour_of_year(current_time)]
+        f = self.feeder
+        return coef * f.base_kw * self.rescale, coef * f.base_kvar * self.rescale   # opendss.py:106-108
+
+    def calculate(self, current_time, p_ctrl=None, q_ctrl=None, K=1):
+        """p_ctrl/q_ctrl: {load_name: array (K,)}.  Returns node pu voltages (K, n)."""
+        kw, kvar = self.base_loads(current_time)
+        kw = np.tile(kw, (K, 1)); kvar = np.tile(kvar, (K, 1))
+        names = self.feeder.load_names
+        for d, arr in ((p_ctrl, kw), (q_ctrl, kvar)):
+            for name, v in (d or {}).items():
+                if name in names:
+                    arr[:, names.index(name)] = arr[:, names.index(name)] + np.asarray(v, float)
+        V, it = self.feeder.solve(kw, kvar, tol=self.tol)
+        self.last_iters = it
+        return self.feeder.pu(V)
+
+
+def bus_name_to_node(name):
+    """opendss.py:173-186: replace every occurrence of the last char."""
+    PHASE_MAP = {'a': '.1', 'b': '.2', 'c': '.3'}
+    if name[-1] in PHASE_MAP:
+        return [name.replace(name[-1], PHASE_MAP[name[-1]])]
+    return [name + p for p in PHASE_MAP.values()]

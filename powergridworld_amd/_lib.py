@@ -1,0 +1,206 @@
+"""ctypes binding of libpgw.so (the C ABI declared in include/pgw.h).
+
+There is no fallback: if the in-tree library is missing or stale the import
+fails loudly -- the product path never silently runs anything but the HIP
+kernels.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpgw.so")
+ABI_VERSION = 1
+
+f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
+P = C.POINTER
+
+BLD_MAX_OBS = 24
+EV_MAX_WORDS = 16
+MAX_COMP = 8
+PF_MAX_M = 16
+PF_MAX_CTRL = 8
+MAX_AGENTS = 8
+
+
+class PgwError(RuntimeError):
+    pass
+
+
+class Mat(C.Structure):
+    _fields_ = [("ptr", vp), ("s_env", i64), ("s_dim", i64)]
+
+
+class BatteryParams(C.Structure):
+    _fields_ = [("soc_min", f64), ("soc_max", f64), ("eta_c", f64), ("eta_d", f64),
+                ("max_power", f64), ("dt_h", f64), ("rescale", i32), ("pad_", i32)]
+
+
+class PVParams(C.Structure):
+    _fields_ = [("obs_low", f64), ("obs_high", f64), ("vmin_low", f64), ("vmin_high", f64),
+                ("rescale", i32), ("grid_aware", i32)]
+
+
+class BuildingParams(C.Structure):
+    _fields_ = [("A", f64 * 5), ("B", (f64 * 4) * 5), ("K", f64 * 5), ("C", f64 * 5),
+                ("mean", f64 * 5), ("act_low", f64 * 6), ("act_high", f64 * 6),
+                ("T_init", f64 * 5), ("obs_low", f64 * BLD_MAX_OBS),
+                ("obs_high", f64 * BLD_MAX_OBS), ("alpha", f64),
+                ("sel", (i32 * 4) * 5), ("nbr", (i32 * 4) * 5),
+                ("obs_var", i32 * BLD_MAX_OBS), ("n_obs", i32), ("rescale", i32)]
+
+
+class BuildingExo(C.Structure):
+    _fields_ = [("T_oa", f64), ("q_solar", f64 * 5), ("q_int", f64 * 5), ("q_cool", f64 * 5),
+                ("comfort_lb", f64), ("comfort_ub", f64), ("time_of_day", f64), ("pad_", f64)]
+
+
+class BuildingExt(C.Structure):
+    _fields_ = [("bus_voltage", vp), ("min_voltage", vp), ("max_voltage", vp), ("p_setpoint", vp)]
+
+
+class EVParams(C.Structure):
+    _fields_ = [("rate", f64), ("hours_per_step", f64), ("mult", f64), ("u_pen", f64),
+                ("p_pen", f64), ("thr", f64), ("reward_scale", f64), ("obs_low", f64 * 6),
+                ("obs_high", f64 * 6), ("n_vehicles", i32), ("rescale", i32)]
+
+
+class EVStepInfo(C.Structure):
+    _fields_ = [("time", f64), ("next_time", f64), ("action_default", f64), ("n_words", i32),
+                ("pad_", i32), ("window", u64 * EV_MAX_WORDS), ("scan", u64 * EV_MAX_WORDS)]
+
+
+class ReduceArgs(C.Structure):
+    _fields_ = [("real_power", vp * MAX_COMP), ("reward", vp * MAX_COMP), ("n_comp", i32),
+                ("pad_", i32)]
+
+
+class PFParams(C.Structure):
+    _fields_ = [("vbase", f64 * PF_MAX_M), ("vmin", f64 * PF_MAX_M), ("vmax", f64 * PF_MAX_M),
+                ("vlow", f64 * PF_MAX_M), ("nph", f64 * PF_MAX_M), ("base_kw", f64 * PF_MAX_M),
+                ("base_kvar", f64 * PF_MAX_M), ("tol", f64), ("elem_ctrl", i32 * PF_MAX_M),
+                ("m", i32), ("n_ctrl", i32), ("n_out", i32), ("max_iter", i32)]
+
+
+class PFTables(C.Structure):
+    _fields_ = [("W", vp), ("U0", vp), ("G", vp), ("V0", vp), ("inv_vbase_out", vp)]
+
+
+class FeederElem(C.Structure):
+    _fields_ = [("kind", i32), ("nphases", i32), ("node1", i32 * 3), ("node2", i32 * 3),
+                ("conn1", i32), ("conn2", i32), ("r", f64 * 9), ("x", f64 * 9), ("c", f64 * 9),
+                ("length", f64), ("freq", f64), ("kv1", f64), ("kv2", f64), ("kva", f64),
+                ("pct_r1", f64), ("pct_r2", f64), ("xhl", f64), ("basekv", f64), ("pu", f64),
+                ("angle", f64), ("mvasc3", f64), ("mvasc1", f64), ("x1r1", f64), ("x0r0", f64)]
+
+
+class CoordParams(C.Structure):
+    _fields_ = [("bld", BuildingParams), ("pv", PVParams), ("bat", BatteryParams),
+                ("vv_lo", f64), ("vv_hi", f64), ("vv_penalty", f64), ("n_agents", i32),
+                ("act_dim", i32), ("obs_dim", i32), ("act_bld", i32), ("act_pv", i32),
+                ("act_bat", i32), ("obs_bld", i32), ("obs_pv", i32), ("obs_bat", i32),
+                ("comp_order", i32 * 3), ("n_comp", i32), ("agent_ctrl", i32 * MAX_AGENTS),
+                ("coordinated", i32), ("vv_row", i32)]
+
+
+class CoordBuffers(C.Structure):
+    _fields_ = [("action", Mat), ("act_stride_agent", i64), ("obs", Mat), ("obs_stride_agent", i64),
+                ("x", vp), ("soc", vp), ("reward", vp), ("agent_power", vp), ("v_out", vp),
+                ("vv", vp), ("iters", vp)]
+
+
+class CoordStepInfo(C.Structure):
+    _fields_ = [("ex_t", BuildingExo), ("ex_next", BuildingExo), ("pv_pmax", f64)]
+
+
+PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE = 1, 2, 3
+
+_SIGS = {
+    "pgw_abi_version": (i32, []),
+    "pgw_struct_sizes": (i32, [P(i64), i32]),
+    "pgw_last_error": (C.c_char_p, []),
+    "pgw_battery_reset": (i32, [P(BatteryParams), i64, vp, vp, Mat, vp]),
+    "pgw_battery_step": (i32, [P(BatteryParams), i64, Mat, vp, Mat, vp, vp]),
+    "pgw_pv_obs": (i32, [P(PVParams), i64, f64, vp, Mat, vp]),
+    "pgw_pv_step": (i32, [P(PVParams), i64, f64, Mat, vp, Mat, vp, vp]),
+    "pgw_building_reset": (i32, [P(BuildingParams), P(BuildingExo), i64, vp, vp, vp, BuildingExt,
+                                 Mat, vp]),
+    "pgw_building_step": (i32, [P(BuildingParams), P(BuildingExo), P(BuildingExo), i64, Mat, vp, vp,
+                                vp, vp, i32, BuildingExt, Mat, vp]),
+    "pgw_ev_reset": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
+    "pgw_ev_step": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
+    "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
+    "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
+    "pgw_pf_padded_m": (i32, [i32]),
+    "pgw_feeder_build": (i32, [P(FeederElem), i32, i32, vp, vp, vp, vp]),
+    "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
+    "pgw_coord_step": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
+                             CoordBuffers, vp]),
+}
+
+EXPORTED = sorted(_SIGS)
+
+STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
+           EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
+           CoordStepInfo]
+
+_lib = None
+
+
+def lib():
+    """Load libpgw.so (once).  Raises PgwError if it is missing or mismatched."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PgwError("libpgw.so not found at %s -- build it with "
+                       "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                       "`make -C powergridworld_amd/csrc`" % LIB_PATH)
+    h = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = args
+    if h.pgw_abi_version() != ABI_VERSION:
+        raise PgwError("libpgw ABI %d != expected %d (rebuild)" % (h.pgw_abi_version(), ABI_VERSION))
+    sizes = (i64 * len(STRUCTS))()
+    h.pgw_struct_sizes(sizes, len(STRUCTS))
+    for st, sz in zip(STRUCTS, sizes):
+        if C.sizeof(st) != sz:
+            raise PgwError("ABI struct %s: ctypes %d B != C %d B" % (st.__name__, C.sizeof(st), sz))
+    _lib = h
+    return h
+
+
+def check(rc):
+    if rc != 0:
+        raise PgwError(lib().pgw_last_error().decode() or ("libpgw error %d" % rc))
+
+
+def stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def dptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def mat(t2d):
+    """pgw_mat for a 2-D [n_envs, dim] fp64 device tensor (any strides)."""
+    if t2d is None:
+        return Mat(None, 0, 0)
+    assert t2d.dim() == 2 and t2d.dtype == torch.float64, (t2d.shape, t2d.dtype)
+    return Mat(t2d.data_ptr(), t2d.stride(0), t2d.stride(1))
+
+
+def require_device(device):
+    device = torch.device(device) if device is not None else torch.device("cuda")
+    if device.type != "cuda":
+        raise PgwError("powergridworld_amd runs its step kernels on the GPU only "
+                       "(got device=%s); there is no CPU fallback" % device)
+    if not torch.cuda.is_available():
+        raise PgwError("no ROCm GPU visible: the HIP step kernels cannot run here")
+    lib()
+    return device

@@ -1,0 +1,121 @@
+"""Batched EnergyStorageEnv (reference: gridworld/agents/energy_storage/energy_storage_env.py)."""
+import math
+
+import numpy as np
+import pandas as pd
+import torch
+
+from powergridworld_amd import _lib, spaces
+from powergridworld_amd.base import ComponentEnv, as_action, as_env_tensor, register_env
+from powergridworld_amd.utils import maybe_rescale_box_space
+
+
+@register_env
+class EnergyStorageEnv(ComponentEnv):
+    """Linear charge/discharge battery model; obs = state of charge, action in
+    [-1, 1] (discharge > 0), reward 0.  Step kernel: pgw_battery_step."""
+
+    fused_kind = "storage"
+
+    def __init__(self, name: str = None, storage_range: tuple = (3.0, 50.0),
+                 initial_storage_mean: float = 30.0, initial_storage_std: float = 5.0,
+                 charge_efficiency: float = 0.95, discharge_efficiency: float = 0.9,
+                 max_power: float = 15.0, max_episode_steps: int = 288,
+                 control_timedelta: pd.Timedelta = pd.Timedelta(300, "s"),
+                 rescale_spaces: bool = True, num_envs: int = 1, device=None, seed=None, **kwargs):
+        super().__init__(name=name, num_envs=num_envs, device=device)
+        self.storage_range = storage_range
+        self.initial_storage_mean = initial_storage_mean
+        self.initial_storage_std = initial_storage_std
+        self.charge_efficiency = charge_efficiency
+        self.discharge_efficiency = discharge_efficiency
+        self.max_power = max_power
+        self.rescale_spaces = rescale_spaces
+        self.simulation_step = 0
+        self.max_episode_steps = max_episode_steps
+        self.control_interval_in_hr = control_timedelta.seconds / 3600.0      # :49
+        self._obs_labels = ["stage_of_charge"]                                 # (sic) :51
+        self._observation_space = spaces.Box(shape=(1,), low=storage_range[0],
+                                             high=storage_range[1], dtype=np.float64)
+        self.observation_space = maybe_rescale_box_space(self._observation_space, rescale_spaces)
+        self._action_space = spaces.Box(shape=(1,), low=-1.0, high=1.0, dtype=np.float64)
+        self.action_space = maybe_rescale_box_space(self._action_space, rescale_spaces)
+        self.params = _lib.BatteryParams(
+            soc_min=float(storage_range[0]), soc_max=float(storage_range[1]),
+            eta_c=float(charge_efficiency), eta_d=float(discharge_efficiency),
+            max_power=float(max_power), dt_h=float(self.control_interval_in_hr),
+            rescale=int(bool(rescale_spaces)))
+        self.soc = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._obs = self._new_obs(1)
+        self._gen = torch.Generator(device=self.device)
+        self.seed(seed)
+
+    def seed(self, seed=None):
+        """Seed the initial-SoC sampler (the reference draws from NumPy's global RNG)."""
+        self._gen.manual_seed(int(seed) if seed is not None else int(torch.seed() % (2 ** 63)))
+
+    def _sample_initial_storage(self):
+        """truncnorm(-1, 1) * std + mean (energy_storage_env.py:82-84), drawn on the
+        device by inverse-CDF sampling: z = sqrt(2) erfinv(2 u' - 1),
+        u' ~ U[Phi(-1), Phi(1)]."""
+        lo = 0.5 * (1.0 + math.erf(-1.0 / math.sqrt(2.0)))
+        hi = 0.5 * (1.0 + math.erf(1.0 / math.sqrt(2.0)))
+        u = torch.rand(self.num_envs, dtype=torch.float64, device=self.device, generator=self._gen)
+        z = math.sqrt(2.0) * torch.special.erfinv(2.0 * (lo + u * (hi - lo)) - 1.0)
+        return z * self.initial_storage_std + self.initial_storage_mean
+
+    @property
+    def current_storage(self):
+        return self.soc
+
+    def _adopt(self, soc=None, obs=None):
+        """Re-point state/obs at externally owned views (fused multi-agent buffers)."""
+        if soc is not None:
+            soc.copy_(self.soc)
+            self.soc = soc
+        if obs is not None:
+            self._obs = obs
+
+    def reset(self, init_storage=None, **kwargs):
+        """(:72-97) SoC ~ mean + std * truncnorm(-1, 1) unless init_storage is given
+        (a scalar or one value per env)."""
+        self.simulation_step = 0
+        n = self.num_envs
+        if init_storage is None:
+            init = self._sample_initial_storage()
+        else:
+            try:
+                init = init_storage
+                if not isinstance(init, torch.Tensor):
+                    init = np.asarray(init, dtype=np.float64)
+            except (TypeError, ValueError) as e:
+                print(e)
+                print("init_storage value needs to be a float, use default value instead")
+                init = self.initial_storage_mean
+        init = as_env_tensor(init, n, self.device, "init_storage")
+        _lib.check(_lib.lib().pgw_battery_reset(self.params, n, _lib.dptr(init), _lib.dptr(self.soc),
+                                                _lib.mat(self._obs), self._stream()))
+        self._real_power.zero_()
+        return self.get_obs(**kwargs)
+
+    def step(self, action, **kwargs):
+        """(:131-157)"""
+        a = as_action(action, self.num_envs, 1, self.device)
+        _lib.check(_lib.lib().pgw_battery_step(self.params, self.num_envs, _lib.mat(a),
+                                               _lib.dptr(self.soc), _lib.mat(self._obs),
+                                               _lib.dptr(self._real_power), self._stream()))
+        obs, meta = self.get_obs()
+        self.simulation_step += 1
+        return obs, self._zero_reward, self.is_terminal(), meta
+
+    def step_reward(self, **kwargs):
+        return self._zero_reward, {}
+
+    def _current_reward(self):
+        return None
+
+    def get_obs(self, **kwargs):
+        return self._obs, {"state_of_charge": self.soc.unsqueeze(1)}
+
+    def is_terminal(self):
+        return self.simulation_step + 1 == self.max_episode_steps      # :180-181

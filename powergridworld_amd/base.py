@@ -1,0 +1,218 @@
+"""Batched ComponentEnv / MultiComponentEnv (reference: gridworld/base.py:12-182).
+
+Every env object here simulates ``num_envs`` independent copies of the
+reference env in lockstep on the GPU.  The API is the reference's -- same
+constructor arguments, ``reset``/``step``/``step_reward``/``get_obs``,
+``real_power``/``reactive_power``/``obs_labels`` -- with these batch rules:
+
+* observations, rewards and real powers are fp64 device tensors with a leading
+  env axis ([N, dim] / [N]); they are VIEWS of persistent buffers that the next
+  ``step``/``reset`` overwrites (clone them to keep them);
+* actions may be [N, dim] tensors (any strides, zero-copy when fp64 on the
+  device), a single [dim] action broadcast to all envs, or numpy/lists;
+* ``done`` is a Python bool: all copies share the time axis, so they finish
+  together exactly as the reference's single env does.
+"""
+from abc import ABC, abstractmethod
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from powergridworld_amd import _lib
+from powergridworld_amd import spaces
+from powergridworld_amd.log import logger
+
+
+def as_env_tensor(x, n, device, what="value"):
+    """Scalar / [N] / [N,1] input -> fp64 [N] device tensor (broadcast allowed)."""
+    if x is None:
+        return None
+    t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x, dtype=np.float64))
+    if t.dtype != torch.float64 or t.device != device:
+        t = t.to(device=device, dtype=torch.float64)
+    t = t.reshape(-1)
+    if t.numel() == 1:
+        return t.expand(n).contiguous()
+    if t.numel() != n:
+        raise ValueError("%s: expected %d values, got shape %s" % (what, n, tuple(t.shape)))
+    return t.contiguous()
+
+
+def as_action(a, n, dim, device):
+    """Normalise an action to a [n, dim] fp64 device tensor (views where possible)."""
+    if a is None:
+        return None
+    t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a, dtype=np.float64))
+    if t.dtype != torch.float64 or t.device != device:
+        t = t.to(device=device, dtype=torch.float64)
+    if t.dim() == 0:
+        return t.reshape(1, 1).expand(n, dim)
+    if t.dim() == 1:
+        if t.shape[0] == dim:
+            return t.reshape(1, dim).expand(n, dim)   # one reference-shaped action for all envs
+        if dim == 1 and t.shape[0] == n:
+            return t.reshape(n, 1)
+    if t.dim() == 2 and tuple(t.shape) == (n, dim):
+        return t
+    raise ValueError("action of shape %s does not fit (num_envs=%d, action_dim=%d)"
+                     % (tuple(t.shape), n, dim))
+
+
+class ComponentEnv(spaces.Env, ABC):
+    """Base class for any environment used in the multiagent simulation
+    (gridworld/base.py:12-71), batched over ``num_envs`` copies."""
+
+    def __init__(self, name: str = None, num_envs: int = 1, device=None, **kwargs):
+        super().__init__()
+        self.name = name
+        self.num_envs = int(num_envs)
+        if self.num_envs < 1:
+            raise ValueError("num_envs must be >= 1")
+        self.device = _lib.require_device(device)
+        n = self.num_envs
+        self._real_power = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self._reactive_power = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self._zero_reward = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self._obs_labels = []
+        self._in_multicomponent = False
+
+    # ---- buffers ------------------------------------------------------------
+    def _new_obs(self, dim):
+        """Env-minor obs buffer [dim, N]; the returned [N, dim] view is what
+        step()/reset() hand out (coalesced device writes, zero-copy for the caller)."""
+        buf = torch.zeros((dim, self.num_envs), dtype=torch.float64, device=self.device)
+        return buf.t()
+
+    def _stream(self):
+        return _lib.stream_ptr(self.device)
+
+    @abstractmethod
+    def reset(self, **kwargs):
+        """Standard gym reset method but with kwargs."""
+
+    @abstractmethod
+    def step(self, action, **kwargs) -> Tuple[torch.Tensor, torch.Tensor, bool, dict]:
+        """Standard gym step method but with kwargs."""
+
+    @abstractmethod
+    def step_reward(self, **kwargs) -> Tuple[torch.Tensor, dict]:
+        """Returns the current step reward and metadata dict."""
+
+    @abstractmethod
+    def get_obs(self, **kwargs) -> Tuple[torch.Tensor, dict]:
+        """Returns the current observation (state) and any metadata."""
+
+    @property
+    def real_power(self) -> torch.Tensor:
+        """Real power per env, positive for load and negative for generation."""
+        return self._real_power
+
+    @property
+    def reactive_power(self) -> torch.Tensor:
+        return self._reactive_power
+
+    @property
+    def obs_labels(self) -> list:
+        return self._obs_labels
+
+    # For the fused multi-agent kernel: which kernel component this env is.
+    fused_kind = None
+
+
+def resolve_env_class(cls):
+    """Accept this package's classes, or reference classes by name (drop-in for
+    configs built against gridworld.*)."""
+    if isinstance(cls, type) and issubclass(cls, (ComponentEnv,)):
+        return cls
+    from powergridworld_amd import agents   # noqa: F401  (registers classes)
+    name = getattr(cls, "__name__", str(cls))
+    reg = ENV_REGISTRY.get(name)
+    if reg is None:
+        raise TypeError("no MI355X implementation for env class %r" % (name,))
+    return reg
+
+
+ENV_REGISTRY = {}
+
+
+def register_env(cls):
+    ENV_REGISTRY[cls.__name__] = cls
+    return cls
+
+
+@register_env
+class MultiComponentEnv(ComponentEnv):
+    """Single agent composed of several component envs (gridworld/base.py:74-182):
+    the action/observation spaces are the union, real power and reward the sum
+    over components (reward recomputed after all components stepped, base.py:137)."""
+
+    def __init__(self, name: str = None, components: List[dict] = None, num_envs: int = 1,
+                 device=None, **kwargs):
+        super().__init__(name=name, num_envs=num_envs, device=device, **kwargs)
+        self.envs = []
+        for c in components:
+            cls = resolve_env_class(c["cls"])
+            env = cls(name=c["name"], num_envs=self.num_envs, device=self.device, **c["config"])
+            env._in_multicomponent = True
+            self.envs.append(env)
+        self.observation_space = spaces.Dict({e.name: e.observation_space for e in self.envs})
+        self.action_space = spaces.Dict({e.name: e.action_space for e in self.envs})
+        self._obs_labels_dict = {e.name: e.obs_labels for e in self.envs}
+        obs_labels = []
+        for e in self.envs:
+            obs_labels += e.obs_labels
+        self._obs_labels = list(set(obs_labels))
+        self._reward = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        if len(self.envs) > _lib.MAX_COMP:
+            raise ValueError("at most %d components per agent" % _lib.MAX_COMP)
+
+    def reset(self, **kwargs):
+        """Resets each component and returns (obs dict, meta dict) (base.py:108-111)."""
+        for e in self.envs:
+            e.reset(**kwargs)
+        self._real_power.zero_()
+        return self.get_obs(**kwargs)
+
+    def _reduce(self):
+        a = _lib.ReduceArgs()
+        a.n_comp = len(self.envs)
+        for i, e in enumerate(self.envs):
+            a.real_power[i] = e.real_power.data_ptr()
+            r = e._current_reward()
+            a.reward[i] = None if r is None else r.data_ptr()
+        _lib.check(_lib.lib().pgw_agent_reduce(a, self.num_envs, _lib.dptr(self._real_power),
+                                               _lib.dptr(self._reward), self._stream()))
+
+    def step(self, action: dict, **kwargs):
+        obs, dones, metas = {}, [], {}
+        for env in self.envs:
+            env_kwargs = {k: v for k, v in kwargs.items() if k in env.obs_labels}
+            ob, _, done, meta = env.step(action[env.name], **env_kwargs)
+            obs[env.name] = ob
+            dones.append(done)
+            metas[env.name] = meta
+        self._reduce()
+        return obs, self._reward, any(dones), metas
+
+    def step_reward(self, **kwargs):
+        meta = {e.name: e.step_reward()[1] for e in self.envs}
+        return self._reward, meta
+
+    def get_obs(self, **kwargs):
+        obs, meta = {}, {}
+        for env in self.envs:
+            env_kwargs = {k: v for k, v in kwargs.items() if k in env.obs_labels}
+            obs[env.name], meta[env.name] = env.get_obs(**env_kwargs)
+        return obs, meta
+
+    @property
+    def obs_labels_dict(self) -> Dict[str, list]:
+        return self._obs_labels_dict
+
+    @property
+    def env_dict(self) -> Dict[str, ComponentEnv]:
+        return {e.name: e for e in self.envs}
+
+    def _current_reward(self):
+        return self._reward

@@ -1,0 +1,220 @@
+// Shared device helpers for libpgw (gfx950).  Built with -ffp-contract=off so
+// every expression rounds exactly as the reference's NumPy fp64 arithmetic;
+// the power-flow kernel opts into fma() explicitly where it wants it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pgw.h"
+
+namespace pgw {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+int32_t check_launch(const char* what);
+
+#define PGW_REQUIRE(cond, ...)            \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::pgw::set_error(__VA_ARGS__);      \
+      return PGW_ERR_ARG;                 \
+    }                                     \
+  } while (0)
+
+constexpr int kBlock = 256;   // 4 waves of 64
+
+inline unsigned grid_for(int64_t n) {
+  return static_cast<unsigned>((n + kBlock - 1) / kBlock);
+}
+
+// ---------------------------------------------------------------- numpy semantics
+// np.clip(x, lo, hi) == minimum(maximum(x, lo), hi), NaN-propagating.
+__device__ __forceinline__ double clip(double x, double lo, double hi) {
+  double y = (x < lo) ? lo : x;
+  return (y > hi) ? hi : y;
+}
+
+// gridworld/utils.py:9-24
+__device__ __forceinline__ double to_scaled(double x, double lo, double hi) {
+  x = clip(x, lo, hi);
+  return (2.0 * x - (lo + hi)) / (hi - lo);
+}
+
+// gridworld/utils.py:27-43 (the out-of-range warning is not reproduced)
+__device__ __forceinline__ double to_raw(double y, double lo, double hi) {
+  y = clip(y, -1.0, 1.0);
+  return (y * (hi - lo) + (hi + lo)) / 2.0;
+}
+
+// Python's max(a, b) for floats (first argument wins ties / NaN on the right).
+__device__ __forceinline__ double pymax(double a, double b) { return (b > a) ? b : a; }
+__device__ __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
+
+__device__ __forceinline__ double ld(const pgw_mat& m, int64_t e, int j) {
+  return m.ptr[e * m.s_env + (int64_t)j * m.s_dim];
+}
+__device__ __forceinline__ void st(const pgw_mat& m, int64_t e, int j, double v) {
+  m.ptr[e * m.s_env + (int64_t)j * m.s_dim] = v;
+}
+
+// ---------------------------------------------------------------- battery
+// energy_storage_env.py:100-157.  Returns the (validated) power; updates soc.
+__device__ __forceinline__ double battery_step(const pgw_battery_params& p, double a, double& soc) {
+  if (p.rescale) a = to_raw(a, -1.0, 1.0);
+  double power = a * p.max_power;
+  // validate_power :112-126 (the clamps omit the efficiencies, as in the reference)
+  if (power > 0.0) {
+    if (soc - power * p.dt_h / p.eta_d < p.soc_min)
+      power = pymax(soc - p.soc_min, 0.0) / p.dt_h;
+  } else if (power < 0.0) {
+    if (soc - p.eta_c * power * p.dt_h > p.soc_max)
+      power = -(pymax(p.soc_max - soc, 0.0) / p.dt_h);
+  }
+  if (power < 0.0) {
+    soc = soc - p.eta_c * power * p.dt_h;
+    soc = pymin(soc, p.soc_max);
+  } else if (power > 0.0) {
+    soc = soc - power * p.dt_h / p.eta_d;
+    soc = pymax(soc, p.soc_min);
+  }
+  return power;
+}
+
+__device__ __forceinline__ double battery_obs(const pgw_battery_params& p, double soc) {
+  return p.rescale ? to_scaled(soc, p.soc_min, p.soc_max) : soc;
+}
+
+// ---------------------------------------------------------------- PV
+__device__ __forceinline__ double pv_obs(const pgw_pv_params& p, double pmax) {
+  double raw = -pmax;
+  return p.rescale ? to_scaled(raw, p.obs_low, p.obs_high) : raw;
+}
+
+__device__ __forceinline__ double pv_real_power(const pgw_pv_params& p, double a, double pmax) {
+  if (p.rescale) a = to_raw(a, 0.0, 1.0);
+  return a * (-pmax);
+}
+
+// ---------------------------------------------------------------- building
+struct BuildingExt {
+  double bus_v, min_v, max_v, p_set;
+};
+
+__device__ __forceinline__ BuildingExt building_ext(const pgw_building_ext& x, int64_t e) {
+  BuildingExt r;
+  r.bus_v = x.bus_voltage ? x.bus_voltage[e] : 1.0;
+  double dflt = x.bus_voltage ? r.bus_v : 1.0;       // five_zone_rom_env.py:260-262
+  r.min_v = x.min_voltage ? x.min_voltage[e] : dflt;
+  r.max_v = x.max_voltage ? x.max_voltage[e] : dflt;
+  r.p_set = x.p_setpoint ? x.p_setpoint[e] : __builtin_huge_val();
+  return r;
+}
+
+// u-vector (dynamics.py:12-41) and state update (:44-55) for all zones.
+// action == nullptr: reset form (u_pos[7] = q_cool).
+__device__ __forceinline__ void building_state_update(const pgw_building_params& p,
+                                                      const pgw_building_exo& ex,
+                                                      const double T[5], const double* act,
+                                                      double x[5]) {
+  double u[5][4];
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    double upos[8];
+    upos[0] = ex.T_oa - T[z];
+    upos[1] = ex.q_solar[z];
+    upos[2] = ex.q_int[z];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // neighbour id is uniform (kernel argument): select with a constant-index switch
+      int y = p.nbr[z][i];
+      double ty = (y == 0) ? T[0] : (y == 1) ? T[1] : (y == 2) ? T[2] : (y == 3) ? T[3] : T[4];
+      upos[3 + i] = ty - T[z];
+    }
+    upos[7] = act ? act[z] * (act[5] - T[z]) : ex.q_cool[z];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int s = p.sel[z][j];
+      double v = upos[0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) v = (s == k) ? upos[k] : v;
+      u[z][j] = v;
+    }
+  }
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    double bu = p.B[z][0] * u[z][0];
+    bu = bu + p.B[z][1] * u[z][1];
+    bu = bu + p.B[z][2] * u[z][2];
+    bu = bu + p.B[z][3] * u[z][3];
+    x[z] = p.A[z] * x[z] + bu;
+  }
+}
+
+// get_p_consumed (dynamics.py:106-114)
+__device__ __forceinline__ double building_p_consumed(const double act[6], double T_oa) {
+  double s = (((act[0] + act[1]) + act[2]) + act[3]) + act[4];
+  double fan = 0.0076 * pow(s, 3.0) + 4.8865;
+  double chiller = pymax(0.0, s * (T_oa - act[5]));
+  return fan + chiller;
+}
+
+// FiveZoneROMThermalEnergyEnv.step_reward (five_zone_rom_env.py:315-335)
+__device__ __forceinline__ double building_reward(const pgw_building_params& p, const double T[5],
+                                                  double lb, double ub, double p_cons) {
+  double e = -p_cons / 12.0;
+  double c = 0.0;
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    double up = T[z] - ub, lo = lb - T[z];
+    double m = pymax(pymax(up, lo), 0.0);
+    c = c + m * m;
+  }
+  c = -c;
+  return p.alpha * e * 0.5 + (1.0 - p.alpha) * c;
+}
+
+// get_obs (five_zone_rom_env.py:228-283): values in state-dict order, bounds in
+// make_obs_space order (exactly as the reference zips them).
+__device__ __forceinline__ double building_obs_value(int var, const double T[5],
+                                                     const pgw_building_exo& ex, double p_cons,
+                                                     const BuildingExt& xv) {
+  if (var < 5) {
+    return (var == 0) ? T[0] : (var == 1) ? T[1] : (var == 2) ? T[2] : (var == 3) ? T[3] : T[4];
+  }
+  if (var < 10) {
+    int z = var - 5;
+    double t = (z == 0) ? T[0] : (z == 1) ? T[1] : (z == 2) ? T[2] : (z == 3) ? T[3] : T[4];
+    return t - ex.comfort_ub;
+  }
+  if (var < 15) {
+    int z = var - 10;
+    double t = (z == 0) ? T[0] : (z == 1) ? T[1] : (z == 2) ? T[2] : (z == 3) ? T[3] : T[4];
+    return ex.comfort_lb - t;
+  }
+  switch (var) {
+    case PGW_BV_COMFORT_LOWER: return ex.comfort_lb;
+    case PGW_BV_COMFORT_UPPER: return ex.comfort_ub;
+    case PGW_BV_OUTDOOR_TEMP: return ex.T_oa;
+    case PGW_BV_P_CONSUMED: return p_cons;
+    case PGW_BV_TIME_OF_DAY: return ex.time_of_day;
+    case PGW_BV_BUS_VOLTAGE: return xv.bus_v;
+    case PGW_BV_MIN_VOLTAGE: return xv.min_v;
+    case PGW_BV_MAX_VOLTAGE: return xv.max_v;
+    default: return xv.p_set;
+  }
+}
+
+template <typename Store>
+__device__ __forceinline__ void building_write_obs(const pgw_building_params& p, const double T[5],
+                                                   const pgw_building_exo& ex, double p_cons,
+                                                   const BuildingExt& xv, Store store) {
+  for (int j = 0; j < p.n_obs; ++j) {
+    double v = building_obs_value(p.obs_var[j], T, ex, p_cons, xv);
+    v = clip(v, p.obs_low[j], p.obs_high[j]);
+    if (p.rescale) v = to_scaled(v, p.obs_low[j], p.obs_high[j]);
+    store(j, v);
+  }
+}
+
+}  // namespace pgw

@@ -1,0 +1,316 @@
+// Component step kernels: battery, PV, building, EV, multi-component reduce.
+// One thread per env; env-minor SoA state, so every per-env load/store of a
+// field is a contiguous, fully coalesced 512-B wave access.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "pgw_common.h"
+
+namespace pgw {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int32_t check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return PGW_ERR_HIP;
+  }
+  return PGW_OK;
+}
+
+// ====================================================================== battery
+__global__ void __launch_bounds__(kBlock) k_battery_reset(pgw_battery_params p, int64_t n,
+                                                          const double* __restrict__ init,
+                                                          double* __restrict__ soc, pgw_mat obs) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double s = clip(init[e], p.soc_min, p.soc_max);   // energy_storage_env.py:86-95
+  soc[e] = s;
+  st(obs, e, 0, battery_obs(p, s));
+}
+
+__global__ void __launch_bounds__(kBlock) k_battery_step(pgw_battery_params p, int64_t n,
+                                                         pgw_mat act, double* __restrict__ soc,
+                                                         pgw_mat obs, double* __restrict__ rp) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double s = soc[e];
+  double power = battery_step(p, ld(act, e, 0), s);
+  soc[e] = s;
+  rp[e] = -power;                                     // :150
+  st(obs, e, 0, battery_obs(p, s));
+}
+
+// ====================================================================== PV
+__global__ void __launch_bounds__(kBlock) k_pv(pgw_pv_params p, int64_t n, double pmax, pgw_mat act,
+                                               const double* __restrict__ vmin, pgw_mat obs,
+                                               double* __restrict__ rp) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  st(obs, e, 0, pv_obs(p, pmax));
+  if (p.grid_aware) {
+    double v = vmin[e];
+    st(obs, e, 1, p.rescale ? to_scaled(v, p.vmin_low, p.vmin_high) : v);
+  }
+  if (rp) rp[e] = pv_real_power(p, ld(act, e, 0), pmax);
+}
+
+// ====================================================================== building
+__global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p, pgw_building_exo ex0,
+                                                           int64_t n, double* __restrict__ x,
+                                                           double* __restrict__ pcons,
+                                                           double* __restrict__ rstate,
+                                                           pgw_building_ext ext, pgw_mat obs) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double xs[5], T[5];
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    xs[z] = x[z * n + e];
+    T[z] = p.T_init[z];
+  }
+  // two filter updates with the same u (five_zone_rom_env.py:160-173)
+  for (int it = 0; it < 2; ++it) {
+    building_state_update(p, ex0, T, nullptr, xs);
+#pragma unroll
+    for (int z = 0; z < 5; ++z) {
+      double yhat = p.C[z] * xs[z];
+      double yact = T[z] - p.mean[z];
+      xs[z] = xs[z] + p.K[z] * (yact - yhat);
+    }
+  }
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    x[z * n + e] = xs[z];
+    T[z] = p.C[z] * xs[z] + p.mean[z];               // temp_dynamics (dynamics.py:75-85)
+  }
+  pcons[e] = 0.0;
+  BuildingExt xv = building_ext(ext, e);
+  building_write_obs(p, T, ex0, 0.0, xv, [&](int j, double v) { st(obs, e, j, v); });
+  if (rstate) rstate[e] = building_reward(p, T, ex0.comfort_lb, ex0.comfort_ub, 0.0);
+}
+
+__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p, pgw_building_exo ex,
+                                                          pgw_building_exo exn, int64_t n, pgw_mat act,
+                                                          double* __restrict__ x,
+                                                          double* __restrict__ pcons,
+                                                          double* __restrict__ rout,
+                                                          double* __restrict__ rstate, int32_t lagged,
+                                                          pgw_building_ext ext, pgw_mat obs) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double a[6], xs[5], T[5];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double v = ld(act, e, j);
+    a[j] = p.rescale ? to_raw(v, p.act_low[j], p.act_high[j]) : v;
+  }
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    xs[z] = x[z * n + e];
+    T[z] = p.C[z] * xs[z] + p.mean[z];   // zone temps are a pure function of x_k
+  }
+  building_state_update(p, ex, T, a, xs);
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    x[z * n + e] = xs[z];
+    T[z] = p.C[z] * xs[z] + p.mean[z];
+  }
+  double pc = building_p_consumed(a, ex.T_oa);
+  pcons[e] = pc;
+  double fresh = building_reward(p, T, exn.comfort_lb, exn.comfort_ub, pc);
+  if (rout) rout[e] = lagged ? rstate[e] : fresh;
+  if (rstate) rstate[e] = fresh;
+  BuildingExt xv = building_ext(ext, e);
+  building_write_obs(p, T, exn, pc, xv, [&](int j, double v) { st(obs, e, j, v); });
+}
+
+// ====================================================================== EV
+__global__ void __launch_bounds__(kBlock) k_ev_reset(int64_t n, int32_t V, int32_t W,
+                                                     const double* __restrict__ req0,
+                                                     double* __restrict__ req,
+                                                     uint64_t* __restrict__ chg) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  for (int v = 0; v < V; ++v) req[(int64_t)v * n + e] = req0[v];
+  for (int w = 0; w < W; ++w) chg[(int64_t)w * n + e] = 0ull;
+}
+
+// ev_charging_env.py:171-264.  Vehicles are visited in ascending index order
+// (the reference iterates a Python set of small ints); only vehicles parked now
+// or at the previous step can contribute (`scan`, uniform across the wave).
+__global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step_info s, int64_t n,
+                                                    pgw_mat act, const double* __restrict__ endp,
+                                                    double* __restrict__ req,
+                                                    uint64_t* __restrict__ chg, pgw_mat obs,
+                                                    double* __restrict__ rp,
+                                                    double* __restrict__ rew) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double a = act.ptr ? ld(act, e, 0) : s.action_default;
+  if (p.rescale) a = to_raw(a, 0.0, 1.0);
+  double kwh = a * p.rate * p.hours_per_step;
+  double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
+  int dcnt = 0, nact = 0;
+  for (int w = 0; w < s.n_words; ++w) {
+    uint64_t scan = s.scan[w], win = s.window[w];
+    uint64_t prev = chg[(int64_t)w * n + e];
+    uint64_t now_bits = 0ull;
+    while (scan) {
+      int b = __builtin_ctzll(scan);
+      scan &= scan - 1;
+      int v = w * 64 + b;
+      double r = req[(int64_t)v * n + e];
+      bool active = ((win >> b) & 1ull) && (r > 0.0);
+      if (active) {
+        now_bits |= 1ull << b;
+        ++nact;
+        demand = demand + r;
+        double tl = (endp[v] - s.time) / 60.0;
+        if (tl > 0.0) {
+          double def = pymax(0.0, p.rate - r / tl);
+          dsum = dsum + def;
+          ++dcnt;
+          double ch = pymin(kwh, r);
+          req[(int64_t)v * n + e] = r - ch;
+          consumed = consumed + ch;
+        }
+      } else if ((prev >> b) & 1ull) {
+        unserved = unserved + r;          // departed: not charging now (:239-243)
+      }
+    }
+    chg[(int64_t)w * n + e] = now_bits;
+  }
+  double st_[6];
+  st_[0] = s.next_time;
+  st_[1] = p.mult * (double)nact;
+  st_[2] = p.mult * consumed;
+  st_[3] = p.mult * demand;
+  st_[4] = dcnt ? dsum / (double)dcnt : 0.0;
+  st_[5] = unserved;
+  rp[e] = p.mult * consumed;                         // :255
+  // step_reward :135-142
+  double ur = -p.u_pen * (st_[5] * st_[5]);
+  double pk = pymax(0.0, st_[2] - p.thr);
+  double pr = -p.p_pen * (pk * pk);
+  rew[e] = (ur + pr) / p.reward_scale;
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    st(obs, e, j, p.rescale ? to_scaled(st_[j], p.obs_low[j], p.obs_high[j]) : st_[j]);
+}
+
+// ====================================================================== MC reduce
+__global__ void __launch_bounds__(kBlock) k_agent_reduce(pgw_reduce_args a, int64_t n,
+                                                         double* __restrict__ rp,
+                                                         double* __restrict__ rew) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double r = 0.0, w = 0.0;
+  for (int c = 0; c < a.n_comp; ++c) {
+    r = r + (a.reward[c] ? a.reward[c][e] : 0.0);
+    w = w + (a.real_power[c] ? a.real_power[c][e] : 0.0);
+  }
+  if (rp) rp[e] = w;
+  if (rew) rew[e] = r;
+}
+
+}  // namespace pgw
+
+using namespace pgw;
+
+#define PGW_LAUNCH(kernel, n, stream, ...)                                             \
+  do {                                                                                 \
+    if ((n) > 0)                                                                       \
+      hipLaunchKernelGGL(kernel, dim3(grid_for(n)), dim3(kBlock), 0,                   \
+                         (hipStream_t)(stream), __VA_ARGS__);                          \
+    return check_launch(#kernel);                                                      \
+  } while (0)
+
+extern "C" {
+
+int32_t pgw_abi_version(void) { return PGW_ABI_VERSION; }
+const char* pgw_last_error(void) { return g_err; }
+
+int32_t pgw_battery_reset(const pgw_battery_params* p, int64_t n, const double* init, double* soc,
+                          pgw_mat obs, void* stream) {
+  PGW_REQUIRE(p && init && soc && obs.ptr && n >= 0, "pgw_battery_reset: null argument");
+  PGW_LAUNCH(k_battery_reset, n, stream, *p, n, init, soc, obs);
+}
+
+int32_t pgw_battery_step(const pgw_battery_params* p, int64_t n, pgw_mat action, double* soc,
+                         pgw_mat obs, double* real_power, void* stream) {
+  PGW_REQUIRE(p && action.ptr && soc && obs.ptr && real_power && n >= 0,
+              "pgw_battery_step: null argument");
+  PGW_LAUNCH(k_battery_step, n, stream, *p, n, action, soc, obs, real_power);
+}
+
+int32_t pgw_pv_obs(const pgw_pv_params* p, int64_t n, double pmax, const double* min_voltage,
+                   pgw_mat obs, void* stream) {
+  PGW_REQUIRE(p && obs.ptr && n >= 0, "pgw_pv_obs: null argument");
+  PGW_REQUIRE(!p->grid_aware || min_voltage, "pgw_pv_obs: grid_aware needs min_voltage");
+  pgw_mat none{nullptr, 0, 0};
+  PGW_LAUNCH(k_pv, n, stream, *p, n, pmax, none, min_voltage, obs, (double*)nullptr);
+}
+
+int32_t pgw_pv_step(const pgw_pv_params* p, int64_t n, double pmax, pgw_mat action,
+                    const double* min_voltage, pgw_mat obs, double* real_power, void* stream) {
+  PGW_REQUIRE(p && action.ptr && obs.ptr && real_power && n >= 0, "pgw_pv_step: null argument");
+  PGW_REQUIRE(!p->grid_aware || min_voltage, "pgw_pv_step: grid_aware needs min_voltage");
+  PGW_LAUNCH(k_pv, n, stream, *p, n, pmax, action, min_voltage, obs, real_power);
+}
+
+int32_t pgw_building_reset(const pgw_building_params* p, const pgw_building_exo* ex0, int64_t n,
+                           double* x, double* p_consumed, double* reward_state,
+                           pgw_building_ext ext, pgw_mat obs, void* stream) {
+  PGW_REQUIRE(p && ex0 && x && p_consumed && obs.ptr && n >= 0, "pgw_building_reset: null argument");
+  PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_reset: bad n_obs");
+  PGW_LAUNCH(k_building_reset, n, stream, *p, *ex0, n, x, p_consumed, reward_state, ext, obs);
+}
+
+int32_t pgw_building_step(const pgw_building_params* p, const pgw_building_exo* ex_t,
+                          const pgw_building_exo* ex_next, int64_t n, pgw_mat action, double* x,
+                          double* p_consumed, double* reward_out, double* reward_state,
+                          int32_t lagged, pgw_building_ext ext, pgw_mat obs, void* stream) {
+  PGW_REQUIRE(p && ex_t && ex_next && action.ptr && x && p_consumed && obs.ptr && n >= 0,
+              "pgw_building_step: null argument");
+  PGW_REQUIRE(!lagged || reward_state, "pgw_building_step: lagged reward needs reward_state");
+  PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_step: bad n_obs");
+  PGW_LAUNCH(k_building_step, n, stream, *p, *ex_t, *ex_next, n, action, x, p_consumed, reward_out,
+             reward_state, lagged, ext, obs);
+}
+
+int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, double* req,
+                     uint64_t* charging, void* stream) {
+  PGW_REQUIRE(p && req0 && req && charging && n >= 0, "pgw_ev_reset: null argument");
+  PGW_REQUIRE(p->n_vehicles >= 0 && p->n_vehicles <= 64 * PGW_EV_MAX_WORDS,
+              "pgw_ev_reset: too many vehicles");
+  int32_t W = (p->n_vehicles + 63) / 64;
+  PGW_LAUNCH(k_ev_reset, n, stream, n, p->n_vehicles, W, req0, req, charging);
+}
+
+int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
+                    const double* endp, double* req, uint64_t* charging, pgw_mat obs,
+                    double* real_power, double* reward, void* stream) {
+  PGW_REQUIRE(p && s && endp && req && charging && obs.ptr && real_power && reward && n >= 0,
+              "pgw_ev_step: null argument");
+  PGW_REQUIRE(s->n_words == (p->n_vehicles + 63) / 64 && s->n_words <= PGW_EV_MAX_WORDS,
+              "pgw_ev_step: n_words does not match n_vehicles");
+  PGW_LAUNCH(k_ev_step, n, stream, *p, *s, n, action, endp, req, charging, obs, real_power, reward);
+}
+
+int32_t pgw_agent_reduce(const pgw_reduce_args* a, int64_t n, double* real_power, double* reward,
+                         void* stream) {
+  PGW_REQUIRE(a && a->n_comp >= 0 && a->n_comp <= PGW_MAX_COMP, "pgw_agent_reduce: bad args");
+  PGW_LAUNCH(k_agent_reduce, n, stream, *a, n, real_power, reward);
+}
+
+}  // extern "C"

@@ -1,0 +1,208 @@
+"""Nodal feeder model: turns a parsed feeder spec (dss.py) into the flat element
+list of the native builder (pgw_feeder_build, csrc/pgw_feeder.cpp), and reduces
+the inverted admittance onto the PQ-load elements for the batched PF kernel.
+
+Node numbering follows OpenDSS's bus order (buses in order of first reference
+by the circuit's elements: source, transformers, loads, lines; nodes within a
+bus in order of first reference), so ``node_names`` match AllNodeNames().
+"""
+import ctypes as C
+import json
+import math
+import os
+
+import numpy as np
+
+from powergridworld_amd import _lib
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
+
+_TO_MI = {"mi": 1.0, "kft": 1000.0 / 5280.0, "ft": 1.0 / 5280.0, "km": 1.0 / 1.609344,
+          "m": 1.0 / 1609.344, "me": 1.0 / 1609.344, "in": 1.0 / 63360.0, "cm": 1.0 / 160934.4}
+
+
+def load_feeder_spec(feeder_file):
+    """'ieee_13_dss/IEEE13Nodeckt.dss' (the reference's bundled feeder) resolves to
+    the committed data/ieee13.json; any other existing .dss path is parsed."""
+    base = os.path.basename(str(feeder_file)).lower()
+    if os.path.exists(str(feeder_file)) and str(feeder_file).lower().endswith(".dss"):
+        from powergridworld_amd.distribution_system.dss import parse_dss
+        return parse_dss(feeder_file)
+    if base in ("ieee13nodeckt.dss", "ieee13.json"):
+        with open(os.path.join(DATA_DIR, "ieee13.json")) as f:
+            return json.load(f)
+    if os.path.exists(str(feeder_file)) and str(feeder_file).endswith(".json"):
+        with open(feeder_file) as f:
+            return json.load(f)
+    raise FileNotFoundError("feeder file %r not found" % (feeder_file,))
+
+
+def _bus(spec, default):
+    parts = spec.split(".")
+    return parts[0].lower(), ([int(p) for p in parts[1:]] if len(parts) > 1 else list(default))
+
+
+def _seq_matrix(v1, v0, ph):
+    s, m = (2 * v1 + v0) / 3.0, (v0 - v1) / 3.0
+    return [[s if i == j else m for j in range(ph)] for i in range(ph)]
+
+
+class Feeder(object):
+    def __init__(self, spec):
+        self.spec = spec
+        self.freq = float(spec.get("base_frequency", 60.0))
+        self.bus_nodes, self.buses = {}, []
+        src = spec["source"]
+        self._touch(src["bus"], [1, 2, 3])
+        for t in spec["transformers"]:
+            for w in t["windings"]:
+                self._touch(*_bus(w["bus"], [1, 2, 3][:t["phases"]]))
+        for ld in spec["loads"]:
+            self._touch(*_bus(ld["bus1"], [1, 2, 3][:ld["phases"]]))
+        for ln in spec["lines"]:
+            for key in ("bus1", "bus2"):
+                self._touch(*_bus(ln[key], [1, 2, 3][:ln["phases"]]))
+        self.node_names = ["%s.%d" % (b, nd) for b in self.buses for nd in self.bus_nodes[b]]
+        self.node_index = {nm: i for i, nm in enumerate(self.node_names)}
+        self.n = len(self.node_names)
+        self._build()
+        self._bases()
+        self._loads()
+
+    def _touch(self, bus, nodes):
+        if bus not in self.bus_nodes:
+            self.bus_nodes[bus] = []
+            self.buses.append(bus)
+        for nd in nodes:
+            if nd != 0 and nd not in self.bus_nodes[bus]:
+                self.bus_nodes[bus].append(nd)
+
+    def node(self, bus, nd):
+        return -1 if nd == 0 else self.node_index["%s.%d" % (bus, nd)]
+
+    # ------------------------------------------------------------ native build
+    def elements(self):
+        spec, els = self.spec, []
+        s = spec["source"]
+        e = _lib.FeederElem(kind=_lib.PGW_ELEM_VSOURCE, nphases=3, basekv=s["basekv"], pu=s["pu"],
+                            angle=s["angle"], mvasc3=s["mvasc3"], mvasc1=s["mvasc1"],
+                            x1r1=s["x1r1"], x0r0=s["x0r0"], freq=self.freq)
+        for p in range(3):
+            e.node1[p], e.node2[p] = self.node(s["bus"], p + 1), -1
+        els.append(e)
+        for t in spec["transformers"]:
+            ph = t["phases"]
+            w1, w2 = t["windings"]
+            (b1, n1), (b2, n2) = _bus(w1["bus"], [1, 2, 3][:ph]), _bus(w2["bus"], [1, 2, 3][:ph])
+            e = _lib.FeederElem(kind=_lib.PGW_ELEM_XFMR, nphases=ph,
+                                conn1=int(w1["conn"] == "delta"), conn2=int(w2["conn"] == "delta"),
+                                kv1=w1["kv"], kv2=w2["kv"], kva=w1["kva"], pct_r1=w1["pct_r"],
+                                pct_r2=w2["pct_r"], xhl=t["xhl"], freq=self.freq)
+            for p in range(ph):
+                e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
+            els.append(e)
+        for ln in spec["lines"]:
+            ph = ln["phases"]
+            if ln.get("sequence") is not None or ln["linecode"] is None:
+                sq = ln.get("sequence") or {}
+                R = _seq_matrix(sq.get("r1", 0.058), sq.get("r0", 0.1784), ph)
+                X = _seq_matrix(sq.get("x1", 0.1206), sq.get("x0", 0.4047), ph)
+                Cm = _seq_matrix(sq.get("c1", 3.4), sq.get("c0", 1.6), ph)
+                length = ln["length"] * (1.0 if ln["units"] == "none" else _TO_MI[ln["units"]])
+            else:
+                lc = self.spec["linecodes"][ln["linecode"]]
+                R, X = lc["rmatrix"], lc["xmatrix"]
+                # OpenDSS keeps the LineCode's default C1/C0 when only R/X matrices are given
+                Cm = lc["cmatrix"] if lc.get("cmatrix") is not None else _seq_matrix(lc["c1"], lc["c0"], ph)
+                if ln["units"] != "none" and lc["units"] != "none":
+                    length = ln["length"] * _TO_MI[ln["units"]] / _TO_MI[lc["units"]]
+                else:
+                    length = ln["length"]
+            e = _lib.FeederElem(kind=_lib.PGW_ELEM_LINE, nphases=ph, length=length, freq=self.freq)
+            for i in range(ph):
+                for j in range(ph):
+                    e.r[i * ph + j], e.x[i * ph + j], e.c[i * ph + j] = R[i][j], X[i][j], Cm[i][j]
+            (b1, n1), (b2, n2) = _bus(ln["bus1"], [1, 2, 3][:ph]), _bus(ln["bus2"], [1, 2, 3][:ph])
+            for p in range(ph):
+                e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
+            els.append(e)
+        return els
+
+    def _build(self):
+        els = self.elements()
+        arr = (_lib.FeederElem * len(els))(*els)
+        n = self.n
+        Z = np.zeros(2 * n * n)
+        Y = np.zeros(2 * n * n)
+        I = np.zeros(2 * n)
+        V0 = np.zeros(2 * n)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        _lib.check(_lib.lib().pgw_feeder_build(arr, len(els), n, p(Y), p(Z), p(I), p(V0)))
+        self.Y = Y.view(np.complex128).reshape(n, n)
+        self.Z = Z.view(np.complex128).reshape(n, n)
+        self.I_src = I.view(np.complex128)
+        self.V0 = V0.view(np.complex128)
+
+    def _bases(self):
+        """Set Voltagebases + calcv: nearest base to each bus's no-load LL voltage."""
+        bases = np.array(self.spec["voltagebases"], float)
+        self.kv_ln = np.zeros(self.n)
+        for b in self.buses:
+            ids = [self.node_index["%s.%d" % (b, nd)] for nd in self.bus_nodes[b]]
+            vll = np.abs(self.V0[ids]).mean() * math.sqrt(3) / 1000.0
+            self.kv_ln[ids] = bases[np.argmin(np.abs(bases - vll))] / math.sqrt(3)
+
+    def _loads(self):
+        self.load_names = [ld["name"] for ld in self.spec["loads"]]
+        ep, eq, vb, el, nph, vmin, vmax, vlow = [], [], [], [], [], [], [], []
+        for li, ld in enumerate(self.spec["loads"]):
+            if ld.get("model", 1) != 1:
+                continue          # the reference only drives model-1 (PQ) loads (opendss.py:71,149)
+            ph = ld["phases"]
+            b, nds = _bus(ld["bus1"], [1, 2, 3][:ph])
+            for p in range(ph):
+                ep.append(self.node(b, nds[p]))
+                if ld["conn"] == "delta":
+                    eq.append(self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1]))
+                    vb.append(ld["kv"] * 1000.0)
+                else:
+                    eq.append(-1)
+                    vb.append(ld["kv"] * 1000.0 / (math.sqrt(3) if ph == 3 else 1.0))
+                el.append(li)
+                nph.append(float(ph))
+                vmin.append(ld.get("vminpu", 0.95))
+                vmax.append(ld.get("vmaxpu", 1.05))
+                vlow.append(ld.get("vlowpu", 0.50))
+        self.elem_p, self.elem_q = np.array(ep, np.int32), np.array(eq, np.int32)
+        self.elem_vbase, self.elem_load = np.array(vb), np.array(el)
+        self.elem_nph = np.array(nph)
+        self.elem_vmin, self.elem_vmax, self.elem_vlow = np.array(vmin), np.array(vmax), np.array(vlow)
+        self.m = len(ep)
+        self.base_kw = np.array([ld["kw"] for ld in self.spec["loads"]], float)
+        self.base_kvar = np.array([ld["kvar"] for ld in self.spec["loads"]], float)
+
+    def reduce(self, out_nodes):
+        """-> (M, W [M*M], U0 [M], G [n_out*M], V0_out [n_out]) complex, padded to the
+        kernel's instantiated element count M with inert zero-power elements."""
+        m, n = self.m, self.n
+        M = int(_lib.lib().pgw_pf_padded_m(m))
+        if m > _lib.PF_MAX_M:
+            raise ValueError("feeder has %d load phase elements (max %d)" % (m, _lib.PF_MAX_M))
+        out_nodes = np.asarray(out_nodes, np.int32)
+        no = len(out_nodes)
+        W = np.zeros(2 * m * m)
+        U0 = np.zeros(2 * m)
+        G = np.zeros(2 * max(no, 1) * m)
+        V0o = np.zeros(2 * max(no, 1))
+        Zf = np.ascontiguousarray(self.Z).view(np.float64).ravel()
+        V0f = np.ascontiguousarray(self.V0).view(np.float64).ravel()
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        _lib.check(_lib.lib().pgw_pf_reduce(n, p(Zf), p(V0f), m, p(self.elem_p), p(self.elem_q), no,
+                                            p(out_nodes), p(W), p(U0), p(G), p(V0o)))
+        Wc = np.zeros((M, M), complex)
+        Wc[:m, :m] = W.view(np.complex128).reshape(m, m)
+        U0c = np.zeros(M, complex)
+        U0c[:m] = U0.view(np.complex128)
+        Gc = np.zeros((max(no, 1), M), complex)
+        Gc[:, :m] = G.view(np.complex128).reshape(max(no, 1), m)
+        return M, Wc, U0c, Gc[:no], V0o.view(np.complex128)[:no]

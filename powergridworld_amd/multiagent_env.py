@@ -1,0 +1,418 @@
+"""Batched MultiAgentEnv (reference: gridworld/multiagent_env.py:20-230).
+
+Two execution paths behind the reference API:
+
+* generic: each agent steps through its own component kernels, bus loads are
+  summed on the device, the batched power flow runs (pgw_pf_solve), then the
+  Python hooks ``get_external_obs_vars`` / ``reward_transform`` /
+  ``meta_transform`` run on [N] tensors -- any agent mix, any override;
+* fused (the BASELINE C4 hot path): when every agent is a MultiComponentEnv of
+  {FiveZoneROMThermalEnergyEnv, PVEnv, EnergyStorageEnv} with identical
+  configs, no agent observes grid voltages and the reward transform is the
+  base pass-through or CoordinatedMultiBuildingControlEnv's, the whole
+  MultiAgentEnv.step -- all agents, the power flow and the voltage-violation
+  reward -- is ONE kernel launch (pgw_coord_step).  Component envs keep
+  their state as views of the fused buffers, so resets and queries still go
+  through them.
+"""
+from abc import abstractmethod
+from typing import Dict, Tuple, Union
+
+import ctypes as C
+import numpy as np
+import pandas as pd
+import torch
+
+from powergridworld_amd import _lib
+from powergridworld_amd.base import ComponentEnv, MultiComponentEnv, as_action, resolve_env_class
+from powergridworld_amd.log import logger
+
+try:
+    from ray.rllib.env.multi_agent_env import MultiAgentEnv as Env      # multiagent_env.py:13-17
+except ImportError:
+    Env = object
+    logger.warning("rllib MultiAgentEnv not found, using generic object class")
+
+_KIND_ID = {"building": 0, "pv": 1, "storage": 2}
+
+
+def resolve_pf_class(cls):
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    from powergridworld_amd.distribution_system.powerflow import PowerFlowSolver
+    if isinstance(cls, type) and issubclass(cls, PowerFlowSolver):
+        return cls
+    if getattr(cls, "__name__", None) == "OpenDSSSolver":
+        return OpenDSSSolver
+    raise TypeError("unsupported power flow solver class %r" % (cls,))
+
+
+class MultiAgentEnv(Env):
+
+    # Subclasses that implement a reward transform the fused kernel knows set this.
+    fused_reward_transform = None
+
+    def __init__(self, common_config: dict = {}, pf_config: dict = {}, agents: list = None,
+                 max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
+                 device=None, fused: Union[bool, str] = "auto", record_history: bool = False,
+                 **kwargs):
+        self.common_config = common_config
+        self.rescale_spaces = rescale_spaces
+        assert len(agents) > 0, "need at least one agent!"
+        self.num_envs = int(num_envs)
+        self.device = _lib.require_device(device)
+        self.start_time = pd.Timestamp(common_config["start_time"])
+        self.end_time = pd.Timestamp(common_config["end_time"])
+        self.control_timedelta = common_config["control_timedelta"]
+        self.pf_config = pf_config
+        self.max_episode_steps = max_episode_steps if max_episode_steps is not None else np.inf
+        self.episode_step = None
+        self.time = None
+        self.history = None
+        self.voltages = None
+        self.obs_dict = {}
+        self.record_history = record_history
+
+        self.agents = []
+        for a in agents:
+            _config = a["config"]
+            if "name" in a["config"]:
+                _config = {k: v for k, v in _config.items() if k != "name"}
+                logger.warning("ignoring 'name' in config dict in favor of constructor argument")
+            cls = resolve_env_class(a["cls"])
+            new_agent = cls(name=a["name"], num_envs=self.num_envs, device=self.device,
+                            **_config, **self.common_config)
+            self.agents.append(new_agent)
+        self.agent_name_bus_map = {a["name"]: a["bus"] for a in agents}
+        self.agent_names = list(set([a.name for a in self.agents]))
+        assert len(self.agent_names) == len(agents), "all agents need unique names"
+
+        pf_cls = resolve_pf_class(pf_config["cls"])
+        self.pf_solver = pf_cls(**pf_config["config"], num_envs=self.num_envs, device=self.device)
+
+        self.observation_space = {agent.name: agent.observation_space for agent in self.agents}
+        self.action_space = {agent.name: agent.action_space for agent in self.agents}
+
+        self._fused = None
+        if fused:
+            why = self._fusable()
+            if why is None:
+                self._setup_fused()
+            elif fused is True:
+                raise ValueError("fused=True but this configuration cannot be fused: " + why)
+            else:
+                logger.info("MultiAgentEnv: generic path (%s)", why)
+        if self._fused is None:
+            buses = sorted(set(self.agent_name_bus_map.values()))
+            self.pf_solver.set_controllable_loads(buses)
+
+    # ================================================================ hooks
+    @abstractmethod
+    def get_external_obs_vars(self, agent: Union[ComponentEnv, MultiComponentEnv]) -> dict:
+        """multiagent_env.py:90-115: bus_voltage / max_voltage / min_voltage from the
+        PREVIOUS power flow, only when the agent lists them in obs_labels."""
+        kwargs = {}
+        if "bus_voltage" in agent.obs_labels:
+            kwargs["bus_voltage"] = self.pf_solver.get_bus_voltage_by_name(
+                self.agent_name_bus_map[agent.name])
+        if "max_voltage" in agent.obs_labels:
+            kwargs["max_voltage"] = torch.stack(list(self.voltages.values())).max(0).values
+        if "min_voltage" in agent.obs_labels:
+            kwargs["min_voltage"] = torch.stack(list(self.voltages.values())).min(0).values
+        return kwargs
+
+    def reward_transform(self, rew_dict) -> dict:
+        """Pass-through by default (multiagent_env.py:215-218)."""
+        return rew_dict
+
+    def meta_transform(self, meta) -> dict:
+        """Pass-through by default (multiagent_env.py:221-225)."""
+        return meta
+
+    # ================================================================ API
+    def reset(self) -> Dict[str, any]:
+        """multiagent_env.py:125-140"""
+        self.episode_step = 0
+        self.time = self.start_time
+        self.history = {"timestamp": [], "voltage": [], "agent_power_p": []}
+        self.pf_solver.calculate_power_flow(current_time=self.time)
+        self.voltages = self.pf_solver.get_bus_voltages()
+        for agent in self.agents:
+            kwargs = self.get_external_obs_vars(agent)
+            _ = agent.reset(**kwargs)
+        return self.get_obs()
+
+    def get_obs(self) -> Dict[str, any]:
+        obs = {}
+        for agent in self.agents:
+            kwargs = self.get_external_obs_vars(agent)
+            obs[agent.name], _ = agent.get_obs(**kwargs)
+        return obs
+
+    def step(self, action) -> Tuple[dict, dict, dict, dict]:
+        """multiagent_env.py:151-212.  ``action`` is the reference's
+        {agent: {component: [N, d]}} dict, or -- fused path -- one packed tensor
+        [n_agents, N, act_dim] (any strides; zero-copy)."""
+        self.episode_step += 1
+        self.time += self.control_timedelta
+        self.obs_dict = {}
+        if self._fused is not None:
+            obs, rew, done, meta = self._step_fused(action)
+        else:
+            obs, rew, done, meta = self._step_generic(action)
+        any_done = any(done.values())
+        max_steps_reached = (self.episode_step == self.max_episode_steps - 1)
+        time_up = self.time >= self.end_time
+        d = bool(any_done or max_steps_reached or time_up)
+        dones = {a.name: d for a in self.agents}
+        dones["__all__"] = d
+        return obs, rew, dones, meta
+
+    def _step_generic(self, action):
+        obs, rew, done, meta = {}, {}, {}, {}
+        load_p, load_q = {}, {}
+        agent_power_p = []
+        for agent in self.agents:
+            name = agent.name
+            kwargs = self.get_external_obs_vars(agent)
+            obs[name], r, done[name], meta[name] = agent.step(action=action[name], **kwargs)
+            rew[name] = r.clone()
+            load_bus = self.agent_name_bus_map[name]
+            p, q = agent.real_power, agent.reactive_power
+            agent_power_p.append(p)
+            if load_bus in load_p:
+                load_p[load_bus] = load_p[load_bus] + p
+                load_q[load_bus] = load_q[load_bus] + q
+            else:
+                load_p[load_bus] = p
+                load_q[load_bus] = q
+        self.pf_solver.calculate_power_flow(current_time=self.time, p_controllable_consumed=load_p,
+                                            q_controllable_consumed=load_q)
+        self.voltages = self.pf_solver.get_bus_voltages()
+        self._record(agent_power_p)
+        rew = self.reward_transform(rew)
+        meta = self.meta_transform(meta)
+        return obs, rew, done, meta
+
+    def _record(self, agent_power_p):
+        if self.record_history:
+            self.history["timestamp"].append(self.time)
+            self.history["voltage"].append({k: v.clone() for k, v in self.voltages.items()})
+            self.history["agent_power_p"].append([p.clone() for p in agent_power_p])
+
+    @property
+    def agent_dict(self) -> Dict[str, ComponentEnv]:
+        return {a.name: a for a in self.agents}
+
+    # ================================================================ fused path
+    def _fusable(self):
+        from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+        if not isinstance(self.pf_solver, OpenDSSSolver):
+            return "power flow solver is not the batched OpenDSSSolver"
+        if len(self.agents) > _lib.MAX_AGENTS:
+            return "more than %d agents" % _lib.MAX_AGENTS
+        cls = type(self)
+        for hook in ("get_external_obs_vars", "step", "reset", "get_obs"):
+            if getattr(cls, hook) is not getattr(MultiAgentEnv, hook):
+                return "%s is overridden" % hook
+        # reward/meta transforms must be the ones the fused kernel implements: the
+        # base pass-through, or those of the class that declares fused_reward_transform
+        owner = MultiAgentEnv
+        for klass in cls.__mro__:
+            if klass.__dict__.get("fused_reward_transform") is not None:
+                owner = klass
+                break
+        for hook in ("reward_transform", "meta_transform", "get_voltage_violation"):
+            if getattr(cls, hook, None) is not getattr(owner, hook, None):
+                return "%s is overridden" % hook
+        kinds0 = None
+        for a in self.agents:
+            if not isinstance(a, MultiComponentEnv) or type(a) is not MultiComponentEnv:
+                return "agent %s is not a plain MultiComponentEnv" % a.name
+            kinds = [type(e).fused_kind for e in a.envs]
+            if any(k is None for k in kinds) or len(set(kinds)) != len(kinds):
+                return "agent %s has components the fused kernel does not implement" % a.name
+            if kinds0 is None:
+                kinds0 = kinds
+            elif kinds != kinds0:
+                return "agents differ in components"
+            for e in a.envs:
+                if any(l in ("bus_voltage", "min_voltage", "max_voltage") for l in e.obs_labels):
+                    return "agent %s observes grid voltages" % a.name
+                if getattr(e, "grid_aware", False):
+                    return "grid-aware PV"
+        ref = self.agents[0]
+        for a in self.agents[1:]:
+            for e0, e1 in zip(ref.envs, a.envs):
+                if bytes(e0.params) != bytes(e1.params):
+                    return "agents have different component parameters"
+                if hasattr(e0, "data") and not np.array_equal(e0.data, e1.data):
+                    return "agents have different PV profiles"
+                if hasattr(e0, "_exo") and (e0.df.index[0] != e1.df.index[0] or
+                                            not np.array_equal(e0._T_oa, e1._T_oa)):
+                    return "agents have different exogenous data"
+        if self.fused_reward_transform not in (None, "coordinated"):
+            return "unknown fused reward transform"
+        if self.fused_reward_transform == "coordinated" and \
+                len(set(self.agent_name_bus_map.values())) != 1:
+            return "coordinated reward needs all agents on one bus"
+        return None
+
+    def _setup_fused(self):
+        n, na = self.num_envs, len(self.agents)
+        dev = self.device
+        a0 = self.agents[0]
+        kinds = [type(e).fused_kind for e in a0.envs]
+        act_dims = [e.action_space.shape[0] for e in a0.envs]
+        obs_dims = [e.observation_space.shape[0] for e in a0.envs]
+        act_off = np.concatenate([[0], np.cumsum(act_dims)])[:-1]
+        obs_off = np.concatenate([[0], np.cumsum(obs_dims)])[:-1]
+        act_dim, obs_dim = int(sum(act_dims)), int(sum(obs_dims))
+
+        buses = [self.agent_name_bus_map[a.name] for a in self.agents]
+        ctrl = sorted(set(b for b in buses if b in self.pf_solver.load_bus_name))
+        self.pf_solver.set_controllable_loads(ctrl)
+        out_nodes = []
+        if self.fused_reward_transform == "coordinated":
+            out_nodes = [x for x in _bus_nodes(buses[0])]
+        for b in sorted(set(buses)):
+            for x in _bus_nodes(b):
+                if x in self.pf_solver.feeder.node_index and x not in out_nodes:
+                    out_nodes.append(x)
+        if not out_nodes:
+            out_nodes = [self.pf_solver.feeder.node_names[0]]
+        self.pf_solver.set_output_nodes(out_nodes)
+        if self.fused_reward_transform == "coordinated" and len(_bus_nodes(buses[0])) != 1:
+            raise ValueError("coordinated reward needs a single-phase common bus (e.g. '675c')")
+
+        p = _lib.CoordParams()
+        p.n_agents, p.act_dim, p.obs_dim, p.n_comp = na, act_dim, obs_dim, len(kinds)
+        p.act_bld = p.act_pv = p.act_bat = -1
+        p.obs_bld = p.obs_pv = p.obs_bat = -1
+        for i, (k, e) in enumerate(zip(kinds, a0.envs)):
+            p.comp_order[i] = _KIND_ID[k]
+            if k == "building":
+                p.bld, p.act_bld, p.obs_bld = e.params, int(act_off[i]), int(obs_off[i])
+            elif k == "pv":
+                p.pv, p.act_pv, p.obs_pv = e.params, int(act_off[i]), int(obs_off[i])
+            else:
+                p.bat, p.act_bat, p.obs_bat = e.params, int(act_off[i]), int(obs_off[i])
+        for i, b in enumerate(buses):
+            p.agent_ctrl[i] = ctrl.index(b) if b in ctrl else -1
+        p.coordinated = int(self.fused_reward_transform == "coordinated")
+        p.vv_row = 0
+        p.vv_lo, p.vv_hi = [float(v) for v in getattr(self, "VOLTAGE_LIMITS", [0.95, 1.05])]
+        p.vv_penalty = float(getattr(self, "VV_UNIT_PENALTY", 1e4))
+
+        F = dict(params=p, kinds=kinds, act_off=act_off, obs_off=obs_off, act_dims=act_dims,
+                 obs_dims=obs_dims, act_dim=act_dim, obs_dim=obs_dim)
+        F["obs"] = torch.zeros((na, obs_dim, n), dtype=torch.float64, device=dev)
+        F["act"] = torch.zeros((na, act_dim, n), dtype=torch.float64, device=dev)
+        F["x"] = torch.zeros((na, 5, n), dtype=torch.float64, device=dev)
+        F["soc"] = torch.zeros((na, n), dtype=torch.float64, device=dev)
+        F["reward"] = torch.zeros((na, n), dtype=torch.float64, device=dev)
+        F["agent_power"] = torch.zeros((na, n), dtype=torch.float64, device=dev)
+        F["vv"] = torch.zeros(n, dtype=torch.float64, device=dev)
+        F["iters"] = torch.zeros(n, dtype=torch.int32, device=dev)
+        for ai, agent in enumerate(self.agents):
+            for i, (k, e) in enumerate(zip(kinds, agent.envs)):
+                view = F["obs"][ai, int(obs_off[i]):int(obs_off[i]) + obs_dims[i]].t()
+                if k == "building":
+                    e._adopt(x=F["x"][ai], obs=view)
+                elif k == "pv":
+                    e._adopt(obs=view)
+                else:
+                    e._adopt(soc=F["soc"][ai], obs=view)
+            agent._real_power = F["agent_power"][ai]
+            agent._reward = F["reward"][ai]
+        self._fused = F
+
+    def action_buffer(self):
+        """Packed [n_agents, N, act_dim] action tensor the fused step reads
+        zero-copy, plus the {agent: {component: [N, d]}} views into it."""
+        F = self._fused
+        if F is None:
+            raise RuntimeError("action_buffer() is only available on the fused path")
+        packed = F["act"].transpose(1, 2)
+        views = {}
+        for ai, agent in enumerate(self.agents):
+            views[agent.name] = {e.name: packed[ai, :, int(F["act_off"][i]):int(F["act_off"][i]) + F["act_dims"][i]]
+                                 for i, e in enumerate(agent.envs)}
+        return packed, views
+
+    def _pack_actions(self, action):
+        F = self._fused
+        if isinstance(action, torch.Tensor):
+            na, n = len(self.agents), self.num_envs
+            if action.dim() != 3 or tuple(action.shape) != (na, n, F["act_dim"]):
+                raise ValueError("packed action must be [n_agents=%d, N=%d, act_dim=%d], got %s"
+                                 % (na, n, F["act_dim"], tuple(action.shape)))
+            if action.dtype != torch.float64 or action.device != self.device:
+                action = action.to(device=self.device, dtype=torch.float64)
+            return action
+        packed, views = self.action_buffer()
+        for ai, agent in enumerate(self.agents):
+            for i, e in enumerate(agent.envs):
+                src = as_action(action[agent.name][e.name], self.num_envs, F["act_dims"][i], self.device)
+                views[agent.name][e.name].copy_(src)
+        return packed
+
+    def _step_fused(self, action):
+        F = self._fused
+        act = self._pack_actions(action)
+        a0 = self.agents[0]
+        info = _lib.CoordStepInfo()
+        for k, e in zip(F["kinds"], a0.envs):
+            if k == "building":
+                t = e.time_index
+                if t + 1 >= len(e._exo):
+                    raise IndexError("building stepped past the end of its exogenous data")
+                info.ex_t, info.ex_next = e._exo[t], e._exo[t + 1]
+            elif k == "pv":
+                info.pv_pmax = float(e.data[e.index])
+        pfp = self.pf_solver.step_params(self.time)
+        bufs = _lib.CoordBuffers()
+        bufs.action = _lib.Mat(act.data_ptr(), act.stride(1), act.stride(2))
+        bufs.act_stride_agent = act.stride(0)
+        obs = F["obs"]
+        bufs.obs = _lib.Mat(obs.data_ptr(), 1, obs.stride(1))
+        bufs.obs_stride_agent = obs.stride(0)
+        bufs.x, bufs.soc = F["x"].data_ptr(), F["soc"].data_ptr()
+        bufs.reward, bufs.agent_power = F["reward"].data_ptr(), F["agent_power"].data_ptr()
+        bufs.v_out = self.pf_solver.v_out.data_ptr()
+        bufs.vv, bufs.iters = F["vv"].data_ptr(), F["iters"].data_ptr()
+        _lib.check(_lib.lib().pgw_coord_step(F["params"], pfp, self.pf_solver.tables, info,
+                                             self.num_envs, bufs, _lib.stream_ptr(self.device)))
+        self.pf_solver.iterations = F["iters"]
+        self.pf_solver._prepare_bus_voltages()
+        self.voltages = self.pf_solver.get_bus_voltages()
+        obs_d, rew, done, meta = {}, {}, {}, {}
+        for ai, agent in enumerate(self.agents):
+            comp_done = []
+            ob = {}
+            for k, e in zip(F["kinds"], agent.envs):
+                ob[e.name] = e._obs
+                if k == "building":
+                    e.time_index += 1
+                    e.time = e.df.index[e.time_index]
+                elif k == "pv":
+                    e.index += 1
+                else:
+                    e.simulation_step += 1
+                comp_done.append(e.is_terminal())
+            obs_d[agent.name] = ob
+            rew[agent.name] = F["reward"][ai]
+            done[agent.name] = any(comp_done)
+            meta[agent.name] = {}
+        if self.fused_reward_transform == "coordinated":
+            meta["voltage_violation"] = F["vv"]
+        self._record([F["agent_power"][ai] for ai in range(len(self.agents))])
+        return obs_d, rew, done, meta
+
+    def packed_obs(self):
+        """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""
+        return self._fused["obs"].transpose(1, 2)
+
+
+def _bus_nodes(bus):
+    from powergridworld_amd.distribution_system.opendss import bus_name_to_nodes
+    return bus_name_to_nodes(bus)

@@ -1,0 +1,46 @@
+"""CoordinatedMultiBuildingControlEnv and the BASELINE C4 scenario
+(reference: examples/marl/openai/train.py:37-88 and make_env :165-188)."""
+import torch
+
+from powergridworld_amd.multiagent_env import MultiAgentEnv
+from powergridworld_amd.scenarios.buildings import make_env_config
+
+
+class CoordinatedMultiBuildingControlEnv(MultiAgentEnv):
+    """Shared voltage-violation penalty split evenly over the agents.  On the
+    fused path the same transform runs inside pgw_coord_step."""
+
+    VOLTAGE_LIMITS = [0.95, 1.05]
+    VV_UNIT_PENALTY = 1e4
+    fused_reward_transform = "coordinated"
+
+    def reward_transform(self, rew_dict) -> dict:
+        voltage_violation = self.get_voltage_violation()
+        sys_penalty = voltage_violation * self.VV_UNIT_PENALTY
+        agent_num = len(rew_dict)
+        for key in rew_dict.keys():
+            rew_dict[key] = rew_dict[key] - (sys_penalty / agent_num)
+        return rew_dict
+
+    def meta_transform(self, meta) -> dict:
+        meta.update({'voltage_violation': self.get_voltage_violation()})
+        return meta
+
+    def get_voltage_violation(self):
+        assert len(set(self.agent_name_bus_map.values())) == 1, \
+            "In this example, all buildings should be on the same bus."
+        bus_id = list(set(self.agent_name_bus_map.values()))[0]
+        v = self.pf_solver.get_bus_voltage_by_name(bus_id)
+        zero = torch.zeros_like(v)
+        return torch.maximum(torch.maximum(zero, self.VOLTAGE_LIMITS[0] - v),
+                             v - self.VOLTAGE_LIMITS[1])
+
+
+def make_c4_config(num_buildings=5, sys_load=1.2):
+    """The BASELINE C4 scenario: make_env (train.py:165-188) with 5 buildings."""
+    return make_env_config(
+        building_config={},
+        pv_config={"profile_csv": "pv_profile.csv", "scaling_factor": 40.},
+        storage_config={"max_power": 15., "storage_range": (3., 50.)},
+        system_load_rescale_factor=sys_load,
+        num_buildings=num_buildings)

@@ -20,7 +20,8 @@ def golden_path(name):
 
 @pytest.fixture(scope="session")
 def exo_frame():
+    import numpy as np
     import pandas as pd
-    df = pd.read_csv(os.path.join(GOLDEN, "exogenous_synthetic.csv.gz"), index_col=0)
-    df.index = pd.DatetimeIndex(df.index)
-    return df
+    with np.load(os.path.join(GOLDEN, "exogenous_synthetic.npz"), allow_pickle=False) as z:
+        idx = pd.DatetimeIndex(z["index_ns"].astype("datetime64[ns]"))
+        return pd.DataFrame(z["values"], index=idx, columns=[str(c) for c in z["columns"]])

@@ -126,3 +126,22 @@ def test_mc_c3(exo_frame):
         np.testing.assert_allclose(r, g["reward"][t], 1e-10, 1e-10)
         np.testing.assert_allclose(mc.real_power, g["real_power"][t], 1e-10, 1e-10)
         assert (d == g["done"][t]).all()
+
+
+def test_c4_coordinated_oracle():
+    """MultiAgentEnv + CoordinatedMultiBuildingControlEnv (reference, oracle PF behind
+    its PowerFlowSolver ABC) vs the oracle's end-to-end C4 restatement."""
+    from oracle.ma_oracle import CoordinatedOracle
+    g = load("c4_coordinated")
+    T, NA, K, _ = g["actions"].shape
+    orc = CoordinatedOracle(K, n_agents=NA)
+    obs0 = orc.reset(g["init_storage"])
+    np.testing.assert_allclose(obs0, g["obs"][0], 1e-10, 1e-10)
+    np.testing.assert_allclose(orc.v, g["v675"][0], 1e-12, 1e-12)
+    for t in range(T):
+        obs, rew, vv = orc.step(g["actions"][t])
+        np.testing.assert_allclose(obs, g["obs"][t + 1], 1e-10, 1e-10)
+        np.testing.assert_allclose(rew, g["reward"][t], 1e-9, 1e-9)
+        np.testing.assert_allclose(vv, g["voltage_violation"][t], 1e-12, 1e-12)
+        np.testing.assert_allclose(orc.v, g["v675"][t + 1], 1e-12, 1e-12)
+        assert orc.done == bool(g["done"][t, 0])
