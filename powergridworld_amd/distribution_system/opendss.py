@@ -134,14 +134,15 @@ class OpenDSSSolver(PowerFlowSolver):
     def calculate_power_flow(self, p_controllable_consumed: dict = None,
                              q_controllable_consumed: dict = None, current_time: str = None) -> None:
         n = self.num_envs
-        keys = []
         if p_controllable_consumed is not None:
             keys = [k for k in self.load_bus_name
                     if k in p_controllable_consumed or k in (q_controllable_consumed or {})]
-        self.set_controllable_loads(keys)
+            if not set(keys) <= set(self._ctrl_names):     # the controllable set only grows
+                grown = set(keys) | set(self._ctrl_names)
+                self.set_controllable_loads([k for k in self.load_bus_name if k in grown])
         p = self.step_params(current_time)
         cp = cq = None
-        if self._ctrl_names:
+        if self._ctrl_names and p_controllable_consumed is not None:
             zeros = torch.zeros(n, dtype=torch.float64, device=self.device)
             get = lambda d, k: as_env_tensor(d[k], n, self.device, k) if (d and k in d) else zeros
             cp = torch.stack([get(p_controllable_consumed, k) for k in self._ctrl_names])
