@@ -31,37 +31,44 @@ namespace {
 
 using cplx = std::complex<double>;
 using Mat = std::vector<cplx>;   // row-major square
+using xcplx = std::complex<long double>;   // x87 80-bit: 64-bit mantissa
+using XMat = std::vector<xcplx>;
 
 // Gauss-Jordan inversion with partial pivoting; returns false if singular.
-bool invert(Mat& a, int n) {
-  Mat inv(static_cast<size_t>(n) * n, cplx(0.0, 0.0));
-  for (int i = 0; i < n; ++i) inv[i * n + i] = 1.0;
+// Templated so the feeder matrix is inverted in extended precision: the
+// near-ideal switch (1e-7 ohm) gives Y a condition number ~1e7, and an fp64
+// inverse would carry ~1e-9 relative error into every load-element voltage.
+template <typename CT>
+bool invert(std::vector<CT>& a, int n) {
+  using R = typename CT::value_type;
+  std::vector<CT> inv(static_cast<size_t>(n) * n, CT(0, 0));
+  for (int i = 0; i < n; ++i) inv[i * n + i] = R(1);
   for (int c = 0; c < n; ++c) {
     int piv = c;
-    double best = std::abs(a[c * n + c]);
+    R best = std::abs(a[c * n + c]);
     for (int r = c + 1; r < n; ++r) {
-      double v = std::abs(a[r * n + c]);
+      R v = std::abs(a[r * n + c]);
       if (v > best) {
         best = v;
         piv = r;
       }
     }
-    if (best == 0.0 || !std::isfinite(best)) return false;
+    if (best == R(0) || !std::isfinite(best)) return false;
     if (piv != c) {
       for (int j = 0; j < n; ++j) {
         std::swap(a[c * n + j], a[piv * n + j]);
         std::swap(inv[c * n + j], inv[piv * n + j]);
       }
     }
-    cplx d = 1.0 / a[c * n + c];
+    CT d = R(1) / a[c * n + c];
     for (int j = 0; j < n; ++j) {
       a[c * n + j] *= d;
       inv[c * n + j] *= d;
     }
     for (int r = 0; r < n; ++r) {
       if (r == c) continue;
-      cplx f = a[r * n + c];
-      if (f == cplx(0.0, 0.0)) continue;
+      CT f = a[r * n + c];
+      if (f == CT(0, 0)) continue;
       for (int j = 0; j < n; ++j) {
         a[r * n + j] -= f * a[c * n + j];
         inv[r * n + j] -= f * inv[c * n + j];
@@ -229,18 +236,23 @@ int32_t pgw_feeder_build(const pgw_feeder_elem* elems, int32_t n_elems, int32_t 
     }
     if (Y) put(Y, B.Y.data(), B.Y.size());
     if (I_src) put(I_src, B.I.data(), B.I.size());
-    Mat Zm = B.Y;
-    if (!invert(Zm, n_nodes)) {
+    XMat Zx(B.Y.size());
+    for (size_t i = 0; i < B.Y.size(); ++i) Zx[i] = xcplx(B.Y[i].real(), B.Y[i].imag());
+    if (!invert(Zx, n_nodes)) {
       pgw::set_error("pgw_feeder_build: singular admittance matrix (floating node?)");
       return PGW_ERR_ARG;
     }
+    Mat Zm(Zx.size());
+    for (size_t i = 0; i < Zx.size(); ++i)
+      Zm[i] = cplx((double)Zx[i].real(), (double)Zx[i].imag());
     if (Z) put(Z, Zm.data(), Zm.size());
     if (V0) {
       std::vector<cplx> v(n_nodes);
       for (int r = 0; r < n_nodes; ++r) {
-        cplx s(0.0, 0.0);
-        for (int c = 0; c < n_nodes; ++c) s += Zm[r * n_nodes + c] * B.I[c];
-        v[r] = s;
+        xcplx s(0, 0);
+        for (int c = 0; c < n_nodes; ++c)
+          s += Zx[r * n_nodes + c] * xcplx(B.I[c].real(), B.I[c].imag());
+        v[r] = cplx((double)s.real(), (double)s.imag());
       }
       put(V0, v.data(), v.size());
     }
