@@ -17,9 +17,13 @@ class CoordinatedMultiBuildingControlEnv(MultiAgentEnv):
     def reward_transform(self, rew_dict) -> dict:
         voltage_violation = self.get_voltage_violation()
         sys_penalty = voltage_violation * self.VV_UNIT_PENALTY
-        agent_num = len(rew_dict)
+        # a device-tensor divisor keeps the IEEE division of the reference's Python
+        # floats (tensor / python-scalar multiplies by the reciprocal: 1-ulp off)
+        agent_num = torch.tensor(float(len(rew_dict)), dtype=sys_penalty.dtype,
+                                 device=sys_penalty.device)
+        share = sys_penalty / agent_num
         for key in rew_dict.keys():
-            rew_dict[key] = rew_dict[key] - (sys_penalty / agent_num)
+            rew_dict[key] = rew_dict[key] - share
         return rew_dict
 
     def meta_transform(self, meta) -> dict:
