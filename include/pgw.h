@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 1
+#define PGW_ABI_VERSION 2
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -232,6 +232,7 @@ typedef struct pgw_pf_params {
   double base_kw[PGW_PF_MAX_M];     /* the element's LOAD total kW this step  */
   double base_kvar[PGW_PF_MAX_M];   /*   (loadshape x base x rescale)         */
   double tol;                       /* max |dU|/vbase convergence tolerance   */
+  double pred_p[3];                 /* controllable kW of the 3 predictor solutions */
   int32_t elem_ctrl[PGW_PF_MAX_M];  /* controllable-load slot of the element, -1 none */
   int32_t m, n_ctrl, n_out, max_iter;
 } pgw_pf_params;
@@ -243,6 +244,13 @@ typedef struct pgw_pf_tables {
   const double* G;      /* n_out x m complex: node voltage response     */
   const double* V0;     /* n_out complex: no-load node voltages         */
   const double* inv_vbase_out;  /* n_out: 1 / (kV_LN * 1000)           */
+  /* Optional initial guess (n_ctrl == 1 only): 3 x m complex element voltages
+   * solved at controllable load pred_p[0..2] for this step's base loads; each
+   * env starts from their quadratic (Lagrange) interpolant in its own
+   * controllable kW instead of from U0.  NULL = cold start from U0. */
+  const double* U_pred;
+  /* Optional output: converged element voltages, n x m complex (env-major). */
+  double* U_out;
 } pgw_pf_tables;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

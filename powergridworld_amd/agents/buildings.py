@@ -174,7 +174,11 @@ class FiveZoneROMEnv(ComponentEnv):
         self._reward_out = torch.zeros(n, dtype=torch.float64, device=self.device)
         self._obs = self._new_obs(len(self._obs_labels))
         self.time_index = None
-        self.time = None
+
+    @property
+    def time(self):
+        """Timestamp of the current exogenous row (five_zone_rom_env.py:188,219)."""
+        return None if self.time_index is None else self.df.index[self.time_index]
 
     # ---------------------------------------------------------------- setup
     def make_comfort_bounds_df(self) -> pd.DataFrame:
@@ -260,7 +264,6 @@ class FiveZoneROMEnv(ComponentEnv):
     def reset(self, **obs_kwargs):
         """(:147-180) -- x_k carries over from the previous episode."""
         self.time_index = 0
-        self.time = self.df.index[0]
         ext, keep = self._ext(obs_kwargs)
         _lib.check(_lib.lib().pgw_building_reset(
             self.params, self._exo[0], self.num_envs, _lib.dptr(self.x), _lib.dptr(self.p_consumed),
@@ -284,7 +287,6 @@ class FiveZoneROMEnv(ComponentEnv):
             _lib.dptr(self.x), _lib.dptr(self.p_consumed), _lib.dptr(self._reward_out),
             _lib.dptr(self._reward_state), lagged, ext, _lib.mat(self._obs), self._stream()))
         self.time_index += 1
-        self.time = self.df.index[self.time_index]
         rew = self._reward_out
         if self.reward_kind == "viol":
             rew = prev if lagged else self._viol_reward()

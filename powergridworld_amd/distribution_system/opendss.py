@@ -116,18 +116,29 @@ class OpenDSSSolver(PowerFlowSolver):
         p.tol, p.m, p.n_ctrl = self.tol, M, len(self._ctrl_names)
         p.n_out, p.max_iter = len(self.output_names), self.max_iter
         self.params = p
+        self._cfg_version = getattr(self, "_cfg_version", 0) + 1
+        self._step_cache = {}
 
     def step_params(self, current_time):
         """PFParams with this step's base loads: loadshape[hour] * base * rescale
-        (opendss.py:96-108)."""
-        current_time = pd.Timestamp(current_time)
-        coef = self.annual_hourly_load_profile[get_hour_of_year(current_time)]
+        (opendss.py:96-108).  Cached per (time, configuration): the base loads
+        only change hourly."""
+        key = (current_time, self._cfg_version)
+        p = self._step_cache.get(key)
+        if p is not None:
+            return p
+        ts = pd.Timestamp(current_time)
+        coef = self.annual_hourly_load_profile[get_hour_of_year(ts)]
         step_load = coef * self.base_load * self.system_load_rescale_factor
-        f, p = self.feeder, self.params
+        f = self.feeder
+        p = _lib.PFParams.from_buffer_copy(self.params)
         for k in range(self.M):
             real = k < f.m
             p.base_kw[k] = step_load[f.elem_load[k], 0] if real else 0.0
             p.base_kvar[k] = step_load[f.elem_load[k], 1] if real else 0.0
+        if len(self._step_cache) > 4096:
+            self._step_cache.clear()
+        self._step_cache[key] = p
         return p
 
     # ------------------------------------------------------------ reference API

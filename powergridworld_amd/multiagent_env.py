@@ -71,6 +71,8 @@ class MultiAgentEnv(Env):
         self.voltages = None
         self.obs_dict = {}
         self.record_history = record_history
+        self._times, self._end_step = [], 10 ** 12
+        self._time_at(0)
 
         self.agents = []
         for a in agents:
@@ -129,10 +131,20 @@ class MultiAgentEnv(Env):
         return meta
 
     # ================================================================ API
+    def _time_at(self, step):
+        """start_time + step * control_timedelta (cached: pandas arithmetic is slow)."""
+        times = self._times
+        if step >= len(times):
+            n = max(2 * len(times), step + 1, 512)
+            self._times = times = [self.start_time + i * self.control_timedelta for i in range(n)]
+            # first step whose time is >= end_time (multiagent_env.py:201)
+            self._end_step = next((i for i, t in enumerate(times) if t >= self.end_time), n + 10 ** 9)
+        return times[step]
+
     def reset(self) -> Dict[str, any]:
         """multiagent_env.py:125-140"""
         self.episode_step = 0
-        self.time = self.start_time
+        self.time = self._time_at(0)
         self.history = {"timestamp": [], "voltage": [], "agent_power_p": []}
         self.pf_solver.calculate_power_flow(current_time=self.time)
         self.voltages = self.pf_solver.get_bus_voltages()
@@ -153,7 +165,7 @@ class MultiAgentEnv(Env):
         {agent: {component: [N, d]}} dict, or -- fused path -- one packed tensor
         [n_agents, N, act_dim] (any strides; zero-copy)."""
         self.episode_step += 1
-        self.time += self.control_timedelta
+        self.time = self._time_at(self.episode_step)
         self.obs_dict = {}
         if self._fused is not None:
             obs, rew, done, meta = self._step_fused(action)
@@ -161,7 +173,7 @@ class MultiAgentEnv(Env):
             obs, rew, done, meta = self._step_generic(action)
         any_done = any(done.values())
         max_steps_reached = (self.episode_step == self.max_episode_steps - 1)
-        time_up = self.time >= self.end_time
+        time_up = self.episode_step >= self._end_step
         d = bool(any_done or max_steps_reached or time_up)
         dones = {a.name: d for a in self.agents}
         dones["__all__"] = d
@@ -324,6 +336,29 @@ class MultiAgentEnv(Env):
                     e._adopt(soc=F["soc"][ai], obs=view)
             agent._real_power = F["agent_power"][ai]
             agent._reward = F["reward"][ai]
+        # ---- constant per-step launch state and return values (views)
+        bufs = _lib.CoordBuffers()
+        obs = F["obs"]
+        bufs.obs = _lib.Mat(obs.data_ptr(), 1, obs.stride(1))
+        bufs.obs_stride_agent = obs.stride(0)
+        bufs.x, bufs.soc = F["x"].data_ptr(), F["soc"].data_ptr()
+        bufs.reward, bufs.agent_power = F["reward"].data_ptr(), F["agent_power"].data_ptr()
+        bufs.v_out = self.pf_solver.v_out.data_ptr()
+        bufs.vv, bufs.iters = F["vv"].data_ptr(), F["iters"].data_ptr()
+        F["bufs"], F["act_key"], F["info_cache"] = bufs, None, {}
+        comps = [dict(zip(kinds, agent.envs)) for agent in self.agents]
+        F["bld0"], F["pv0"] = comps[0].get("building"), comps[0].get("pv")
+        F["bld_envs"] = [c["building"] for c in comps if "building" in c]
+        F["pv_envs"] = [c["pv"] for c in comps if "pv" in c]
+        F["bat_envs"] = [c["storage"] for c in comps if "storage" in c]
+        F["agent0_envs"] = list(self.agents[0].envs)
+        F["obs_dict"] = {agent.name: {e.name: e._obs for e in agent.envs} for agent in self.agents}
+        F["rew_dict"] = {agent.name: F["reward"][ai] for ai, agent in enumerate(self.agents)}
+        F["done_true"] = {agent.name: True for agent in self.agents}
+        F["done_false"] = {agent.name: False for agent in self.agents}
+        F["meta"] = {agent.name: {} for agent in self.agents}
+        if self.fused_reward_transform == "coordinated":
+            F["meta"]["voltage_violation"] = F["vv"]
         self._fused = F
 
     def action_buffer(self):
@@ -359,54 +394,43 @@ class MultiAgentEnv(Env):
     def _step_fused(self, action):
         F = self._fused
         act = self._pack_actions(action)
-        a0 = self.agents[0]
-        info = _lib.CoordStepInfo()
-        for k, e in zip(F["kinds"], a0.envs):
-            if k == "building":
-                t = e.time_index
-                if t + 1 >= len(e._exo):
+        key = (act.data_ptr(), act.stride(0), act.stride(1), act.stride(2))
+        bufs = F["bufs"]
+        if key != F["act_key"]:
+            bufs.action = _lib.Mat(key[0], key[2], key[3])
+            bufs.act_stride_agent = key[1]
+            F["act_key"] = key
+        bld, pv = F["bld0"], F["pv0"]
+        ikey = (bld.time_index if bld is not None else -1, pv.index if pv is not None else -1)
+        info = F["info_cache"].get(ikey)
+        if info is None:
+            info = _lib.CoordStepInfo()
+            if bld is not None:
+                t = bld.time_index
+                if t + 1 >= len(bld._exo):
                     raise IndexError("building stepped past the end of its exogenous data")
-                info.ex_t, info.ex_next = e._exo[t], e._exo[t + 1]
-            elif k == "pv":
-                info.pv_pmax = float(e.data[e.index])
+                info.ex_t, info.ex_next = bld._exo[t], bld._exo[t + 1]
+            if pv is not None:
+                info.pv_pmax = float(pv.data[pv.index])
+            F["info_cache"][ikey] = info
         pfp = self.pf_solver.step_params(self.time)
-        bufs = _lib.CoordBuffers()
-        bufs.action = _lib.Mat(act.data_ptr(), act.stride(1), act.stride(2))
-        bufs.act_stride_agent = act.stride(0)
-        obs = F["obs"]
-        bufs.obs = _lib.Mat(obs.data_ptr(), 1, obs.stride(1))
-        bufs.obs_stride_agent = obs.stride(0)
-        bufs.x, bufs.soc = F["x"].data_ptr(), F["soc"].data_ptr()
-        bufs.reward, bufs.agent_power = F["reward"].data_ptr(), F["agent_power"].data_ptr()
-        bufs.v_out = self.pf_solver.v_out.data_ptr()
-        bufs.vv, bufs.iters = F["vv"].data_ptr(), F["iters"].data_ptr()
-        _lib.check(_lib.lib().pgw_coord_step(F["params"], pfp, self.pf_solver.tables, info,
-                                             self.num_envs, bufs, _lib.stream_ptr(self.device)))
+        rc = _lib.lib().pgw_coord_step(F["params"], pfp, self.pf_solver.tables, info,
+                                       self.num_envs, bufs, _lib.stream_ptr(self.device))
+        if rc:
+            _lib.check(rc)
         self.pf_solver.iterations = F["iters"]
-        self.pf_solver._prepare_bus_voltages()
-        self.voltages = self.pf_solver.get_bus_voltages()
-        obs_d, rew, done, meta = {}, {}, {}, {}
-        for ai, agent in enumerate(self.agents):
-            comp_done = []
-            ob = {}
-            for k, e in zip(F["kinds"], agent.envs):
-                ob[e.name] = e._obs
-                if k == "building":
-                    e.time_index += 1
-                    e.time = e.df.index[e.time_index]
-                elif k == "pv":
-                    e.index += 1
-                else:
-                    e.simulation_step += 1
-                comp_done.append(e.is_terminal())
-            obs_d[agent.name] = ob
-            rew[agent.name] = F["reward"][ai]
-            done[agent.name] = any(comp_done)
-            meta[agent.name] = {}
-        if self.fused_reward_transform == "coordinated":
-            meta["voltage_violation"] = F["vv"]
-        self._record([F["agent_power"][ai] for ai in range(len(self.agents))])
-        return obs_d, rew, done, meta
+        self.voltages = self.pf_solver.bus_voltages
+        # advance the component clocks (their is_terminal() drives `done`)
+        for e in F["bld_envs"]:
+            e.time_index += 1
+        for e in F["pv_envs"]:
+            e.index += 1
+        for e in F["bat_envs"]:
+            e.simulation_step += 1
+        d = any(e.is_terminal() for e in F["agent0_envs"])
+        if self.record_history:
+            self._record([F["agent_power"][ai] for ai in range(len(self.agents))])
+        return F["obs_dict"], F["rew_dict"], F["done_true"] if d else F["done_false"], F["meta"]
 
     def packed_obs(self):
         """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""
