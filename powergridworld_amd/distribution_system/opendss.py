@@ -50,9 +50,13 @@ def get_hour_of_year(dt):
 
 class OpenDSSSolver(PowerFlowSolver):
 
+    # controllable kW of the three per-hour reference solutions the batched solve
+    # interpolates its initial guess from (single controllable load only)
+    PREDICTOR_KW = (-150.0, 100.0, 350.0)
+
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = 1e-10, max_iter: int = 100,
-                 output_nodes=None, **kwargs):
+                 output_nodes=None, predictor: bool = True, **kwargs):
         super().__init__(**kwargs)
         self.num_envs = int(num_envs)
         self.device = _lib.require_device(device)
@@ -68,6 +72,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self.bus_voltages = {}
         self.iterations = None
         self._ctrl_names = []
+        self.use_predictor = bool(predictor)
         self.set_output_nodes(output_nodes)
 
     # ------------------------------------------------------------ configuration
@@ -90,6 +95,9 @@ class OpenDSSSolver(PowerFlowSolver):
                                     inv_vbase_out=self._inv_vb.data_ptr())
         self.v_out = torch.zeros((max(len(names), 1), self.num_envs), dtype=torch.float64, device=dev)
         self._iters = torch.zeros(self.num_envs, dtype=torch.int32, device=dev)
+        self._pred_v = torch.zeros((max(len(names), 1), 3), dtype=torch.float64, device=dev)
+        self._pred_table = torch.zeros((32, 3, M, 2), dtype=torch.float64, device=dev)
+        self._pred_index = {}
         self._base_params()
 
     def set_controllable_loads(self, names):
@@ -115,9 +123,14 @@ class OpenDSSSolver(PowerFlowSolver):
             p.elem_ctrl[k] = self._ctrl_names.index(ln) if ln in self._ctrl_names else -1
         p.tol, p.m, p.n_ctrl = self.tol, M, len(self._ctrl_names)
         p.n_out, p.max_iter = len(self.output_names), self.max_iter
+        for i, v in enumerate(self.PREDICTOR_KW):
+            p.pred_p[i] = v
         self.params = p
         self._cfg_version = getattr(self, "_cfg_version", 0) + 1
         self._step_cache = {}
+        self._tables_cache = {}
+        if hasattr(self, "_pred_index"):
+            self._pred_index = {}
 
     def step_params(self, current_time):
         """PFParams with this step's base loads: loadshape[hour] * base * rescale
@@ -141,6 +154,45 @@ class OpenDSSSolver(PowerFlowSolver):
         self._step_cache[key] = p
         return p
 
+    def step_tables(self, current_time):
+        """PFTables for this step: with a single controllable load, the per-hour
+        predictor (3 reference solutions, solved here on the device the first
+        time an hour is seen) is attached; otherwise the cold-start tables."""
+        if not (self.use_predictor and len(self._ctrl_names) == 1):
+            return self.tables
+        key = (current_time, self._cfg_version)
+        t = self._tables_cache.get(key)
+        if t is not None:
+            return t
+        p = self.step_params(current_time)
+        hkey = (tuple(p.base_kw), tuple(p.base_kvar))
+        idx = self._pred_index.get(hkey)
+        if idx is None:
+            idx = len(self._pred_index)
+            if idx >= self._pred_table.shape[0]:
+                grown = torch.zeros((2 * idx, 3, self.M, 2), dtype=torch.float64, device=self.device)
+                grown[:idx] = self._pred_table
+                self._pred_table = grown
+                self._tables_cache = {}
+            self._pred_index[hkey] = idx
+            sp = _lib.PFParams.from_buffer_copy(p)
+            sp.tol = min(self.tol, 1e-12)
+            cp = torch.tensor([self.PREDICTOR_KW], dtype=torch.float64, device=self.device)
+            cq = torch.zeros_like(cp)
+            tb = _lib.PFTables.from_buffer_copy(self.tables)
+            tb.U_pred = None
+            tb.U_out = self._pred_table[idx].data_ptr()
+            _lib.check(_lib.lib().pgw_pf_solve(sp, tb, 3, _lib.dptr(cp), _lib.dptr(cq),
+                                               _lib.dptr(self._pred_v), None,
+                                               _lib.stream_ptr(self.device)))
+            self._pred_keepalive = (cp, cq)
+        t = _lib.PFTables.from_buffer_copy(self.tables)
+        t.U_pred = self._pred_table[idx].data_ptr()
+        if len(self._tables_cache) > 4096:
+            self._tables_cache.clear()
+        self._tables_cache[key] = t
+        return t
+
     # ------------------------------------------------------------ reference API
     def calculate_power_flow(self, p_controllable_consumed: dict = None,
                              q_controllable_consumed: dict = None, current_time: str = None) -> None:
@@ -158,7 +210,8 @@ class OpenDSSSolver(PowerFlowSolver):
             get = lambda d, k: as_env_tensor(d[k], n, self.device, k) if (d and k in d) else zeros
             cp = torch.stack([get(p_controllable_consumed, k) for k in self._ctrl_names])
             cq = torch.stack([get(q_controllable_consumed, k) for k in self._ctrl_names])
-        _lib.check(_lib.lib().pgw_pf_solve(p, self.tables, n, _lib.dptr(cp), _lib.dptr(cq),
+        tables = self.step_tables(current_time) if cp is not None else self.tables
+        _lib.check(_lib.lib().pgw_pf_solve(p, tables, n, _lib.dptr(cp), _lib.dptr(cq),
                                            _lib.dptr(self.v_out), _lib.dptr(self._iters),
                                            _lib.stream_ptr(self.device)))
         self.iterations = self._iters

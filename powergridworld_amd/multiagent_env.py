@@ -414,7 +414,8 @@ class MultiAgentEnv(Env):
                 info.pv_pmax = float(pv.data[pv.index])
             F["info_cache"][ikey] = info
         pfp = self.pf_solver.step_params(self.time)
-        rc = _lib.lib().pgw_coord_step(F["params"], pfp, self.pf_solver.tables, info,
+        pft = self.pf_solver.step_tables(self.time)
+        rc = _lib.lib().pgw_coord_step(F["params"], pfp, pft, info,
                                        self.num_envs, bufs, _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
