@@ -166,6 +166,10 @@ def main():
                          "kernel_ms": kernel_ms,
                          "bytes_per_launch": BYTES_PER_ENV_STEP * n},
         }
+        it = env.pf_solver.iterations
+        if it is not None:
+            itf = it.double()
+            out["pf_iterations"] = {"mean": float(itf.mean()), "max": int(it.max())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(out))

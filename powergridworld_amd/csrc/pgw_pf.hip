@@ -24,42 +24,41 @@ namespace pgw {
 constexpr int kMaxOutLds = 48;   // output rows staged in LDS (IEEE-13 has 38 nodes)
 
 // ----------------------------------------------------------------------------
-// Quad layout: the 4 consecutive lanes q = lane & 3 of a quad solve ONE env.
-// Element k is owned by lane k & 3 (slot r = k >> 2): that lane holds U_k, the
-// element power and computes I_k and row k of the matvec.  Each iteration the
-// J currents are exchanged inside the quad with DPP quad_perm broadcasts, so
-// the per-env work is split four ways with no LDS traffic for per-env data:
-// 4x the waves of a one-lane-per-env solver (latency hiding at 1 wave/SIMD was
-// the bottleneck), identical arithmetic per row.
+// MFMA layout (v_mfma_f64_16x16x4f64, decoded on gfx950 by
+// tools/micro/mfma_f64_layout.hip): A lane l holds A[l%16][l/16], B lane l holds
+// B[l/16][l%16], and D lane l holds D[4r + l/16][l%16] for r = 0..3.
+//
+// A wave solves 16 envs: env = lane % 16, sub-lane q = lane / 16.  Element k
+// (padded to 16) is owned by sub-lane q = k % 4 in slot r = k / 4.  In real form
+//     [Ur; Ui] = U0 + [[Wre, -Wim], [Wim, Wre]] [Ir; Ii]      (32 x 32)
+// the B operand of k-step s is x[4s + q] -- the lane's OWN current (slot s % 4,
+// real part for s < 4, imaginary part otherwise) -- and D row 4r + q of row
+// block rb is the real (rb 0) / imaginary (rb 1) part of the lane's OWN element
+// 4r + q.  So one iteration = currents on the VALU + 16 MFMAs on the matrix
+// pipe, with no cross-lane data movement at all; W lives in 16 f64 registers
+// per lane for the whole solve.
 // ----------------------------------------------------------------------------
-template <int J>
-struct QuadDims {
-  static constexpr int R = (J + 3) / 4;   // element slots per lane
-  static constexpr int K = 4 * R;         // padded row count
-};
+typedef double pgw_double4 __attribute__((ext_vector_type(4)));
 
-template <int J>
+constexpr int kPfElem = 16;       // padded element count of the MFMA layout
+
 struct PFShared {
-  double2 W[QuadDims<J>::K * J];          // rows padded to K with zeros
-  double2 U0[QuadDims<J>::K];
-  double4 thr[QuadDims<J>::K];            // (lo^2, mn^2, mx^2, 1/vb^2) in V^2
-  double4 gsc[QuadDims<J>::K];            // (g_low, g_min, g_max, -)
-  double2 G[kMaxOutLds * J];
+  double2 U0[kPfElem];
+  double4 thr[kPfElem];            // (lo^2, mn^2, mx^2, 1/vb^2) in V^2
+  double4 gsc[kPfElem];            // (g_low, g_min, g_max, -)
+  double2 G[kMaxOutLds * kPfElem];
   double2 V0[kMaxOutLds];
   double inv_vbase_out[kMaxOutLds];
-  double2 Upred[3][QuadDims<J>::K];       // predictor solutions (if any)
+  double2 Upred[3][kPfElem];       // predictor solutions (if any)
 };
 
 // Cooperative staging of the shared PF tables (all threads of the block).
-template <int J>
-__device__ __forceinline__ void pf_stage(PFShared<J>& S, const pgw_pf_params& p,
-                                         const pgw_pf_tables& t, int n_out_lds) {
-  constexpr int K = QuadDims<J>::K;
+// Tables from the host are J x J (W), J (U0), n_out x J (G) with J <= 16.
+__device__ __forceinline__ void pf_stage(PFShared& S, const pgw_pf_params& p,
+                                         const pgw_pf_tables& t, int J, int n_out_lds) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const double2* W = reinterpret_cast<const double2*>(t.W);
-  for (int i = tid; i < K * J; i += nt) S.W[i] = (i < J * J) ? W[i] : make_double2(0.0, 0.0);
   const double2* U0 = reinterpret_cast<const double2*>(t.U0);
-  for (int i = tid; i < K; i += nt) {
+  for (int i = tid; i < kPfElem; i += nt) {
     const bool real = i < J;
     S.U0[i] = real ? U0[i] : make_double2(0.0, 0.0);
     const double vb = real ? p.vbase[i] : 1.0;
@@ -71,7 +70,10 @@ __device__ __forceinline__ void pf_stage(PFShared<J>& S, const pgw_pf_params& p,
     S.gsc[i] = make_double4(1.0 / vb2, 1.0 / (vb2 * (vmin * vmin)), 1.0 / (vb2 * (vmax * vmax)), 0.0);
   }
   const double2* G = reinterpret_cast<const double2*>(t.G);
-  for (int i = tid; i < n_out_lds * J; i += nt) S.G[i] = G[i];
+  for (int i = tid; i < n_out_lds * kPfElem; i += nt) {
+    const int o = i / kPfElem, k = i % kPfElem;
+    S.G[i] = (k < J) ? G[o * J + k] : make_double2(0.0, 0.0);
+  }
   const double2* V0 = reinterpret_cast<const double2*>(t.V0);
   for (int i = tid; i < n_out_lds; i += nt) {
     S.V0[i] = V0[i];
@@ -79,8 +81,8 @@ __device__ __forceinline__ void pf_stage(PFShared<J>& S, const pgw_pf_params& p,
   }
   if (t.U_pred) {
     const double2* Up = reinterpret_cast<const double2*>(t.U_pred);
-    for (int i = tid; i < 3 * K; i += nt) {
-      const int c = i / K, k = i % K;
+    for (int i = tid; i < 3 * kPfElem; i += nt) {
+      const int c = i / kPfElem, k = i % kPfElem;
       S.Upred[c][k] = (k < J) ? Up[c * J + k] : make_double2(0.0, 0.0);
     }
   }
@@ -96,26 +98,16 @@ __device__ __forceinline__ double fast_rcp(double m) {
   return fma(r, e, r);
 }
 
-// DPP quad_perm on a double (two 32-bit moves).  CTRL = quad_perm selector.
-template <int CTRL>
-__device__ __forceinline__ double dpp_quad(double v) {
-  unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), CTRL, 0xF, 0xF, false);
-  int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, false);
-  unsigned long long w = ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-  return __builtin_bit_cast(double, w);
-}
-template <int S>
-__device__ __forceinline__ double quad_bcast(double v) { return dpp_quad<S * 0x55>(v); }
-__device__ __forceinline__ double quad_max(double v) {
-  double o = dpp_quad<0xB1>(v);      // [1,0,3,2]
+// Reductions over the 4 sub-lanes of an env (lanes n, n+16, n+32, n+48).
+__device__ __forceinline__ double sub_max(double v) {
+  double o = __shfl_xor(v, 16);
   v = (o > v) ? o : v;
-  o = dpp_quad<0x4E>(v);             // [2,3,0,1]
+  o = __shfl_xor(v, 32);
   return (o > v) ? o : v;
 }
-__device__ __forceinline__ double quad_sum(double v) {
-  v = v + dpp_quad<0xB1>(v);
-  return v + dpp_quad<0x4E>(v);
+__device__ __forceinline__ double sub_sum(double v) {
+  v = v + __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
 }
 
 // OpenDSS Load.DoConstantPQLoad: every case is I = conj(S) U g with
@@ -133,43 +125,53 @@ __device__ __forceinline__ void pf_current(const double4& th, const double4& gs,
   ii = (sw * ui - sv * ur) * g;
 }
 
-// Per-lane state of one quad lane.
-template <int J>
+// Per-lane state: the lane's 4 owned elements k = 4r + q.
 struct PFLane {
-  static constexpr int R = QuadDims<J>::R;
-  double sw[R], sv[R];        // own element powers (W, var)
-  double ur[R], ui[R];        // own element voltages
-  double ir[R], ii[R];        // own element currents
+  double sw[4], sv[4];        // element powers (W, var)
+  double ur[4], ui[4];        // element voltages
+  double ir[4], ii[4];        // element currents
 };
 
-// All J currents of the env, gathered from the quad.
-template <int J>
-__device__ __forceinline__ void quad_gather(const PFLane<J>& L, double Ir[J], double Ii[J]) {
-  constexpr int R = QuadDims<J>::R;
+// The lane's 16 A operands: A[rb][s] = Wreal[16 rb + (l%16)][4 s + q].
+struct PFMatrix {
+  double a[2][8];
+};
+
+__device__ __forceinline__ void pf_load_matrix(const pgw_pf_tables& t, int J, int lane,
+                                               PFMatrix& Mx) {
+  const int i = lane & 15, q = lane >> 4;
+  const double2* W = reinterpret_cast<const double2*>(t.W);
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (4 * r + 0 < J) { Ir[4 * r + 0] = quad_bcast<0>(L.ir[r]); Ii[4 * r + 0] = quad_bcast<0>(L.ii[r]); }
-    if (4 * r + 1 < J) { Ir[4 * r + 1] = quad_bcast<1>(L.ir[r]); Ii[4 * r + 1] = quad_bcast<1>(L.ii[r]); }
-    if (4 * r + 2 < J) { Ir[4 * r + 2] = quad_bcast<2>(L.ir[r]); Ii[4 * r + 2] = quad_bcast<2>(L.ii[r]); }
-    if (4 * r + 3 < J) { Ir[4 * r + 3] = quad_bcast<3>(L.ir[r]); Ii[4 * r + 3] = quad_bcast<3>(L.ii[r]); }
+  for (int s = 0; s < 8; ++s) {
+    const int c = 4 * (s & 3) + q;           // element column
+    const bool imag_col = s >= 4;            // x = Ii for k-steps 4..7
+    double wre = 0.0, wim = 0.0;
+    if (i < J && c < J) {
+      const double2 w = W[i * J + c];
+      wre = w.x;
+      wim = w.y;
+    }
+    // rb 0 (real rows): Wre Ir - Wim Ii ;  rb 1 (imag rows): Wim Ir + Wre Ii
+    Mx.a[0][s] = imag_col ? -wim : wre;
+    Mx.a[1][s] = imag_col ? wre : wim;
   }
 }
 
-template <int J>
-__device__ __forceinline__ void pf_own_currents(const PFShared<J>& S, int q, PFLane<J>& L) {
+__device__ __forceinline__ void pf_own_currents(const PFShared& S, int q, PFLane& L) {
 #pragma unroll
-  for (int r = 0; r < QuadDims<J>::R; ++r) {
+  for (int r = 0; r < 4; ++r) {
     const int k = 4 * r + q;
     pf_current(S.thr[k], S.gsc[k], L.sw[r], L.sv[r], L.ur[r], L.ui[r], L.ir[r], L.ii[r]);
   }
 }
 
-// Fixed-point solve for the quad's env; every lane of the quad leaves with the
-// same iteration count and its own converged currents in L.ir / L.ii.
-template <int J>
-__device__ __forceinline__ int pf_solve(const PFShared<J>& S, const pgw_pf_params& p, int q,
-                                        PFLane<J>& L, bool pred, double pc) {
-  constexpr int R = QuadDims<J>::R;
+// Fixed-point solve for the wave's 16 envs.  Every lane of a wave stays in the
+// loop (the MFMAs need the full wave) until all 16 envs have converged; an env
+// that converged keeps its voltages (frozen), so each env's result and
+// iteration count are those of iterating it alone.
+__device__ __forceinline__ int pf_solve(const PFShared& S, const PFMatrix& Mx,
+                                        const pgw_pf_params& p, int q, bool valid, PFLane& L,
+                                        bool pred, double pc) {
   if (pred) {
     // quadratic Lagrange interpolation of the 3 reference solutions at pc
     const double x0 = p.pred_p[0], x1 = p.pred_p[1], x2 = p.pred_p[2];
@@ -177,93 +179,92 @@ __device__ __forceinline__ int pf_solve(const PFShared<J>& S, const pgw_pf_param
     const double w1 = ((pc - x0) * (pc - x2)) / ((x1 - x0) * (x1 - x2));
     const double w2 = ((pc - x0) * (pc - x1)) / ((x2 - x0) * (x2 - x1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < 4; ++r) {
       const int k = 4 * r + q;
       L.ur[r] = w0 * S.Upred[0][k].x + w1 * S.Upred[1][k].x + w2 * S.Upred[2][k].x;
       L.ui[r] = w0 * S.Upred[0][k].y + w1 * S.Upred[1][k].y + w2 * S.Upred[2][k].y;
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < 4; ++r) {
       L.ur[r] = S.U0[4 * r + q].x;
       L.ui[r] = S.U0[4 * r + q].y;
     }
   }
   const double tol2 = p.tol * p.tol;
-  int it = 0;
+  int it = 0, my_it = 0;
+  bool done = !valid;
   while (it < p.max_iter) {
     ++it;
-    // compiler-only fence: keeps the loop-invariant LDS tables from being
-    // hoisted into (and spilled out of) registers
     asm volatile("" ::: "memory");
-    pf_own_currents<J>(S, q, L);
-    double Ir[J], Ii[J];
-    quad_gather<J>(L, Ir, Ii);
+    pf_own_currents(S, q, L);
+    pgw_double4 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc0[r] = S.U0[4 * r + q].x;
+      acc1[r] = S.U0[4 * r + q].y;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const double b = (s < 4) ? L.ir[s & 3] : L.ii[s & 3];
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Mx.a[0][s], b, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Mx.a[1][s], b, acc1, 0, 0, 0);
+    }
     double err2 = 0.0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < 4; ++r) {
       const int k = 4 * r + q;
-      double ar = S.U0[k].x, ai = S.U0[k].y;
-      const double2* w = S.W + k * J;
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const double2 wk = w[j];
-        ar = fma(wk.x, Ir[j], ar);
-        ar = fma(-wk.y, Ii[j], ar);
-        ai = fma(wk.x, Ii[j], ai);
-        ai = fma(wk.y, Ir[j], ai);
-      }
-      const double dr = ar - L.ur[r], di = ai - L.ui[r];
+      const double dr = acc0[r] - L.ur[r], di = acc1[r] - L.ui[r];
       const double e2 = (dr * dr + di * di) * S.thr[k].w;
       err2 = (e2 > err2) ? e2 : err2;
-      L.ur[r] = ar;
-      L.ui[r] = ai;
+      L.ur[r] = done ? L.ur[r] : acc0[r];
+      L.ui[r] = done ? L.ui[r] : acc1[r];
     }
-    err2 = quad_max(err2);
-    if (err2 < tol2) break;
+    err2 = sub_max(err2);
+    if (!done) {
+      my_it = it;
+      done = err2 < tol2;
+    }
+    if (__ballot(!done) == 0ull) break;
   }
-  pf_own_currents<J>(S, q, L);
-  return it;
+  pf_own_currents(S, q, L);
+  return valid ? (done ? my_it : it) : 0;
 }
 
-// |V| pu of output row o: V0 + sum_k G[o][k] I_k, each lane summing its own
-// elements, then a quad sum (all four lanes return the value).
-template <int J>
-__device__ __forceinline__ double pf_node_pu(const PFShared<J>& S, const pgw_pf_tables& t, int o,
-                                             int q, const PFLane<J>& L) {
+// |V| pu of output row o: V0 + sum_k G[o][k] I_k -- each sub-lane sums its own
+// elements, then a sum over the 4 sub-lanes (every lane returns the value).
+__device__ __forceinline__ double pf_node_pu(const PFShared& S, const pgw_pf_tables& t, int J,
+                                             int o, int q, const PFLane& L) {
   double vr = 0.0, vi = 0.0;
   const bool lds = o < kMaxOutLds;
 #pragma unroll
-  for (int r = 0; r < QuadDims<J>::R; ++r) {
+  for (int r = 0; r < 4; ++r) {
     const int k = 4 * r + q;
-    if (k < J) {
-      double gx, gy;
-      if (lds) {
-        gx = S.G[o * J + k].x;
-        gy = S.G[o * J + k].y;
-      } else {
-        gx = t.G[2 * (o * J + k)];
-        gy = t.G[2 * (o * J + k) + 1];
-      }
-      vr = fma(gx, L.ir[r], vr);
-      vr = fma(-gy, L.ii[r], vr);
-      vi = fma(gx, L.ii[r], vi);
-      vi = fma(gy, L.ir[r], vi);
+    double gx = 0.0, gy = 0.0;
+    if (lds) {
+      gx = S.G[o * kPfElem + k].x;
+      gy = S.G[o * kPfElem + k].y;
+    } else if (k < J) {
+      gx = t.G[2 * (o * J + k)];
+      gy = t.G[2 * (o * J + k) + 1];
     }
+    vr = fma(gx, L.ir[r], vr);
+    vr = fma(-gy, L.ii[r], vr);
+    vi = fma(gx, L.ii[r], vi);
+    vi = fma(gy, L.ir[r], vi);
   }
-  vr = quad_sum(vr);
-  vi = quad_sum(vi);
+  vr = sub_sum(vr);
+  vi = sub_sum(vi);
   const double v0r = lds ? S.V0[o].x : t.V0[2 * o], v0i = lds ? S.V0[o].y : t.V0[2 * o + 1];
   vr = v0r + vr;
   vi = v0i + vi;
   return sqrt(vr * vr + vi * vi) * (lds ? S.inv_vbase_out[o] : t.inv_vbase_out[o]);
 }
 
-template <int J>
-__device__ __forceinline__ void pf_store_u(const pgw_pf_tables& t, int64_t e, int q,
-                                           const PFLane<J>& L) {
+__device__ __forceinline__ void pf_store_u(const pgw_pf_tables& t, int J, int64_t e, int q,
+                                           const PFLane& L) {
 #pragma unroll
-  for (int r = 0; r < QuadDims<J>::R; ++r) {
+  for (int r = 0; r < 4; ++r) {
     const int k = 4 * r + q;
     if (k < J) {
       t.U_out[2 * (e * J + k)] = L.ur[r];
@@ -273,11 +274,10 @@ __device__ __forceinline__ void pf_store_u(const pgw_pf_tables& t, int64_t e, in
 }
 
 // Own element powers (opendss.py:107-129; OpenDSS WNominal = kW*1000/nphases).
-template <int J>
-__device__ __forceinline__ void pf_element_powers(const pgw_pf_params& p, const double* cp,
-                                                  const double* cq, int q, PFLane<J>& L) {
+__device__ __forceinline__ void pf_element_powers(const pgw_pf_params& p, int J, const double* cp,
+                                                  const double* cq, int q, PFLane& L) {
 #pragma unroll
-  for (int r = 0; r < QuadDims<J>::R; ++r) {
+  for (int r = 0; r < 4; ++r) {
     const int k = 4 * r + q;
     double sw = 0.0, sv = 0.0;
     if (k < J) {
@@ -301,36 +301,43 @@ __device__ __forceinline__ void pf_element_powers(const pgw_pf_params& p, const 
   }
 }
 
-constexpr int kEnvsPerBlock = kBlock / 4;
+constexpr int kEnvsPerBlock = kBlock / 4;   // 16 envs per wave
 
-template <int J>
+__device__ __forceinline__ int64_t pf_env_index(int lane) {
+  return (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * 16 + (lane & 15);
+}
+
 __global__ void __launch_bounds__(kBlock) k_pf_solve(pgw_pf_params p, pgw_pf_tables t, int64_t n,
                                                      const double* __restrict__ ctrl_p,
                                                      const double* __restrict__ ctrl_q,
                                                      double* __restrict__ v_out,
                                                      int32_t* __restrict__ iters) {
-  __shared__ PFShared<J> S;
+  __shared__ PFShared S;
+  const int J = p.m;
   const int n_lds = p.n_out < kMaxOutLds ? p.n_out : kMaxOutLds;
-  pf_stage<J>(S, p, t, n_lds);
+  pf_stage(S, p, t, J, n_lds);
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  PFMatrix Mx;
+  pf_load_matrix(t, J, lane, Mx);
   __syncthreads();
-  const int q = threadIdx.x & 3;
-  const int64_t e = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 2);
-  if (e >= n) return;                      // whole quads exit together
+  const int64_t e = pf_env_index(lane);
+  const bool valid = e < n;
+  if (__ballot(valid) == 0ull) return;      // whole wave out of range
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
-    cp[c] = (c < p.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
-    cq[c] = (c < p.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
+    cp[c] = (valid && c < p.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
+    cq[c] = (valid && c < p.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
-  PFLane<J> L;
-  pf_element_powers<J>(p, cp, cq, q, L);
-  const int it = pf_solve<J>(S, p, q, L, t.U_pred != nullptr && p.n_ctrl == 1, cp[0]);
+  PFLane L;
+  pf_element_powers(p, J, cp, cq, q, L);
+  const int it = pf_solve(S, Mx, p, q, valid, L, t.U_pred != nullptr && p.n_ctrl == 1, cp[0]);
   for (int o = 0; o < p.n_out; ++o) {
-    const double v = pf_node_pu<J>(S, t, o, q, L);
-    if (q == 0) v_out[(int64_t)o * n + e] = v;
+    const double v = pf_node_pu(S, t, J, o, q, L);
+    if (valid && q == 0) v_out[(int64_t)o * n + e] = v;
   }
-  if (t.U_out) pf_store_u<J>(t, e, q, L);
-  if (iters && q == 0) iters[e] = it;
+  if (valid && t.U_out) pf_store_u(t, J, e, q, L);
+  if (valid && iters && q == 0) iters[e] = it;
 }
 
 // ============================================================ coordinated step
@@ -501,41 +508,47 @@ static bool coord_is_std(const pgw_coord_params& p) {
   return true;
 }
 
-// K2: one quad per env -- bus loads (multiagent_env.py:171-181), power flow
-// (opendss.py:80-135), CoordinatedMultiBuildingControlEnv.reward_transform
+// K2: 4 lanes per env (MFMA layout above) -- bus loads (multiagent_env.py:171-181),
+// power flow (opendss.py:80-135), CoordinatedMultiBuildingControlEnv.reward_transform
 // (train.py:51-63, 71-88) applied to the agent rewards in place.
-template <int J>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(pgw_coord_params p, pgw_pf_params pf,
                                                      pgw_pf_tables pft, int64_t n,
                                                      pgw_coord_buffers b) {
-  __shared__ PFShared<J> S;
+  __shared__ PFShared S;
+  const int J = pf.m;
   const int n_lds = pf.n_out < kMaxOutLds ? pf.n_out : kMaxOutLds;
-  pf_stage<J>(S, pf, pft, n_lds);
+  pf_stage(S, pf, pft, J, n_lds);
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  PFMatrix Mx;
+  pf_load_matrix(pft, J, lane, Mx);
   __syncthreads();
-  const int q = threadIdx.x & 3;
-  const int64_t e = (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 2);
-  if (e >= n) return;
+  const int64_t e = pf_env_index(lane);
+  const bool valid = e < n;
+  if (__ballot(valid) == 0ull) return;
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
     cp[c] = 0.0;
     cq[c] = 0.0;
   }
-  for (int a = 0; a < p.n_agents; ++a) {
-    const double rp = b.agent_power[(int64_t)a * n + e];
-    const int slot = p.agent_ctrl[a];
+  if (valid) {
+    for (int a = 0; a < p.n_agents; ++a) {
+      const double rp = b.agent_power[(int64_t)a * n + e];
+      const int slot = p.agent_ctrl[a];
 #pragma unroll
-    for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) cp[c] = (c == slot) ? cp[c] + rp : cp[c];
+      for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) cp[c] = (c == slot) ? cp[c] + rp : cp[c];
+    }
   }
-  PFLane<J> L;
-  pf_element_powers<J>(pf, cp, cq, q, L);
-  const int it = pf_solve<J>(S, pf, q, L, pft.U_pred != nullptr && pf.n_ctrl == 1, cp[0]);
+  PFLane L;
+  pf_element_powers(pf, J, cp, cq, q, L);
+  const int it = pf_solve(S, Mx, pf, q, valid, L, pft.U_pred != nullptr && pf.n_ctrl == 1, cp[0]);
   double vsel = 0.0;
   for (int o = 0; o < pf.n_out; ++o) {
-    const double v = pf_node_pu<J>(S, pft, o, q, L);
-    if (b.v_out && q == 0) b.v_out[(int64_t)o * n + e] = v;
+    const double v = pf_node_pu(S, pft, J, o, q, L);
+    if (valid && b.v_out && q == 0) b.v_out[(int64_t)o * n + e] = v;
     vsel = (o == p.vv_row) ? v : vsel;
   }
+  if (!valid) return;
   if (b.iters && q == 0) b.iters[e] = it;
   if (p.coordinated) {
     const double vv = pymax(pymax(0.0, p.vv_lo - vsel), vsel - p.vv_hi);
@@ -548,28 +561,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(pgw_coord_params p, pgw_pf_
   }
 }
 
-template <template <int> class K, typename... Args>
-int32_t launch_m(int m, dim3 grid, hipStream_t stream, Args... args) {
-  dim3 blk(kBlock);
-  if (m <= 4) hipLaunchKernelGGL(K<4>::fn, grid, blk, 0, stream, args...);
-  else if (m <= 8) hipLaunchKernelGGL(K<8>::fn, grid, blk, 0, stream, args...);
-  else if (m <= 12) hipLaunchKernelGGL(K<12>::fn, grid, blk, 0, stream, args...);
-  else if (m <= 14) hipLaunchKernelGGL(K<14>::fn, grid, blk, 0, stream, args...);
-  else hipLaunchKernelGGL(K<16>::fn, grid, blk, 0, stream, args...);
-  return check_launch("pgw power-flow kernel");
-}
-
-template <int M>
-struct PFKernel {
-  static constexpr auto fn = k_pf_solve<M>;
-};
-template <int M>
-struct CoordPFKernel {
-  static constexpr auto fn = k_coord_pf<M>;
-};
-
 // padded element count actually used by the device tables for a given m
-static int padded_m(int m) { return m <= 4 ? 4 : m <= 8 ? 8 : m <= 12 ? 12 : m <= 14 ? 14 : 16; }
+// (the MFMA layout pads to 16 internally; host tables are m x m, m <= 16)
+static int padded_m(int m) { return m; }
 
 }  // namespace pgw
 
@@ -584,13 +578,14 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      void* stream) {
   PGW_REQUIRE(p && t && t->W && t->U0 && v_out && n >= 0, "pgw_pf_solve: null argument");
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M && p->m == padded_m(p->m),
-              "pgw_pf_solve: m=%d must be one of 4,8,12,14,16 (pad the tables)", p->m);
+              "pgw_pf_solve: m=%d out of range", p->m);
   PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve: bad n_ctrl");
   PGW_REQUIRE(p->n_out == 0 || (t->G && t->V0 && t->inv_vbase_out), "pgw_pf_solve: missing G/V0");
   PGW_REQUIRE(p->max_iter >= 1, "pgw_pf_solve: max_iter < 1");
   if (n == 0) return PGW_OK;
-  return launch_m<PFKernel>(p->m, dim3(grid_for(4 * n)), (hipStream_t)stream, *p, *t, n, ctrl_p,
-                            ctrl_q, v_out, iters);
+  hipLaunchKernelGGL(k_pf_solve, dim3(grid_for(4 * n)), dim3(kBlock), 0, (hipStream_t)stream, *p,
+                     *t, n, ctrl_p, ctrl_q, v_out, iters);
+  return check_launch("k_pf_solve");
 }
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
@@ -628,7 +623,8 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
-  return launch_m<CoordPFKernel>(pf->m, dim3(grid_for(4 * n)), st, *p, *pf, *pft, n, b);
+  hipLaunchKernelGGL(k_coord_pf, dim3(grid_for(4 * n)), dim3(kBlock), 0, st, *p, *pf, *pft, n, b);
+  return check_launch("k_coord_pf");
 }
 
 }  // extern "C"
