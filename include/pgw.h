@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 2
+#define PGW_ABI_VERSION 3
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -232,24 +232,34 @@ typedef struct pgw_pf_params {
   double base_kw[PGW_PF_MAX_M];     /* the element's LOAD total kW this step  */
   double base_kvar[PGW_PF_MAX_M];   /*   (loadshape x base x rescale)         */
   double tol;                       /* max |dU|/vbase convergence tolerance   */
-  double pred_p[3];                 /* controllable kW of the 3 predictor solutions */
+  double pred_x0, pred_h;           /* predictor grid: kW of point j = x0 + j h */
   int32_t elem_ctrl[PGW_PF_MAX_M];  /* controllable-load slot of the element, -1 none */
-  int32_t m, n_ctrl, n_out, max_iter;
+  int32_t m;                        /* element count, = pgw_pf_padded_m(true m) */
+  int32_t n_ctrl, n_out, max_iter;
+  int32_t pred_n;                   /* predictor grid points (>= 3 to use U_pred) */
 } pgw_pf_params;
 
-/* Device tables built once by pgw_feeder_build / pgw_pf_reduce. */
+/* Device tables.  `block` is the wave-uniform operand block the solve streams
+ * through the scalar cache every iteration; build it on the host with
+ * pgw_pf_pack from W = -C Z C^T and U0 = C V0 (pgw_pf_reduce) and copy it to
+ * the device once per feeder / output-node set. */
 typedef struct pgw_pf_tables {
-  const double* W;      /* m x m complex (re,im interleaved), row-major */
-  const double* U0;     /* m complex                                    */
+  const double* block;  /* pgw_pf_pack_size(m) doubles (device)           */
   const double* G;      /* n_out x m complex: node voltage response     */
   const double* V0;     /* n_out complex: no-load node voltages         */
   const double* inv_vbase_out;  /* n_out: 1 / (kV_LN * 1000)           */
-  /* Optional initial guess (n_ctrl == 1 only): 3 x m complex element voltages
-   * solved at controllable load pred_p[0..2] for this step's base loads; each
-   * env starts from their quadratic (Lagrange) interpolant in its own
-   * controllable kW instead of from U0.  NULL = cold start from U0. */
+  /* Optional initial guess (n_ctrl == 1 only): pred_n x m complex element
+   * voltages solved at controllable load x_j = pred_x0 + j pred_h for this
+   * step's base loads; each env starts from the quadratic through the 3 grid
+   * points nearest its own controllable kW instead of from U0.  The converged
+   * result is the same fixed point (to tol); only the iteration count drops.
+   * NULL = cold start from U0. */
   const double* U_pred;
-  /* Optional output: converged element voltages, n x m complex (env-major). */
+  /* Optional per-env initial guess, n x m complex element voltages in per unit
+   * of each element's vbase (env-major); overrides U_pred.  NULL = none. */
+  const double* U_init;
+  /* Optional output: converged element voltages, n x m complex in per unit of
+   * each element's vbase (env-major). */
   double* U_out;
 } pgw_pf_tables;
 
@@ -260,6 +270,15 @@ typedef struct pgw_pf_tables {
 int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out,
                      int32_t* iters, void* stream);
+
+/* Element count the kernels are instantiated for (8, 14 or 16): pad the
+ * feeder's m load phase elements to it with inert elements (zero power). */
+int32_t pgw_pf_padded_m(int32_t m);
+/* Doubles in the packed operand block for padded element count m. */
+int64_t pgw_pf_pack_size(int32_t m);
+/* Host memory: pack W (m x m complex, row-major), U0 (m complex) and the
+ * per-element voltage bands of p into `out` (pgw_pf_pack_size(p->m) doubles). */
+int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, double* out);
 
 /* ------------------------------------------------------------------------
  * Host-side feeder construction (C++, no GPU): the native stand-in for the

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -79,14 +79,15 @@ class ReduceArgs(C.Structure):
 class PFParams(C.Structure):
     _fields_ = [("vbase", f64 * PF_MAX_M), ("vmin", f64 * PF_MAX_M), ("vmax", f64 * PF_MAX_M),
                 ("vlow", f64 * PF_MAX_M), ("nph", f64 * PF_MAX_M), ("base_kw", f64 * PF_MAX_M),
-                ("base_kvar", f64 * PF_MAX_M), ("tol", f64), ("pred_p", f64 * 3),
+                ("base_kvar", f64 * PF_MAX_M), ("tol", f64), ("pred_x0", f64), ("pred_h", f64),
                 ("elem_ctrl", i32 * PF_MAX_M),
-                ("m", i32), ("n_ctrl", i32), ("n_out", i32), ("max_iter", i32)]
+                ("m", i32), ("n_ctrl", i32), ("n_out", i32), ("max_iter", i32), ("pred_n", i32),
+                ("pad_", i32)]
 
 
 class PFTables(C.Structure):
-    _fields_ = [("W", vp), ("U0", vp), ("G", vp), ("V0", vp), ("inv_vbase_out", vp),
-                ("U_pred", vp), ("U_out", vp)]
+    _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("inv_vbase_out", vp), ("U_pred", vp),
+                ("U_init", vp), ("U_out", vp)]
 
 
 class FeederElem(C.Structure):
@@ -135,6 +136,8 @@ _SIGS = {
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_padded_m": (i32, [i32]),
+    "pgw_pf_pack_size": (i64, [i32]),
+    "pgw_pf_pack": (i32, [P(PFParams), vp, vp, vp]),
     "pgw_feeder_build": (i32, [P(FeederElem), i32, i32, vp, vp, vp, vp]),
     "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
     "pgw_coord_step": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,

@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Generate pgw_pf_dpp.inc: the DPP-broadcast asm groups of the power-flow solve.
+
+The PF kernels keep the shared operand block resident in VGPRs, 16 entries per
+register pair (entry e in lane e % 16 of every 16-lane row of pair e // 16), and
+feed each entry to its FMA with `row_newbcast:(e % 16)`.  The lane index must be
+an immediate, so every group is spelled out here per padded element count M.
+
+Hazard rule (CDNA3/4): a VALU write of a VGPR followed by a DPP read of it needs
+2 wait states, and hipcc pads nothing inside an asm string.  Each group
+therefore opens with `s_nop 1`: whatever the compiler did right before the group
+(a reload of a resident pair from an AGPR, the producer of x) is covered, and
+inside the group the sources are read-only.  Outputs written by a movs-only
+group are early-clobber so they never share a register with a source.
+
+Usage: python3 gen_pf_dpp.py > pgw_pf_dpp.inc   (run by the Makefile)
+"""
+import sys
+
+SIZES = (8, 14, 16)
+DPP = "row_mask:0xf bank_mask:0xf"
+
+
+def pairs_of(entries):
+    ps = sorted({e // 16 for e in entries})
+    return ps, {p: i for i, p in enumerate(ps)}
+
+
+def asm_stmt(lines, outs, ins):
+    body = "".join('      "%s\\n"\n' % ln for ln in ["s_nop 1"] + lines)
+    return ("  asm(\n%s      : %s\n      : %s);\n" % (body, ", ".join(outs), ", ".join(ins)))
+
+
+def block_layout(M):
+    u0re = 3 * M * M
+    return dict(u0re=u0re, u0im=u0re + M, u0sum=u0re + 2 * M, lo2=u0re + 3 * M,
+                mn2=u0re + 4 * M, mx2=u0re + 5 * M, size=u0re + 6 * M)
+
+
+def gen_column(M, k):
+    """A[i] += Wr'[i][k] ir ; B[i] += Wi'[i][k] ii ; C[i] += (Wr'+Wi')[i][k] is."""
+    ents = [(3 * k + c) * M + i for c in range(3) for i in range(M)]
+    ps, pidx = pairs_of(ents)
+    n_out = 3 * M
+    xs = n_out + len(ps)              # operand index of ir, ii, is
+    lines = []
+    for c in range(3):
+        for i in range(M):
+            e = (3 * k + c) * M + i
+            lines.append("v_fmac_f64_dpp %%%d, %%%d, %%%d row_newbcast:%d %s"
+                         % (c * M + i, n_out + pidx[e // 16], xs + c, e % 16, DPP))
+    outs = ['"+v"(A[%d])' % i for i in range(M)] + ['"+v"(B[%d])' % i for i in range(M)] + \
+           ['"+v"(C[%d])' % i for i in range(M)]
+    ins = ['"v"(w[%d])' % p for p in ps] + ['"v"(ir)', '"v"(ii)', '"v"(is)']
+    return ("template <> __device__ __forceinline__ void pf_column<%d, %d>(\n"
+            "    double (&A)[%d], double (&B)[%d], double (&C)[%d], const double (&w)[%d],\n"
+            "    double ir, double ii, double is) {\n%s}\n"
+            % (M, k, M, M, M, (block_layout(M)["size"] + 15) // 16, asm_stmt(lines, outs, ins)))
+
+
+def gen_bcast_group(name, M, groups, nr, extra_sig=""):
+    """Outputs out_j[i] = entry groups[j] + i, i < M (early-clobber movs)."""
+    ents = [g + i for g in groups for i in range(M)]
+    ps, pidx = pairs_of(ents)
+    n_out = len(groups) * M
+    lines = []
+    for j, g in enumerate(groups):
+        for i in range(M):
+            e = g + i
+            lines.append("v_mov_b64_dpp %%%d, %%%d row_newbcast:%d %s"
+                         % (j * M + i, n_out + pidx[e // 16], e % 16, DPP))
+    outs = ['"=&v"(o%d[%d])' % (j, i) for j in range(len(groups)) for i in range(M)]
+    ins = ['"v"(w[%d])' % p for p in ps]
+    args = ", ".join("double (&o%d)[%d]" % (j, M) for j in range(len(groups)))
+    return ("template <> __device__ __forceinline__ void %s<%d>(%s, const double (&w)[%d]) {\n%s}\n"
+            % (name, M, args, nr, asm_stmt(lines, outs, ins)))
+
+
+def gen_power(M, k, ns):
+    """s_r = s0r[k] + pc fr[k] ; s_i = s0i[k] + qc fi[k]  (resident s tables, ns pairs)."""
+    e_sr, e_si, e_fr, e_fi = k, M + k, 2 * M + k, 3 * M + k
+    ps, pidx = pairs_of([e_sr, e_si, e_fr, e_fi])
+    base = 2
+    op = lambda e: "%%%d" % (base + pidx[e // 16])
+    pc = "%%%d" % (base + len(ps))
+    qc = "%%%d" % (base + len(ps) + 1)
+    lines = ["v_mov_b64_dpp %%0, %s row_newbcast:%d %s" % (op(e_sr), e_sr % 16, DPP),
+             "v_fmac_f64_dpp %%0, %s, %s row_newbcast:%d %s" % (op(e_fr), pc, e_fr % 16, DPP),
+             "v_mov_b64_dpp %%1, %s row_newbcast:%d %s" % (op(e_si), e_si % 16, DPP),
+             "v_fmac_f64_dpp %%1, %s, %s row_newbcast:%d %s" % (op(e_fi), qc, e_fi % 16, DPP)]
+    outs = ['"=&v"(s_r)', '"=&v"(s_i)']
+    ins = ['"v"(s[%d])' % p for p in ps] + ['"v"(pc)', '"v"(qc)']
+    return ("template <> __device__ __forceinline__ void pf_power<%d, %d>(\n"
+            "    double& s_r, double& s_i, const double (&s)[%d], double pc, double qc) {\n%s}\n"
+            % (M, k, ns, asm_stmt(lines, outs, ins)))
+
+
+def gen_band(M, k, nr):
+    L = block_layout(M)
+    es = [L["lo2"] + k, L["mn2"] + k, L["mx2"] + k]
+    ps, pidx = pairs_of(es)
+    lines = ["v_mov_b64_dpp %%%d, %%%d row_newbcast:%d %s" % (j, 3 + pidx[e // 16], e % 16, DPP)
+             for j, e in enumerate(es)]
+    outs = ['"=&v"(lo2)', '"=&v"(mn2)', '"=&v"(mx2)']
+    ins = ['"v"(w[%d])' % p for p in ps]
+    return ("template <> __device__ __forceinline__ void pf_band<%d, %d>(\n"
+            "    double& lo2, double& mn2, double& mx2, const double (&w)[%d]) {\n%s}\n"
+            % (M, k, nr, asm_stmt(lines, outs, ins)))
+
+
+def main():
+    ns = (4 * 16 + 15) // 16          # resident s tables: 4 x PGW_PF_MAX_M entries
+    out = ["// GENERATED by gen_pf_dpp.py -- do not edit.  DPP-broadcast asm groups of",
+           "// the power-flow solve (see gen_pf_dpp.py for the layout and hazard rule).",
+           "template <int M, int K> __device__ __forceinline__ void pf_column(",
+           "    double (&A)[M], double (&B)[M], double (&C)[M], const double (&w)[PFBlock<M>::kPairs],",
+           "    double ir, double ii, double is);",
+           "template <int M> __device__ __forceinline__ void pf_acc_init(",
+           "    double (&o0)[M], double (&o1)[M], const double (&w)[PFBlock<M>::kPairs]);",
+           "template <int M> __device__ __forceinline__ void pf_u0(",
+           "    double (&o0)[M], double (&o1)[M], const double (&w)[PFBlock<M>::kPairs]);",
+           "template <int M, int K> __device__ __forceinline__ void pf_power(",
+           "    double& s_r, double& s_i, const double (&s)[kSPairs], double pc, double qc);",
+           "template <int M, int K> __device__ __forceinline__ void pf_band(",
+           "    double& lo2, double& mn2, double& mx2, const double (&w)[PFBlock<M>::kPairs]);",
+           ""]
+    for M in SIZES:
+        L = block_layout(M)
+        nr = (L["size"] + 15) // 16
+        out.append("// ---- M = %d (%d resident pairs)" % (M, nr))
+        out.append(gen_bcast_group("pf_acc_init", M, [L["u0re"], L["u0sum"]], nr))
+        out.append(gen_bcast_group("pf_u0", M, [L["u0re"], L["u0im"]], nr))
+        for k in range(M):
+            out.append(gen_column(M, k))
+            out.append(gen_power(M, k, ns))
+            out.append(gen_band(M, k, nr))
+    sys.stdout.write("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -4,89 +4,75 @@
 // fixed-point current injection on the m load-element voltages
 //     U <- U0 + W f(U),   f = OpenDSS PQ-load current law (model 1),
 // with W = -C Z C^T, U0 = C V0 precomputed on the host (pgw_feeder.cpp) and
-// shared by every env.  One thread per env keeps its U, I and element powers
-// in registers; everything shared (W, U0, the output rows of G, per-element
-// thresholds) is staged ONCE per workgroup in LDS and read as wave-uniform
-// broadcasts, so the inner loop is fp64 FMAs + broadcast ds_reads.
+// shared by every env.  The kernels iterate in per unit of each element's base
+// voltage (u = U / vb, W'_ik = W_ik / vb_i, s_k = conj(S_k) / vb_k): the band
+// limits and the convergence test then need no per-element scale.
+//
+// Layout: ONE LANE PER ENV, everything in registers.  The lane keeps its m
+// element voltages; the operands shared by all envs -- W' (as the three real
+// matrices of the 3-multiply complex product: Re = Wr Ir - Wi Ii, Im = (Wr+Wi)
+// (Ir+Ii) - Wr Ir - Wi Ii), u0 and the element powers -- stay RESIDENT in VGPRs
+// for the whole solve, 16 entries per register pair (entry e in lane e % 16 of
+// each 16-lane row of pair e / 16), and reach the FMA through a DPP broadcast
+// operand: v_fmac_f64_dpp acc, w, x row_newbcast:(e % 16).  So one iteration is
+// ~1000 fp64 VALU instructions per 64 envs with no memory or scalar traffic
+// (588 FMAs of the matvec).  Lanes whose env has converged leave the loop (exec
+// mask), so each env's result and iteration count are those of iterating it
+// alone.  On MI355X fp64 MFMA has the same peak as the fp64 VALU and does not
+// co-issue with it (measured, profiles/r01/), so the matrix cores gain nothing.
 //
 // Coordinated step (the BASELINE C4 path) = two launches on one stream:
 //   k_coord_agents  one thread per (env, agent): building + PV + storage step,
 //                   obs/state writes, agent real power and (pre-transform) reward
 //                   -- pure HBM streaming, 5x the waves of a per-env kernel;
-//   k_coord_pf      one thread per env: bus loads = sum of agent powers, power
+//   k_coord_pf      one lane per env: bus loads = sum of agent powers, power
 //                   flow, voltage-violation penalty folded into the rewards.
 #include <algorithm>
+#include <cmath>
+#include <type_traits>
 
 #include "pgw_common.h"
 
 namespace pgw {
 
-constexpr int kMaxOutLds = 48;   // output rows staged in LDS (IEEE-13 has 38 nodes)
-
-// ----------------------------------------------------------------------------
-// MFMA layout (v_mfma_f64_16x16x4f64, decoded on gfx950 by
-// tools/micro/mfma_f64_layout.hip): A lane l holds A[l%16][l/16], B lane l holds
-// B[l/16][l%16], and D lane l holds D[4r + l/16][l%16] for r = 0..3.
-//
-// A wave solves 16 envs: env = lane % 16, sub-lane q = lane / 16.  Element k
-// (padded to 16) is owned by sub-lane q = k % 4 in slot r = k / 4.  In real form
-//     [Ur; Ui] = U0 + [[Wre, -Wim], [Wim, Wre]] [Ir; Ii]      (32 x 32)
-// the B operand of k-step s is x[4s + q] -- the lane's OWN current (slot s % 4,
-// real part for s < 4, imaginary part otherwise) -- and D row 4r + q of row
-// block rb is the real (rb 0) / imaginary (rb 1) part of the lane's OWN element
-// 4r + q.  So one iteration = currents on the VALU + 16 MFMAs on the matrix
-// pipe, with no cross-lane data movement at all; W lives in 16 f64 registers
-// per lane for the whole solve.
-// ----------------------------------------------------------------------------
-typedef double pgw_double4 __attribute__((ext_vector_type(4)));
-
-constexpr int kPfElem = 16;       // padded element count of the MFMA layout
-
-struct PFShared {
-  double2 U0[kPfElem];
-  double4 thr[kPfElem];            // (lo^2, mn^2, mx^2, 1/vb^2) in V^2
-  double4 gsc[kPfElem];            // (g_low, g_min, g_max, -)
-  double2 G[kMaxOutLds * kPfElem];
-  double2 V0[kMaxOutLds];
-  double inv_vbase_out[kMaxOutLds];
-  double2 Upred[3][kPfElem];       // predictor solutions (if any)
-};
-
-// Cooperative staging of the shared PF tables (all threads of the block).
-// Tables from the host are J x J (W), J (U0), n_out x J (G) with J <= 16.
-__device__ __forceinline__ void pf_stage(PFShared& S, const pgw_pf_params& p,
-                                         const pgw_pf_tables& t, int J, int n_out_lds) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const double2* U0 = reinterpret_cast<const double2*>(t.U0);
-  for (int i = tid; i < kPfElem; i += nt) {
-    const bool real = i < J;
-    S.U0[i] = real ? U0[i] : make_double2(0.0, 0.0);
-    const double vb = real ? p.vbase[i] : 1.0;
-    const double vmin = real ? p.vmin[i] : 0.95, vmax = real ? p.vmax[i] : 1.05;
-    const double vlow = real ? p.vlow[i] : 0.5;
-    const double vb2 = vb * vb;
-    const double lo = vlow * vb, mn = vmin * vb, mx = vmax * vb;
-    S.thr[i] = make_double4(lo * lo, mn * mn, mx * mx, 1.0 / vb2);
-    S.gsc[i] = make_double4(1.0 / vb2, 1.0 / (vb2 * (vmin * vmin)), 1.0 / (vb2 * (vmax * vmax)), 0.0);
-  }
-  const double2* G = reinterpret_cast<const double2*>(t.G);
-  for (int i = tid; i < n_out_lds * kPfElem; i += nt) {
-    const int o = i / kPfElem, k = i % kPfElem;
-    S.G[i] = (k < J) ? G[o * J + k] : make_double2(0.0, 0.0);
-  }
-  const double2* V0 = reinterpret_cast<const double2*>(t.V0);
-  for (int i = tid; i < n_out_lds; i += nt) {
-    S.V0[i] = V0[i];
-    S.inv_vbase_out[i] = t.inv_vbase_out[i];
-  }
-  if (t.U_pred) {
-    const double2* Up = reinterpret_cast<const double2*>(t.U_pred);
-    for (int i = tid; i < 3 * kPfElem; i += nt) {
-      const int c = i / kPfElem, k = i % kPfElem;
-      S.Upred[c][k] = (k < J) ? Up[c * J + k] : make_double2(0.0, 0.0);
-    }
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
   }
 }
+
+// ---- resident operand block ------------------------------------------------
+// Packed block (pgw_pf_pack, doubles), M = padded element count:
+//   [0, 3M^2)   entry (3k + c) M + i: c = 0 Re W'[i][k], 1 Im W'[i][k], 2 their sum
+//   [3M^2, +3M) u0re[i], u0im[i], u0re[i] + u0im[i]
+//   [.., +3M)   vlow^2, vmin^2, vmax^2 per element (pu^2)
+template <int M> struct PFBlock {
+  static constexpr int kU0re = 3 * M * M, kU0im = kU0re + M, kU0sum = kU0im + M;
+  static constexpr int kLo2 = kU0sum + M, kMn2 = kLo2 + M, kMx2 = kMn2 + M;
+  static constexpr int kSize = kMx2 + M;
+  static constexpr int kPairs = (kSize + 15) / 16;
+};
+static int64_t pf_block_size(int m) { return 3LL * m * m + 6LL * m; }
+
+// Per-launch scalars derived on the host from pgw_pf_params (pu).
+struct PFArgs {
+  double sr0[PGW_PF_MAX_M], si0[PGW_PF_MAX_M];   // s0 = conj(S_base) / vb per phase
+  double fr[PGW_PF_MAX_M], fi[PGW_PF_MAX_M];     // d s / d (ctrl kW, kvar): slot-0 elements
+  double kw[PGW_PF_MAX_M], kvar[PGW_PF_MAX_M], nph[PGW_PF_MAX_M], vb[PGW_PF_MAX_M];
+  int32_t ctrl[PGW_PF_MAX_M];
+  double lo2, mn2, mx2;                          // band limits when uniform (pu^2)
+  double tol2;
+  double pred_x0, pred_inv_h;
+  int32_t pred_n, use_pred, max_iter, n_ctrl, n_out;
+};
+constexpr int kSPairs = (4 * PGW_PF_MAX_M + 15) / 16;   // resident s0 / f entries
+
+// The DPP-broadcast groups (generated: gen_pf_dpp.py).  Entry e of a resident
+// table lives in lane e % 16 of every 16-lane row of register pair e / 16 and is
+// fed to its instruction with row_newbcast:(e % 16).
+#include "pgw_pf_dpp.inc"
 
 __device__ __forceinline__ double fast_rcp(double m) {
   // v_rcp_f64 + two Newton steps (~1 ulp; the exact IEEE divide sequence costs
@@ -98,246 +84,216 @@ __device__ __forceinline__ double fast_rcp(double m) {
   return fma(r, e, r);
 }
 
-// Reductions over the 4 sub-lanes of an env (lanes n, n+16, n+32, n+48).
-__device__ __forceinline__ double sub_max(double v) {
-  double o = __shfl_xor(v, 16);
-  v = (o > v) ? o : v;
-  o = __shfl_xor(v, 32);
-  return (o > v) ? o : v;
-}
-__device__ __forceinline__ double sub_sum(double v) {
-  v = v + __shfl_xor(v, 16);
-  return v + __shfl_xor(v, 32);
-}
+// Per-lane solver state.  UB: every element has the same (vlow, vmin, vmax);
+// GC: more than one controllable slot (per-lane s for every element).
+template <int M, bool UB, bool GC> struct PFSolver {
+  using Lo = PFBlock<M>;
+  static constexpr int NR = Lo::kPairs;
+  double w[NR];            // resident block
+  double sres[kSPairs];    // resident s0r, s0i, fr, fi (entry k, M+k, 2M+k, 3M+k)
+  double ur[M], ui[M];     // element voltages (pu)
+  double sr[GC ? M : 1], si[GC ? M : 1];
+  double pc, qc;           // slot-0 controllable kW / kvar of the env
+  double lo2, mn2, mx2, tol2;
 
-// OpenDSS Load.DoConstantPQLoad: every case is I = conj(S) U g with
-//   g = 1/|U|^2 (constant PQ, vmin < |U|/vb <= vmax) or the constant-Z scale
-//   1/(vb vmin)^2 (below vmin), 1/(vb vmax)^2 (above vmax), 1/vb^2 (below vlow).
-__device__ __forceinline__ void pf_current(const double4& th, const double4& gs, double sw,
-                                           double sv, double ur, double ui, double& ir,
-                                           double& ii) {
-  const double m2 = ur * ur + ui * ui;
-  double g = fast_rcp(m2);
-  g = (m2 > th.z) ? gs.z : g;
-  g = (m2 <= th.y) ? gs.y : g;
-  g = (m2 <= th.x) ? gs.x : g;
-  ir = (sw * ur + sv * ui) * g;
-  ii = (sw * ui - sv * ur) * g;
-}
-
-// Per-lane state: the lane's 4 owned elements k = 4r + q.
-struct PFLane {
-  double sw[4], sv[4];        // element powers (W, var)
-  double ur[4], ui[4];        // element voltages
-  double ir[4], ii[4];        // element currents
-};
-
-// The lane's 16 A operands: A[rb][s] = Wreal[16 rb + (l%16)][4 s + q].
-struct PFMatrix {
-  double a[2][8];
-};
-
-__device__ __forceinline__ void pf_load_matrix(const pgw_pf_tables& t, int J, int lane,
-                                               PFMatrix& Mx) {
-  const int i = lane & 15, q = lane >> 4;
-  const double2* W = reinterpret_cast<const double2*>(t.W);
+  __device__ __forceinline__ void load(const PFArgs& a, const double* block) {
+    const int l = threadIdx.x & 15;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int c = 4 * (s & 3) + q;           // element column
-    const bool imag_col = s >= 4;            // x = Ii for k-steps 4..7
-    double wre = 0.0, wim = 0.0;
-    if (i < J && c < J) {
-      const double2 w = W[i * J + c];
-      wre = w.x;
-      wim = w.y;
+    for (int j = 0; j < NR; ++j) {
+      const int e = 16 * j + l;
+      w[j] = e < Lo::kSize ? block[e] : 0.0;
     }
-    // rb 0 (real rows): Wre Ir - Wim Ii ;  rb 1 (imag rows): Wim Ir + Wre Ii
-    Mx.a[0][s] = imag_col ? -wim : wre;
-    Mx.a[1][s] = imag_col ? wre : wim;
+#pragma unroll
+    for (int j = 0; j < kSPairs; ++j) {
+      const int e = 16 * j + l;              // 4 tables of M entries
+      const int t = e / M, k = e - t * M;
+      const double* src = t == 0 ? a.sr0 : t == 1 ? a.si0 : t == 2 ? a.fr : a.fi;
+      sres[j] = t < 4 ? src[k] : 0.0;
+    }
+    lo2 = a.lo2;
+    mn2 = a.mn2;
+    mx2 = a.mx2;
+    tol2 = a.tol2;
   }
-}
 
-__device__ __forceinline__ void pf_own_currents(const PFShared& S, int q, PFLane& L) {
+  // element powers of the env (opendss.py:107-129; OpenDSS WNominal = kW*1000/nphases)
+  __device__ __forceinline__ void powers(const PFArgs& a, const double* cp, const double* cq) {
+    pc = cp[0];
+    qc = cq[0];
+    if constexpr (GC) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = 4 * r + q;
-    pf_current(S.thr[k], S.gsc[k], L.sw[r], L.sv[r], L.ur[r], L.ui[r], L.ir[r], L.ii[r]);
-  }
-}
-
-// Fixed-point solve for the wave's 16 envs.  Every lane of a wave stays in the
-// loop (the MFMAs need the full wave) until all 16 envs have converged; an env
-// that converged keeps its voltages (frozen), so each env's result and
-// iteration count are those of iterating it alone.
-__device__ __forceinline__ int pf_solve(const PFShared& S, const PFMatrix& Mx,
-                                        const pgw_pf_params& p, int q, bool valid, PFLane& L,
-                                        bool pred, double pc) {
-  if (pred) {
-    // quadratic Lagrange interpolation of the 3 reference solutions at pc
-    const double x0 = p.pred_p[0], x1 = p.pred_p[1], x2 = p.pred_p[2];
-    const double w0 = ((pc - x1) * (pc - x2)) / ((x0 - x1) * (x0 - x2));
-    const double w1 = ((pc - x0) * (pc - x2)) / ((x1 - x0) * (x1 - x2));
-    const double w2 = ((pc - x0) * (pc - x1)) / ((x2 - x0) * (x2 - x1));
+      for (int k = 0; k < M; ++k) {
+        const int c = a.ctrl[k];
+        double p = 0.0, q = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = 4 * r + q;
-      L.ur[r] = w0 * S.Upred[0][k].x + w1 * S.Upred[1][k].x + w2 * S.Upred[2][k].x;
-      L.ui[r] = w0 * S.Upred[0][k].y + w1 * S.Upred[1][k].y + w2 * S.Upred[2][k].y;
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      L.ur[r] = S.U0[4 * r + q].x;
-      L.ui[r] = S.U0[4 * r + q].y;
-    }
-  }
-  const double tol2 = p.tol * p.tol;
-  int it = 0, my_it = 0;
-  bool done = !valid;
-  while (it < p.max_iter) {
-    ++it;
-    asm volatile("" ::: "memory");
-    pf_own_currents(S, q, L);
-    pgw_double4 acc0, acc1;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      acc0[r] = S.U0[4 * r + q].x;
-      acc1[r] = S.U0[4 * r + q].y;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const double b = (s < 4) ? L.ir[s & 3] : L.ii[s & 3];
-      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Mx.a[0][s], b, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Mx.a[1][s], b, acc1, 0, 0, 0);
-    }
-    double err2 = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = 4 * r + q;
-      const double dr = acc0[r] - L.ur[r], di = acc1[r] - L.ui[r];
-      const double e2 = (dr * dr + di * di) * S.thr[k].w;
-      err2 = (e2 > err2) ? e2 : err2;
-      L.ur[r] = done ? L.ur[r] : acc0[r];
-      L.ui[r] = done ? L.ui[r] : acc1[r];
-    }
-    err2 = sub_max(err2);
-    if (!done) {
-      my_it = it;
-      done = err2 < tol2;
-    }
-    if (__ballot(!done) == 0ull) break;
-  }
-  pf_own_currents(S, q, L);
-  return valid ? (done ? my_it : it) : 0;
-}
-
-// |V| pu of output row o: V0 + sum_k G[o][k] I_k -- each sub-lane sums its own
-// elements, then a sum over the 4 sub-lanes (every lane returns the value).
-__device__ __forceinline__ double pf_node_pu(const PFShared& S, const pgw_pf_tables& t, int J,
-                                             int o, int q, const PFLane& L) {
-  double vr = 0.0, vi = 0.0;
-  const bool lds = o < kMaxOutLds;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = 4 * r + q;
-    double gx = 0.0, gy = 0.0;
-    if (lds) {
-      gx = S.G[o * kPfElem + k].x;
-      gy = S.G[o * kPfElem + k].y;
-    } else if (k < J) {
-      gx = t.G[2 * (o * J + k)];
-      gy = t.G[2 * (o * J + k) + 1];
-    }
-    vr = fma(gx, L.ir[r], vr);
-    vr = fma(-gy, L.ii[r], vr);
-    vi = fma(gx, L.ii[r], vi);
-    vi = fma(gy, L.ir[r], vi);
-  }
-  vr = sub_sum(vr);
-  vi = sub_sum(vi);
-  const double v0r = lds ? S.V0[o].x : t.V0[2 * o], v0i = lds ? S.V0[o].y : t.V0[2 * o + 1];
-  vr = v0r + vr;
-  vi = v0i + vi;
-  return sqrt(vr * vr + vi * vi) * (lds ? S.inv_vbase_out[o] : t.inv_vbase_out[o]);
-}
-
-__device__ __forceinline__ void pf_store_u(const pgw_pf_tables& t, int J, int64_t e, int q,
-                                           const PFLane& L) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = 4 * r + q;
-    if (k < J) {
-      t.U_out[2 * (e * J + k)] = L.ur[r];
-      t.U_out[2 * (e * J + k) + 1] = L.ui[r];
-    }
-  }
-}
-
-// Own element powers (opendss.py:107-129; OpenDSS WNominal = kW*1000/nphases).
-__device__ __forceinline__ void pf_element_powers(const pgw_pf_params& p, int J, const double* cp,
-                                                  const double* cq, int q, PFLane& L) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = 4 * r + q;
-    double sw = 0.0, sv = 0.0;
-    if (k < J) {
-      double kw = p.base_kw[k], kvar = p.base_kvar[k];
-      const int c = p.elem_ctrl[k];
-      if (c >= 0) {
-        double pc = cp[0], qc = cq[0];
-#pragma unroll
-        for (int s = 1; s < PGW_PF_MAX_CTRL; ++s) {
-          pc = (c == s) ? cp[s] : pc;
-          qc = (c == s) ? cq[s] : qc;
+        for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
+          p = (c == s) ? cp[s] : p;
+          q = (c == s) ? cq[s] : q;
         }
-        kw = kw + pc;
-        kvar = kvar + qc;
+        const double sw = ((a.kw[k] + p) * 1000.0) / a.nph[k];
+        const double sv = ((a.kvar[k] + q) * 1000.0) / a.nph[k];
+        sr[k] = sw / a.vb[k];
+        si[k] = -sv / a.vb[k];
       }
-      sw = (kw * 1000.0) / p.nph[k];
-      sv = (kvar * 1000.0) / p.nph[k];
     }
-    L.sw[r] = sw;
-    L.sv[r] = sv;
   }
+
+  // OpenDSS Load.DoConstantPQLoad (model 1), in pu: I = s u g with
+  //   g = 1/|u|^2 for vmin < |u| <= vmax, the constant-Z scales 1/vmin^2 below
+  //   vmin and 1/vmax^2 above vmax -- i.e. 1/clamp(|u|^2, vmin^2, vmax^2), exact
+  //   at both band edges -- and 1 at or below vlow.  I comes out in amperes.
+  template <int K>
+  __device__ __forceinline__ void current(double& ir, double& ii) const {
+    double s_r, s_i;
+    if constexpr (GC) {
+      s_r = sr[K];
+      s_i = si[K];
+    } else {
+      pf_power<M, K>(s_r, s_i, sres, pc, qc);
+    }
+    double vlo2, vmn2, vmx2;
+    if constexpr (UB) {
+      vlo2 = lo2;
+      vmn2 = mn2;
+      vmx2 = mx2;
+    } else {
+      pf_band<M, K>(vlo2, vmn2, vmx2, w);
+    }
+    const double m2 = fma(ui[K], ui[K], ur[K] * ur[K]);
+    double mc = fmin(fmax(m2, vmn2), vmx2);
+    mc = (m2 <= vlo2) ? 1.0 : mc;
+    const double g = fast_rcp(mc);
+    const double gr = g * ur[K], gi = g * ui[K];
+    ir = fma(s_r, gr, -(s_i * gi));
+    ii = fma(s_r, gi, s_i * gr);
+  }
+
+  // Initial guess: quadratic through the 3 predictor grid points nearest pc, or u0.
+  __device__ __forceinline__ void initial(const PFArgs& a, const pgw_pf_tables& t, int64_t e,
+                                          bool valid) {
+    const double* U_pred = t.U_pred;
+    if (t.U_init) {
+      const double2* P = reinterpret_cast<const double2*>(t.U_init) + (valid ? e : 0) * M;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const double2 v = P[k];
+        ur[k] = v.x;
+        ui[k] = v.y;
+      }
+    } else if (a.use_pred) {
+      const double u = (pc - a.pred_x0) * a.pred_inv_h;
+      double sj = rint(u);
+      sj = fmin(fmax(sj, 1.0), (double)(a.pred_n - 2));
+      const double t = u - sj;
+      const double wm = 0.5 * t * (t - 1.0), w0 = 1.0 - t * t, wp = 0.5 * t * (t + 1.0);
+      const double2* P = reinterpret_cast<const double2*>(U_pred) + ((int)sj - 1) * M;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const double2 pm = P[k], p0 = P[M + k], pp = P[2 * M + k];
+        ur[k] = fma(wp, pp.x, fma(w0, p0.x, wm * pm.x));
+        ui[k] = fma(wp, pp.y, fma(w0, p0.y, wm * pm.y));
+      }
+    } else {
+      pf_u0<M>(ur, ui, w);
+    }
+  }
+
+  // Fixed-point iteration until max_k |du_k|^2 < tol^2 or max_iter.  The loop
+  // is wave-uniform with the exec mask FULL: a lane disabled in EXEC is an
+  // invalid DPP source, and every lane holds resident entries the others
+  // broadcast from.  An env that has converged (or a lane past n) keeps its
+  // voltages by select, so each env's result and iteration count are those of
+  // iterating it alone.
+  __device__ __forceinline__ int iterate(int max_iter, bool valid) {
+    int it = 0, my_it = 0;
+    bool done = !valid;
+    while (true) {
+      double A[M], Bs[M], C[M];
+      pf_acc_init<M>(A, C, w);
+#pragma unroll
+      for (int i = 0; i < M; ++i) Bs[i] = 0.0;
+      static_for<0, M>([&](auto k) {
+        double ir, ii;
+        current<k>(ir, ii);
+        const double is = ir + ii;
+        pf_column<M, k>(A, Bs, C, w, ir, ii, is);
+      });
+      bool conv = true;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const double nr = A[i] - Bs[i];
+        const double ni = (C[i] - A[i]) - Bs[i];
+        const double dr = nr - ur[i], di = ni - ui[i];
+        conv &= fma(dr, dr, di * di) < tol2;
+        ur[i] = done ? ur[i] : nr;
+        ui[i] = done ? ui[i] : ni;
+      }
+      ++it;
+      my_it = done ? my_it : it;
+      done = done || conv || it >= max_iter;
+      if (__ballot(!done) == 0ull) break;
+    }
+    return my_it;
+  }
+
+  __device__ __forceinline__ void currents(double* ir, double* ii) const {
+    static_for<0, M>([&](auto k) { current<k>(ir[k], ii[k]); });
+  }
+};
+
+// |V| pu of output node o: V0 + sum_k G[o][k] I_k (wave-uniform G, V0 rows
+// through the scalar cache).
+typedef const __attribute__((address_space(4))) double* sdptr;
+__device__ __forceinline__ sdptr scalar_ptr(const double* p) { return (sdptr)p; }
+
+template <int M>
+__device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, const double* ir,
+                                             const double* ii) {
+  const sdptr G = scalar_ptr(t.G) + 2 * M * o;
+  double vr = scalar_ptr(t.V0)[2 * o], vi = scalar_ptr(t.V0)[2 * o + 1];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double gr = G[2 * k], gi = G[2 * k + 1];
+    vr = fma(gr, ir[k], vr);
+    vr = fma(-gi, ii[k], vr);
+    vi = fma(gr, ii[k], vi);
+    vi = fma(gi, ir[k], vi);
+  }
+  return sqrt(fma(vi, vi, vr * vr)) * scalar_ptr(t.inv_vbase_out)[o];
 }
 
-constexpr int kEnvsPerBlock = kBlock / 4;   // 16 envs per wave
-
-__device__ __forceinline__ int64_t pf_env_index(int lane) {
-  return (int64_t)blockIdx.x * kEnvsPerBlock + (threadIdx.x >> 6) * 16 + (lane & 15);
-}
-
-__global__ void __launch_bounds__(kBlock) k_pf_solve(pgw_pf_params p, pgw_pf_tables t, int64_t n,
+template <int M, bool UB, bool GC>
+__global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, int64_t n,
                                                      const double* __restrict__ ctrl_p,
                                                      const double* __restrict__ ctrl_q,
                                                      double* __restrict__ v_out,
                                                      int32_t* __restrict__ iters) {
-  __shared__ PFShared S;
-  const int J = p.m;
-  const int n_lds = p.n_out < kMaxOutLds ? p.n_out : kMaxOutLds;
-  pf_stage(S, p, t, J, n_lds);
-  const int lane = threadIdx.x & 63, q = lane >> 4;
-  PFMatrix Mx;
-  pf_load_matrix(t, J, lane, Mx);
-  __syncthreads();
-  const int64_t e = pf_env_index(lane);
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
-  if (__ballot(valid) == 0ull) return;      // whole wave out of range
+  // every lane stays to the end of the solve: the DPP broadcasts read all lanes
+  PFSolver<M, UB, GC> S;
+  S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
-    cp[c] = (valid && c < p.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
-    cq[c] = (valid && c < p.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
+    cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
+    cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
-  PFLane L;
-  pf_element_powers(p, J, cp, cq, q, L);
-  const int it = pf_solve(S, Mx, p, q, valid, L, t.U_pred != nullptr && p.n_ctrl == 1, cp[0]);
-  for (int o = 0; o < p.n_out; ++o) {
-    const double v = pf_node_pu(S, t, J, o, q, L);
-    if (valid && q == 0) v_out[(int64_t)o * n + e] = v;
+  S.powers(a, cp, cq);
+  S.initial(a, t, e, valid);
+  const int it = S.iterate(a.max_iter, valid);
+  double ir[M], ii[M];
+  S.currents(ir, ii);
+  if (!valid) return;
+  for (int o = 0; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
+  if (t.U_out) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      t.U_out[2 * (e * M + k)] = S.ur[k];
+      t.U_out[2 * (e * M + k) + 1] = S.ui[k];
+    }
   }
-  if (valid && t.U_out) pf_store_u(t, J, e, q, L);
-  if (valid && iters && q == 0) iters[e] = it;
+  if (iters) iters[e] = it;
 }
 
 // ============================================================ coordinated step
@@ -508,62 +464,132 @@ static bool coord_is_std(const pgw_coord_params& p) {
   return true;
 }
 
-// K2: 4 lanes per env (MFMA layout above) -- bus loads (multiagent_env.py:171-181),
-// power flow (opendss.py:80-135), CoordinatedMultiBuildingControlEnv.reward_transform
+// K2: one lane per env -- bus loads (multiagent_env.py:171-181), power flow
+// (opendss.py:80-135), CoordinatedMultiBuildingControlEnv.reward_transform
 // (train.py:51-63, 71-88) applied to the agent rewards in place.
-__global__ void __launch_bounds__(kBlock) k_coord_pf(pgw_coord_params p, pgw_pf_params pf,
-                                                     pgw_pf_tables pft, int64_t n,
-                                                     pgw_coord_buffers b) {
-  __shared__ PFShared S;
-  const int J = pf.m;
-  const int n_lds = pf.n_out < kMaxOutLds ? pf.n_out : kMaxOutLds;
-  pf_stage(S, pf, pft, J, n_lds);
-  const int lane = threadIdx.x & 63, q = lane >> 4;
-  PFMatrix Mx;
-  pf_load_matrix(pft, J, lane, Mx);
-  __syncthreads();
-  const int64_t e = pf_env_index(lane);
+struct CoordPFArgs {
+  int32_t n_agents, coordinated, vv_row;
+  int32_t agent_ctrl[PGW_MAX_AGENTS];
+  double vv_lo, vv_hi, vv_penalty;
+};
+
+template <int M, bool UB, bool GC>
+__global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
+                                                     int64_t n, pgw_coord_buffers b) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
-  if (__ballot(valid) == 0ull) return;
+  // every lane stays to the end of the solve: the DPP broadcasts read all lanes
+  PFSolver<M, UB, GC> S;
+  S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
-  for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
-    cp[c] = 0.0;
-    cq[c] = 0.0;
+  for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
+    cp[s] = 0.0;
+    cq[s] = 0.0;
   }
   if (valid) {
-    for (int a = 0; a < p.n_agents; ++a) {
-      const double rp = b.agent_power[(int64_t)a * n + e];
-      const int slot = p.agent_ctrl[a];
+    for (int ag = 0; ag < c.n_agents; ++ag) {
+      const double rp = b.agent_power[(int64_t)ag * n + e];
+      const int slot = c.agent_ctrl[ag];
 #pragma unroll
-      for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) cp[c] = (c == slot) ? cp[c] + rp : cp[c];
+      for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp : cp[s];
     }
   }
-  PFLane L;
-  pf_element_powers(pf, J, cp, cq, q, L);
-  const int it = pf_solve(S, Mx, pf, q, valid, L, pft.U_pred != nullptr && pf.n_ctrl == 1, cp[0]);
-  double vsel = 0.0;
-  for (int o = 0; o < pf.n_out; ++o) {
-    const double v = pf_node_pu(S, pft, J, o, q, L);
-    if (valid && b.v_out && q == 0) b.v_out[(int64_t)o * n + e] = v;
-    vsel = (o == p.vv_row) ? v : vsel;
-  }
+  S.powers(a, cp, cq);
+  S.initial(a, t, e, valid);
+  const int it = S.iterate(a.max_iter, valid);
+  double ir[M], ii[M];
+  S.currents(ir, ii);
   if (!valid) return;
-  if (b.iters && q == 0) b.iters[e] = it;
-  if (p.coordinated) {
-    const double vv = pymax(pymax(0.0, p.vv_lo - vsel), vsel - p.vv_hi);
-    if (b.vv && q == 0) b.vv[e] = vv;
-    const double share = (vv * p.vv_penalty) / (double)p.n_agents;
-    for (int a = q; a < p.n_agents; a += 4) {
-      double* r = b.reward + (int64_t)a * n + e;
+  double vsel = 0.0;
+  for (int o = 0; o < a.n_out; ++o) {
+    const double v = pf_node_pu<M>(t, o, ir, ii);
+    if (b.v_out) b.v_out[(int64_t)o * n + e] = v;
+    vsel = (o == c.vv_row) ? v : vsel;
+  }
+  if (b.iters) b.iters[e] = it;
+  if (c.coordinated) {
+    const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
+    if (b.vv) b.vv[e] = vv;
+    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
+    for (int ag = 0; ag < c.n_agents; ++ag) {
+      double* r = b.reward + (int64_t)ag * n + e;
       *r = *r - share;
     }
   }
 }
 
-// padded element count actually used by the device tables for a given m
-// (the MFMA layout pads to 16 internally; host tables are m x m, m <= 16)
-static int padded_m(int m) { return m; }
+// Kernel instantiations: the element count is a template parameter so the
+// matvec is fully unrolled with compile-time block offsets.
+static int padded_m(int m) { return m <= 8 ? 8 : (m <= 14 ? 14 : 16); }
+
+static bool uniform_band(const pgw_pf_params& p) {
+  for (int k = 1; k < p.m; ++k)
+    if (p.vlow[k] != p.vlow[0] || p.vmin[k] != p.vmin[0] || p.vmax[k] != p.vmax[0]) return false;
+  return true;
+}
+
+static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
+  PFArgs a = {};
+  for (int k = 0; k < PGW_PF_MAX_M; ++k) {
+    const bool real = k < p.m;
+    const double nph = real ? p.nph[k] : 1.0, vb = real ? p.vbase[k] : 1.0;
+    const double sw = real ? (p.base_kw[k] * 1000.0) / nph : 0.0;
+    const double sv = real ? (p.base_kvar[k] * 1000.0) / nph : 0.0;
+    const int c = real ? p.elem_ctrl[k] : -1;
+    a.sr0[k] = sw / vb;
+    a.si0[k] = -sv / vb;
+    a.fr[k] = (c == 0) ? 1000.0 / (nph * vb) : 0.0;
+    a.fi[k] = (c == 0) ? -1000.0 / (nph * vb) : 0.0;
+    a.kw[k] = real ? p.base_kw[k] : 0.0;
+    a.kvar[k] = real ? p.base_kvar[k] : 0.0;
+    a.nph[k] = nph;
+    a.vb[k] = vb;
+    a.ctrl[k] = c;
+  }
+  a.lo2 = p.vlow[0] * p.vlow[0];
+  a.mn2 = p.vmin[0] * p.vmin[0];
+  a.mx2 = p.vmax[0] * p.vmax[0];
+  a.tol2 = p.tol * p.tol;
+  a.pred_x0 = p.pred_x0;
+  a.pred_inv_h = p.pred_h != 0.0 ? 1.0 / p.pred_h : 0.0;
+  a.pred_n = p.pred_n;
+  a.use_pred = (t.U_pred != nullptr && p.n_ctrl == 1 && p.pred_n >= 3 && p.pred_h > 0.0) ? 1 : 0;
+  a.max_iter = p.max_iter;
+  a.n_ctrl = p.n_ctrl;
+  a.n_out = p.n_out;
+  return a;
+}
+
+template <int M, bool UB, bool GC>
+static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t n, const double* cp,
+                               const double* cq, double* v_out, int32_t* iters, hipStream_t st) {
+  hipLaunchKernelGGL((k_pf_solve<M, UB, GC>), dim3(grid_for(n)), dim3(kBlock), 0, st, a, t, n, cp,
+                     cq, v_out, iters);
+  return check_launch("k_pf_solve");
+}
+
+template <int M, bool UB, bool GC>
+static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_pf_tables& t,
+                               int64_t n, const pgw_coord_buffers& b, hipStream_t st) {
+  hipLaunchKernelGGL((k_coord_pf<M, UB, GC>), dim3(grid_for(n)), dim3(kBlock), 0, st, c, a, t, n, b);
+  return check_launch("k_coord_pf");
+}
+
+// Instantiated variants: IEEE-13 (m = 14) with a uniform band and at most one
+// controllable slot is the fast path; everything else runs the general variant
+// of its padded size.
+#define PGW_PF_DISPATCH(p, fn, ...)                                        \
+  do {                                                                     \
+    const bool ub_ = uniform_band(p), gc_ = (p).n_ctrl > 1;               \
+    switch ((p).m) {                                                       \
+      case 8: return fn<8, false, true>(__VA_ARGS__);                      \
+      case 14:                                                             \
+        if (ub_ && !gc_) return fn<14, true, false>(__VA_ARGS__);          \
+        return fn<14, false, true>(__VA_ARGS__);                           \
+      default: return fn<16, false, true>(__VA_ARGS__);                    \
+    }                                                                      \
+  } while (0)
 
 }  // namespace pgw
 
@@ -573,19 +599,48 @@ extern "C" {
 
 int32_t pgw_pf_padded_m(int32_t m) { return padded_m(m); }
 
+int64_t pgw_pf_pack_size(int32_t m) { return pf_block_size(m); }
+
+int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, double* out) {
+  PGW_REQUIRE(p && W && U0 && out, "pgw_pf_pack: null argument");
+  const int M = p->m;
+  PGW_REQUIRE(M >= 1 && M <= PGW_PF_MAX_M && M == padded_m(M), "pgw_pf_pack: m=%d not padded", M);
+  for (int k = 0; k < M; ++k)
+    PGW_REQUIRE(p->vbase[k] > 0.0, "pgw_pf_pack: vbase[%d] <= 0", k);
+  const int64_t u0 = 3LL * M * M;
+  // per unit of the ROW element's base voltage: u_i = U_i / vb_i
+  for (int k = 0; k < M; ++k)
+    for (int i = 0; i < M; ++i) {
+      const double wr = W[2 * (i * M + k)] / p->vbase[i], wi = W[2 * (i * M + k) + 1] / p->vbase[i];
+      out[(3 * k + 0) * M + i] = wr;
+      out[(3 * k + 1) * M + i] = wi;
+      out[(3 * k + 2) * M + i] = wr + wi;
+    }
+  for (int k = 0; k < M; ++k) {
+    const double ur = U0[2 * k] / p->vbase[k], ui = U0[2 * k + 1] / p->vbase[k];
+    out[u0 + k] = ur;
+    out[u0 + M + k] = ui;
+    out[u0 + 2 * M + k] = ur + ui;
+    out[u0 + 3 * M + k] = p->vlow[k] * p->vlow[k];
+    out[u0 + 4 * M + k] = p->vmin[k] * p->vmin[k];
+    out[u0 + 5 * M + k] = p->vmax[k] * p->vmax[k];
+  }
+  return PGW_OK;
+}
+
 int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out, int32_t* iters,
                      void* stream) {
-  PGW_REQUIRE(p && t && t->W && t->U0 && v_out && n >= 0, "pgw_pf_solve: null argument");
+  PGW_REQUIRE(p && t && t->block && n >= 0, "pgw_pf_solve: null argument");
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M && p->m == padded_m(p->m),
-              "pgw_pf_solve: m=%d out of range", p->m);
+              "pgw_pf_solve: m=%d not padded (pgw_pf_padded_m)", p->m);
   PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve: bad n_ctrl");
-  PGW_REQUIRE(p->n_out == 0 || (t->G && t->V0 && t->inv_vbase_out), "pgw_pf_solve: missing G/V0");
+  PGW_REQUIRE(p->n_out == 0 || (v_out && t->G && t->V0 && t->inv_vbase_out),
+              "pgw_pf_solve: missing v_out/G/V0");
   PGW_REQUIRE(p->max_iter >= 1, "pgw_pf_solve: max_iter < 1");
   if (n == 0) return PGW_OK;
-  hipLaunchKernelGGL(k_pf_solve, dim3(grid_for(4 * n)), dim3(kBlock), 0, (hipStream_t)stream, *p,
-                     *t, n, ctrl_p, ctrl_q, v_out, iters);
-  return check_launch("k_pf_solve");
+  const PFArgs a = make_pf_args(*p, *t);
+  PGW_PF_DISPATCH(*p, launch_pf_solve, a, *t, n, ctrl_p, ctrl_q, v_out, iters, (hipStream_t)stream);
 }
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
@@ -595,11 +650,14 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   PGW_REQUIRE(p->n_comp >= 1 && p->n_comp <= 3, "pgw_coord_step: bad n_comp");
   PGW_REQUIRE(b.action.ptr && b.obs.ptr && b.reward && b.agent_power,
               "pgw_coord_step: null buffer");
+  PGW_REQUIRE(pft->block, "pgw_coord_step: null PF block");
   PGW_REQUIRE(pf->m >= 1 && pf->m <= PGW_PF_MAX_M && pf->m == padded_m(pf->m),
               "pgw_coord_step: pf m=%d not padded", pf->m);
   PGW_REQUIRE(pf->n_out >= 1 && p->vv_row >= 0 && p->vv_row < pf->n_out,
               "pgw_coord_step: bad vv_row");
+  PGW_REQUIRE(pft->G && pft->V0 && pft->inv_vbase_out, "pgw_coord_step: missing G/V0");
   PGW_REQUIRE(pf->max_iter >= 1, "pgw_coord_step: max_iter < 1");
+  PGW_REQUIRE(pf->n_ctrl >= 0 && pf->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_coord_step: bad n_ctrl");
   for (int a = 0; a < p->n_agents; ++a)
     PGW_REQUIRE(p->agent_ctrl[a] < pf->n_ctrl, "pgw_coord_step: agent_ctrl out of range");
   for (int c = 0; c < p->n_comp; ++c) {
@@ -623,8 +681,16 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_coord_pf, dim3(grid_for(4 * n)), dim3(kBlock), 0, st, *p, *pf, *pft, n, b);
-  return check_launch("k_coord_pf");
+  CoordPFArgs c = {};
+  c.n_agents = p->n_agents;
+  c.coordinated = p->coordinated;
+  c.vv_row = p->vv_row;
+  for (int a = 0; a < p->n_agents; ++a) c.agent_ctrl[a] = p->agent_ctrl[a];
+  c.vv_lo = p->vv_lo;
+  c.vv_hi = p->vv_hi;
+  c.vv_penalty = p->vv_penalty;
+  const PFArgs a = make_pf_args(*pf, *pft);
+  PGW_PF_DISPATCH(*pf, launch_coord_pf, c, a, *pft, n, b, st);
 }
 
 }  // extern "C"

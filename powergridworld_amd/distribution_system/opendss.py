@@ -50,9 +50,10 @@ def get_hour_of_year(dt):
 
 class OpenDSSSolver(PowerFlowSolver):
 
-    # controllable kW of the three per-hour reference solutions the batched solve
-    # interpolates its initial guess from (single controllable load only)
-    PREDICTOR_KW = (-150.0, 100.0, 350.0)
+    # Per-hour predictor grid (single controllable load): the batched solve
+    # starts each env from the quadratic through the 3 grid solutions nearest its
+    # controllable kW.  Envs outside the grid extrapolate (slower, same result).
+    PREDICTOR_X0, PREDICTOR_H, PREDICTOR_N = -1000.0, 10.0, 401
 
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = 1e-10, max_iter: int = 100,
@@ -84,21 +85,31 @@ class OpenDSSSolver(PowerFlowSolver):
         self.output_names = names
         idx = [f.node_index[n] for n in names]
         M, W, U0, G, V0o = f.reduce(idx)
+        self.M = M
+        self._base_params()
         dev = self.device
         as_dev = lambda c: torch.tensor(np.ascontiguousarray(c).view(np.float64).ravel(),
                                         dtype=torch.float64, device=dev)
-        self._W, self._U0, self._G, self._V0 = as_dev(W), as_dev(U0), as_dev(G), as_dev(V0o)
+        block = np.zeros(int(_lib.lib().pgw_pf_pack_size(M)))
+        Wf = np.ascontiguousarray(W).view(np.float64).ravel()
+        U0f = np.ascontiguousarray(U0).view(np.float64).ravel()
+        cp = lambda a: a.ctypes.data_as(_lib.C.c_void_p)
+        _lib.check(_lib.lib().pgw_pf_pack(self.params, cp(Wf), cp(U0f), cp(block)))
+        self._block = torch.tensor(block, dtype=torch.float64, device=dev)
+        self._G, self._V0 = as_dev(G), as_dev(V0o)
         self._inv_vb = torch.tensor(1.0 / (f.kv_ln[idx] * 1000.0), dtype=torch.float64, device=dev)
-        self.M = M
-        self.tables = _lib.PFTables(W=self._W.data_ptr(), U0=self._U0.data_ptr(),
-                                    G=self._G.data_ptr(), V0=self._V0.data_ptr(),
-                                    inv_vbase_out=self._inv_vb.data_ptr())
+        self.tables = _lib.PFTables(block=self._block.data_ptr(), G=self._G.data_ptr(),
+                                    V0=self._V0.data_ptr(), inv_vbase_out=self._inv_vb.data_ptr())
         self.v_out = torch.zeros((max(len(names), 1), self.num_envs), dtype=torch.float64, device=dev)
         self._iters = torch.zeros(self.num_envs, dtype=torch.int32, device=dev)
-        self._pred_v = torch.zeros((max(len(names), 1), 3), dtype=torch.float64, device=dev)
-        self._pred_table = torch.zeros((32, 3, M, 2), dtype=torch.float64, device=dev)
+        n_pred = self.PREDICTOR_N
+        self._pred_x = torch.tensor([[self.PREDICTOR_X0 + j * self.PREDICTOR_H for j in range(n_pred)]],
+                                    dtype=torch.float64, device=dev)
+        self._pred_q = torch.zeros_like(self._pred_x)
+        self._pred_v = torch.zeros((max(len(names), 1), n_pred), dtype=torch.float64, device=dev)
+        self._pred_table = torch.zeros((8, n_pred, M, 2), dtype=torch.float64, device=dev)
         self._pred_index = {}
-        self._base_params()
+        self._pred_last = None
 
     def set_controllable_loads(self, names):
         """Load names that receive per-env controllable P/Q (<= 8)."""
@@ -123,14 +134,13 @@ class OpenDSSSolver(PowerFlowSolver):
             p.elem_ctrl[k] = self._ctrl_names.index(ln) if ln in self._ctrl_names else -1
         p.tol, p.m, p.n_ctrl = self.tol, M, len(self._ctrl_names)
         p.n_out, p.max_iter = len(self.output_names), self.max_iter
-        for i, v in enumerate(self.PREDICTOR_KW):
-            p.pred_p[i] = v
+        p.pred_x0, p.pred_h, p.pred_n = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N
         self.params = p
         self._cfg_version = getattr(self, "_cfg_version", 0) + 1
         self._step_cache = {}
         self._tables_cache = {}
-        if hasattr(self, "_pred_index"):
-            self._pred_index = {}
+        self._pred_index = {}
+        self._pred_last = None
 
     def step_params(self, current_time):
         """PFParams with this step's base loads: loadshape[hour] * base * rescale
@@ -156,8 +166,9 @@ class OpenDSSSolver(PowerFlowSolver):
 
     def step_tables(self, current_time):
         """PFTables for this step: with a single controllable load, the per-hour
-        predictor (3 reference solutions, solved here on the device the first
-        time an hour is seen) is attached; otherwise the cold-start tables."""
+        predictor table (PREDICTOR_N solutions on the kW grid, solved here on the
+        device the first time an hour is seen, warm-started from the previous
+        hour's table) is attached; otherwise the cold-start tables."""
         if not (self.use_predictor and len(self._ctrl_names) == 1):
             return self.tables
         key = (current_time, self._cfg_version)
@@ -170,22 +181,24 @@ class OpenDSSSolver(PowerFlowSolver):
         if idx is None:
             idx = len(self._pred_index)
             if idx >= self._pred_table.shape[0]:
-                grown = torch.zeros((2 * idx, 3, self.M, 2), dtype=torch.float64, device=self.device)
+                grown = torch.zeros((2 * idx,) + tuple(self._pred_table.shape[1:]),
+                                    dtype=torch.float64, device=self.device)
                 grown[:idx] = self._pred_table
                 self._pred_table = grown
                 self._tables_cache = {}
             self._pred_index[hkey] = idx
             sp = _lib.PFParams.from_buffer_copy(p)
             sp.tol = min(self.tol, 1e-12)
-            cp = torch.tensor([self.PREDICTOR_KW], dtype=torch.float64, device=self.device)
-            cq = torch.zeros_like(cp)
+            sp.max_iter = max(self.max_iter, 200)
             tb = _lib.PFTables.from_buffer_copy(self.tables)
             tb.U_pred = None
+            tb.U_init = (self._pred_table[self._pred_last].data_ptr()
+                         if self._pred_last is not None else None)
             tb.U_out = self._pred_table[idx].data_ptr()
-            _lib.check(_lib.lib().pgw_pf_solve(sp, tb, 3, _lib.dptr(cp), _lib.dptr(cq),
-                                               _lib.dptr(self._pred_v), None,
-                                               _lib.stream_ptr(self.device)))
-            self._pred_keepalive = (cp, cq)
+            _lib.check(_lib.lib().pgw_pf_solve(sp, tb, self.PREDICTOR_N, _lib.dptr(self._pred_x),
+                                               _lib.dptr(self._pred_q), _lib.dptr(self._pred_v),
+                                               None, _lib.stream_ptr(self.device)))
+        self._pred_last = idx
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.U_pred = self._pred_table[idx].data_ptr()
         if len(self._tables_cache) > 4096:

@@ -197,6 +197,36 @@ def test_pf_vs_oracle():
         assert (N(pf.iterations) == orc.last_iters).mean() > 0.99
 
 
+def test_pf_predictor_vs_oracle_and_cold_start():
+    """Single controllable load: the per-hour predictor grid (warm start) must
+    converge to the oracle's fixed point -- inside the grid, across band kinks and
+    outside it (extrapolated stencil) -- and agree with the cold start."""
+    from oracle.pf_oracle import BatchedPF
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    n = 2048
+    rng = np.random.default_rng(5)
+    mk = lambda pred: OpenDSSSolver("ieee_13_dss/IEEE13Nodeckt.dss",
+                                    "ieee_13_dss/annual_hourly_load_profile.csv",
+                                    system_load_rescale_factor=1.2, num_envs=n, device=DEV,
+                                    predictor=pred)
+    warm, cold = mk(True), mk(False)
+    orc = BatchedPF(system_load_rescale_factor=1.2)
+    for ts in ["2021-08-12 01:00", "2021-08-12 14:00", "2021-08-12 15:00", "2021-08-12 18:00"]:
+        p675 = np.concatenate([rng.uniform(0, 1000, n - 64), rng.uniform(-3000, 5000, 64)])
+        want = orc.calculate(ts, {"675c": p675}, K=n)
+        # past ~4.5 MW on one phase the fixed point barely contracts and the
+        # oracle stops at max_iter unconverged: compare converged envs only
+        ok = orc.last_iters < 100
+        assert ok[:n - 64].all() and ok.sum() > n - 32
+        for pf in (warm, cold):
+            pf.calculate_power_flow({"675c": T(p675)}, {}, current_time=ts)
+            v = pf.get_bus_voltages()
+            got = np.stack([N(v[name]) for name in orc.feeder.node_names], 1)
+            np.testing.assert_allclose(got[ok], want[ok], rtol=1e-9, atol=0)
+        it_w, it_c = N(warm.iterations), N(cold.iterations)
+        assert np.median(it_w[:n - 64]) < np.median(it_c) / 2, (np.median(it_w), np.median(it_c))
+
+
 # ------------------------------------------------------------------ C4 (coordinated)
 @pytest.mark.parametrize("fused", [True, False])
 def test_c4_golden(fused):
