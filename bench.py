@@ -2,10 +2,12 @@
 with the IEEE-13 power flow (BASELINE.json config C4), batch 65,536 per GPU.
 
 One "step" = one MultiAgentEnv.step of the whole batch through the public API
-(fused path: ONE pgw_coord_step launch: 5 x [building, PV, storage] agents +
-power flow + coordinated reward), actions already resident in HBM.  Episodes
-(286 steps) end with done["__all__"]; the following env.reset() is inside the
-timed region.
+(fused path: one pgw_coord_step call = k_coord_agents_std (5 x [building, PV,
+storage] per env) + k_coord_pf (power flow + coordinated reward); once per
+simulated hour also the predictor-table solve), actions already resident in
+HBM.  Episodes (286 steps) end with done["__all__"]; the following env.reset()
+is inside the timed region.  Kernel durations come from HIP events the library
+records around every --time-every-th launch, on the launch's stream.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
          (N>1 via torch.distributed.run: one rank per GPU, weak scaling,
@@ -26,12 +28,21 @@ sys.path.insert(0, REPO)
 N_AGENTS = 5
 ACT_DIM = 8
 BATCH_PER_GPU = 65536
-HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# Algorithmic HBM bytes per env-step of pgw_coord_step (fp64, env-minor SoA), per agent:
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.3 measured achievable)
+FP64_PEAK_TFS = 78.6         # MI355X spec, FP64 vector (= FP64 matrix); tools/micro MFMA probe 68.7
+# k_coord_agents_std -- algorithmic HBM bytes per (env, agent), fp64 env-minor SoA:
 #   reads  actions 8x8 + x_k 5x8 + soc 8                       = 112
 #   writes x_k 5x8 + soc 8 + obs 17x8 + reward 8 + power 8     = 200
-# plus per env the bus voltage and the voltage violation (2 x 8).   (1,568)
-BYTES_PER_ENV_STEP = N_AGENTS * (112 + 200) + 16
+AGENT_BYTES = 112 + 200
+# k_coord_pf -- per env: reads 5 agent powers + 5 rewards, writes 5 rewards + v + vv + iters
+PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
+# k_coord_pf -- algorithmic fp64 FLOPs (m = 14 load phase elements): per fixed-point
+# iteration 8 m^2 (complex matvec) + 12 m (PQ current law) + 6 m (update, |du|^2 test);
+# per env once more the final currents (12 m), one node voltage (8 m + 4) and the reward.
+M_ELEM = 14
+PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
+PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
+KERNELS = ("k_coord_agents_std", "k_coord_pf<14,true,false>", "k_pf_solve<14,true,false>")
 
 
 def parse():
@@ -45,6 +56,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-envs", type=int, default=2048)
     ap.add_argument("--cpu-sample-steps", type=int, default=30)
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="HIP-event-time every k-th launch of each kernel in the timed region")
     return ap.parse_args()
 
 
@@ -69,12 +82,12 @@ def cpu_baseline(envs, steps):
 
 
 def load_traffic():
+    """HBM bytes per launch from the committed PMC summary (tools/gpu/pmc_traffic.py)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
         with open(p) as f:
-            d = json.load(f)
-        return d.get("bytes_per_launch")
-    return None
+            return json.load(f).get("bytes_per_launch", {})
+    return {}
 
 
 def main():
@@ -106,32 +119,30 @@ def main():
     env.reset()
     step_count = 0
 
-    def run(k, events=None):
+    def run(k):
         nonlocal step_count
-        for i in range(k):
-            if events is not None:
-                events[i][0].record()
+        for _ in range(k):
             _, _, dones, _ = env.step(packed[step_count % P])
-            if events is not None:
-                events[i][1].record()
             step_count += 1
             if dones["__all__"]:
                 env.reset()
 
+    from powergridworld_amd import _lib
     run(args.warmup)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
     torch.cuda.synchronize()
+    _lib.check(_lib.lib().pgw_timing_start(args.time_every))
     t0 = time.perf_counter()
-    run(args.steps, ev)
+    run(args.steps)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    tot = (_lib.C.c_double * 3)()
+    cnt = (_lib.C.c_int64 * 3)()
+    _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -139,8 +150,36 @@ def main():
     total_envs = n * world
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
-        achieved = BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
+        avg_us = {KERNELS[k]: (tot[k] / cnt[k] * 1e3 if cnt[k] else None) for k in range(3)}
+        it = env.pf_solver.iterations.double()
+        mean_it, max_it = float(it.mean()), int(it.max())
         traffic = load_traffic()
+        kernels = {}
+        a_us, p_us = avg_us[KERNELS[0]], avg_us[KERNELS[1]]
+        if a_us:
+            gbs = AGENT_BYTES * N_AGENTS * n / (a_us * 1e-6) / 1e9
+            kernels[KERNELS[0]] = {"avg_us": a_us, "timed_launches": cnt[0], "bound": "hbm",
+                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": gbs / HBM_PEAK_GBS,
+                                   "bytes_per_launch": AGENT_BYTES * N_AGENTS * n,
+                                   "traffic": traffic.get(KERNELS[0])}
+        if p_us:
+            tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (p_us * 1e-6) / 1e12
+            kernels[KERNELS[1]] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
+                                   "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); "
+                                           "one wave per SIMD, latency-bound",
+                                   "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                                   "frac": tfs / FP64_PEAK_TFS,
+                                   "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
+                                   "traffic": traffic.get(KERNELS[1])}
+        if avg_us[KERNELS[2]]:
+            kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
+                                   "note": "per-hour predictor table (801 grid solves)"}
+        dom = max((k for k in kernels if "achieved" in kernels[k]), key=lambda k: kernels[k]["avg_us"])
+        d = kernels[dom]
+        roof = {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
+                "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"],
+                "avg_launch_us": d["avg_us"]}
         out = {
             "metric": "agent-env-steps/sec at batch 65536, 5-agent scenario, 1/2/4/8 MI355X",
             "value": value,
@@ -159,17 +198,10 @@ def main():
                                    "+ IEEE-13 power flow + voltage-violation reward",
                        "batch_per_gpu": n, "global_batch": total_envs, "episode_steps": 286,
                        "parallelism": "env-sharded x%d (no collective on the step path)" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "kernel": "pgw_coord_step (k_coord_step<14>)",
-                         "kernel_ms": kernel_ms,
-                         "bytes_per_launch": BYTES_PER_ENV_STEP * n},
+            "roofline": roof,
+            "kernels": kernels,
+            "pf_iterations": {"mean": mean_it, "max": max_it},
         }
-        it = env.pf_solver.iterations
-        if it is not None:
-            itf = it.double()
-            out["pf_iterations"] = {"mean": float(itf.mean()), "max": int(it.max())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(out))

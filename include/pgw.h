@@ -255,12 +255,21 @@ typedef struct pgw_pf_tables {
    * result is the same fixed point (to tol); only the iteration count drops.
    * NULL = cold start from U0. */
   const double* U_pred;
+  /* Optional band signatures of the pred_n grid solutions (sig_out of the solve
+   * that produced U_pred).  With them, an env whose 3-point stencil straddles a
+   * load-band switch (an element crossing vlow/vmin/vmax, where the solution is
+   * not smooth in the controllable kW) takes the nearest stencil whose points
+   * share the band signature of its own first guess.  NULL = plain stencil. */
+  const int32_t* U_pred_sig;
   /* Optional per-env initial guess, n x m complex element voltages in per unit
    * of each element's vbase (env-major); overrides U_pred.  NULL = none. */
   const double* U_init;
   /* Optional output: converged element voltages, n x m complex in per unit of
    * each element's vbase (env-major). */
   double* U_out;
+  /* Optional output: per env, the band of every element in 2 bits (element k
+   * in bits 2k..2k+1: 0 |u| <= vlow, 1 <= vmin, 2 <= vmax, 3 above). */
+  int32_t* sig_out;
 } pgw_pf_tables;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)
@@ -279,6 +288,16 @@ int64_t pgw_pf_pack_size(int32_t m);
 /* Host memory: pack W (m x m complex, row-major), U0 (m complex) and the
  * per-element voltage bands of p into `out` (pgw_pf_pack_size(p->m) doubles). */
 int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, double* out);
+
+/* ------------------------------------------------------------------------
+ * Kernel timing (benchmark instrumentation): while on, every `every`-th launch
+ * of each kernel below is bracketed by HIP events on its own stream.
+ * pgw_timing_stop synchronizes the recorded events and returns, per kernel,
+ * the summed duration (ms) and the number of timed launches.
+ * ---------------------------------------------------------------------- */
+enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COUNT = 3 };
+int32_t pgw_timing_start(int32_t every);
+int32_t pgw_timing_stop(double* total_ms, int64_t* count);
 
 /* ------------------------------------------------------------------------
  * Host-side feeder construction (C++, no GPU): the native stand-in for the

@@ -87,7 +87,7 @@ class PFParams(C.Structure):
 
 class PFTables(C.Structure):
     _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("inv_vbase_out", vp), ("U_pred", vp),
-                ("U_init", vp), ("U_out", vp)]
+                ("U_pred_sig", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp)]
 
 
 class FeederElem(C.Structure):
@@ -137,6 +137,8 @@ _SIGS = {
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_padded_m": (i32, [i32]),
     "pgw_pf_pack_size": (i64, [i32]),
+    "pgw_timing_start": (i32, [i32]),
+    "pgw_timing_stop": (i32, [vp, vp]),
     "pgw_pf_pack": (i32, [P(PFParams), vp, vp, vp]),
     "pgw_feeder_build": (i32, [P(FeederElem), i32, i32, vp, vp, vp, vp]),
     "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),

@@ -3,6 +3,7 @@
 // the power-flow kernel opts into fma() explicitly where it wants it.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -21,6 +22,27 @@ int32_t check_launch(const char* what);
       return PGW_ERR_ARG;                 \
     }                                     \
   } while (0)
+
+// Sampled launch timing (pgw_timing.hip).  A sampled launch goes through
+// hipExtLaunchKernelGGL with a start/stop event pair, whose timestamps come
+// from the kernel's own dispatch (the same interval rocprofv3 reports);
+// every other launch is a plain hipLaunchKernelGGL.
+struct TimingSlot {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+TimingSlot timing_begin(int kernel);
+void timing_commit(int kernel, const TimingSlot& s);
+
+template <typename K, typename... A>
+inline void launch_timed(int id, K kernel, dim3 grid, dim3 block, hipStream_t st, A... args) {
+  const TimingSlot s = timing_begin(id);
+  if (s.start) {
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, st, s.start, s.stop, 0, args...);
+    timing_commit(id, s);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+  }
+}
 
 constexpr int kBlock = 256;   // 4 waves of 64
 

@@ -152,13 +152,7 @@ template <int M, bool UB, bool GC> struct PFSolver {
       pf_power<M, K>(s_r, s_i, sres, pc, qc);
     }
     double vlo2, vmn2, vmx2;
-    if constexpr (UB) {
-      vlo2 = lo2;
-      vmn2 = mn2;
-      vmx2 = mx2;
-    } else {
-      pf_band<M, K>(vlo2, vmn2, vmx2, w);
-    }
+    band<K>(vlo2, vmn2, vmx2);
     const double m2 = fma(ui[K], ui[K], ur[K] * ur[K]);
     double mc = fmin(fmax(m2, vmn2), vmx2);
     mc = (m2 <= vlo2) ? 1.0 : mc;
@@ -169,9 +163,51 @@ template <int M, bool UB, bool GC> struct PFSolver {
   }
 
   // Initial guess: quadratic through the 3 predictor grid points nearest pc, or u0.
+  // Band limits of element K (pu^2).
+  template <int K>
+  __device__ __forceinline__ void band(double& vlo2, double& vmn2, double& vmx2) const {
+    if constexpr (UB) {
+      vlo2 = lo2;
+      vmn2 = mn2;
+      vmx2 = mx2;
+    } else {
+      pf_band<M, K>(vlo2, vmn2, vmx2, w);
+    }
+  }
+
+  // Band of every element in 2 bits (0 |u| <= vlow, 1 <= vmin, 2 <= vmax, 3 above),
+  // the states the load law switches between.  Whole wave (DPP in pf_band).
+  __device__ __forceinline__ int32_t signature() const {
+    uint32_t sg = 0;
+    static_for<0, M>([&](auto k) {
+      double vlo2, vmn2, vmx2;
+      band<k>(vlo2, vmn2, vmx2);
+      const double m2 = fma(ui[k], ui[k], ur[k] * ur[k]);
+      const uint32_t b = (uint32_t)(m2 > vlo2) + (uint32_t)(m2 > vmn2) + (uint32_t)(m2 > vmx2);
+      sg |= b << (2 * k);
+    });
+    return (int32_t)sg;
+  }
+
+  // Quadratic through predictor grid points a, a+1, a+2 at grid coordinate g.
+  __device__ __forceinline__ void pred_quad(const double* U_pred, int a, double g) {
+    const double t = g - (double)(a + 1);
+    const double wm = 0.5 * t * (t - 1.0), w0 = 1.0 - t * t, wp = 0.5 * t * (t + 1.0);
+    const double2* P = reinterpret_cast<const double2*>(U_pred) + (int64_t)a * M;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      const double2 pm = P[k], p0 = P[M + k], pp = P[2 * M + k];
+      ur[k] = fma(wp, pp.x, fma(w0, p0.x, wm * pm.x));
+      ui[k] = fma(wp, pp.y, fma(w0, p0.y, wm * pm.y));
+    }
+  }
+
+  // Initial guess: per-env U_init; or the predictor -- the quadratic through the
+  // 3 grid solutions nearest pc, moved to the nearest stencil whose 3 points
+  // share the band signature of that first guess when the centred one
+  // straddles a band switch; or u0.
   __device__ __forceinline__ void initial(const PFArgs& a, const pgw_pf_tables& t, int64_t e,
                                           bool valid) {
-    const double* U_pred = t.U_pred;
     if (t.U_init) {
       const double2* P = reinterpret_cast<const double2*>(t.U_init) + (valid ? e : 0) * M;
 #pragma unroll
@@ -181,17 +217,26 @@ template <int M, bool UB, bool GC> struct PFSolver {
         ui[k] = v.y;
       }
     } else if (a.use_pred) {
-      const double u = (pc - a.pred_x0) * a.pred_inv_h;
-      double sj = rint(u);
-      sj = fmin(fmax(sj, 1.0), (double)(a.pred_n - 2));
-      const double t = u - sj;
-      const double wm = 0.5 * t * (t - 1.0), w0 = 1.0 - t * t, wp = 0.5 * t * (t + 1.0);
-      const double2* P = reinterpret_cast<const double2*>(U_pred) + ((int)sj - 1) * M;
+      const double g = (pc - a.pred_x0) * a.pred_inv_h;
+      const int s = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
+      pred_quad(t.U_pred, s - 1, g);
+      if (t.U_pred_sig) {
+        const int32_t sg = signature();
+        int32_t sv[7];                      // signatures of grid points s-3 .. s+3
+        bool in[7];
 #pragma unroll
-      for (int k = 0; k < M; ++k) {
-        const double2 pm = P[k], p0 = P[M + k], pp = P[2 * M + k];
-        ur[k] = fma(wp, pp.x, fma(w0, p0.x, wm * pm.x));
-        ui[k] = fma(wp, pp.y, fma(w0, p0.y, wm * pm.y));
+        for (int j = 0; j < 7; ++j) {
+          const int q = s - 3 + j;
+          in[j] = q >= 0 && q < a.pred_n;
+          sv[j] = t.U_pred_sig[in[j] ? q : s];
+        }
+        auto same = [&](int j) {           // stencil starting at grid point s - 3 + j
+          return in[j] && in[j + 2] && sv[j] == sg && sv[j + 1] == sg && sv[j + 2] == sg;
+        };
+        if (!same(2)) {
+          const int pick = same(3) ? 3 : same(1) ? 1 : same(4) ? 4 : same(0) ? 0 : -1;
+          if (pick >= 0) pred_quad(t.U_pred, s - 3 + pick, g);
+        }
       }
     } else {
       pf_u0<M>(ur, ui, w);
@@ -284,7 +329,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   const int it = S.iterate(a.max_iter, valid);
   double ir[M], ii[M];
   S.currents(ir, ii);
+  const int32_t sig = t.sig_out ? S.signature() : 0;
   if (!valid) return;
+  if (t.sig_out) t.sig_out[e] = sig;
   for (int o = 0; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
   if (t.U_out) {
 #pragma unroll
@@ -478,6 +525,11 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
                                                      int64_t n, pgw_coord_buffers b) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
+  // HBM first: the agent powers gate the predictor
+  double rp[PGW_MAX_AGENTS];
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+    rp[ag] = (valid && ag < c.n_agents) ? b.agent_power[(int64_t)ag * n + e] : 0.0;
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
   S.load(a, t.block);
@@ -487,17 +539,20 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     cp[s] = 0.0;
     cq[s] = 0.0;
   }
-  if (valid) {
-    for (int ag = 0; ag < c.n_agents; ++ag) {
-      const double rp = b.agent_power[(int64_t)ag * n + e];
-      const int slot = c.agent_ctrl[ag];
 #pragma unroll
-      for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp : cp[s];
-    }
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag) {
+    const int slot = ag < c.n_agents ? c.agent_ctrl[ag] : -1;
+#pragma unroll
+    for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
   S.powers(a, cp, cq);
   S.initial(a, t, e, valid);
   const int it = S.iterate(a.max_iter, valid);
+  // the rewards are read-modify-written below: issue their loads now
+  double rw[PGW_MAX_AGENTS];
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+    rw[ag] = (valid && c.coordinated && ag < c.n_agents) ? b.reward[(int64_t)ag * n + e] : 0.0;
   double ir[M], ii[M];
   S.currents(ir, ii);
   if (!valid) return;
@@ -512,10 +567,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
     if (b.vv) b.vv[e] = vv;
     const double share = (vv * c.vv_penalty) / (double)c.n_agents;
-    for (int ag = 0; ag < c.n_agents; ++ag) {
-      double* r = b.reward + (int64_t)ag * n + e;
-      *r = *r - share;
-    }
+#pragma unroll
+    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+      if (ag < c.n_agents) b.reward[(int64_t)ag * n + e] = rw[ag] - share;
   }
 }
 
@@ -564,15 +618,16 @@ static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
 template <int M, bool UB, bool GC>
 static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t n, const double* cp,
                                const double* cq, double* v_out, int32_t* iters, hipStream_t st) {
-  hipLaunchKernelGGL((k_pf_solve<M, UB, GC>), dim3(grid_for(n)), dim3(kBlock), 0, st, a, t, n, cp,
-                     cq, v_out, iters);
+  launch_timed(PGW_T_PF_SOLVE, k_pf_solve<M, UB, GC>, dim3(grid_for(n)), dim3(kBlock), st, a, t, n,
+               cp, cq, v_out, iters);
   return check_launch("k_pf_solve");
 }
 
 template <int M, bool UB, bool GC>
 static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_pf_tables& t,
                                int64_t n, const pgw_coord_buffers& b, hipStream_t st) {
-  hipLaunchKernelGGL((k_coord_pf<M, UB, GC>), dim3(grid_for(n)), dim3(kBlock), 0, st, c, a, t, n, b);
+  launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC>, dim3(grid_for(n)), dim3(kBlock), st, c, a, t,
+               n, b);
   return check_launch("k_coord_pf");
 }
 
@@ -673,11 +728,11 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
     const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
                                           - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
                                        : -s->pv_pmax;
-    hipLaunchKernelGGL(k_coord_agents_std, dim3(grid_for(n), p->n_agents), dim3(kBlock), 0, st, *p,
-                       *s, n, b, pv_ob);
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std, dim3(grid_for(n), p->n_agents),
+                 dim3(kBlock), st, *p, *s, n, b, pv_ob);
   } else {
-    hipLaunchKernelGGL(k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock), 0, st, *p, *s,
-                       n, b);
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
+                 st, *p, *s, n, b);
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;

@@ -51,9 +51,12 @@ def get_hour_of_year(dt):
 class OpenDSSSolver(PowerFlowSolver):
 
     # Per-hour predictor grid (single controllable load): the batched solve
-    # starts each env from the quadratic through the 3 grid solutions nearest its
-    # controllable kW.  Envs outside the grid extrapolate (slower, same result).
-    PREDICTOR_X0, PREDICTOR_H, PREDICTOR_N = -1000.0, 10.0, 401
+    # starts each env from the quadratic through 3 grid solutions near its
+    # controllable kW (chosen so that they share its load-band signature).  Envs
+    # outside the grid extrapolate (more iterations, same result).
+    PREDICTOR_X0, PREDICTOR_H, PREDICTOR_N = -500.0, 2.5, 801
+    PREDICTOR_TOL = 1e-12
+    PREDICTOR_MAX_TABLES = 64      # hours kept on the device (~180 KB each)
 
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = 1e-10, max_iter: int = 100,
@@ -72,6 +75,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self.tol, self.max_iter = float(tol), int(max_iter)
         self.bus_voltages = {}
         self.iterations = None
+        self._hour_memo = {}
         self._ctrl_names = []
         self.use_predictor = bool(predictor)
         self.set_output_nodes(output_nodes)
@@ -107,7 +111,10 @@ class OpenDSSSolver(PowerFlowSolver):
                                     dtype=torch.float64, device=dev)
         self._pred_q = torch.zeros_like(self._pred_x)
         self._pred_v = torch.zeros((max(len(names), 1), n_pred), dtype=torch.float64, device=dev)
-        self._pred_table = torch.zeros((8, n_pred, M, 2), dtype=torch.float64, device=dev)
+        # preallocated: cached PFTables hold raw pointers into these
+        self._pred_table = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred, M, 2), dtype=torch.float64,
+                                       device=dev)
+        self._pred_sig = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred), dtype=torch.int32, device=dev)
         self._pred_index = {}
         self._pred_last = None
 
@@ -137,21 +144,32 @@ class OpenDSSSolver(PowerFlowSolver):
         p.pred_x0, p.pred_h, p.pred_n = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N
         self.params = p
         self._cfg_version = getattr(self, "_cfg_version", 0) + 1
+        # bumped whenever a PFTables handed out earlier may no longer be valid
+        self.tables_version = getattr(self, "tables_version", 0) + 1
         self._step_cache = {}
         self._tables_cache = {}
         self._pred_index = {}
         self._pred_last = None
 
+    def hour_of(self, current_time):
+        """Hour of year of a step time (opendss.py:98-103), memoized per time."""
+        h = self._hour_memo.get(current_time)
+        if h is None:
+            if len(self._hour_memo) > 1 << 16:
+                self._hour_memo.clear()
+            h = self._hour_memo[current_time] = get_hour_of_year(pd.Timestamp(current_time))
+        return h
+
     def step_params(self, current_time):
         """PFParams with this step's base loads: loadshape[hour] * base * rescale
-        (opendss.py:96-108).  Cached per (time, configuration): the base loads
+        (opendss.py:96-108).  Cached per (hour, configuration): the base loads
         only change hourly."""
-        key = (current_time, self._cfg_version)
+        hour = self.hour_of(current_time)
+        key = (hour, self._cfg_version)
         p = self._step_cache.get(key)
         if p is not None:
             return p
-        ts = pd.Timestamp(current_time)
-        coef = self.annual_hourly_load_profile[get_hour_of_year(ts)]
+        coef = self.annual_hourly_load_profile[hour]
         step_load = coef * self.base_load * self.system_load_rescale_factor
         f = self.feeder
         p = _lib.PFParams.from_buffer_copy(self.params)
@@ -171,7 +189,7 @@ class OpenDSSSolver(PowerFlowSolver):
         hour's table) is attached; otherwise the cold-start tables."""
         if not (self.use_predictor and len(self._ctrl_names) == 1):
             return self.tables
-        key = (current_time, self._cfg_version)
+        key = (self.hour_of(current_time), self._cfg_version)
         t = self._tables_cache.get(key)
         if t is not None:
             return t
@@ -179,28 +197,27 @@ class OpenDSSSolver(PowerFlowSolver):
         hkey = (tuple(p.base_kw), tuple(p.base_kvar))
         idx = self._pred_index.get(hkey)
         if idx is None:
+            if len(self._pred_index) >= self.PREDICTOR_MAX_TABLES:
+                self._pred_index, self._tables_cache, self._pred_last = {}, {}, None
+                self.tables_version += 1
             idx = len(self._pred_index)
-            if idx >= self._pred_table.shape[0]:
-                grown = torch.zeros((2 * idx,) + tuple(self._pred_table.shape[1:]),
-                                    dtype=torch.float64, device=self.device)
-                grown[:idx] = self._pred_table
-                self._pred_table = grown
-                self._tables_cache = {}
             self._pred_index[hkey] = idx
             sp = _lib.PFParams.from_buffer_copy(p)
-            sp.tol = min(self.tol, 1e-12)
+            sp.tol = min(self.tol, self.PREDICTOR_TOL)
             sp.max_iter = max(self.max_iter, 200)
             tb = _lib.PFTables.from_buffer_copy(self.tables)
             tb.U_pred = None
             tb.U_init = (self._pred_table[self._pred_last].data_ptr()
                          if self._pred_last is not None else None)
             tb.U_out = self._pred_table[idx].data_ptr()
+            tb.sig_out = self._pred_sig[idx].data_ptr()
             _lib.check(_lib.lib().pgw_pf_solve(sp, tb, self.PREDICTOR_N, _lib.dptr(self._pred_x),
                                                _lib.dptr(self._pred_q), _lib.dptr(self._pred_v),
                                                None, _lib.stream_ptr(self.device)))
         self._pred_last = idx
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.U_pred = self._pred_table[idx].data_ptr()
+        t.U_pred_sig = self._pred_sig[idx].data_ptr()
         if len(self._tables_cache) > 4096:
             self._tables_cache.clear()
         self._tables_cache[key] = t

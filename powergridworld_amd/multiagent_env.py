@@ -345,7 +345,7 @@ class MultiAgentEnv(Env):
         bufs.reward, bufs.agent_power = F["reward"].data_ptr(), F["agent_power"].data_ptr()
         bufs.v_out = self.pf_solver.v_out.data_ptr()
         bufs.vv, bufs.iters = F["vv"].data_ptr(), F["iters"].data_ptr()
-        F["bufs"], F["act_key"], F["info_cache"] = bufs, None, {}
+        F["bufs"], F["act_key"], F["step_cache"] = bufs, None, {}
         comps = [dict(zip(kinds, agent.envs)) for agent in self.agents]
         F["bld0"], F["pv0"] = comps[0].get("building"), comps[0].get("pv")
         F["bld_envs"] = [c["building"] for c in comps if "building" in c]
@@ -401,9 +401,11 @@ class MultiAgentEnv(Env):
             bufs.act_stride_agent = key[1]
             F["act_key"] = key
         bld, pv = F["bld0"], F["pv0"]
-        ikey = (bld.time_index if bld is not None else -1, pv.index if pv is not None else -1)
-        info = F["info_cache"].get(ikey)
-        if info is None:
+        solver = self.pf_solver
+        skey = (bld.time_index if bld is not None else -1, pv.index if pv is not None else -1,
+                self.time, solver.tables_version)
+        ent = F["step_cache"].get(skey)
+        if ent is None:
             info = _lib.CoordStepInfo()
             if bld is not None:
                 t = bld.time_index
@@ -412,9 +414,15 @@ class MultiAgentEnv(Env):
                 info.ex_t, info.ex_next = bld._exo[t], bld._exo[t + 1]
             if pv is not None:
                 info.pv_pmax = float(pv.data[pv.index])
-            F["info_cache"][ikey] = info
-        pfp = self.pf_solver.step_params(self.time)
-        pft = self.pf_solver.step_tables(self.time)
+            pfp = solver.step_params(self.time)
+            pft = solver.step_tables(self.time)
+            if len(F["step_cache"]) > 1 << 14:
+                F["step_cache"].clear()
+            ent = F["step_cache"][skey] = (info, pfp, pft, solver.tables_version)
+        info, pfp, pft, tv = ent
+        if tv != solver.tables_version:    # the table solve above recycled the device tables
+            F["step_cache"].clear()
+            return self._step_fused(action)
         rc = _lib.lib().pgw_coord_step(F["params"], pfp, pft, info,
                                        self.num_envs, bufs, _lib.stream_ptr(self.device))
         if rc:

@@ -11,7 +11,7 @@ run_pass() {
   rc=$?; cd "$GRAFT_REPO_ROOT"; return $rc
 }
 run_pass p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS || exit $?
-run_pass p2 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64 || exit $?
+run_pass p2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64 SQ_THREAD_CYCLES_VALU || exit $?
 run_pass p3 FETCH_SIZE || exit $?
 run_pass p4 WRITE_SIZE || exit $?
 echo pmc-done
