@@ -3,7 +3,9 @@
 
 The PF kernels keep the shared operand block resident in VGPRs, 16 entries per
 register pair (entry e in lane e % 16 of every 16-lane row of pair e // 16), and
-feed each entry to its FMA with `row_newbcast:(e % 16)`.  The lane index must be
+feed each entry to its FMA with `row_newbcast:(e % 16)`.  The scaled matrix
+W''_ik = W_ik / (vb_i vb_k) is complex symmetric, so only its upper triangle is
+resident (three real parts: Re, Im, Re + Im).  The lane index must be
 an immediate, so every group is spelled out here per padded element count M.
 
 Hazard rule (CDNA3/4): a VALU write of a VGPR followed by a DPP read of it needs
@@ -31,22 +33,31 @@ def asm_stmt(lines, outs, ins):
     return ("  asm(\n%s      : %s\n      : %s);\n" % (body, ", ".join(outs), ", ".join(ins)))
 
 
+def tri(M, i, k):
+    """Index of (i, k) in the row-major upper triangle of a symmetric M x M matrix."""
+    i, k = min(i, k), max(i, k)
+    return i * M - i * (i - 1) // 2 + (k - i)
+
+
 def block_layout(M):
-    u0re = 3 * M * M
-    return dict(u0re=u0re, u0im=u0re + M, u0sum=u0re + 2 * M, lo2=u0re + 3 * M,
+    t = M * (M + 1) // 2
+    u0re = 3 * t
+    return dict(tri=t, u0re=u0re, u0im=u0re + M, u0sum=u0re + 2 * M, lo2=u0re + 3 * M,
                 mn2=u0re + 4 * M, mx2=u0re + 5 * M, size=u0re + 6 * M)
 
 
 def gen_column(M, k):
-    """A[i] += Wr'[i][k] ir ; B[i] += Wi'[i][k] ii ; C[i] += (Wr'+Wi')[i][k] is."""
-    ents = [(3 * k + c) * M + i for c in range(3) for i in range(M)]
+    """A[i] += Wr[i][k] ir ; B[i] += Wi[i][k] ii ; C[i] += (Wr+Wi)[i][k] is  (W symmetric:
+    part c of entry (i, k) is block entry c * tri + tri(i, k))."""
+    T = block_layout(M)["tri"]
+    ents = [c * T + tri(M, i, k) for c in range(3) for i in range(M)]
     ps, pidx = pairs_of(ents)
     n_out = 3 * M
     xs = n_out + len(ps)              # operand index of ir, ii, is
     lines = []
     for c in range(3):
         for i in range(M):
-            e = (3 * k + c) * M + i
+            e = c * T + tri(M, i, k)
             lines.append("v_fmac_f64_dpp %%%d, %%%d, %%%d row_newbcast:%d %s"
                          % (c * M + i, n_out + pidx[e // 16], xs + c, e % 16, DPP))
     outs = ['"+v"(A[%d])' % i for i in range(M)] + ['"+v"(B[%d])' % i for i in range(M)] + \

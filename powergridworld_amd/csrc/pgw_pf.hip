@@ -44,23 +44,28 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ---- resident operand block ------------------------------------------------
-// Packed block (pgw_pf_pack, doubles), M = padded element count:
-//   [0, 3M^2)   entry (3k + c) M + i: c = 0 Re W'[i][k], 1 Im W'[i][k], 2 their sum
-//   [3M^2, +3M) u0re[i], u0im[i], u0re[i] + u0im[i]
-//   [.., +3M)   vlow^2, vmin^2, vmax^2 per element (pu^2)
+// Packed block (pgw_pf_pack, doubles), M = padded element count, T = M(M+1)/2:
+//   [0, 3T)      part c of the upper triangle of W'' = W_ik / (vb_i vb_k), which is
+//                complex symmetric: c = 0 Re, 1 Im, 2 Re + Im; entry (i <= k) at
+//                c T + i M - i(i-1)/2 + (k - i)
+//   [3T, +3M)    u0re[i], u0im[i], u0re[i] + u0im[i]   (u0 = U0 / vb)
+//   [.., +3M)    vlow^2, vmin^2, vmax^2 per element (pu^2)
+// The iteration runs on u = U / vb and the scaled currents I' = I vb =
+// conj(S) u g, so u_i = u0_i + sum_k W''_ik I'_k.
 template <int M> struct PFBlock {
-  static constexpr int kU0re = 3 * M * M, kU0im = kU0re + M, kU0sum = kU0im + M;
+  static constexpr int kTri = M * (M + 1) / 2;
+  static constexpr int kU0re = 3 * kTri, kU0im = kU0re + M, kU0sum = kU0im + M;
   static constexpr int kLo2 = kU0sum + M, kMn2 = kLo2 + M, kMx2 = kMn2 + M;
   static constexpr int kSize = kMx2 + M;
   static constexpr int kPairs = (kSize + 15) / 16;
 };
-static int64_t pf_block_size(int m) { return 3LL * m * m + 6LL * m; }
+static int64_t pf_block_size(int m) { return 3LL * m * (m + 1) / 2 + 6LL * m; }
 
 // Per-launch scalars derived on the host from pgw_pf_params (pu).
 struct PFArgs {
-  double sr0[PGW_PF_MAX_M], si0[PGW_PF_MAX_M];   // s0 = conj(S_base) / vb per phase
+  double sr0[PGW_PF_MAX_M], si0[PGW_PF_MAX_M];   // s0 = conj(S_base) per phase (W, var)
   double fr[PGW_PF_MAX_M], fi[PGW_PF_MAX_M];     // d s / d (ctrl kW, kvar): slot-0 elements
-  double kw[PGW_PF_MAX_M], kvar[PGW_PF_MAX_M], nph[PGW_PF_MAX_M], vb[PGW_PF_MAX_M];
+  double kw[PGW_PF_MAX_M], kvar[PGW_PF_MAX_M], nph[PGW_PF_MAX_M], inv_vb[PGW_PF_MAX_M];
   int32_t ctrl[PGW_PF_MAX_M];
   double lo2, mn2, mx2;                          // band limits when uniform (pu^2)
   double tol2;
@@ -130,18 +135,16 @@ template <int M, bool UB, bool GC> struct PFSolver {
           p = (c == s) ? cp[s] : p;
           q = (c == s) ? cq[s] : q;
         }
-        const double sw = ((a.kw[k] + p) * 1000.0) / a.nph[k];
-        const double sv = ((a.kvar[k] + q) * 1000.0) / a.nph[k];
-        sr[k] = sw / a.vb[k];
-        si[k] = -sv / a.vb[k];
+        sr[k] = ((a.kw[k] + p) * 1000.0) / a.nph[k];
+        si[k] = -(((a.kvar[k] + q) * 1000.0) / a.nph[k]);
       }
     }
   }
 
-  // OpenDSS Load.DoConstantPQLoad (model 1), in pu: I = s u g with
+  // OpenDSS Load.DoConstantPQLoad (model 1), in pu: I' = I vb = conj(S) u g with
   //   g = 1/|u|^2 for vmin < |u| <= vmax, the constant-Z scales 1/vmin^2 below
   //   vmin and 1/vmax^2 above vmax -- i.e. 1/clamp(|u|^2, vmin^2, vmax^2), exact
-  //   at both band edges -- and 1 at or below vlow.  I comes out in amperes.
+  //   at both band edges -- and 1 at or below vlow.
   template <int K>
   __device__ __forceinline__ void current(double& ir, double& ii) const {
     double s_r, s_i;
@@ -219,17 +222,19 @@ template <int M, bool UB, bool GC> struct PFSolver {
     } else if (a.use_pred) {
       const double g = (pc - a.pred_x0) * a.pred_inv_h;
       const int s = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
-      pred_quad(t.U_pred, s - 1, g);
-      if (t.U_pred_sig) {
-        const int32_t sg = signature();
-        int32_t sv[7];                      // signatures of grid points s-3 .. s+3
-        bool in[7];
+      // signatures of grid points s-3 .. s+3, loaded with the first gather
+      int32_t sv[7];
+      bool in[7];
+      const bool sig = t.U_pred_sig != nullptr;
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          const int q = s - 3 + j;
-          in[j] = q >= 0 && q < a.pred_n;
-          sv[j] = t.U_pred_sig[in[j] ? q : s];
-        }
+      for (int j = 0; j < 7; ++j) {
+        const int q = s - 3 + j;
+        in[j] = q >= 0 && q < a.pred_n;
+        sv[j] = sig ? t.U_pred_sig[in[j] ? q : s] : 0;
+      }
+      pred_quad(t.U_pred, s - 1, g);
+      if (sig) {
+        const int32_t sg = signature();
         auto same = [&](int j) {           // stencil starting at grid point s - 3 + j
           return in[j] && in[j + 2] && sv[j] == sg && sv[j + 1] == sg && sv[j + 2] == sg;
         };
@@ -257,12 +262,24 @@ template <int M, bool UB, bool GC> struct PFSolver {
       pf_acc_init<M>(A, C, w);
 #pragma unroll
       for (int i = 0; i < M; ++i) Bs[i] = 0.0;
-      static_for<0, M>([&](auto k) {
-        double ir, ii;
-        current<k>(ir, ii);
-        const double is = ir + ii;
-        pf_column<M, k>(A, Bs, C, w, ir, ii, is);
+      // two elements at a time: their current-law chains (v_rcp_f64 + Newton)
+      // are independent, so the scheduler interleaves them instead of stalling
+      // on one dependent chain between two FMA blocks
+      static_for<0, M / 2>([&](auto h) {
+        constexpr int k0 = 2 * h, k1 = 2 * h + 1;
+        double ir0, ii0, ir1, ii1;
+        current<k0>(ir0, ii0);
+        current<k1>(ir1, ii1);
+        const double is0 = ir0 + ii0, is1 = ir1 + ii1;
+        pf_column<M, k0>(A, Bs, C, w, ir0, ii0, is0);
+        pf_column<M, k1>(A, Bs, C, w, ir1, ii1, is1);
       });
+      if constexpr (M % 2) {
+        double ir, ii;
+        current<M - 1>(ir, ii);
+        const double is = ir + ii;
+        pf_column<M, M - 1>(A, Bs, C, w, ir, ii, is);
+      }
       bool conv = true;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
@@ -281,8 +298,13 @@ template <int M, bool UB, bool GC> struct PFSolver {
     return my_it;
   }
 
-  __device__ __forceinline__ void currents(double* ir, double* ii) const {
-    static_for<0, M>([&](auto k) { current<k>(ir[k], ii[k]); });
+  // physical element currents (A) for the node-voltage rows
+  __device__ __forceinline__ void currents(const PFArgs& a, double* ir, double* ii) const {
+    static_for<0, M>([&](auto k) {
+      current<k>(ir[k], ii[k]);
+      ir[k] *= a.inv_vb[k];
+      ii[k] *= a.inv_vb[k];
+    });
   }
 };
 
@@ -328,7 +350,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   S.initial(a, t, e, valid);
   const int it = S.iterate(a.max_iter, valid);
   double ir[M], ii[M];
-  S.currents(ir, ii);
+  S.currents(a, ir, ii);
   const int32_t sig = t.sig_out ? S.signature() : 0;
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
@@ -548,13 +570,8 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   S.powers(a, cp, cq);
   S.initial(a, t, e, valid);
   const int it = S.iterate(a.max_iter, valid);
-  // the rewards are read-modify-written below: issue their loads now
-  double rw[PGW_MAX_AGENTS];
-#pragma unroll
-  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-    rw[ag] = (valid && c.coordinated && ag < c.n_agents) ? b.reward[(int64_t)ag * n + e] : 0.0;
   double ir[M], ii[M];
-  S.currents(ir, ii);
+  S.currents(a, ir, ii);
   if (!valid) return;
   double vsel = 0.0;
   for (int o = 0; o < a.n_out; ++o) {
@@ -567,9 +584,14 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
     if (b.vv) b.vv[e] = vv;
     const double share = (vv * c.vv_penalty) / (double)c.n_agents;
+    // reward -= share as a no-return atomic add of -share: one IEEE add per
+    // address (bit-identical to the subtraction, deterministic), no load
+    // round trip at the end of the kernel
 #pragma unroll
     for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-      if (ag < c.n_agents) b.reward[(int64_t)ag * n + e] = rw[ag] - share;
+      if (ag < c.n_agents)
+        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, -share, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -591,14 +613,14 @@ static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
     const double sw = real ? (p.base_kw[k] * 1000.0) / nph : 0.0;
     const double sv = real ? (p.base_kvar[k] * 1000.0) / nph : 0.0;
     const int c = real ? p.elem_ctrl[k] : -1;
-    a.sr0[k] = sw / vb;
-    a.si0[k] = -sv / vb;
-    a.fr[k] = (c == 0) ? 1000.0 / (nph * vb) : 0.0;
-    a.fi[k] = (c == 0) ? -1000.0 / (nph * vb) : 0.0;
+    a.sr0[k] = sw;
+    a.si0[k] = -sv;
+    a.fr[k] = (c == 0) ? 1000.0 / nph : 0.0;
+    a.fi[k] = (c == 0) ? -1000.0 / nph : 0.0;
     a.kw[k] = real ? p.base_kw[k] : 0.0;
     a.kvar[k] = real ? p.base_kvar[k] : 0.0;
     a.nph[k] = nph;
-    a.vb[k] = vb;
+    a.inv_vb[k] = 1.0 / vb;
     a.ctrl[k] = c;
   }
   a.lo2 = p.vlow[0] * p.vlow[0];
@@ -662,15 +684,28 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, d
   PGW_REQUIRE(M >= 1 && M <= PGW_PF_MAX_M && M == padded_m(M), "pgw_pf_pack: m=%d not padded", M);
   for (int k = 0; k < M; ++k)
     PGW_REQUIRE(p->vbase[k] > 0.0, "pgw_pf_pack: vbase[%d] <= 0", k);
-  const int64_t u0 = 3LL * M * M;
-  // per unit of the ROW element's base voltage: u_i = U_i / vb_i
-  for (int k = 0; k < M; ++k)
-    for (int i = 0; i < M; ++i) {
-      const double wr = W[2 * (i * M + k)] / p->vbase[i], wi = W[2 * (i * M + k) + 1] / p->vbase[i];
-      out[(3 * k + 0) * M + i] = wr;
-      out[(3 * k + 1) * M + i] = wi;
-      out[(3 * k + 2) * M + i] = wr + wi;
+  auto w = [&](int i, int k, int c) { return W[2 * (i * M + k) + c]; };
+  double wmax = 0.0, asym = 0.0;
+  for (int i = 0; i < M; ++i)
+    for (int k = 0; k < M; ++k)
+      for (int c = 0; c < 2; ++c) {
+        wmax = std::max(wmax, std::fabs(w(i, k, c)));
+        asym = std::max(asym, std::fabs(w(i, k, c) - w(k, i, c)));
+      }
+  // W = -C Z C^T is complex symmetric for a reciprocal network (no phase shifters)
+  PGW_REQUIRE(asym <= 1e-12 * wmax, "pgw_pf_pack: W not symmetric (%.3g relative)",
+              wmax > 0 ? asym / wmax : asym);
+  const int T = M * (M + 1) / 2;
+  for (int i = 0; i < M; ++i)
+    for (int k = i; k < M; ++k) {
+      const double sc = 1.0 / (p->vbase[i] * p->vbase[k]);
+      const double wr = 0.5 * (w(i, k, 0) + w(k, i, 0)) * sc, wi = 0.5 * (w(i, k, 1) + w(k, i, 1)) * sc;
+      const int e = i * M - i * (i - 1) / 2 + (k - i);
+      out[e] = wr;
+      out[T + e] = wi;
+      out[2 * T + e] = wr + wi;
     }
+  const int64_t u0 = 3LL * T;
   for (int k = 0; k < M; ++k) {
     const double ur = U0[2 * k] / p->vbase[k], ui = U0[2 * k + 1] / p->vbase[k];
     out[u0 + k] = ur;
