@@ -92,25 +92,22 @@ def load_traffic():
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from powergridworld_amd import distributed as pgd
+    rank, local, world = pgd.env_rank()
     dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    pgd.init("nccl", dev)
+    if dist:
+        import torch.distributed as tdist
 
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     n = args.batch
     env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=dev, fused=True)
     for i, agent in enumerate(env.agents):         # per-rank seed offset
-        agent.env_dict["storage"].seed(1000 * rank + i)
-    gen = torch.Generator(dev).manual_seed(rank)
+        agent.env_dict["storage"].seed(pgd.rank_seed(0, rank, i))
+    gen = torch.Generator(dev).manual_seed(pgd.rank_seed(0, rank))     # seed 0 at rank 0
     P = args.action_pool
     pool = torch.empty((P, N_AGENTS, ACT_DIM, n), dtype=torch.float64, device=dev)
     pool.uniform_(-1.0, 1.0, generator=gen)
@@ -143,10 +140,7 @@ def main():
     tot = (_lib.C.c_double * 3)()
     cnt = (_lib.C.c_int64 * 3)()
     _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = pgd.max_over_ranks(elapsed, dev)
     total_envs = n * world
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
