@@ -54,9 +54,9 @@ def parse():
     ap.add_argument("--action-pool", type=int, default=64,
                     help="distinct pre-generated action batches cycled through (HBM resident)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-envs", type=int, default=2048)
-    ap.add_argument("--cpu-sample-steps", type=int, default=30)
-    ap.add_argument("--time-every", type=int, default=4,
+    ap.add_argument("--cpu-sample-envs", type=int, default=8192)
+    ap.add_argument("--cpu-sample-steps", type=int, default=286)
+    ap.add_argument("--time-every", type=int, default=16,
                     help="HIP-event-time every k-th launch of each kernel in the timed region")
     return ap.parse_args()
 
@@ -137,14 +137,14 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
-    tot = (_lib.C.c_double * 3)()
-    cnt = (_lib.C.c_int64 * 3)()
+    tot = (_lib.C.c_double * len(KERNELS))()
+    cnt = (_lib.C.c_int64 * len(KERNELS))()
     _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
     elapsed = pgd.max_over_ranks(elapsed, dev)
     total_envs = n * world
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
-        avg_us = {KERNELS[k]: (tot[k] / cnt[k] * 1e3 if cnt[k] else None) for k in range(3)}
+        avg_us = {KERNELS[k]: (tot[k] / cnt[k] * 1e3 if cnt[k] else None) for k in range(len(KERNELS))}
         it = env.pf_solver.iterations.double()
         mean_it, max_it = float(it.mean()), int(it.max())
         traffic = load_traffic()

@@ -270,6 +270,10 @@ typedef struct pgw_pf_tables {
   /* Optional output: per env, the band of every element in 2 bits (element k
    * in bits 2k..2k+1: 0 |u| <= vlow, 1 <= vmin, 2 <= vmax, 3 above). */
   int32_t* sig_out;
+  /* Optional per-env multiplier of base_kw / base_kvar (n doubles): solves
+   * several load levels (e.g. the loadshape hours of an episode) in one launch.
+   * NULL = 1. */
+  const double* load_scale;
 } pgw_pf_tables;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

@@ -87,7 +87,8 @@ class PFParams(C.Structure):
 
 class PFTables(C.Structure):
     _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("inv_vbase_out", vp), ("U_pred", vp),
-                ("U_pred_sig", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp)]
+                ("U_pred_sig", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp),
+                ("load_scale", vp)]
 
 
 class FeederElem(C.Structure):

@@ -122,7 +122,8 @@ template <int M, bool UB, bool GC> struct PFSolver {
   }
 
   // element powers of the env (opendss.py:107-129; OpenDSS WNominal = kW*1000/nphases)
-  __device__ __forceinline__ void powers(const PFArgs& a, const double* cp, const double* cq) {
+  __device__ __forceinline__ void powers(const PFArgs& a, const double* cp, const double* cq,
+                                         double scale) {
     pc = cp[0];
     qc = cq[0];
     if constexpr (GC) {
@@ -135,8 +136,8 @@ template <int M, bool UB, bool GC> struct PFSolver {
           p = (c == s) ? cp[s] : p;
           q = (c == s) ? cq[s] : q;
         }
-        sr[k] = ((a.kw[k] + p) * 1000.0) / a.nph[k];
-        si[k] = -(((a.kvar[k] + q) * 1000.0) / a.nph[k]);
+        sr[k] = ((a.kw[k] * scale + p) * 1000.0) / a.nph[k];
+        si[k] = -(((a.kvar[k] * scale + q) * 1000.0) / a.nph[k]);
       }
     }
   }
@@ -346,7 +347,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
     cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
     cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
-  S.powers(a, cp, cq);
+  S.powers(a, cp, cq, (t.load_scale && valid) ? t.load_scale[e] : 1.0);
   S.initial(a, t, e, valid);
   const int it = S.iterate(a.max_iter, valid);
   double ir[M], ii[M];
@@ -433,22 +434,35 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents(pgw_coord_params p, pgw
 // operation, as the generic device functions (the fused-vs-generic test checks
 // bit equality); only the uniform selects become compile-time indices.
 
-__global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
-                                                             pgw_coord_step_info s, int64_t n,
-                                                             pgw_coord_buffers b, double pv_ob) {
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int a = blockIdx.y;
-  if (e >= n) return;
-  const pgw_building_params& B = p.bld;
+struct StdAgentIn {
+  double av[8];     // actions: building 0..5, pv 6, storage 7
+  double xs[5];     // building state x_k
+  double soc;
+};
+
+__device__ __forceinline__ void std_agent_load(const pgw_coord_buffers& b, int a, int64_t e,
+                                               int64_t n, StdAgentIn& in) {
   const double* ap = b.action.ptr + a * b.act_stride_agent + e * b.action.s_env;
   const int64_t sd = b.action.s_dim;
-  double av[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) av[j] = ap[j * sd];
+  for (int j = 0; j < 8; ++j) in.av[j] = ap[j * sd];
+  const double* xp = b.x + (int64_t)a * 5 * n + e;
+#pragma unroll
+  for (int z = 0; z < 5; ++z) in.xs[z] = xp[z * n];
+  in.soc = b.soc[(int64_t)a * n + e];
+}
+
+// One standard agent step for env e: writes x_k, SoC and the 17 observations;
+// returns the agent's real power and (pre-transform) reward.
+__device__ __forceinline__ void std_agent_step(const pgw_coord_params& p, const pgw_coord_step_info& s,
+                                               const pgw_coord_buffers& b, int a, int64_t e,
+                                               int64_t n, double pv_ob, StdAgentIn& in,
+                                               double& agent_rp, double& agent_rew) {
+  const pgw_building_params& B = p.bld;
+  double* av = in.av;
+  double* xs = in.xs;
   double* xp = b.x + (int64_t)a * 5 * n + e;
-  double xs[5], T[5];
-#pragma unroll
-  for (int z = 0; z < 5; ++z) xs[z] = xp[z * n];
+  double T[5];
   // ---- building
 #pragma unroll
   for (int j = 0; j < 6; ++j) av[j] = B.rescale ? to_raw(av[j], B.act_low[j], B.act_high[j]) : av[j];
@@ -499,20 +513,31 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
   op[15 * so] = pv_ob;
   const double rp_pv = pv_real_power(p.pv, av[6], s.pv_pmax);
   // ---- storage
-  double* socp = b.soc + (int64_t)a * n + e;
-  double soc = *socp;
+  double soc = in.soc;
   const double power = battery_step(p.bat, av[7], soc);
-  *socp = soc;
+  b.soc[(int64_t)a * n + e] = soc;
   op[16 * so] = battery_obs(p.bat, soc);
   // MultiComponentEnv sums (base.py:131-137)
-  double agent_rp = 0.0;
+  agent_rp = 0.0;
   agent_rp = agent_rp + pc;
   agent_rp = agent_rp + rp_pv;
   agent_rp = agent_rp + (-power);
-  double agent_rew = 0.0;
+  agent_rew = 0.0;
   agent_rew = agent_rew + r_bld;
   agent_rew = agent_rew + 0.0;
   agent_rew = agent_rew + 0.0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
+                                                             pgw_coord_step_info s, int64_t n,
+                                                             pgw_coord_buffers b, double pv_ob) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int a = blockIdx.y;
+  if (e >= n) return;
+  StdAgentIn in;
+  std_agent_load(b, a, e, n, in);
+  double agent_rp, agent_rew;
+  std_agent_step(p, s, b, a, e, n, pv_ob, in, agent_rp, agent_rew);
   b.agent_power[(int64_t)a * n + e] = agent_rp;
   b.reward[(int64_t)a * n + e] = agent_rew;
 }
@@ -567,7 +592,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
 #pragma unroll
     for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
-  S.powers(a, cp, cq);
+  S.powers(a, cp, cq, 1.0);
   S.initial(a, t, e, valid);
   const int it = S.iterate(a.max_iter, valid);
   double ir[M], ii[M];
@@ -653,12 +678,12 @@ static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_
   return check_launch("k_coord_pf");
 }
 
-// Instantiated variants: IEEE-13 (m = 14) with a uniform band and at most one
-// controllable slot is the fast path; everything else runs the general variant
-// of its padded size.
-#define PGW_PF_DISPATCH(p, fn, ...)                                        \
+// Instantiated variants: IEEE-13 (m = 14) with a uniform band, at most one
+// controllable slot and no per-env load scale is the fast path; everything
+// else runs the general variant (per-lane element powers) of its padded size.
+#define PGW_PF_DISPATCH(p, t, fn, ...)                                     \
   do {                                                                     \
-    const bool ub_ = uniform_band(p), gc_ = (p).n_ctrl > 1;               \
+    const bool ub_ = uniform_band(p), gc_ = (p).n_ctrl > 1 || (t).load_scale; \
     switch ((p).m) {                                                       \
       case 8: return fn<8, false, true>(__VA_ARGS__);                      \
       case 14:                                                             \
@@ -730,7 +755,7 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
   PGW_REQUIRE(p->max_iter >= 1, "pgw_pf_solve: max_iter < 1");
   if (n == 0) return PGW_OK;
   const PFArgs a = make_pf_args(*p, *t);
-  PGW_PF_DISPATCH(*p, launch_pf_solve, a, *t, n, ctrl_p, ctrl_q, v_out, iters, (hipStream_t)stream);
+  PGW_PF_DISPATCH(*p, *t, launch_pf_solve, a, *t, n, ctrl_p, ctrl_q, v_out, iters, (hipStream_t)stream);
 }
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
@@ -741,6 +766,7 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   PGW_REQUIRE(b.action.ptr && b.obs.ptr && b.reward && b.agent_power,
               "pgw_coord_step: null buffer");
   PGW_REQUIRE(pft->block, "pgw_coord_step: null PF block");
+  PGW_REQUIRE(!pft->load_scale && !pft->U_init, "pgw_coord_step: load_scale / U_init not supported");
   PGW_REQUIRE(pf->m >= 1 && pf->m <= PGW_PF_MAX_M && pf->m == padded_m(pf->m),
               "pgw_coord_step: pf m=%d not padded", pf->m);
   PGW_REQUIRE(pf->n_out >= 1 && p->vv_row >= 0 && p->vv_row < pf->n_out,
@@ -758,19 +784,11 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   }
   if (n == 0) return PGW_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (coord_is_std(*p)) {
-    // PVEnv.get_obs is the same for every env: evaluate it once here
-    const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
-                                          - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
-                                       : -s->pv_pmax;
-    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std, dim3(grid_for(n), p->n_agents),
-                 dim3(kBlock), st, *p, *s, n, b, pv_ob);
-  } else {
-    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
-                 st, *p, *s, n, b);
-  }
-  int32_t rc = check_launch("k_coord_agents");
-  if (rc) return rc;
+  const bool std_layout = coord_is_std(*p);
+  // PVEnv.get_obs is the same for every env: evaluate it once here
+  const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
+                                        - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
+                                     : -s->pv_pmax;
   CoordPFArgs c = {};
   c.n_agents = p->n_agents;
   c.coordinated = p->coordinated;
@@ -780,7 +798,16 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   c.vv_hi = p->vv_hi;
   c.vv_penalty = p->vv_penalty;
   const PFArgs a = make_pf_args(*pf, *pft);
-  PGW_PF_DISPATCH(*pf, launch_coord_pf, c, a, *pft, n, b, st);
+  if (std_layout) {
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std, dim3(grid_for(n), p->n_agents),
+                 dim3(kBlock), st, *p, *s, n, b, pv_ob);
+  } else {
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
+                 st, *p, *s, n, b);
+  }
+  int32_t rc = check_launch("k_coord_agents");
+  if (rc) return rc;
+  PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
 }
 
 }  // extern "C"

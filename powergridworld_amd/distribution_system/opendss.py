@@ -57,6 +57,7 @@ class OpenDSSSolver(PowerFlowSolver):
     PREDICTOR_X0, PREDICTOR_H, PREDICTOR_N = -500.0, 2.5, 801
     PREDICTOR_TOL = 1e-12
     PREDICTOR_MAX_TABLES = 64      # hours kept on the device (~180 KB each)
+    PREDICTOR_LOOKAHEAD = 24       # hours solved per table launch
 
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = 1e-10, max_iter: int = 100,
@@ -109,14 +110,11 @@ class OpenDSSSolver(PowerFlowSolver):
         n_pred = self.PREDICTOR_N
         self._pred_x = torch.tensor([[self.PREDICTOR_X0 + j * self.PREDICTOR_H for j in range(n_pred)]],
                                     dtype=torch.float64, device=dev)
-        self._pred_q = torch.zeros_like(self._pred_x)
-        self._pred_v = torch.zeros((max(len(names), 1), n_pred), dtype=torch.float64, device=dev)
         # preallocated: cached PFTables hold raw pointers into these
         self._pred_table = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred, M, 2), dtype=torch.float64,
                                        device=dev)
         self._pred_sig = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred), dtype=torch.int32, device=dev)
         self._pred_index = {}
-        self._pred_last = None
 
     def set_controllable_loads(self, names):
         """Load names that receive per-env controllable P/Q (<= 8)."""
@@ -149,7 +147,6 @@ class OpenDSSSolver(PowerFlowSolver):
         self._step_cache = {}
         self._tables_cache = {}
         self._pred_index = {}
-        self._pred_last = None
 
     def hour_of(self, current_time):
         """Hour of year of a step time (opendss.py:98-103), memoized per time."""
@@ -164,7 +161,9 @@ class OpenDSSSolver(PowerFlowSolver):
         """PFParams with this step's base loads: loadshape[hour] * base * rescale
         (opendss.py:96-108).  Cached per (hour, configuration): the base loads
         only change hourly."""
-        hour = self.hour_of(current_time)
+        return self._params_for_hour(self.hour_of(current_time))
+
+    def _params_for_hour(self, hour):
         key = (hour, self._cfg_version)
         p = self._step_cache.get(key)
         if p is not None:
@@ -184,37 +183,22 @@ class OpenDSSSolver(PowerFlowSolver):
 
     def step_tables(self, current_time):
         """PFTables for this step: with a single controllable load, the per-hour
-        predictor table (PREDICTOR_N solutions on the kW grid, solved here on the
-        device the first time an hour is seen, warm-started from the previous
-        hour's table) is attached; otherwise the cold-start tables."""
+        predictor table is attached (PREDICTOR_N solutions on the kW grid).  A
+        missing hour is solved on the device together with the next
+        PREDICTOR_LOOKAHEAD - 1 hours in ONE launch (the hours differ only by
+        the loadshape coefficient, passed as a per-env load scale), so an
+        episode pays for about one table solve.  Otherwise the cold-start tables."""
         if not (self.use_predictor and len(self._ctrl_names) == 1):
             return self.tables
-        key = (self.hour_of(current_time), self._cfg_version)
+        hour = self.hour_of(current_time)
+        key = (hour, self._cfg_version)
         t = self._tables_cache.get(key)
         if t is not None:
             return t
-        p = self.step_params(current_time)
-        hkey = (tuple(p.base_kw), tuple(p.base_kvar))
-        idx = self._pred_index.get(hkey)
+        idx = self._pred_index.get(self._hour_key(hour))
         if idx is None:
-            if len(self._pred_index) >= self.PREDICTOR_MAX_TABLES:
-                self._pred_index, self._tables_cache, self._pred_last = {}, {}, None
-                self.tables_version += 1
-            idx = len(self._pred_index)
-            self._pred_index[hkey] = idx
-            sp = _lib.PFParams.from_buffer_copy(p)
-            sp.tol = min(self.tol, self.PREDICTOR_TOL)
-            sp.max_iter = max(self.max_iter, 200)
-            tb = _lib.PFTables.from_buffer_copy(self.tables)
-            tb.U_pred = None
-            tb.U_init = (self._pred_table[self._pred_last].data_ptr()
-                         if self._pred_last is not None else None)
-            tb.U_out = self._pred_table[idx].data_ptr()
-            tb.sig_out = self._pred_sig[idx].data_ptr()
-            _lib.check(_lib.lib().pgw_pf_solve(sp, tb, self.PREDICTOR_N, _lib.dptr(self._pred_x),
-                                               _lib.dptr(self._pred_q), _lib.dptr(self._pred_v),
-                                               None, _lib.stream_ptr(self.device)))
-        self._pred_last = idx
+            self._solve_tables(hour)
+            idx = self._pred_index[self._hour_key(hour)]
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.U_pred = self._pred_table[idx].data_ptr()
         t.U_pred_sig = self._pred_sig[idx].data_ptr()
@@ -222,6 +206,52 @@ class OpenDSSSolver(PowerFlowSolver):
             self._tables_cache.clear()
         self._tables_cache[key] = t
         return t
+
+    def _hour_key(self, hour):
+        p = self._params_for_hour(hour)
+        return (tuple(p.base_kw), tuple(p.base_kvar))
+
+    def _solve_tables(self, hour):
+        """Predictor tables for `hour` and the following hours of the year that
+        have none yet (one k_pf_solve over n_hours x PREDICTOR_N grid points)."""
+        hours, keys = [], []
+        for h in range(hour, min(hour + self.PREDICTOR_LOOKAHEAD, len(self.annual_hourly_load_profile))):
+            k = self._hour_key(h)
+            if k not in self._pred_index and k not in keys:
+                hours.append(h)
+                keys.append(k)
+        if len(self._pred_index) + len(keys) > self.PREDICTOR_MAX_TABLES:
+            self._pred_index, self._tables_cache = {}, {}
+            self.tables_version += 1
+        idx0 = len(self._pred_index)
+        for j, k in enumerate(keys):
+            self._pred_index[k] = idx0 + j
+        P, H = self.PREDICTOR_N, len(hours)
+        # base loads at coefficient 1, per-env scale = loadshape[hour] (the same
+        # product as step_params up to rounding; the table only seeds the solve)
+        sp = _lib.PFParams.from_buffer_copy(self.params)
+        base = self.base_load * self.system_load_rescale_factor
+        f = self.feeder
+        for k in range(self.M):
+            real = k < f.m
+            sp.base_kw[k] = base[f.elem_load[k], 0] if real else 0.0
+            sp.base_kvar[k] = base[f.elem_load[k], 1] if real else 0.0
+        sp.tol = min(self.tol, self.PREDICTOR_TOL)
+        sp.max_iter = max(self.max_iter, 200)
+        sp.n_out = 0
+        dev = self.device
+        scale = torch.tensor(np.repeat(self.annual_hourly_load_profile[hours], P), dtype=torch.float64,
+                             device=dev)
+        cp = self._pred_x.repeat(1, H)
+        cq = torch.zeros_like(cp)
+        tb = _lib.PFTables.from_buffer_copy(self.tables)
+        tb.U_pred = None
+        tb.U_out = self._pred_table[idx0].data_ptr()
+        tb.sig_out = self._pred_sig[idx0].data_ptr()
+        tb.load_scale = scale.data_ptr()
+        _lib.check(_lib.lib().pgw_pf_solve(sp, tb, H * P, _lib.dptr(cp), _lib.dptr(cq), None, None,
+                                           _lib.stream_ptr(dev)))
+        self._pred_keepalive = (scale, cp, cq)     # until the stream has consumed them
 
     # ------------------------------------------------------------ reference API
     def calculate_power_flow(self, p_controllable_consumed: dict = None,
