@@ -147,6 +147,10 @@ def main():
         avg_us = {KERNELS[k]: (tot[k] / cnt[k] * 1e3 if cnt[k] else None) for k in range(len(KERNELS))}
         it = env.pf_solver.iterations.double()
         mean_it, max_it = float(it.mean()), int(it.max())
+        # the PF kernel runs one wave (64 envs) per SIMD: its time follows the
+        # slowest wave, so report how many waves need 1, 2, ... iterations
+        wmax = env.pf_solver.iterations[: (n // 64) * 64].view(-1, 64).max(1).values
+        wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
         traffic = load_traffic()
         kernels = {}
         a_us, p_us = avg_us[KERNELS[0]], avg_us[KERNELS[1]]
@@ -194,7 +198,7 @@ def main():
                        "parallelism": "env-sharded x%d (no collective on the step path)" % world},
             "roofline": roof,
             "kernels": kernels,
-            "pf_iterations": {"mean": mean_it, "max": max_it},
+            "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)

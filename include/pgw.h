@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 3
+#define PGW_ABI_VERSION 6
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -40,8 +40,8 @@ const char* pgw_last_error(void);
 /* sizeof() of every ABI struct, in the order pgw_mat, battery_params, pv_params,
  * building_params, building_exo, building_ext, ev_params, ev_step_info,
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
- * coord_step_info -- lets a binding verify its layouts.  Writes min(n, 15)
- * values, returns 15. */
+ * coord_step_info, pred_meta -- lets a binding verify its layouts.  Writes
+ * min(n, 16) values, returns 16. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -239,28 +239,37 @@ typedef struct pgw_pf_params {
   int32_t pred_n;                   /* predictor grid points (>= 3 to use U_pred) */
 } pgw_pf_params;
 
+/* Predictor stencil metadata of one grid segment (see pgw_pf_tables.U_pred_meta). */
+typedef struct pgw_pred_meta {
+  double tstar;           /* switch position inside the segment, in [0, 1] */
+  int32_t left, right;    /* record (stencil centre) used left / right of it */
+} pgw_pred_meta;
+
 /* Device tables.  `block` is the wave-uniform operand block the solve streams
  * through the scalar cache every iteration; build it on the host with
  * pgw_pf_pack from W = -C Z C^T and U0 = C V0 (pgw_pf_reduce) and copy it to
  * the device once per feeder / output-node set. */
 typedef struct pgw_pf_tables {
   const double* block;  /* pgw_pf_pack_size(m) doubles (device)           */
-  const double* G;      /* n_out x m complex: node voltage response     */
-  const double* V0;     /* n_out complex: no-load node voltages         */
-  const double* inv_vbase_out;  /* n_out: 1 / (kV_LN * 1000)           */
-  /* Optional initial guess (n_ctrl == 1 only): pred_n x m complex element
-   * voltages solved at controllable load x_j = pred_x0 + j pred_h for this
-   * step's base loads; each env starts from the quadratic through the 3 grid
-   * points nearest its own controllable kW instead of from U0.  The converged
-   * result is the same fixed point (to tol); only the iteration count drops.
-   * NULL = cold start from U0. */
+  /* Output rows in per unit, against the scaled element currents I'_k = I_k vb_k:
+   * G: n_out x m complex, G_ok / (vb_k vb_o) with G = -(Z C^T)[output nodes];
+   * V0: n_out complex, V0_o / vb_o (no-load node voltage). */
+  const double* G;
+  const double* V0;
+  /* Optional initial guess (n_ctrl == 1 only): pred_n predictor records
+   * (pgw_pf_pred_pack) of the grid solutions at controllable load
+   * x_j = pred_x0 + j pred_h for this step's base loads; each env starts from
+   * the quadratic of a record near its own controllable kW instead of from U0.
+   * The converged result is the same fixed point (to tol); only the iteration
+   * count drops.  NULL = cold start from U0. */
   const double* U_pred;
-  /* Optional band signatures of the pred_n grid solutions (sig_out of the solve
-   * that produced U_pred).  With them, an env whose 3-point stencil straddles a
-   * load-band switch (an element crossing vlow/vmin/vmax, where the solution is
-   * not smooth in the controllable kW) takes the nearest stencil whose points
-   * share the band signature of its own first guess.  NULL = plain stencil. */
-  const int32_t* U_pred_sig;
+  /* Optional stencil choice per grid segment (pgw_pf_pred_meta, pred_n - 1
+   * entries): an env in segment j at fractional position t uses the record
+   * centred at meta[j].left if t < meta[j].tstar, else at meta[j].right -- so
+   * its quadratic never straddles a load-band switch (an element crossing
+   * vlow/vmin/vmax, where the solution is not smooth in the controllable kW).
+   * NULL = the record nearest the env. */
+  const struct pgw_pred_meta* U_pred_meta;
   /* Optional per-env initial guess, n x m complex element voltages in per unit
    * of each element's vbase (env-major); overrides U_pred.  NULL = none. */
   const double* U_init;
@@ -284,14 +293,32 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out,
                      int32_t* iters, void* stream);
 
+/* Predictor records from grid solutions (device): U_grid n_tables x n_points x m
+ * complex (U_out of the grid solve) -> rec, n_tables x n_points records of
+ * 32 m bytes: u_j (m complex fp64), then d1 = u_{j+1} - u_{j-1} and
+ * d2 = u_{j+1} - 2 u_j + u_{j-1} (m complex fp32 each; end points use the
+ * neighbouring interior centre's differences).  u(t) = u_j + t d1/2 + t^2 d2/2
+ * is the 3-point quadratic centred at j.  16-byte aligned. */
+int32_t pgw_pf_pred_pack(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,
+                         const double* U_grid, double* rec, void* stream);
+/* Stencil metadata for n_tables predictor grids of n_points solutions each
+ * (U_grid: n_tables x n_points x m complex, sig: their sig_out) -> meta:
+ * n_tables x (n_points - 1).  Uses p's per-element voltage bands.  Device. */
+int32_t pgw_pf_pred_meta(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,
+                         const double* U_pred, const int32_t* sig, pgw_pred_meta* meta,
+                         void* stream);
+
 /* Element count the kernels are instantiated for (8, 14 or 16): pad the
  * feeder's m load phase elements to it with inert elements (zero power). */
 int32_t pgw_pf_padded_m(int32_t m);
 /* Doubles in the packed operand block for padded element count m. */
 int64_t pgw_pf_pack_size(int32_t m);
-/* Host memory: pack W (m x m complex, row-major), U0 (m complex) and the
- * per-element voltage bands of p into `out` (pgw_pf_pack_size(p->m) doubles). */
-int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, double* out);
+/* Host memory: pack W (m x m complex, row-major; must be complex symmetric),
+ * U0 (m complex), the per-element voltage bands of p and output row 0 of the
+ * tables (G0: m complex, V0_0: complex -- required if p->n_out > 0) into `out`
+ * (pgw_pf_pack_size(p->m) doubles). */
+int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, const double* G0,
+                    const double* V0_0, double* out);
 
 /* ------------------------------------------------------------------------
  * Kernel timing (benchmark instrumentation): while on, every `every`-th launch
@@ -300,6 +327,9 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, d
  * the summed duration (ms) and the number of timed launches.
  * ---------------------------------------------------------------------- */
 enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COUNT = 3 };
+/* Debug: device buffer of 8 int64 per k_coord_pf wave (NULL = off); lane 0 of
+ * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
+int32_t pgw_debug_pf_trace(long long* buf);
 int32_t pgw_timing_start(int32_t every);
 int32_t pgw_timing_stop(double* total_ms, int64_t* count);
 

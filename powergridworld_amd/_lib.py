@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 3
+ABI_VERSION = 6
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -86,9 +86,13 @@ class PFParams(C.Structure):
 
 
 class PFTables(C.Structure):
-    _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("inv_vbase_out", vp), ("U_pred", vp),
-                ("U_pred_sig", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp),
+    _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("U_pred", vp),
+                ("U_pred_meta", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp),
                 ("load_scale", vp)]
+
+
+class PredMeta(C.Structure):
+    _fields_ = [("tstar", f64), ("left", i32), ("right", i32)]
 
 
 class FeederElem(C.Structure):
@@ -139,8 +143,11 @@ _SIGS = {
     "pgw_pf_padded_m": (i32, [i32]),
     "pgw_pf_pack_size": (i64, [i32]),
     "pgw_timing_start": (i32, [i32]),
+    "pgw_debug_pf_trace": (i32, [vp]),
+    "pgw_pf_pred_meta": (i32, [P(PFParams), i32, i32, vp, vp, vp, vp]),
+    "pgw_pf_pred_pack": (i32, [P(PFParams), i32, i32, vp, vp, vp]),
     "pgw_timing_stop": (i32, [vp, vp]),
-    "pgw_pf_pack": (i32, [P(PFParams), vp, vp, vp]),
+    "pgw_pf_pack": (i32, [P(PFParams), vp, vp, vp, vp, vp]),
     "pgw_feeder_build": (i32, [P(FeederElem), i32, i32, vp, vp, vp, vp]),
     "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
     "pgw_coord_step": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
@@ -151,7 +158,7 @@ EXPORTED = sorted(_SIGS)
 
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
-           CoordStepInfo]
+           CoordStepInfo, PredMeta]
 
 _lib = None
 

@@ -42,8 +42,34 @@ def tri(M, i, k):
 def block_layout(M):
     t = M * (M + 1) // 2
     u0re = 3 * t
+    g0re = u0re + 6 * M
     return dict(tri=t, u0re=u0re, u0im=u0re + M, u0sum=u0re + 2 * M, lo2=u0re + 3 * M,
-                mn2=u0re + 4 * M, mx2=u0re + 5 * M, size=u0re + 6 * M)
+                mn2=u0re + 4 * M, mx2=u0re + 5 * M, g0re=g0re, g0im=g0re + M,
+                v0re=g0re + 2 * M, v0im=g0re + 2 * M + 1, size=g0re + 2 * M + 2)
+
+
+def gen_node0(M, nr):
+    """(vr, vi) = V0' + sum_k G'_k I'_k for output node 0 (pu, resident row)."""
+    L = block_layout(M)
+    ents = [L["v0re"], L["v0im"]] + [L["g0re"] + k for k in range(M)] + [L["g0im"] + k for k in range(M)]
+    ps, pidx = pairs_of(ents)
+    w = lambda e: "%%%d" % (2 + pidx[e // 16])
+    ir = lambda k: "%%%d" % (2 + len(ps) + k)
+    ii = lambda k: "%%%d" % (2 + len(ps) + M + k)
+    lines = ["v_mov_b64_dpp %%0, %s row_newbcast:%d %s" % (w(L["v0re"]), L["v0re"] % 16, DPP),
+             "v_mov_b64_dpp %%1, %s row_newbcast:%d %s" % (w(L["v0im"]), L["v0im"] % 16, DPP)]
+    for k in range(M):
+        gr, gi = L["g0re"] + k, L["g0im"] + k
+        lines += ["v_fmac_f64_dpp %%0, %s, %s row_newbcast:%d %s" % (w(gr), ir(k), gr % 16, DPP),
+                  "v_fmac_f64_dpp %%0, -%s, %s row_newbcast:%d %s" % (w(gi), ii(k), gi % 16, DPP),
+                  "v_fmac_f64_dpp %%1, %s, %s row_newbcast:%d %s" % (w(gr), ii(k), gr % 16, DPP),
+                  "v_fmac_f64_dpp %%1, %s, %s row_newbcast:%d %s" % (w(gi), ir(k), gi % 16, DPP)]
+    outs = ['"=&v"(vr)', '"=&v"(vi)']
+    ins = ['"v"(w[%d])' % p for p in ps] + ['"v"(ir[%d])' % k for k in range(M)] + \
+          ['"v"(ii[%d])' % k for k in range(M)]
+    return ("template <> __device__ __forceinline__ void pf_node0<%d>(\n"
+            "    double& vr, double& vi, const double (&w)[%d], const double (&ir)[%d],\n"
+            "    const double (&ii)[%d]) {\n%s}\n" % (M, nr, M, M, asm_stmt(lines, outs, ins)))
 
 
 def gen_column(M, k):
@@ -134,6 +160,9 @@ def main():
            "    double& s_r, double& s_i, const double (&s)[kSPairs], double pc, double qc);",
            "template <int M, int K> __device__ __forceinline__ void pf_band(",
            "    double& lo2, double& mn2, double& mx2, const double (&w)[PFBlock<M>::kPairs]);",
+           "template <int M> __device__ __forceinline__ void pf_node0(",
+           "    double& vr, double& vi, const double (&w)[PFBlock<M>::kPairs], const double (&ir)[M],",
+           "    const double (&ii)[M]);",
            ""]
     for M in SIZES:
         L = block_layout(M)
@@ -141,6 +170,7 @@ def main():
         out.append("// ---- M = %d (%d resident pairs)" % (M, nr))
         out.append(gen_bcast_group("pf_acc_init", M, [L["u0re"], L["u0sum"]], nr))
         out.append(gen_bcast_group("pf_u0", M, [L["u0re"], L["u0im"]], nr))
+        out.append(gen_node0(M, nr))
         for k in range(M):
             out.append(gen_column(M, k))
             out.append(gen_power(M, k, ns))

@@ -50,22 +50,24 @@ __device__ __forceinline__ void static_for(F&& f) {
 //                c T + i M - i(i-1)/2 + (k - i)
 //   [3T, +3M)    u0re[i], u0im[i], u0re[i] + u0im[i]   (u0 = U0 / vb)
 //   [.., +3M)    vlow^2, vmin^2, vmax^2 per element (pu^2)
+//   [.., +2M+2)  output row 0 of the tables (pu): G re, im; V0 re, im
 // The iteration runs on u = U / vb and the scaled currents I' = I vb =
 // conj(S) u g, so u_i = u0_i + sum_k W''_ik I'_k.
 template <int M> struct PFBlock {
   static constexpr int kTri = M * (M + 1) / 2;
   static constexpr int kU0re = 3 * kTri, kU0im = kU0re + M, kU0sum = kU0im + M;
   static constexpr int kLo2 = kU0sum + M, kMn2 = kLo2 + M, kMx2 = kMn2 + M;
-  static constexpr int kSize = kMx2 + M;
+  static constexpr int kG0re = kMx2 + M, kG0im = kG0re + M, kV0re = kG0im + M, kV0im = kV0re + 1;
+  static constexpr int kSize = kV0im + 1;
   static constexpr int kPairs = (kSize + 15) / 16;
 };
-static int64_t pf_block_size(int m) { return 3LL * m * (m + 1) / 2 + 6LL * m; }
+static int64_t pf_block_size(int m) { return 3LL * m * (m + 1) / 2 + 8LL * m + 2; }
 
 // Per-launch scalars derived on the host from pgw_pf_params (pu).
 struct PFArgs {
   double sr0[PGW_PF_MAX_M], si0[PGW_PF_MAX_M];   // s0 = conj(S_base) per phase (W, var)
   double fr[PGW_PF_MAX_M], fi[PGW_PF_MAX_M];     // d s / d (ctrl kW, kvar): slot-0 elements
-  double kw[PGW_PF_MAX_M], kvar[PGW_PF_MAX_M], nph[PGW_PF_MAX_M], inv_vb[PGW_PF_MAX_M];
+  double kw[PGW_PF_MAX_M], kvar[PGW_PF_MAX_M], nph[PGW_PF_MAX_M];
   int32_t ctrl[PGW_PF_MAX_M];
   double lo2, mn2, mx2;                          // band limits when uniform (pu^2)
   double tol2;
@@ -193,23 +195,27 @@ template <int M, bool UB, bool GC> struct PFSolver {
     return (int32_t)sg;
   }
 
-  // Quadratic through predictor grid points a, a+1, a+2 at grid coordinate g.
-  __device__ __forceinline__ void pred_quad(const double* U_pred, int a, double g) {
-    const double t = g - (double)(a + 1);
-    const double wm = 0.5 * t * (t - 1.0), w0 = 1.0 - t * t, wp = 0.5 * t * (t + 1.0);
-    const double2* P = reinterpret_cast<const double2*>(U_pred) + (int64_t)a * M;
+  // Quadratic of predictor record c (pgw_pf_pred_pack) at grid coordinate g:
+  // u = u_c + t (d1/2 + t d2/2), t = g - c.
+  __device__ __forceinline__ void pred_quad(const double* rec, int c, double g) {
+    const double t = g - (double)c;
+    const double h1 = 0.5 * t, h2 = 0.5 * t * t;
+    const char* r = reinterpret_cast<const char*>(rec) + (int64_t)c * (32 * M);
+    const double2* v = reinterpret_cast<const double2*>(r);
+    const float2* d1 = reinterpret_cast<const float2*>(r + 16 * M);
+    const float2* d2 = reinterpret_cast<const float2*>(r + 24 * M);
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-      const double2 pm = P[k], p0 = P[M + k], pp = P[2 * M + k];
-      ur[k] = fma(wp, pp.x, fma(w0, p0.x, wm * pm.x));
-      ui[k] = fma(wp, pp.y, fma(w0, p0.y, wm * pm.y));
+      const double2 u = v[k];
+      const float2 a1 = d1[k], a2 = d2[k];
+      ur[k] = fma(h2, (double)a2.x, fma(h1, (double)a1.x, u.x));
+      ui[k] = fma(h2, (double)a2.y, fma(h1, (double)a1.y, u.y));
     }
   }
 
-  // Initial guess: per-env U_init; or the predictor -- the quadratic through the
-  // 3 grid solutions nearest pc, moved to the nearest stencil whose 3 points
-  // share the band signature of that first guess when the centred one
-  // straddles a band switch; or u0.
+  // Initial guess: per-env U_init; or the predictor -- the quadratic through 3
+  // grid solutions, the stencil chosen per grid segment by pgw_pf_pred_meta so
+  // that it never straddles a load-band switch; or u0.
   __device__ __forceinline__ void initial(const PFArgs& a, const pgw_pf_tables& t, int64_t e,
                                           bool valid) {
     if (t.U_init) {
@@ -222,28 +228,15 @@ template <int M, bool UB, bool GC> struct PFSolver {
       }
     } else if (a.use_pred) {
       const double g = (pc - a.pred_x0) * a.pred_inv_h;
-      const int s = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
-      // signatures of grid points s-3 .. s+3, loaded with the first gather
-      int32_t sv[7];
-      bool in[7];
-      const bool sig = t.U_pred_sig != nullptr;
-#pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        const int q = s - 3 + j;
-        in[j] = q >= 0 && q < a.pred_n;
-        sv[j] = sig ? t.U_pred_sig[in[j] ? q : s] : 0;
+      int c;
+      if (t.U_pred_meta) {
+        const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
+        const pgw_pred_meta m = t.U_pred_meta[j];
+        c = (g - (double)j < m.tstar) ? m.left : m.right;
+      } else {
+        c = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
       }
-      pred_quad(t.U_pred, s - 1, g);
-      if (sig) {
-        const int32_t sg = signature();
-        auto same = [&](int j) {           // stencil starting at grid point s - 3 + j
-          return in[j] && in[j + 2] && sv[j] == sg && sv[j + 1] == sg && sv[j + 2] == sg;
-        };
-        if (!same(2)) {
-          const int pick = same(3) ? 3 : same(1) ? 1 : same(4) ? 4 : same(0) ? 0 : -1;
-          if (pick >= 0) pred_quad(t.U_pred, s - 3 + pick, g);
-        }
-      }
+      pred_quad(t.U_pred, c, g);
     } else {
       pf_u0<M>(ur, ui, w);
     }
@@ -299,21 +292,38 @@ template <int M, bool UB, bool GC> struct PFSolver {
     return my_it;
   }
 
-  // physical element currents (A) for the node-voltage rows
-  __device__ __forceinline__ void currents(const PFArgs& a, double* ir, double* ii) const {
-    static_for<0, M>([&](auto k) {
-      current<k>(ir[k], ii[k]);
-      ir[k] *= a.inv_vb[k];
-      ii[k] *= a.inv_vb[k];
-    });
+  // scaled element currents I' = I vb of the final voltages
+  __device__ __forceinline__ void currents(double (&ir)[M], double (&ii)[M]) const {
+    static_for<0, M>([&](auto k) { current<k>(ir[k], ii[k]); });
+  }
+
+  // |V| pu of output node 0 from the resident row (whole wave: DPP)
+  __device__ __forceinline__ double node0_pu(const double (&ir)[M], const double (&ii)[M]) const {
+    double vr, vi;
+    pf_node0<M>(vr, vi, w, ir, ii);
+    return sqrt(fma(vi, vi, vr * vr));
   }
 };
 
 // |V| pu of output node o: V0 + sum_k G[o][k] I_k (wave-uniform G, V0 rows
 // through the scalar cache).
+// Debug phase trace (pgw_debug_pf_trace): when set, lane 0 of every k_coord_pf
+// wave records wall_clock64() (100 MHz) at each phase boundary.
+__device__ long long* g_pf_trace = nullptr;
+__device__ __forceinline__ void pf_trace(int phase) {
+  long long* tr = g_pf_trace;
+  if (tr && (threadIdx.x & 63) == 0) {
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    tr[wave * 8 + phase] = wall_clock64();
+  }
+}
+
 typedef const __attribute__((address_space(4))) double* sdptr;
 __device__ __forceinline__ sdptr scalar_ptr(const double* p) { return (sdptr)p; }
 
+// (ir, ii: the scaled currents I' = I vb; the rows are pu-scaled on the host.
+// The same operations in the same order as the resident node-0 group, so an
+// output node gets bit-identical voltages whichever row it occupies.)
 template <int M>
 __device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, const double* ir,
                                              const double* ii) {
@@ -327,7 +337,7 @@ __device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, cons
     vi = fma(gr, ii[k], vi);
     vi = fma(gi, ir[k], vi);
   }
-  return sqrt(fma(vi, vi, vr * vr)) * scalar_ptr(t.inv_vbase_out)[o];
+  return sqrt(fma(vi, vi, vr * vr));
 }
 
 template <int M, bool UB, bool GC>
@@ -351,11 +361,13 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   S.initial(a, t, e, valid);
   const int it = S.iterate(a.max_iter, valid);
   double ir[M], ii[M];
-  S.currents(a, ir, ii);
+  S.currents(ir, ii);
   const int32_t sig = t.sig_out ? S.signature() : 0;
+  const double v0 = a.n_out > 0 ? S.node0_pu(ir, ii) : 0.0;
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
-  for (int o = 0; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
+  if (a.n_out > 0) v_out[e] = v0;
+  for (int o = 1; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
   if (t.U_out) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
@@ -440,106 +452,128 @@ struct StdAgentIn {
   double soc;
 };
 
-__device__ __forceinline__ void std_agent_load(const pgw_coord_buffers& b, int a, int64_t e,
-                                               int64_t n, StdAgentIn& in) {
-  const double* ap = b.action.ptr + a * b.act_stride_agent + e * b.action.s_env;
-  const int64_t sd = b.action.s_dim;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) in.av[j] = ap[j * sd];
-  const double* xp = b.x + (int64_t)a * 5 * n + e;
-#pragma unroll
-  for (int z = 0; z < 5; ++z) in.xs[z] = xp[z * n];
-  in.soc = b.soc[(int64_t)a * n + e];
-}
+// Output slots handed to the store callback as soon as they are final.
+enum StdSlot { kSlotX = 0, kSlotSoc = 5, kSlotObs = 6, kSlotPower = 23, kSlotReward = 24 };
 
-// One standard agent step for env e: writes x_k, SoC and the 17 observations;
-// returns the agent's real power and (pre-transform) reward.
-__device__ __forceinline__ void std_agent_step(const pgw_coord_params& p, const pgw_coord_step_info& s,
-                                               const pgw_coord_buffers& b, int a, int64_t e,
-                                               int64_t n, double pv_ob, StdAgentIn& in,
-                                               double& agent_rp, double& agent_rew) {
+// One standard agent step for E envs at once (E = 1 or 2, computed stage by
+// stage so both envs' chains interleave); every output goes to
+// store(slot, v[E]) the moment it is final, so no output stays live.
+template <int E, class Store>
+__device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p,
+                                                  const pgw_coord_step_info& s, double pv_ob,
+                                                  StdAgentIn (&in)[E], Store&& store) {
   const pgw_building_params& B = p.bld;
-  double* av = in.av;
-  double* xs = in.xs;
-  double* xp = b.x + (int64_t)a * 5 * n + e;
-  double T[5];
+  double T[E][5], v[E];
   // ---- building
 #pragma unroll
-  for (int j = 0; j < 6; ++j) av[j] = B.rescale ? to_raw(av[j], B.act_low[j], B.act_high[j]) : av[j];
+  for (int q = 0; q < E; ++q) {
 #pragma unroll
-  for (int z = 0; z < 5; ++z) T[z] = B.C[z] * xs[z] + B.mean[z];
-  double nb[5];
-  nb[0] = T[4]; nb[1] = T[4]; nb[2] = T[3]; nb[3] = T[2]; nb[4] = T[2];
+    for (int j = 0; j < 6; ++j)
+      in[q].av[j] = B.rescale ? to_raw(in[q].av[j], B.act_low[j], B.act_high[j]) : in[q].av[j];
 #pragma unroll
-  for (int z = 0; z < 5; ++z) {
-    const double u0 = s.ex_t.T_oa - T[z];
-    const double u1 = av[z] * (av[5] - T[z]);
-    const double u2 = nb[z] - T[z];
-    const double u3 = s.ex_t.q_solar[z];
-    double bu = B.B[z][0] * u0;
-    bu = bu + B.B[z][1] * u1;
-    bu = bu + B.B[z][2] * u2;
-    bu = bu + B.B[z][3] * u3;
-    xs[z] = B.A[z] * xs[z] + bu;
+    for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
   }
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
-    xp[z * n] = xs[z];
-    T[z] = B.C[z] * xs[z] + B.mean[z];
+    const int nz = z < 2 ? 4 : (z == 2 ? 3 : 2);
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+      const double u0 = s.ex_t.T_oa - T[q][z];
+      const double u1 = in[q].av[z] * (in[q].av[5] - T[q][z]);
+      const double u2 = T[q][nz] - T[q][z];
+      const double u3 = s.ex_t.q_solar[z];
+      double bu = B.B[z][0] * u0;
+      bu = bu + B.B[z][1] * u1;
+      bu = bu + B.B[z][2] * u2;
+      bu = bu + B.B[z][3] * u3;
+      in[q].xs[z] = B.A[z] * in[q].xs[z] + bu;   // T[q][*] still holds the pre-step temps
+      v[q] = in[q].xs[z];
+    }
+    store(kSlotX + z, v);
   }
-  const double pc = building_p_consumed(av, s.ex_t.T_oa);
+  double pc[E], r_bld[E];
+#pragma unroll
+  for (int q = 0; q < E; ++q) {
+#pragma unroll
+    for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
+    pc[q] = building_p_consumed(in[q].av, s.ex_t.T_oa);
+    r_bld[q] = building_reward(B, T[q], s.ex_next.comfort_lb, s.ex_next.comfort_ub, pc[q]);
+  }
   const double lb = s.ex_next.comfort_lb, ub = s.ex_next.comfort_ub;
-  const double r_bld = building_reward(B, T, lb, ub, pc);
-  double* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;
-  const int64_t so = b.obs.s_dim;
-  double ov[15];
-#pragma unroll
-  for (int z = 0; z < 5; ++z) {
-    ov[z] = T[z] - ub;
-    ov[5 + z] = lb - T[z];
-  }
-  ov[10] = lb;
-  ov[11] = ub;
-  ov[12] = s.ex_next.T_oa;
-  ov[13] = pc;
-  ov[14] = s.ex_next.time_of_day;
 #pragma unroll
   for (int j = 0; j < 15; ++j) {
-    double v = clip(ov[j], B.obs_low[j], B.obs_high[j]);
-    if (B.rescale) v = to_scaled(v, B.obs_low[j], B.obs_high[j]);
-    op[j * so] = v;
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+      const double o = j < 5 ? T[q][j] - ub : j < 10 ? lb - T[q][j - 5] : j == 10 ? lb
+                     : j == 11 ? ub : j == 12 ? s.ex_next.T_oa : j == 13 ? pc[q] : s.ex_next.time_of_day;
+      double c = clip(o, B.obs_low[j], B.obs_high[j]);
+      if (B.rescale) c = to_scaled(c, B.obs_low[j], B.obs_high[j]);
+      v[q] = c;
+    }
+    store(kSlotObs + j, v);
   }
   // ---- pv (obs is env-independent: computed once on the host)
-  op[15 * so] = pv_ob;
-  const double rp_pv = pv_real_power(p.pv, av[6], s.pv_pmax);
+#pragma unroll
+  for (int q = 0; q < E; ++q) v[q] = pv_ob;
+  store(kSlotObs + 15, v);
+  double rp_pv[E], power[E];
+#pragma unroll
+  for (int q = 0; q < E; ++q) rp_pv[q] = pv_real_power(p.pv, in[q].av[6], s.pv_pmax);
   // ---- storage
-  double soc = in.soc;
-  const double power = battery_step(p.bat, av[7], soc);
-  b.soc[(int64_t)a * n + e] = soc;
-  op[16 * so] = battery_obs(p.bat, soc);
+#pragma unroll
+  for (int q = 0; q < E; ++q) {
+    power[q] = battery_step(p.bat, in[q].av[7], in[q].soc);
+    v[q] = in[q].soc;
+  }
+  store(kSlotSoc, v);
+#pragma unroll
+  for (int q = 0; q < E; ++q) v[q] = battery_obs(p.bat, in[q].soc);
+  store(kSlotObs + 16, v);
   // MultiComponentEnv sums (base.py:131-137)
-  agent_rp = 0.0;
-  agent_rp = agent_rp + pc;
-  agent_rp = agent_rp + rp_pv;
-  agent_rp = agent_rp + (-power);
-  agent_rew = 0.0;
-  agent_rew = agent_rew + r_bld;
-  agent_rew = agent_rew + 0.0;
-  agent_rew = agent_rew + 0.0;
+#pragma unroll
+  for (int q = 0; q < E; ++q) {
+    double agent_rp = 0.0;
+    agent_rp = agent_rp + pc[q];
+    agent_rp = agent_rp + rp_pv[q];
+    agent_rp = agent_rp + (-power[q]);
+    v[q] = agent_rp;
+  }
+  store(kSlotPower, v);
+#pragma unroll
+  for (int q = 0; q < E; ++q) {
+    double agent_rew = 0.0;
+    agent_rew = agent_rew + r_bld[q];
+    agent_rew = agent_rew + 0.0;
+    agent_rew = agent_rew + 0.0;
+    v[q] = agent_rew;
+  }
+  store(kSlotReward, v);
 }
 
+// Scalar variant: one thread per (env, agent), any action layout.
 __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
                                                              pgw_coord_step_info s, int64_t n,
                                                              pgw_coord_buffers b, double pv_ob) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int a = blockIdx.y;
   if (e >= n) return;
-  StdAgentIn in;
-  std_agent_load(b, a, e, n, in);
-  double agent_rp, agent_rew;
-  std_agent_step(p, s, b, a, e, n, pv_ob, in, agent_rp, agent_rew);
-  b.agent_power[(int64_t)a * n + e] = agent_rp;
-  b.reward[(int64_t)a * n + e] = agent_rew;
+  StdAgentIn in[1];
+  const double* ap = b.action.ptr + a * b.act_stride_agent + e * b.action.s_env;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) in[0].av[j] = ap[j * b.action.s_dim];
+  double* xp = b.x + (int64_t)a * 5 * n + e;
+#pragma unroll
+  for (int z = 0; z < 5; ++z) in[0].xs[z] = xp[z * n];
+  double* socp = b.soc + (int64_t)a * n + e;
+  in[0].soc = *socp;
+  double* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;
+  std_agent_compute<1>(p, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
+    if (slot < kSlotSoc) xp[slot * n] = v[0];
+    else if (slot == kSlotSoc) *socp = v[0];
+    else if (slot < kSlotPower) op[(slot - kSlotObs) * b.obs.s_dim] = v[0];
+    else if (slot == kSlotPower) b.agent_power[(int64_t)a * n + e] = v[0];
+    else b.reward[(int64_t)a * n + e] = v[0];
+  });
 }
 
 static bool coord_is_std(const pgw_coord_params& p) {
@@ -572,6 +606,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
                                                      int64_t n, pgw_coord_buffers b) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
+  pf_trace(0);
   // HBM first: the agent powers gate the predictor
   double rp[PGW_MAX_AGENTS];
 #pragma unroll
@@ -593,18 +628,25 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
   S.powers(a, cp, cq, 1.0);
+  pf_trace(1);
   S.initial(a, t, e, valid);
+  pf_trace(2);
   const int it = S.iterate(a.max_iter, valid);
+  pf_trace(3);
   double ir[M], ii[M];
-  S.currents(a, ir, ii);
+  S.currents(ir, ii);
+  const double v0 = S.node0_pu(ir, ii);
+  pf_trace(4);
   if (!valid) return;
-  double vsel = 0.0;
-  for (int o = 0; o < a.n_out; ++o) {
+  double vsel = v0;
+  if (b.v_out) b.v_out[e] = v0;
+  for (int o = 1; o < a.n_out; ++o) {
     const double v = pf_node_pu<M>(t, o, ir, ii);
     if (b.v_out) b.v_out[(int64_t)o * n + e] = v;
     vsel = (o == c.vv_row) ? v : vsel;
   }
   if (b.iters) b.iters[e] = it;
+  pf_trace(5);
   if (c.coordinated) {
     const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
     if (b.vv) b.vv[e] = vv;
@@ -617,6 +659,91 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
       if (ag < c.n_agents)
         (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, -share, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Stencil metadata of the predictor grid (one thread per segment): in a
+// segment whose two ends share the band signature the switch sits at t* = 1/2
+// (the nearest-point rule) and both sides use a 3-point stencil of that
+// signature around the segment; in a segment where the signature changes, t*
+// is where the first switching element's |u|^2 crosses its band limit (linear
+// in the segment) and each side takes the nearest 3 points of its own
+// signature.  No matching stencil -> the plain one.
+__global__ void __launch_bounds__(kBlock) k_pf_pred_meta(pgw_pf_params p, int32_t n_tables,
+                                                         int32_t P, const double* __restrict__ U,
+                                                         const int32_t* __restrict__ S,
+                                                         pgw_pred_meta* __restrict__ meta) {
+  const int64_t id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t nseg = P - 1;
+  if (id >= (int64_t)n_tables * nseg) return;
+  const int tab = (int)(id / nseg), j = (int)(id - (int64_t)tab * nseg);
+  const int32_t* Sg = S + (int64_t)tab * P;
+  const double2* Ut = reinterpret_cast<const double2*>(U) + (int64_t)tab * P * p.m;
+  auto same = [&](int a, int32_t sg) {
+    return a >= 0 && a + 2 <= P - 1 && Sg[a] == sg && Sg[a + 1] == sg && Sg[a + 2] == sg;
+  };
+  const int plain_l = max(0, min(j - 1, P - 3)), plain_r = max(0, min(j, P - 3));
+  pgw_pred_meta m;
+  m.tstar = 0.5;
+  m.left = plain_l;
+  m.right = plain_r;
+  const int32_t s0 = Sg[j], s1 = Sg[j + 1];
+  if (s0 == s1) {
+    const int cl[4] = {j - 1, j, j - 2, j + 1}, cr[4] = {j, j - 1, j + 1, j - 2};
+    for (int q = 3; q >= 0; --q) {
+      if (same(cl[q], s0)) m.left = cl[q];
+      if (same(cr[q], s0)) m.right = cr[q];
+    }
+  } else {
+    if (same(j - 2, s0)) m.left = j - 2;
+    else if (same(j - 3, s0)) m.left = j - 3;
+    if (same(j + 1, s1)) m.right = j + 1;
+    else if (same(j + 2, s1)) m.right = j + 2;
+    // the first element whose band differs between the two ends
+    for (int k = 0; k < p.m; ++k) {
+      const int b0 = (s0 >> (2 * k)) & 3, b1 = (s1 >> (2 * k)) & 3;
+      if (b0 == b1) continue;
+      const int lvl = min(b0, b1);   // boundary between band lvl and lvl + 1
+      const double lim = lvl == 0 ? p.vlow[k] : lvl == 1 ? p.vmin[k] : p.vmax[k];
+      const double thr = lim * lim;
+      const double2 u0 = Ut[(int64_t)j * p.m + k], u1 = Ut[(int64_t)(j + 1) * p.m + k];
+      const double m0 = u0.x * u0.x + u0.y * u0.y, m1 = u1.x * u1.x + u1.y * u1.y;
+      m.tstar = (m1 != m0) ? fmin(fmax((thr - m0) / (m1 - m0), 0.0), 1.0) : 0.5;
+      break;
+    }
+  }
+  m.left += 1;      // stencil start -> record (centre) index
+  m.right += 1;
+  meta[id] = m;
+}
+
+// Predictor records (one thread per grid point): value fp64 + centred first and
+// second differences fp32 (end points take their interior neighbour's).
+template <int M>
+__global__ void __launch_bounds__(kBlock) k_pf_pred_pack(int32_t n_tables, int32_t P,
+                                                         const double* __restrict__ U,
+                                                         double* __restrict__ rec) {
+  const int64_t id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (id >= (int64_t)n_tables * P) return;
+  const int tab = (int)(id / P), j = (int)(id - (int64_t)tab * P);
+  const int cj = min(max(j, 1), P - 2);
+  const double2* Ut = reinterpret_cast<const double2*>(U) + (int64_t)tab * P * M;
+  char* r = reinterpret_cast<char*>(rec) + id * (32 * M);
+  double2* v = reinterpret_cast<double2*>(r);
+  float2* d1 = reinterpret_cast<float2*>(r + 16 * M);
+  float2* d2 = reinterpret_cast<float2*>(r + 24 * M);
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double2 um = Ut[(int64_t)(cj - 1) * M + k], u0 = Ut[(int64_t)cj * M + k],
+                  up = Ut[(int64_t)(cj + 1) * M + k];
+    v[k] = Ut[(int64_t)j * M + k];
+    // differences about cj; a record at j != cj (grid ends) re-centres: with
+    // s = j - cj, u_j + t d1/2 + t^2 d2/2 must equal the quadratic of cj at t + s
+    const double s = (double)(j - cj);
+    const double g1r = (up.x - um.x) + s * 2.0 * (up.x - 2.0 * u0.x + um.x);
+    const double g1i = (up.y - um.y) + s * 2.0 * (up.y - 2.0 * u0.y + um.y);
+    d1[k] = make_float2((float)g1r, (float)g1i);
+    d2[k] = make_float2((float)(up.x - 2.0 * u0.x + um.x), (float)(up.y - 2.0 * u0.y + um.y));
   }
 }
 
@@ -634,7 +761,7 @@ static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
   PFArgs a = {};
   for (int k = 0; k < PGW_PF_MAX_M; ++k) {
     const bool real = k < p.m;
-    const double nph = real ? p.nph[k] : 1.0, vb = real ? p.vbase[k] : 1.0;
+    const double nph = real ? p.nph[k] : 1.0;
     const double sw = real ? (p.base_kw[k] * 1000.0) / nph : 0.0;
     const double sv = real ? (p.base_kvar[k] * 1000.0) / nph : 0.0;
     const int c = real ? p.elem_ctrl[k] : -1;
@@ -645,7 +772,6 @@ static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
     a.kw[k] = real ? p.base_kw[k] : 0.0;
     a.kvar[k] = real ? p.base_kvar[k] : 0.0;
     a.nph[k] = nph;
-    a.inv_vb[k] = 1.0 / vb;
     a.ctrl[k] = c;
   }
   a.lo2 = p.vlow[0] * p.vlow[0];
@@ -701,10 +827,49 @@ extern "C" {
 
 int32_t pgw_pf_padded_m(int32_t m) { return padded_m(m); }
 
+int32_t pgw_pf_pred_meta(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,
+                         const double* U_pred, const int32_t* sig, pgw_pred_meta* meta,
+                         void* stream) {
+  PGW_REQUIRE(p && U_pred && sig && meta, "pgw_pf_pred_meta: null argument");
+  PGW_REQUIRE(n_tables >= 0 && n_points >= 3, "pgw_pf_pred_meta: need >= 3 grid points");
+  PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M, "pgw_pf_pred_meta: bad m");
+  const int64_t total = (int64_t)n_tables * (n_points - 1);
+  if (total == 0) return PGW_OK;
+  hipLaunchKernelGGL(k_pf_pred_meta, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream,
+                     *p, n_tables, n_points, U_pred, sig, meta);
+  return check_launch("k_pf_pred_meta");
+}
+
+int32_t pgw_pf_pred_pack(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,
+                         const double* U_grid, double* rec, void* stream) {
+  PGW_REQUIRE(p && U_grid && rec, "pgw_pf_pred_pack: null argument");
+  PGW_REQUIRE(n_tables >= 0 && n_points >= 3, "pgw_pf_pred_pack: need >= 3 grid points");
+  PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M && p->m == padded_m(p->m),
+              "pgw_pf_pred_pack: m=%d not padded", p->m);
+  PGW_REQUIRE((reinterpret_cast<uintptr_t>(rec) & 15) == 0, "pgw_pf_pred_pack: rec not 16-byte aligned");
+  const int64_t total = (int64_t)n_tables * n_points;
+  if (total == 0) return PGW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (p->m) {
+    case 8: hipLaunchKernelGGL(k_pf_pred_pack<8>, dim3(grid_for(total)), dim3(kBlock), 0, st, n_tables, n_points, U_grid, rec); break;
+    case 14: hipLaunchKernelGGL(k_pf_pred_pack<14>, dim3(grid_for(total)), dim3(kBlock), 0, st, n_tables, n_points, U_grid, rec); break;
+    default: hipLaunchKernelGGL(k_pf_pred_pack<16>, dim3(grid_for(total)), dim3(kBlock), 0, st, n_tables, n_points, U_grid, rec); break;
+  }
+  return check_launch("k_pf_pred_pack");
+}
+
+int32_t pgw_debug_pf_trace(long long* buf) {
+  PGW_REQUIRE(hipMemcpyToSymbol(HIP_SYMBOL(g_pf_trace), &buf, sizeof(buf)) == hipSuccess,
+              "pgw_debug_pf_trace: hipMemcpyToSymbol failed");
+  return PGW_OK;
+}
+
 int64_t pgw_pf_pack_size(int32_t m) { return pf_block_size(m); }
 
-int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, double* out) {
+int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, const double* G0,
+                    const double* V0_0, double* out) {
   PGW_REQUIRE(p && W && U0 && out, "pgw_pf_pack: null argument");
+  PGW_REQUIRE(p->n_out == 0 || (G0 && V0_0), "pgw_pf_pack: output node 0 row missing");
   const int M = p->m;
   PGW_REQUIRE(M >= 1 && M <= PGW_PF_MAX_M && M == padded_m(M), "pgw_pf_pack: m=%d not padded", M);
   for (int k = 0; k < M; ++k)
@@ -739,7 +904,12 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, d
     out[u0 + 3 * M + k] = p->vlow[k] * p->vlow[k];
     out[u0 + 4 * M + k] = p->vmin[k] * p->vmin[k];
     out[u0 + 5 * M + k] = p->vmax[k] * p->vmax[k];
+    // output row 0 of the tables, verbatim (already in pu against I'_k)
+    out[u0 + 6 * M + k] = G0 ? G0[2 * k] : 0.0;
+    out[u0 + 7 * M + k] = G0 ? G0[2 * k + 1] : 0.0;
   }
+  out[u0 + 8 * M] = V0_0 ? V0_0[0] : 0.0;
+  out[u0 + 8 * M + 1] = V0_0 ? V0_0[1] : 0.0;
   return PGW_OK;
 }
 
@@ -750,7 +920,7 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M && p->m == padded_m(p->m),
               "pgw_pf_solve: m=%d not padded (pgw_pf_padded_m)", p->m);
   PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve: bad n_ctrl");
-  PGW_REQUIRE(p->n_out == 0 || (v_out && t->G && t->V0 && t->inv_vbase_out),
+  PGW_REQUIRE(p->n_out == 0 || (v_out && t->G && t->V0),
               "pgw_pf_solve: missing v_out/G/V0");
   PGW_REQUIRE(p->max_iter >= 1, "pgw_pf_solve: max_iter < 1");
   if (n == 0) return PGW_OK;
@@ -771,7 +941,7 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
               "pgw_coord_step: pf m=%d not padded", pf->m);
   PGW_REQUIRE(pf->n_out >= 1 && p->vv_row >= 0 && p->vv_row < pf->n_out,
               "pgw_coord_step: bad vv_row");
-  PGW_REQUIRE(pft->G && pft->V0 && pft->inv_vbase_out, "pgw_coord_step: missing G/V0");
+  PGW_REQUIRE(pft->G && pft->V0, "pgw_coord_step: missing G/V0");
   PGW_REQUIRE(pf->max_iter >= 1, "pgw_coord_step: max_iter < 1");
   PGW_REQUIRE(pf->n_ctrl >= 0 && pf->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_coord_step: bad n_ctrl");
   for (int a = 0; a < p->n_agents; ++a)

@@ -54,7 +54,7 @@ class OpenDSSSolver(PowerFlowSolver):
     # starts each env from the quadratic through 3 grid solutions near its
     # controllable kW (chosen so that they share its load-band signature).  Envs
     # outside the grid extrapolate (more iterations, same result).
-    PREDICTOR_X0, PREDICTOR_H, PREDICTOR_N = -500.0, 2.5, 801
+    PREDICTOR_X0, PREDICTOR_H, PREDICTOR_N = -500.0, 0.625, 3201
     PREDICTOR_TOL = 1e-12
     PREDICTOR_MAX_TABLES = 64      # hours kept on the device (~180 KB each)
     PREDICTOR_LOOKAHEAD = 24       # hours solved per table launch
@@ -96,24 +96,35 @@ class OpenDSSSolver(PowerFlowSolver):
         as_dev = lambda c: torch.tensor(np.ascontiguousarray(c).view(np.float64).ravel(),
                                         dtype=torch.float64, device=dev)
         block = np.zeros(int(_lib.lib().pgw_pf_pack_size(M)))
+        # output rows in pu against the scaled currents I'_k = I_k vb_k
+        vb_elem = np.array([self.params.vbase[k] for k in range(M)])
+        inv_vb_out = 1.0 / (f.kv_ln[idx] * 1000.0)
+        Gs = (G / vb_elem[None, :]) * inv_vb_out[:, None]
+        V0s = V0o * inv_vb_out
         Wf = np.ascontiguousarray(W).view(np.float64).ravel()
         U0f = np.ascontiguousarray(U0).view(np.float64).ravel()
+        G0 = np.ascontiguousarray(Gs[0]).view(np.float64).ravel()
+        V00 = np.ascontiguousarray(V0s[:1]).view(np.float64).ravel()
         cp = lambda a: a.ctypes.data_as(_lib.C.c_void_p)
-        _lib.check(_lib.lib().pgw_pf_pack(self.params, cp(Wf), cp(U0f), cp(block)))
+        _lib.check(_lib.lib().pgw_pf_pack(self.params, cp(Wf), cp(U0f), cp(G0), cp(V00), cp(block)))
         self._block = torch.tensor(block, dtype=torch.float64, device=dev)
-        self._G, self._V0 = as_dev(G), as_dev(V0o)
-        self._inv_vb = torch.tensor(1.0 / (f.kv_ln[idx] * 1000.0), dtype=torch.float64, device=dev)
+        self._G, self._V0 = as_dev(Gs), as_dev(V0s)
         self.tables = _lib.PFTables(block=self._block.data_ptr(), G=self._G.data_ptr(),
-                                    V0=self._V0.data_ptr(), inv_vbase_out=self._inv_vb.data_ptr())
+                                    V0=self._V0.data_ptr())
         self.v_out = torch.zeros((max(len(names), 1), self.num_envs), dtype=torch.float64, device=dev)
         self._iters = torch.zeros(self.num_envs, dtype=torch.int32, device=dev)
         n_pred = self.PREDICTOR_N
         self._pred_x = torch.tensor([[self.PREDICTOR_X0 + j * self.PREDICTOR_H for j in range(n_pred)]],
                                     dtype=torch.float64, device=dev)
-        # preallocated: cached PFTables hold raw pointers into these
-        self._pred_table = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred, M, 2), dtype=torch.float64,
+        # preallocated: cached PFTables hold raw pointers into these.  Records
+        # (pgw_pf_pred_pack) are 32 M bytes = 4 M doubles per grid point.
+        self._pred_table = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred, 4 * M), dtype=torch.float64,
                                        device=dev)
+        self._pred_grid = None                         # scratch: grid solutions of one batch
         self._pred_sig = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred), dtype=torch.int32, device=dev)
+        # pgw_pred_meta per grid segment: (tstar f64, left i32, right i32) = 2 x 8 bytes
+        self._pred_meta = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred - 1, 2), dtype=torch.float64,
+                                      device=dev)
         self._pred_index = {}
 
     def set_controllable_loads(self, names):
@@ -201,7 +212,7 @@ class OpenDSSSolver(PowerFlowSolver):
             idx = self._pred_index[self._hour_key(hour)]
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.U_pred = self._pred_table[idx].data_ptr()
-        t.U_pred_sig = self._pred_sig[idx].data_ptr()
+        t.U_pred_meta = self._pred_meta[idx].data_ptr()
         if len(self._tables_cache) > 4096:
             self._tables_cache.clear()
         self._tables_cache[key] = t
@@ -244,13 +255,21 @@ class OpenDSSSolver(PowerFlowSolver):
                              device=dev)
         cp = self._pred_x.repeat(1, H)
         cq = torch.zeros_like(cp)
+        if self._pred_grid is None or self._pred_grid.shape[0] < H * P:
+            self._pred_grid = torch.empty((self.PREDICTOR_LOOKAHEAD * P, self.M, 2), dtype=torch.float64,
+                                          device=dev)
+        grid = self._pred_grid
         tb = _lib.PFTables.from_buffer_copy(self.tables)
         tb.U_pred = None
-        tb.U_out = self._pred_table[idx0].data_ptr()
+        tb.U_out = grid.data_ptr()
         tb.sig_out = self._pred_sig[idx0].data_ptr()
         tb.load_scale = scale.data_ptr()
-        _lib.check(_lib.lib().pgw_pf_solve(sp, tb, H * P, _lib.dptr(cp), _lib.dptr(cq), None, None,
-                                           _lib.stream_ptr(dev)))
+        st = _lib.stream_ptr(dev)
+        lib = _lib.lib()
+        _lib.check(lib.pgw_pf_solve(sp, tb, H * P, _lib.dptr(cp), _lib.dptr(cq), None, None, st))
+        _lib.check(lib.pgw_pf_pred_meta(sp, H, P, grid.data_ptr(), self._pred_sig[idx0].data_ptr(),
+                                        self._pred_meta[idx0].data_ptr(), st))
+        _lib.check(lib.pgw_pf_pred_pack(sp, H, P, grid.data_ptr(), self._pred_table[idx0].data_ptr(), st))
         self._pred_keepalive = (scale, cp, cq)     # until the stream has consumed them
 
     # ------------------------------------------------------------ reference API
