@@ -666,9 +666,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
 // segment whose two ends share the band signature the switch sits at t* = 1/2
 // (the nearest-point rule) and both sides use a 3-point stencil of that
 // signature around the segment; in a segment where the signature changes, t*
-// is where the first switching element's |u|^2 crosses its band limit (linear
-// in the segment) and each side takes the nearest 3 points of its own
-// signature.  No matching stencil -> the plain one.
+// is where the first switching element's |u|^2 crosses its band limit (Newton
+// on one side's quadratic, from the linear estimate) and each side takes the
+// nearest 3 points of its own signature.  No matching stencil -> the plain one.
 __global__ void __launch_bounds__(kBlock) k_pf_pred_meta(pgw_pf_params p, int32_t n_tables,
                                                          int32_t P, const double* __restrict__ U,
                                                          const int32_t* __restrict__ S,
@@ -695,8 +695,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_pred_meta(pgw_pf_params p, int32_
       if (same(cr[q], s0)) m.right = cr[q];
     }
   } else {
-    if (same(j - 2, s0)) m.left = j - 2;
-    else if (same(j - 3, s0)) m.left = j - 3;
+    bool have_left = false;
+    if (same(j - 2, s0)) { m.left = j - 2; have_left = true; }
+    else if (same(j - 3, s0)) { m.left = j - 3; have_left = true; }
     if (same(j + 1, s1)) m.right = j + 1;
     else if (same(j + 2, s1)) m.right = j + 2;
     // the first element whose band differs between the two ends
@@ -706,9 +707,26 @@ __global__ void __launch_bounds__(kBlock) k_pf_pred_meta(pgw_pf_params p, int32_
       const int lvl = min(b0, b1);   // boundary between band lvl and lvl + 1
       const double lim = lvl == 0 ? p.vlow[k] : lvl == 1 ? p.vmin[k] : p.vmax[k];
       const double thr = lim * lim;
-      const double2 u0 = Ut[(int64_t)j * p.m + k], u1 = Ut[(int64_t)(j + 1) * p.m + k];
-      const double m0 = u0.x * u0.x + u0.y * u0.y, m1 = u1.x * u1.x + u1.y * u1.y;
-      m.tstar = (m1 != m0) ? fmin(fmax((thr - m0) / (m1 - m0), 0.0), 1.0) : 0.5;
+      const double2 ua = Ut[(int64_t)j * p.m + k], ub = Ut[(int64_t)(j + 1) * p.m + k];
+      const double m0 = ua.x * ua.x + ua.y * ua.y, m1 = ub.x * ub.x + ub.y * ub.y;
+      double ts = (m1 != m0) ? fmin(fmax((thr - m0) / (m1 - m0), 0.0), 1.0) : 0.5;
+      // refine: where the quadratic of one side (smooth up to the switch) crosses
+      // the limit -- the linear estimate is off by a sliver of the segment, and
+      // envs in that sliver would start from the other side's quadratic
+      const int c = (have_left ? m.left : m.right) + 1;
+      const double2 um = Ut[(int64_t)(c - 1) * p.m + k], u0 = Ut[(int64_t)c * p.m + k],
+                    up = Ut[(int64_t)(c + 1) * p.m + k];
+      const double d1r = 0.5 * (up.x - um.x), d1i = 0.5 * (up.y - um.y);
+      const double d2r = 0.5 * (up.x - 2.0 * u0.x + um.x), d2i = 0.5 * (up.y - 2.0 * u0.y + um.y);
+      for (int q = 0; q < 8; ++q) {
+        const double tau = (double)(j - c) + ts;
+        const double ur = u0.x + tau * (d1r + tau * d2r), ui = u0.y + tau * (d1i + tau * d2i);
+        const double dr = d1r + 2.0 * tau * d2r, di = d1i + 2.0 * tau * d2i;
+        const double f = ur * ur + ui * ui - thr, fp = 2.0 * (ur * dr + ui * di);
+        if (fp == 0.0) break;
+        ts = ts - f / fp;
+      }
+      m.tstar = fmin(fmax(ts, 0.0), 1.0);
       break;
     }
   }
