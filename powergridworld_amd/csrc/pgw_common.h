@@ -57,6 +57,18 @@ __device__ __forceinline__ double clip(double x, double lo, double hi) {
   return (y > hi) ? hi : y;
 }
 
+// x / d correctly rounded, from r = RN(1/d): one multiply and two residual
+// corrections (Markstein: r correctly rounded and q1 faithful => q2 = RN(x/d)),
+// i.e. bit-identical to the IEEE quotient -- checked against it by
+// tests/test_cpu_host.py::test_exact_division.  Zero numerators take x * r (the
+// residual step would turn -0 into +0).  For finite x and normal d only.
+__device__ __forceinline__ double exact_div(double x, double d, double r) {
+  const double q0 = x * r;
+  const double q1 = fma(fma(-d, q0, x), r, q0);
+  const double q2 = fma(fma(-d, q1, x), r, q1);
+  return x == 0.0 ? q0 : q2;
+}
+
 // gridworld/utils.py:9-24
 __device__ __forceinline__ double to_scaled(double x, double lo, double hi) {
   x = clip(x, lo, hi);
@@ -82,25 +94,41 @@ __device__ __forceinline__ void st(const pgw_mat& m, int64_t e, int j, double v)
 
 // ---------------------------------------------------------------- battery
 // energy_storage_env.py:100-157.  Returns the (validated) power; updates soc.
-__device__ __forceinline__ double battery_step(const pgw_battery_params& p, double a, double& soc) {
+// `div(x, which)` divides x by eta_d (which 0) or dt_h (which 1).
+template <class Div>
+__device__ __forceinline__ double battery_step_impl(const pgw_battery_params& p, double a, double& soc,
+                                                    Div&& div) {
   if (p.rescale) a = to_raw(a, -1.0, 1.0);
   double power = a * p.max_power;
   // validate_power :112-126 (the clamps omit the efficiencies, as in the reference)
   if (power > 0.0) {
-    if (soc - power * p.dt_h / p.eta_d < p.soc_min)
-      power = pymax(soc - p.soc_min, 0.0) / p.dt_h;
+    if (soc - div(power * p.dt_h, 0) < p.soc_min)
+      power = div(pymax(soc - p.soc_min, 0.0), 1);
   } else if (power < 0.0) {
     if (soc - p.eta_c * power * p.dt_h > p.soc_max)
-      power = -(pymax(p.soc_max - soc, 0.0) / p.dt_h);
+      power = -div(pymax(p.soc_max - soc, 0.0), 1);
   }
   if (power < 0.0) {
     soc = soc - p.eta_c * power * p.dt_h;
     soc = pymin(soc, p.soc_max);
   } else if (power > 0.0) {
-    soc = soc - power * p.dt_h / p.eta_d;
+    soc = soc - div(power * p.dt_h, 0);
     soc = pymax(soc, p.soc_min);
   }
   return power;
+}
+
+__device__ __forceinline__ double battery_step(const pgw_battery_params& p, double a, double& soc) {
+  return battery_step_impl(p, a, soc, [&](double x, int w) { return x / (w ? p.dt_h : p.eta_d); });
+}
+
+// The same step with the divisions done by exact_div from host reciprocals
+// (bit-identical results).
+__device__ __forceinline__ double battery_step_rcp(const pgw_battery_params& p, double a, double& soc,
+                                                   double rcp_eta_d, double rcp_dt_h) {
+  return battery_step_impl(p, a, soc, [&](double x, int w) {
+    return w ? exact_div(x, p.dt_h, rcp_dt_h) : exact_div(x, p.eta_d, rcp_eta_d);
+  });
 }
 
 __device__ __forceinline__ double battery_obs(const pgw_battery_params& p, double soc) {
@@ -181,10 +209,11 @@ __device__ __forceinline__ double building_p_consumed(const double act[6], doubl
   return fan + chiller;
 }
 
-// FiveZoneROMThermalEnergyEnv.step_reward (five_zone_rom_env.py:315-335)
+// FiveZoneROMThermalEnergyEnv.step_reward (five_zone_rom_env.py:315-335);
+// e = -p_cons / 12 (passed in so a caller can divide by reciprocal).
 __device__ __forceinline__ double building_reward(const pgw_building_params& p, const double T[5],
-                                                  double lb, double ub, double p_cons) {
-  double e = -p_cons / 12.0;
+                                                  double lb, double ub, double p_cons, double e) {
+  (void)p_cons;
   double c = 0.0;
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
@@ -194,6 +223,10 @@ __device__ __forceinline__ double building_reward(const pgw_building_params& p, 
   }
   c = -c;
   return p.alpha * e * 0.5 + (1.0 - p.alpha) * c;
+}
+__device__ __forceinline__ double building_reward(const pgw_building_params& p, const double T[5],
+                                                  double lb, double ub, double p_cons) {
+  return building_reward(p, T, lb, ub, p_cons, -p_cons / 12.0);
 }
 
 // get_obs (five_zone_rom_env.py:228-283): values in state-dict order, bounds in

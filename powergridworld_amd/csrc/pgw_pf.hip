@@ -446,6 +446,30 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents(pgw_coord_params p, pgw
 // operation, as the generic device functions (the fused-vs-generic test checks
 // bit equality); only the uniform selects become compile-time indices.
 
+// Per-launch constants of the std agent step, derived on the host with the
+// same IEEE operations the reference applies (lo + hi, hi - lo), plus the
+// reciprocals exact_div needs.
+struct StdDerived {
+  double obs_sum[15], obs_rng[15], obs_rcp[15];   // building obs: lo + hi, hi - lo, 1 / (hi - lo)
+  double bat_sum, bat_rng, bat_rcp;               // SoC range
+  double rcp_eta_d, rcp_dt_h;                     // storage
+};
+
+static StdDerived make_std_derived(const pgw_coord_params& p) {
+  StdDerived d = {};
+  for (int j = 0; j < 15; ++j) {
+    d.obs_sum[j] = p.bld.obs_low[j] + p.bld.obs_high[j];
+    d.obs_rng[j] = p.bld.obs_high[j] - p.bld.obs_low[j];
+    d.obs_rcp[j] = 1.0 / d.obs_rng[j];
+  }
+  d.bat_sum = p.bat.soc_min + p.bat.soc_max;
+  d.bat_rng = p.bat.soc_max - p.bat.soc_min;
+  d.bat_rcp = 1.0 / d.bat_rng;
+  d.rcp_eta_d = 1.0 / p.bat.eta_d;
+  d.rcp_dt_h = 1.0 / p.bat.dt_h;
+  return d;
+}
+
 struct StdAgentIn {
   double av[8];     // actions: building 0..5, pv 6, storage 7
   double xs[5];     // building state x_k
@@ -459,7 +483,7 @@ enum StdSlot { kSlotX = 0, kSlotSoc = 5, kSlotObs = 6, kSlotPower = 23, kSlotRew
 // stage so both envs' chains interleave); every output goes to
 // store(slot, v[E]) the moment it is final, so no output stays live.
 template <int E, class Store>
-__device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p,
+__device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p, const StdDerived& dv,
                                                   const pgw_coord_step_info& s, double pv_ob,
                                                   StdAgentIn (&in)[E], Store&& store) {
   const pgw_building_params& B = p.bld;
@@ -497,7 +521,8 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p,
 #pragma unroll
     for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
     pc[q] = building_p_consumed(in[q].av, s.ex_t.T_oa);
-    r_bld[q] = building_reward(B, T[q], s.ex_next.comfort_lb, s.ex_next.comfort_ub, pc[q]);
+    r_bld[q] = building_reward(B, T[q], s.ex_next.comfort_lb, s.ex_next.comfort_ub, pc[q],
+                               exact_div(-pc[q], 12.0, 1.0 / 12.0));
   }
   const double lb = s.ex_next.comfort_lb, ub = s.ex_next.comfort_ub;
 #pragma unroll
@@ -507,7 +532,7 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p,
       const double o = j < 5 ? T[q][j] - ub : j < 10 ? lb - T[q][j - 5] : j == 10 ? lb
                      : j == 11 ? ub : j == 12 ? s.ex_next.T_oa : j == 13 ? pc[q] : s.ex_next.time_of_day;
       double c = clip(o, B.obs_low[j], B.obs_high[j]);
-      if (B.rescale) c = to_scaled(c, B.obs_low[j], B.obs_high[j]);
+      if (B.rescale) c = exact_div(2.0 * c - dv.obs_sum[j], dv.obs_rng[j], dv.obs_rcp[j]);
       v[q] = c;
     }
     store(kSlotObs + j, v);
@@ -522,12 +547,15 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p,
   // ---- storage
 #pragma unroll
   for (int q = 0; q < E; ++q) {
-    power[q] = battery_step(p.bat, in[q].av[7], in[q].soc);
+    power[q] = battery_step_rcp(p.bat, in[q].av[7], in[q].soc, dv.rcp_eta_d, dv.rcp_dt_h);
     v[q] = in[q].soc;
   }
   store(kSlotSoc, v);
 #pragma unroll
-  for (int q = 0; q < E; ++q) v[q] = battery_obs(p.bat, in[q].soc);
+  for (int q = 0; q < E; ++q) {
+    const double c = clip(in[q].soc, p.bat.soc_min, p.bat.soc_max);
+    v[q] = p.bat.rescale ? exact_div(2.0 * c - dv.bat_sum, dv.bat_rng, dv.bat_rcp) : in[q].soc;
+  }
   store(kSlotObs + 16, v);
   // MultiComponentEnv sums (base.py:131-137)
 #pragma unroll
@@ -553,7 +581,8 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p,
 // Scalar variant: one thread per (env, agent), any action layout.
 __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
                                                              pgw_coord_step_info s, int64_t n,
-                                                             pgw_coord_buffers b, double pv_ob) {
+                                                             pgw_coord_buffers b, double pv_ob,
+                                                             StdDerived dv) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int a = blockIdx.y;
   if (e >= n) return;
@@ -567,7 +596,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
   double* socp = b.soc + (int64_t)a * n + e;
   in[0].soc = *socp;
   double* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;
-  std_agent_compute<1>(p, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
+  std_agent_compute<1>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
     if (slot < kSlotSoc) xp[slot * n] = v[0];
     else if (slot == kSlotSoc) *socp = v[0];
     else if (slot < kSlotPower) op[(slot - kSlotObs) * b.obs.s_dim] = v[0];
@@ -988,7 +1017,7 @@ int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const
   const PFArgs a = make_pf_args(*pf, *pft);
   if (std_layout) {
     launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std, dim3(grid_for(n), p->n_agents),
-                 dim3(kBlock), st, *p, *s, n, b, pv_ob);
+                 dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
   } else {
     launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
                  st, *p, *s, n, b);
