@@ -57,6 +57,14 @@ __device__ __forceinline__ double clip(double x, double lo, double hi) {
   return (y > hi) ? hi : y;
 }
 
+// The same result (lo <= hi) from v_max/v_min, which take the bounds as SGPR
+// operands: x itself whenever it equals the clamped value (in range, or equal
+// to a bound -- also keeps x's sign of zero) or is NaN, else the bound.
+__device__ __forceinline__ double clip_fast(double x, double lo, double hi) {
+  const double r = fmin(fmax(x, lo), hi);
+  return (r == x || x != x) ? x : r;
+}
+
 // x / d correctly rounded, from r = RN(1/d): one multiply and two residual
 // corrections (Markstein: r correctly rounded and q1 faithful => q2 = RN(x/d)),
 // i.e. bit-identical to the IEEE quotient -- checked against it by
@@ -202,9 +210,19 @@ __device__ __forceinline__ void building_state_update(const pgw_building_params&
 }
 
 // get_p_consumed (dynamics.py:106-114)
+// s^3 correctly rounded (compensated: both products' rounding errors via fma).
+// The reference's s**3 is glibc pow(s, 3.0), which is within ~0.502 ulp but not
+// correctly rounded: the two differ by one ulp in ~0.1% of inputs (checked
+// against exact rationals; the cube was the correctly rounded one each time).
+__device__ __forceinline__ double cube_rn(double s) {
+  const double p = s * s, e1 = fma(s, s, -p);
+  const double q = p * s, e2 = fma(p, s, -q);
+  return q + fma(e1, s, e2);
+}
+
 __device__ __forceinline__ double building_p_consumed(const double act[6], double T_oa) {
   double s = (((act[0] + act[1]) + act[2]) + act[3]) + act[4];
-  double fan = 0.0076 * pow(s, 3.0) + 4.8865;
+  double fan = 0.0076 * cube_rn(s) + 4.8865;
   double chiller = pymax(0.0, s * (T_oa - act[5]));
   return fan + chiller;
 }

@@ -450,6 +450,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents(pgw_coord_params p, pgw
 // same IEEE operations the reference applies (lo + hi, hi - lo), plus the
 // reciprocals exact_div needs.
 struct StdDerived {
+  double act_rng[6], act_sum[6];                  // building actions: hi - lo, hi + lo
   double obs_sum[15], obs_rng[15], obs_rcp[15];   // building obs: lo + hi, hi - lo, 1 / (hi - lo)
   double bat_sum, bat_rng, bat_rcp;               // SoC range
   double rcp_eta_d, rcp_dt_h;                     // storage
@@ -457,6 +458,10 @@ struct StdDerived {
 
 static StdDerived make_std_derived(const pgw_coord_params& p) {
   StdDerived d = {};
+  for (int j = 0; j < 6; ++j) {
+    d.act_rng[j] = p.bld.act_high[j] - p.bld.act_low[j];
+    d.act_sum[j] = p.bld.act_high[j] + p.bld.act_low[j];
+  }
   for (int j = 0; j < 15; ++j) {
     d.obs_sum[j] = p.bld.obs_low[j] + p.bld.obs_high[j];
     d.obs_rng[j] = p.bld.obs_high[j] - p.bld.obs_low[j];
@@ -492,8 +497,9 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p, con
 #pragma unroll
   for (int q = 0; q < E; ++q) {
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
-      in[q].av[j] = B.rescale ? to_raw(in[q].av[j], B.act_low[j], B.act_high[j]) : in[q].av[j];
+    for (int j = 0; j < 6; ++j)   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
+      in[q].av[j] = B.rescale ? (clip_fast(in[q].av[j], -1.0, 1.0) * dv.act_rng[j] + dv.act_sum[j]) * 0.5
+                              : in[q].av[j];
 #pragma unroll
     for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
   }
@@ -531,7 +537,7 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p, con
     for (int q = 0; q < E; ++q) {
       const double o = j < 5 ? T[q][j] - ub : j < 10 ? lb - T[q][j - 5] : j == 10 ? lb
                      : j == 11 ? ub : j == 12 ? s.ex_next.T_oa : j == 13 ? pc[q] : s.ex_next.time_of_day;
-      double c = clip(o, B.obs_low[j], B.obs_high[j]);
+      double c = clip_fast(o, B.obs_low[j], B.obs_high[j]);
       if (B.rescale) c = exact_div(2.0 * c - dv.obs_sum[j], dv.obs_rng[j], dv.obs_rcp[j]);
       v[q] = c;
     }
@@ -553,7 +559,7 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p, con
   store(kSlotSoc, v);
 #pragma unroll
   for (int q = 0; q < E; ++q) {
-    const double c = clip(in[q].soc, p.bat.soc_min, p.bat.soc_max);
+    const double c = clip_fast(in[q].soc, p.bat.soc_min, p.bat.soc_max);
     v[q] = p.bat.rescale ? exact_div(2.0 * c - dv.bat_sum, dv.bat_rng, dv.bat_rcp) : in[q].soc;
   }
   store(kSlotObs + 16, v);
