@@ -310,8 +310,7 @@ template <int M, bool UB, bool GC> struct PFSolver {
 // Debug phase trace (pgw_debug_pf_trace): when set, lane 0 of every k_coord_pf
 // wave records wall_clock64() (100 MHz) at each phase boundary.
 __device__ long long* g_pf_trace = nullptr;
-__device__ __forceinline__ void pf_trace(int phase) {
-  long long* tr = g_pf_trace;
+__device__ __forceinline__ void pf_trace(long long* tr, int phase) {
   if (tr && (threadIdx.x & 63) == 0) {
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     tr[wave * 8 + phase] = wall_clock64();
@@ -641,12 +640,21 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
                                                      int64_t n, pgw_coord_buffers b) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
-  pf_trace(0);
-  // HBM first: the agent powers gate the predictor
+  // read once: a reload per phase would put an L2 round trip on the chain
+  long long* const trace = g_pf_trace;
+  pf_trace(trace, 0);
+  // HBM first: the agent powers gate the predictor.  The loads are
+  // unconditional (clamped indices, then scaled by 1 or 0 -- a select would be
+  // sunk back into a branch around the load) so that all of them issue back
+  // to back: a load under a branch let the compiler place the first sum right
+  // behind it, costing a second HBM round trip.  Lanes past n and agent slots
+  // past n_agents are never used.
   double rp[PGW_MAX_AGENTS];
+  const int64_t ec = valid ? e : 0;
 #pragma unroll
   for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-    rp[ag] = (valid && ag < c.n_agents) ? b.agent_power[(int64_t)ag * n + e] : 0.0;
+    rp[ag] = b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
+             ((valid && ag < c.n_agents) ? 1.0 : 0.0);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
   S.load(a, t.block);
@@ -663,15 +671,15 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
   S.powers(a, cp, cq, 1.0);
-  pf_trace(1);
+  pf_trace(trace, 1);
   S.initial(a, t, e, valid);
-  pf_trace(2);
+  pf_trace(trace, 2);
   const int it = S.iterate(a.max_iter, valid);
-  pf_trace(3);
+  pf_trace(trace, 3);
   double ir[M], ii[M];
   S.currents(ir, ii);
   const double v0 = S.node0_pu(ir, ii);
-  pf_trace(4);
+  pf_trace(trace, 4);
   if (!valid) return;
   double vsel = v0;
   if (b.v_out) b.v_out[e] = v0;
@@ -681,7 +689,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     vsel = (o == c.vv_row) ? v : vsel;
   }
   if (b.iters) b.iters[e] = it;
-  pf_trace(5);
+  pf_trace(trace, 5);
   if (c.coordinated) {
     const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
     if (b.vv) b.vv[e] = vv;
