@@ -42,7 +42,7 @@ PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
 M_ELEM = 14
 PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
 PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
-KERNELS = ("k_coord_agents_std", "k_coord_pf<14,true,false>", "k_pf_solve")
+KERNELS = ("k_coord_agents_std", "k_coord_pf<14,true,false,false>", "k_pf_solve")
 
 
 def parse():

@@ -262,6 +262,7 @@ class Feeder:
         W_ph = load_kw[:, self.elem_load] * 1000.0 / self.elem_nph
         var_ph = load_kvar[:, self.elem_load] * 1000.0 / self.elem_nph
         U = np.tile(self.U0, (K, 1))
+        I_last = np.zeros_like(U)
         iters = np.zeros(K, int)
         active = np.ones(K, bool)
         for it in range(1, max_iter + 1):
@@ -270,12 +271,15 @@ class Feeder:
             Un = self.U0 + I @ self.W.T
             err = np.max(np.abs(Un - U[idx]) / self.elem_vbase, axis=1)
             U[idx] = Un
+            I_last[idx] = I
             iters[idx] = it
             active[idx[err < tol]] = False
             if not active.any():
                 break
-        I = self.load_currents(U, W_ph, var_ph)
-        V = self.V0 + I @ self.G.T
+        # Every node voltage of the accepted solve V_{k+1} = Y^-1 I(V_k), as
+        # OpenDSS reports it (SolveSnap's last SolveSystem): the output nodes
+        # from the same currents as the converged element voltages.
+        V = self.V0 + I_last @ self.G.T
         return V, iters
 
     def pu(self, V):

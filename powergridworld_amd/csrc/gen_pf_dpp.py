@@ -95,6 +95,50 @@ def gen_column(M, k):
             % (M, k, M, M, M, (block_layout(M)["size"] + 15) // 16, asm_stmt(lines, outs, ins)))
 
 
+def gen_column_v(M, k):
+    """pf_column<M, K> plus the output-node-0 accumulation of the same column:
+    vr += G'r_k ir - G'i_k ii ; vi += G'r_k ii + G'i_k ir (the op order of
+    pf_node0, so the in-loop row equals the row evaluated after the loop)."""
+    L = block_layout(M)
+    T = L["tri"]
+    gr, gi = L["g0re"] + k, L["g0im"] + k
+    ents = [c * T + tri(M, i, k) for c in range(3) for i in range(M)] + [gr, gi]
+    ps, pidx = pairs_of(ents)
+    n_out = 3 * M + 2
+    xs = n_out + len(ps)              # operand index of ir, ii, is
+    w = lambda e: "%%%d" % (n_out + pidx[e // 16])
+    lines = []
+    for c in range(3):
+        for i in range(M):
+            e = c * T + tri(M, i, k)
+            lines.append("v_fmac_f64_dpp %%%d, %s, %%%d row_newbcast:%d %s"
+                         % (c * M + i, w(e), xs + c, e % 16, DPP))
+    vr, vi, ir, ii = "%%%d" % (3 * M), "%%%d" % (3 * M + 1), "%%%d" % xs, "%%%d" % (xs + 1)
+    lines += ["v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vr, w(gr), ir, gr % 16, DPP),
+              "v_fmac_f64_dpp %s, -%s, %s row_newbcast:%d %s" % (vr, w(gi), ii, gi % 16, DPP),
+              "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gr), ii, gr % 16, DPP),
+              "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gi), ir, gi % 16, DPP)]
+    outs = ['"+v"(A[%d])' % i for i in range(M)] + ['"+v"(B[%d])' % i for i in range(M)] + \
+           ['"+v"(C[%d])' % i for i in range(M)] + ['"+v"(vr)', '"+v"(vi)']
+    ins = ['"v"(w[%d])' % p for p in ps] + ['"v"(ir)', '"v"(ii)', '"v"(is)']
+    return ("template <> __device__ __forceinline__ void pf_column_v<%d, %d>(\n"
+            "    double (&A)[%d], double (&B)[%d], double (&C)[%d], double& vr, double& vi,\n"
+            "    const double (&w)[%d], double ir, double ii, double is) {\n%s}\n"
+            % (M, k, M, M, M, (L["size"] + 15) // 16, asm_stmt(lines, outs, ins)))
+
+
+def gen_v0(M, nr):
+    """(vr, vi) = V0' of output node 0 (the accumulation's start)."""
+    L = block_layout(M)
+    ps, pidx = pairs_of([L["v0re"], L["v0im"]])
+    lines = ["v_mov_b64_dpp %%0, %%%d row_newbcast:%d %s" % (2 + pidx[L["v0re"] // 16], L["v0re"] % 16, DPP),
+             "v_mov_b64_dpp %%1, %%%d row_newbcast:%d %s" % (2 + pidx[L["v0im"] // 16], L["v0im"] % 16, DPP)]
+    outs = ['"=&v"(vr)', '"=&v"(vi)']
+    ins = ['"v"(w[%d])' % p for p in ps]
+    return ("template <> __device__ __forceinline__ void pf_v0<%d>(double& vr, double& vi, "
+            "const double (&w)[%d]) {\n%s}\n" % (M, nr, asm_stmt(lines, outs, ins)))
+
+
 def gen_bcast_group(name, M, groups, nr, extra_sig=""):
     """Outputs out_j[i] = entry groups[j] + i, i < M (early-clobber movs)."""
     ents = [g + i for g in groups for i in range(M)]
@@ -163,6 +207,11 @@ def main():
            "template <int M> __device__ __forceinline__ void pf_node0(",
            "    double& vr, double& vi, const double (&w)[PFBlock<M>::kPairs], const double (&ir)[M],",
            "    const double (&ii)[M]);",
+           "template <int M, int K> __device__ __forceinline__ void pf_column_v(",
+           "    double (&A)[M], double (&B)[M], double (&C)[M], double& vr, double& vi,",
+           "    const double (&w)[PFBlock<M>::kPairs], double ir, double ii, double is);",
+           "template <int M> __device__ __forceinline__ void pf_v0(",
+           "    double& vr, double& vi, const double (&w)[PFBlock<M>::kPairs]);",
            ""]
     for M in SIZES:
         L = block_layout(M)
@@ -171,8 +220,10 @@ def main():
         out.append(gen_bcast_group("pf_acc_init", M, [L["u0re"], L["u0sum"]], nr))
         out.append(gen_bcast_group("pf_u0", M, [L["u0re"], L["u0im"]], nr))
         out.append(gen_node0(M, nr))
+        out.append(gen_v0(M, nr))
         for k in range(M):
             out.append(gen_column(M, k))
+            out.append(gen_column_v(M, k))
             out.append(gen_power(M, k, ns))
             out.append(gen_band(M, k, nr))
     sys.stdout.write("\n".join(out))

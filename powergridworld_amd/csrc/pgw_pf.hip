@@ -248,14 +248,39 @@ template <int M, bool UB, bool GC> struct PFSolver {
   // broadcast from.  An env that has converged (or a lane past n) keeps its
   // voltages by select, so each env's result and iteration count are those of
   // iterating it alone.
-  __device__ __forceinline__ int iterate(int max_iter, bool valid) {
+  // The output voltages come from the currents of the LAST iteration (the
+  // currents of the voltages it started from), as in OpenDSS, whose reported
+  // node voltages are the solve V_{k+1} = Y^-1 I(V_k) that passed the
+  // convergence test -- every node, output nodes included, from the same I.
+  // KEEP = false (fast kernel, one output row): output node 0 is accumulated
+  // inside the loop, column by column, in pf_node0's operation order.
+  // KEEP = true (general kernels, any outputs): the currents are kept per lane.
+  template <bool KEEP>
+  __device__ __forceinline__ int iterate(int max_iter, bool valid, double& v0r, double& v0i,
+                                         double (&lir)[M], double (&lii)[M]) {
     int it = 0, my_it = 0;
     bool done = !valid;
+    v0r = v0i = 0.0;
+    if constexpr (KEEP) {
+#pragma unroll
+      for (int k = 0; k < M; ++k) lir[k] = lii[k] = 0.0;
+    }
     while (true) {
-      double A[M], Bs[M], C[M];
+      double A[M], Bs[M], C[M], vr, vi;
       pf_acc_init<M>(A, C, w);
+      if constexpr (!KEEP) pf_v0<M>(vr, vi, w);
 #pragma unroll
       for (int i = 0; i < M; ++i) Bs[i] = 0.0;
+      auto column = [&](auto k, double ir, double ii) {
+        const double is = ir + ii;
+        if constexpr (KEEP) {
+          pf_column<M, decltype(k)::value>(A, Bs, C, w, ir, ii, is);
+          lir[k] = done ? lir[k] : ir;
+          lii[k] = done ? lii[k] : ii;
+        } else {
+          pf_column_v<M, decltype(k)::value>(A, Bs, C, vr, vi, w, ir, ii, is);
+        }
+      };
       // two elements at a time: their current-law chains (v_rcp_f64 + Newton)
       // are independent, so the scheduler interleaves them instead of stalling
       // on one dependent chain between two FMA blocks
@@ -264,15 +289,13 @@ template <int M, bool UB, bool GC> struct PFSolver {
         double ir0, ii0, ir1, ii1;
         current<k0>(ir0, ii0);
         current<k1>(ir1, ii1);
-        const double is0 = ir0 + ii0, is1 = ir1 + ii1;
-        pf_column<M, k0>(A, Bs, C, w, ir0, ii0, is0);
-        pf_column<M, k1>(A, Bs, C, w, ir1, ii1, is1);
+        column(std::integral_constant<int, k0>{}, ir0, ii0);
+        column(std::integral_constant<int, k1>{}, ir1, ii1);
       });
       if constexpr (M % 2) {
         double ir, ii;
         current<M - 1>(ir, ii);
-        const double is = ir + ii;
-        pf_column<M, M - 1>(A, Bs, C, w, ir, ii, is);
+        column(std::integral_constant<int, M - 1>{}, ir, ii);
       }
       bool conv = true;
 #pragma unroll
@@ -284,25 +307,19 @@ template <int M, bool UB, bool GC> struct PFSolver {
         ur[i] = done ? ur[i] : nr;
         ui[i] = done ? ui[i] : ni;
       }
+      if constexpr (!KEEP) {
+        v0r = done ? v0r : vr;
+        v0i = done ? v0i : vi;
+      }
       ++it;
       my_it = done ? my_it : it;
       done = done || conv || it >= max_iter;
       if (__ballot(!done) == 0ull) break;
     }
+    if constexpr (KEEP) pf_node0<M>(v0r, v0i, w, lir, lii);
     return my_it;
   }
 
-  // scaled element currents I' = I vb of the final voltages
-  __device__ __forceinline__ void currents(double (&ir)[M], double (&ii)[M]) const {
-    static_for<0, M>([&](auto k) { current<k>(ir[k], ii[k]); });
-  }
-
-  // |V| pu of output node 0 from the resident row (whole wave: DPP)
-  __device__ __forceinline__ double node0_pu(const double (&ir)[M], const double (&ii)[M]) const {
-    double vr, vi;
-    pf_node0<M>(vr, vi, w, ir, ii);
-    return sqrt(fma(vi, vi, vr * vr));
-  }
 };
 
 // |V| pu of output node o: V0 + sum_k G[o][k] I_k (wave-uniform G, V0 rows
@@ -339,7 +356,7 @@ __device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, cons
   return sqrt(fma(vi, vi, vr * vr));
 }
 
-template <int M, bool UB, bool GC>
+template <int M, bool UB, bool GC, bool KEEP>
 __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, int64_t n,
                                                      const double* __restrict__ ctrl_p,
                                                      const double* __restrict__ ctrl_q,
@@ -358,15 +375,16 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   }
   S.powers(a, cp, cq, (t.load_scale && valid) ? t.load_scale[e] : 1.0);
   S.initial(a, t, e, valid);
-  const int it = S.iterate(a.max_iter, valid);
-  double ir[M], ii[M];
-  S.currents(ir, ii);
+  constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
+  double v0r, v0i, ir[M], ii[M];
+  const int it = S.template iterate<kKeep>(a.max_iter, valid, v0r, v0i, ir, ii);
   const int32_t sig = t.sig_out ? S.signature() : 0;
-  const double v0 = a.n_out > 0 ? S.node0_pu(ir, ii) : 0.0;
+  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
   if (a.n_out > 0) v_out[e] = v0;
-  for (int o = 1; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
+  if constexpr (kKeep)
+    for (int o = 1; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
   if (t.U_out) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
@@ -635,7 +653,7 @@ struct CoordPFArgs {
   double vv_lo, vv_hi, vv_penalty;
 };
 
-template <int M, bool UB, bool GC>
+template <int M, bool UB, bool GC, bool KEEP>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
                                                      int64_t n, pgw_coord_buffers b) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -674,20 +692,21 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   pf_trace(trace, 1);
   S.initial(a, t, e, valid);
   pf_trace(trace, 2);
-  const int it = S.iterate(a.max_iter, valid);
+  constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
+  double v0r, v0i, ir[M], ii[M];
+  const int it = S.template iterate<kKeep>(a.max_iter, valid, v0r, v0i, ir, ii);
   pf_trace(trace, 3);
-  double ir[M], ii[M];
-  S.currents(ir, ii);
-  const double v0 = S.node0_pu(ir, ii);
+  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   pf_trace(trace, 4);
   if (!valid) return;
   double vsel = v0;
   if (b.v_out) b.v_out[e] = v0;
-  for (int o = 1; o < a.n_out; ++o) {
-    const double v = pf_node_pu<M>(t, o, ir, ii);
-    if (b.v_out) b.v_out[(int64_t)o * n + e] = v;
-    vsel = (o == c.vv_row) ? v : vsel;
-  }
+  if constexpr (kKeep)
+    for (int o = 1; o < a.n_out; ++o) {
+      const double v = pf_node_pu<M>(t, o, ir, ii);
+      if (b.v_out) b.v_out[(int64_t)o * n + e] = v;
+      vsel = (o == c.vv_row) ? v : vsel;
+    }
   if (b.iters) b.iters[e] = it;
   pf_trace(trace, 5);
   if (c.coordinated) {
@@ -849,34 +868,38 @@ static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
   return a;
 }
 
-template <int M, bool UB, bool GC>
+template <int M, bool UB, bool GC, bool KEEP>
 static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t n, const double* cp,
                                const double* cq, double* v_out, int32_t* iters, hipStream_t st) {
-  launch_timed(PGW_T_PF_SOLVE, k_pf_solve<M, UB, GC>, dim3(grid_for(n)), dim3(kBlock), st, a, t, n,
+  launch_timed(PGW_T_PF_SOLVE, k_pf_solve<M, UB, GC, KEEP>, dim3(grid_for(n)), dim3(kBlock), st, a, t, n,
                cp, cq, v_out, iters);
   return check_launch("k_pf_solve");
 }
 
-template <int M, bool UB, bool GC>
+template <int M, bool UB, bool GC, bool KEEP>
 static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_pf_tables& t,
                                int64_t n, const pgw_coord_buffers& b, hipStream_t st) {
-  launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC>, dim3(grid_for(n)), dim3(kBlock), st, c, a, t,
+  launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP>, dim3(grid_for(n)), dim3(kBlock), st, c, a, t,
                n, b);
   return check_launch("k_coord_pf");
 }
 
 // Instantiated variants: IEEE-13 (m = 14) with a uniform band, at most one
-// controllable slot and no per-env load scale is the fast path; everything
-// else runs the general variant (per-lane element powers) of its padded size.
+// controllable slot and no per-env load scale is the fast path (with one
+// output row accumulated inside the loop, or the last currents kept for any
+// number of rows); everything else runs the general variant (per-lane element
+// powers) of its padded size.
 #define PGW_PF_DISPATCH(p, t, fn, ...)                                     \
   do {                                                                     \
     const bool ub_ = uniform_band(p), gc_ = (p).n_ctrl > 1 || (t).load_scale; \
     switch ((p).m) {                                                       \
-      case 8: return fn<8, false, true>(__VA_ARGS__);                      \
+      case 8: return fn<8, false, true, true>(__VA_ARGS__);                \
       case 14:                                                             \
-        if (ub_ && !gc_) return fn<14, true, false>(__VA_ARGS__);          \
-        return fn<14, false, true>(__VA_ARGS__);                           \
-      default: return fn<16, false, true>(__VA_ARGS__);                    \
+        if (ub_ && !gc_ && (p).n_out <= 1)                                 \
+          return fn<14, true, false, false>(__VA_ARGS__);                  \
+        if (ub_ && !gc_) return fn<14, true, false, true>(__VA_ARGS__);    \
+        return fn<14, false, true, true>(__VA_ARGS__);                     \
+      default: return fn<16, false, true, true>(__VA_ARGS__);              \
     }                                                                      \
   } while (0)
 
