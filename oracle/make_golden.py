@@ -402,8 +402,59 @@ def gen_c4():
           init_storage=soc0, v675=v675)
 
 
+# --------------------------------------------------------------------------
+# Heterogeneous 3-agent scenario (gridworld/scenarios/heterogeneous.py:13-112):
+# MC building (alpha 0) + grid-aware PV farm rewarded on min_voltage + EV 25x40
+# --------------------------------------------------------------------------
+from gridworld.scenarios.heterogeneous import make_env_config as make_het_config  # noqa: E402
+
+
+def gen_het():
+    rng = np.random.default_rng(707)
+    K = 2
+    cfg = make_het_config()
+    cfg["pf_config"] = {"cls": OraclePowerFlowSolver,
+                        "config": {"system_load_rescale_factor": 0.65}}
+    rows = []
+    for k in range(K):
+        env = MultiAgentEnv(**copy.deepcopy(cfg))
+        with quiet():
+            o = env.reset()
+        soc0 = env.agent_dict["building"].env_dict["storage"].current_storage
+        rec = dict(soc0=soc0, obs=[o], rew=[], done=[], volt=[env.pf_solver.trace[-1]], acts=[])
+        while True:
+            a = {"building": {"building": rng.uniform(-1, 1, 6), "pv": rng.uniform(-1, 1, 1),
+                              "storage": rng.uniform(-1, 1, 1)},
+                 "pv": rng.uniform(-1, 1, 1), "ev-charging": rng.uniform(-1, 1, 1)}
+            with quiet():
+                o, r, d, _ = env.step(a)
+            rec["acts"].append(a)
+            rec["obs"].append(o)
+            rec["rew"].append(r)
+            rec["done"].append(d["__all__"])
+            rec["volt"].append(env.pf_solver.trace[-1])
+            if d["__all__"]:
+                break
+        rows.append(rec)
+    T = len(rows[0]["rew"])
+    assert all(len(r["rew"]) == T for r in rows)
+    flat_obs = lambda o: np.concatenate([o["building"]["building"], o["building"]["pv"],
+                                         o["building"]["storage"], o["pv"], o["ev-charging"]])
+    flat_act = lambda a: np.concatenate([a["building"]["building"], a["building"]["pv"],
+                                         a["building"]["storage"], a["pv"], a["ev-charging"]])
+    agents = ["building", "pv", "ev-charging"]
+    _save("het_scenario",
+          init_storage=np.array([r["soc0"] for r in rows]),
+          actions=np.stack([[flat_act(r["acts"][t]) for r in rows] for t in range(T)]),
+          obs=np.stack([[flat_obs(r["obs"][t]) for r in rows] for t in range(T + 1)]),
+          reward=np.stack([[[r["rew"][t][a] for a in agents] for r in rows] for t in range(T)]),
+          done=np.array([[r["done"][t] for r in rows] for t in range(T)]),
+          voltages=np.stack([[r["volt"][t] for r in rows] for t in range(T + 1)]),
+          node_names=np.array(BatchedPF().feeder.node_names))
+
+
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4}
+              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4, "het": gen_het}
 
 
 def main():

@@ -312,3 +312,39 @@ def test_c4_batch_one_and_ragged():
             o, r, vv = orc.step(act)
             close(env.packed_obs(), o, 1e-10, 1e-10)
             close(torch.stack([rew[a.name] for a in env.agents]), r, 1e-7, 1e-7)
+
+
+# ------------------------------------------------------------------ heterogeneous
+def test_heterogeneous_scenario_golden():
+    """The reference's 3-agent heterogeneous scenario (MC building, grid-aware
+    PV farm rewarded on min_voltage, EV 25x40) on the generic path, against the
+    reference run (tests/golden/het_scenario.npz, PF = the oracle behind the
+    reference's PowerFlowSolver ABC), a whole 286-step episode."""
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    g = load("het_scenario")
+    Tn, K, _ = g["actions"].shape
+    env = MultiAgentEnv(**make_env_config(), num_envs=K, device=DEV)
+    assert env._fused is None
+    env.reset()
+    bld = env.agent_dict["building"]
+    bld.env_dict["storage"].reset(init_storage=T(g["init_storage"]))
+
+    def flat(o):
+        return torch.cat([o["building"]["building"], o["building"]["pv"], o["building"]["storage"],
+                          o["pv"], o["ev-charging"]], 1)
+
+    close(flat(env.get_obs()), g["obs"][0], 1e-10, 1e-10)
+    names = [str(x) for x in g["node_names"]]
+    volts = lambda: torch.stack([env.pf_solver.get_bus_voltages()[nm] for nm in names], 1)
+    close(volts(), g["voltages"][0], 1e-9, 0)
+    for t in range(Tn):
+        a = T(g["actions"][t])
+        act = {"building": {"building": a[:, :6], "pv": a[:, 6:7], "storage": a[:, 7:8]},
+               "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
+        obs, rew, dones, _ = env.step(act)
+        close(flat(obs), g["obs"][t + 1], 1e-9, 1e-9)
+        close(volts(), g["voltages"][t + 1], 1e-9, 0)
+        close(torch.stack([rew[nm] for nm in ("building", "pv", "ev-charging")], 1), g["reward"][t],
+              1e-7, 1e-7)
+        assert dones["__all__"] == bool(g["done"][t, 0])

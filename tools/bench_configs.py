@@ -1,0 +1,131 @@
+"""Throughput of the BASELINE configs other than the headline C4 (BASELINE.md
+section 4): C2 = EnergyStorageEnv defaults at batch 4096, C3 = the
+MultiComponentEnv building + PV + storage + EV(100 vehicles) at batch 16384,
+and HET = the reference's 3-agent heterogeneous scenario (scenarios/
+heterogeneous.py) at a chosen batch.  Each step goes through the public API
+with actions resident in HBM (a pool of pre-generated batches); episodes reset
+inside the timed region.  One JSON line per config.
+
+Usage: python tools/bench_configs.py [--configs C2,C3,HET] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# algorithmic HBM bytes per agent-env-step
+BYTES = {"C2": 48, "C3": 1990}
+
+
+def timed_loop(env, step, reset, steps, warmup):
+    reset()
+    for _ in range(warmup):
+        if step():
+            reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if step():
+            reset()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def bench_c2(dev, steps, warmup, n=4096, pool=64):
+    from powergridworld_amd.agents import EnergyStorageEnv
+    env = EnergyStorageEnv(num_envs=n, device=dev)
+    gen = torch.Generator(dev).manual_seed(0)
+    acts = torch.empty((pool, n, 1), dtype=torch.float64, device=dev).uniform_(-1, 1, generator=gen)
+    init = torch.empty(n, dtype=torch.float64, device=dev).uniform_(3.0, 50.0, generator=gen)
+    k = [0]
+
+    def step():
+        _, _, done, _ = env.step(acts[k[0] % pool])
+        k[0] += 1
+        return done
+
+    dt = timed_loop(env, step, lambda: env.reset(init_storage=init), steps, warmup)
+    return dict(config="C2", workload="EnergyStorageEnv defaults", batch=n, agents=1, steps=steps, seconds=dt)
+
+
+def bench_c3(dev, steps, warmup, n=16384, pool=16):
+    from powergridworld_amd import MultiComponentEnv
+    from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv, FiveZoneROMThermalEnergyEnv, PVEnv
+    comps = [
+        {"name": "building", "cls": FiveZoneROMThermalEnergyEnv, "config": {}},
+        {"name": "pv", "cls": PVEnv, "config": {"profile_csv": "pv_profile.csv", "scaling_factor": 40.}},
+        {"name": "storage", "cls": EnergyStorageEnv, "config": {}},
+        {"name": "ev", "cls": EVChargingEnv,
+         "config": dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7.,
+                        peak_threshold=250., vehicle_multiplier=5., rescale_spaces=True)},
+    ]
+    env = MultiComponentEnv(name="mc", components=comps, num_envs=n, device=dev)
+    gen = torch.Generator(dev).manual_seed(0)
+    dims = {"building": 6, "pv": 1, "storage": 1, "ev": 1}
+    acts = [{c: torch.empty((n, d), dtype=torch.float64, device=dev).uniform_(-1, 1, generator=gen)
+             for c, d in dims.items()} for _ in range(pool)]
+    init = torch.empty(n, dtype=torch.float64, device=dev).uniform_(3.0, 50.0, generator=gen)
+    k = [0]
+
+    def step():
+        _, _, done, _ = env.step(acts[k[0] % pool])
+        k[0] += 1
+        return done
+
+    dt = timed_loop(env, step, lambda: env.reset(init_storage=init), steps, warmup)
+    return dict(config="C3", workload="MC building+PV+storage+EV(100 vehicles)", batch=n, agents=1,
+                steps=steps, seconds=dt)
+
+
+def bench_het(dev, steps, warmup, n=65536, pool=16):
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    env = MultiAgentEnv(**make_env_config(), num_envs=n, device=dev)
+    gen = torch.Generator(dev).manual_seed(0)
+    acts = []
+    for _ in range(pool):
+        acts.append({a.name: ({c.name: torch.empty((n, c.action_space.shape[0]), dtype=torch.float64,
+                                                    device=dev).uniform_(-1, 1, generator=gen)
+                               for c in a.envs} if hasattr(a, "envs") else
+                              torch.empty((n, a.action_space.shape[0]), dtype=torch.float64,
+                                          device=dev).uniform_(-1, 1, generator=gen))
+                     for a in env.agents})
+    k = [0]
+
+    def step():
+        _, _, dones, _ = env.step(acts[k[0] % pool])
+        k[0] += 1
+        return dones["__all__"]
+
+    dt = timed_loop(env, step, env.reset, steps, warmup)
+    return dict(config="HET", workload="3-agent heterogeneous (MC building, grid-aware PV farm, "
+                                       "EV 25x40) + IEEE-13 PF", batch=n, agents=3, steps=steps, seconds=dt)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2,C3,HET")
+    ap.add_argument("--steps", type=int, default=572)
+    ap.add_argument("--warmup", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    fns = {"C2": bench_c2, "C3": bench_c3, "HET": bench_het}
+    for name in args.configs.split(","):
+        r = fns[name](dev, args.steps, args.warmup)
+        units = r["batch"] * r["agents"] * r["steps"]
+        r["value"] = units / r["seconds"]
+        r["unit"] = "agent-env-steps/s"
+        r["us_per_step"] = r["seconds"] / r["steps"] * 1e6
+        if name in BYTES:
+            r["step_level_hbm_gbs"] = BYTES[name] * units / r["seconds"] / 1e9
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
