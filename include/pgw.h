@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 6
+#define PGW_ABI_VERSION 7
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -40,8 +40,8 @@ const char* pgw_last_error(void);
 /* sizeof() of every ABI struct, in the order pgw_mat, battery_params, pv_params,
  * building_params, building_exo, building_ext, ev_params, ev_step_info,
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
- * coord_step_info, pred_meta -- lets a binding verify its layouts.  Writes
- * min(n, 16) values, returns 16. */
+ * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers -- lets a
+ * binding verify its layouts.  Writes min(n, 19) values, returns 19. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -413,6 +413,82 @@ typedef struct pgw_coord_step_info {
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf,
                        const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                        pgw_coord_buffers b, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Home-Steward house: HSMultiComponentEnv.reset/step
+ * (gridworld/base_hs.py:66-180) over its components HSPVEnv
+ * (pv_profile_env_hs.py:96-160), HSEnergyStorageEnv
+ * (energy_storage_env_hs.py:76-270), HSEVChargingEnv
+ * (ev_charging_env_hs.py:127-326) and HSDevicesEnv (devices_env_hs.py:106-205).
+ * One thread per env runs the components in chain order and passes the step's
+ * resource state (PV / battery / grid power still available) down the chain
+ * as the reference's meta_state does; the house reward is then evaluated from
+ * the final state (base_hs.py:163, 183-199).
+ * ---------------------------------------------------------------------- */
+#define PGW_HS_MAX_VEHICLES 64
+#define PGW_HS_MAX_DEV 4
+enum { PGW_HS_PV = 0, PGW_HS_STORAGE = 1, PGW_HS_EV = 2, PGW_HS_DEVICES = 3 };
+
+typedef struct pgw_hs_params {
+  int32_t n_comp;                 /* components in chain order, each kind at most once */
+  int32_t kind[4];                /* PGW_HS_*                                 */
+  int32_t obs_off[4];             /* obs column of each chain slot's block    */
+  int32_t rescale[4];             /* rescale_spaces of each chain slot        */
+  int32_t n_veh, n_dev;
+  /* PV: action box (0.98, 1), obs box (-max(data), 0) */
+  double pv_act_low, pv_act_high, pv_obs_low;
+  /* storage */
+  double soc_min, soc_max, eta_c, eta_d, max_power, dt_h, max_storage_cost;
+  /* EV */
+  double ev_rate, ev_hours_per_step, ev_steps_per_hour, ev_mult, ev_unserved_penalty;
+  double ev_obs_low[7], ev_obs_high[7];
+  double ev_end_park[PGW_HS_MAX_VEHICLES];    /* rounded end_time_park_min */
+  double ev_req0[PGW_HS_MAX_VEHICLES];        /* energy_required_kwh * multiplier */
+  /* devices: action box (0.99, 1), obs box (0, column max) */
+  double dev_act_low, dev_act_high, dev_hours_per_step;
+  double dev_obs_high[PGW_HS_MAX_DEV];
+  double max_grid_power;
+} pgw_hs_params;
+
+/* Per-step values shared by all envs (the house steps in lockstep). */
+typedef struct pgw_hs_step_info {
+  double pv_avail;                 /* PV data[index] (scaled)                  */
+  double grid_cost;                /* grid_cost[time_index]                    */
+  double dev_obs[PGW_HS_MAX_DEV];  /* devices data row (scaled), obs          */
+  double dev_power[PGW_HS_MAX_DEV];/* devices data_pd row, summed for power   */
+  double ev_time;                  /* EV loop time (minutes)                   */
+  double ev_next_time;             /* simulation_times[time_index]             */
+  uint64_t ev_window;              /* bit v: start_v <= ev_time <= end_park_v  */
+} pgw_hs_step_info;
+
+/* Per-env state and outputs (device).  action: n x n_comp, column = chain
+ * slot.  obs: n x obs_dim.  ev_req: n_veh x n.  es_power_last: the house's
+ * meta_state es_power, which survives into the next reset's EV step.
+ * meta_out (nullable): 3 x n final pv_power, es_power, grid_power. */
+typedef struct pgw_hs_buffers {
+  pgw_mat action;
+  pgw_mat obs;
+  double* soc;
+  double* soc_cost;        /* storage current_cost (not reset by reset)   */
+  double* ev_req;
+  uint64_t* ev_charging;   /* bit v: vehicle v charged at the last step   */
+  double* ev_cost;         /* EV current_cost                             */
+  double* dev_cost;        /* devices current_cost                        */
+  double* es_power_last;
+  double* reward;
+  double* real_power;
+  double* meta_out;
+} pgw_hs_buffers;
+
+/* reset (base_hs.py:66-91): PV and devices at row 0, storage SoC := clip(
+ * init_soc[e]) (n doubles, device), EV requirements restored and its
+ * action-less step, obs of every component.  s: the reset row's values. */
+int32_t pgw_hs_reset(const pgw_hs_params* p, const pgw_hs_step_info* s, int64_t n,
+                     const double* init_soc, pgw_hs_buffers b, void* stream);
+/* step (base_hs.py:114-180): the chain, obs, real_power (sum in chain order)
+ * and the house reward. */
+int32_t pgw_hs_step(const pgw_hs_params* p, const pgw_hs_step_info* s, int64_t n,
+                    pgw_hs_buffers b, void* stream);
 
 #ifdef __cplusplus
 }

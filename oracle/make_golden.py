@@ -453,8 +453,57 @@ def gen_het():
           node_names=np.array(BatchedPF().feeder.node_names))
 
 
+# --------------------------------------------------------------------------
+# Home-Steward path: HSMultiComponentEnv of [HSPVEnv,
+# HSEnergyStorageEnv, HSEVChargingEnv, HSDevicesEnv] with the shipped JSON
+# scenario (gridworld/base_hs.py, scenarios/heterogeneous_hs.py); two
+# episodes per env so the state that survives reset is exercised.
+# --------------------------------------------------------------------------
+def gen_hs():
+    from gridworld import HSMultiComponentEnv
+    from gridworld.scenarios.heterogeneous_hs import make_env_config as make_hs_config
+    rng = np.random.default_rng(808)
+    K, EPISODES = 4, 2
+    cfg = make_hs_config()
+    names = [c["name"] for c in cfg["components"]]
+    runs = []
+    for k in range(K):
+        env = HSMultiComponentEnv(**copy.deepcopy(cfg))
+        rec = dict(obs=[], act=[], rew=[], rp=[], done=[], meta=[], soc=[])
+        for ep in range(EPISODES):
+            with quiet():
+                o = env.reset()
+            rec["obs"].append(np.concatenate([np.ravel(o[n]) for n in names]))
+            rec["meta"].append([np.nan] * 3)
+            rec["soc"].append(env.env_dict["storage"].current_storage)
+            while True:
+                # actions slightly beyond [-1, 1] exercise the clips; a few exact
+                # zeros and ends exercise the zero-power branches
+                a = rng.uniform(-1.1, 1.1, len(names))
+                a[rng.random(len(names)) < 0.05] = 0.0
+                a[rng.random(len(names)) < 0.03] = -1.0
+                with quiet():
+                    o, r, d, m = env.step({n: a[i:i + 1].copy() for i, n in enumerate(names)})
+                rec["act"].append(a)
+                rec["obs"].append(np.concatenate([np.ravel(o[n]) for n in names]))
+                rec["rew"].append(float(r))
+                rec["rp"].append(float(env.real_power))
+                rec["done"].append(bool(d))
+                rec["meta"].append([m["pv_power"], m["es_power"], m["grid_power"]])
+                rec["soc"].append(env.env_dict["storage"].current_storage)
+                if d:
+                    break
+        runs.append(rec)
+    T = len(runs[0]["rew"])
+    assert all(len(r["rew"]) == T for r in runs)
+    stack = lambda key: np.stack([np.asarray(r[key], dtype=np.float64) for r in runs], 1)
+    _save("hs_scenario", names=np.array(names), actions=stack("act"), obs=stack("obs"),
+          reward=stack("rew"), real_power=stack("rp"), done=stack("done").astype(bool),
+          meta=stack("meta"), soc=stack("soc"), episodes=np.array(EPISODES))
+
+
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4, "het": gen_het}
+              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4, "het": gen_het, "hs": gen_hs}
 
 
 def main():

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -122,6 +122,34 @@ class CoordStepInfo(C.Structure):
     _fields_ = [("ex_t", BuildingExo), ("ex_next", BuildingExo), ("pv_pmax", f64)]
 
 
+HS_MAX_VEHICLES, HS_MAX_DEV = 64, 4
+
+
+class HSParams(C.Structure):
+    _fields_ = [("n_comp", i32), ("kind", i32 * 4), ("obs_off", i32 * 4), ("rescale", i32 * 4),
+                ("n_veh", i32), ("n_dev", i32),
+                ("pv_act_low", f64), ("pv_act_high", f64), ("pv_obs_low", f64),
+                ("soc_min", f64), ("soc_max", f64), ("eta_c", f64), ("eta_d", f64), ("max_power", f64),
+                ("dt_h", f64), ("max_storage_cost", f64),
+                ("ev_rate", f64), ("ev_hours_per_step", f64), ("ev_steps_per_hour", f64), ("ev_mult", f64),
+                ("ev_unserved_penalty", f64), ("ev_obs_low", f64 * 7), ("ev_obs_high", f64 * 7),
+                ("ev_end_park", f64 * HS_MAX_VEHICLES), ("ev_req0", f64 * HS_MAX_VEHICLES),
+                ("dev_act_low", f64), ("dev_act_high", f64), ("dev_hours_per_step", f64),
+                ("dev_obs_high", f64 * HS_MAX_DEV), ("max_grid_power", f64)]
+
+
+class HSStepInfo(C.Structure):
+    _fields_ = [("pv_avail", f64), ("grid_cost", f64), ("dev_obs", f64 * HS_MAX_DEV),
+                ("dev_power", f64 * HS_MAX_DEV), ("ev_time", f64), ("ev_next_time", f64),
+                ("ev_window", C.c_uint64)]
+
+
+class HSBuffers(C.Structure):
+    _fields_ = [("action", Mat), ("obs", Mat), ("soc", vp), ("soc_cost", vp), ("ev_req", vp),
+                ("ev_charging", vp), ("ev_cost", vp), ("dev_cost", vp), ("es_power_last", vp),
+                ("reward", vp), ("real_power", vp), ("meta_out", vp)]
+
+
 PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE = 1, 2, 3
 
 _SIGS = {
@@ -152,13 +180,15 @@ _SIGS = {
     "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
     "pgw_coord_step": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
                              CoordBuffers, vp]),
+    "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
+    "pgw_hs_step": (i32, [P(HSParams), P(HSStepInfo), i64, HSBuffers, vp]),
 }
 
 EXPORTED = sorted(_SIGS)
 
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
-           CoordStepInfo, PredMeta]
+           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers]
 
 _lib = None
 

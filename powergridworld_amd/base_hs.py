@@ -1,0 +1,235 @@
+"""Batched HSMultiComponentEnv (reference: gridworld/base_hs.py:12-199).
+
+The Home-Steward house: PV, battery, EV charger and other devices share the
+PV / battery / grid power of each 5-minute step in a fixed order -- each
+component draws on what the previous ones left and the weighted cost of what
+it drew feeds its reward.  The reference passes that state down the chain in a
+`meta_state` dict; here the whole chain runs in one kernel per step
+(pgw_hs_step, one thread per env, include/pgw.h), so a step is one launch
+whatever the number of envs.
+
+Differences from the reference, all of them batching:
+  * obs / reward / real_power are [N] / [N, dim] fp64 device tensors (views of
+    the house's buffers: copy them to keep them across steps);
+  * the returned meta is the batched meta_state: timestamp and grid_cost
+    (shared), pv_power / es_power / grid_power ([N]); the per-device
+    `step_meta` logging records are not produced;
+  * reset(init_storage=...) accepts a per-env [N] SoC.
+"""
+from typing import List
+
+import numpy as np
+import pandas as pd
+import torch
+
+from powergridworld_amd import _lib
+from powergridworld_amd.base import MultiComponentEnv, as_action, register_env
+
+
+@register_env
+class HSMultiComponentEnv(MultiComponentEnv):
+
+    def __init__(self, name: str = None, components: List[dict] = None, start_time: str = "",
+                 end_time: str = "", control_timedelta=pd.Timedelta(300, "s"), max_grid_power: float = 48,
+                 max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
+                 device=None, **kwargs):
+        self.max_grid_power = max_grid_power
+        super().__init__(name=name, components=components, num_envs=num_envs, device=device)
+        from powergridworld_amd.agents.hs import _HSComponent
+        self.rescale_spaces = rescale_spaces
+        self._grid_cost_data = [float(x) for x in kwargs["grid_cost"]]
+        self._timestamps = kwargs["timestamps"]
+        self.max_episode_steps = max_episode_steps if max_episode_steps is not None else np.inf
+        kinds = []
+        for e in self.envs:
+            if not isinstance(e, _HSComponent):
+                raise TypeError("HSMultiComponentEnv components must be HS components, got %s"
+                                % type(e).__name__)
+            kinds.append(e.hs_kind)
+        if len(set(kinds)) != len(kinds):
+            raise ValueError("each HS component kind may appear once")
+        if kinds[0] != 0:
+            raise NotImplementedError("the HS chain must start with the PV (it sets pv_power)")
+        self._kinds = kinds
+        self._by_kind = {k: e for k, e in zip(kinds, self.envs)}
+        self.time_index = None
+        self.meta_state = {"timestamp": None, "grid_cost": None, "es_cost": 0.0, "grid_power": None,
+                           "pv_power": None, "es_power": None, "pv_cost": 0.0}
+        self._setup()
+
+    # ------------------------------------------------------------ buffers, params
+    def _setup(self):
+        n, dev = self.num_envs, self.device
+        p = _lib.HSParams()
+        p.n_comp = len(self.envs)
+        off = 0
+        dims = []
+        for c, (k, e) in enumerate(zip(self._kinds, self.envs)):
+            p.kind[c] = k
+            p.obs_off[c] = off
+            p.rescale[c] = int(bool(e.rescale_spaces))
+            d = e._observation_space.shape[0]
+            dims.append(d)
+            off += d
+        self._obs_dim = off
+        pv = self._by_kind.get(0)
+        if pv is not None:
+            p.pv_act_low, p.pv_act_high = 0.98, 1.0
+            p.pv_obs_low = float(-np.max(pv.data))
+        st = self._by_kind.get(1)
+        if st is not None:
+            p.soc_min, p.soc_max = float(st.storage_range[0]), float(st.storage_range[1])
+            if max(st.storage_range) != p.soc_max:
+                raise ValueError("storage_range must be (low, high)")
+            p.eta_c, p.eta_d = float(st.charge_efficiency), float(st.discharge_efficiency)
+            p.max_power, p.dt_h = float(st.max_power), float(st.control_interval_in_hr)
+            p.max_storage_cost = float(st.max_storage_cost)
+        ev = self._by_kind.get(2)
+        if ev is not None:
+            p.n_veh = len(ev.req0)
+            p.ev_rate = float(ev.max_charge_rate_kw)
+            p.ev_hours_per_step = ev.minutes_per_step / 60.
+            p.ev_steps_per_hour = 60.0 / ev.minutes_per_step
+            p.ev_mult = float(ev.vehicle_multiplier)
+            p.ev_unserved_penalty = float(ev.unserved_penalty)
+            for j in range(7):
+                p.ev_obs_low[j], p.ev_obs_high[j] = ev.obs_low[j], ev.obs_high[j]
+            for v in range(p.n_veh):
+                p.ev_end_park[v] = ev.end_park_min[v]
+                p.ev_req0[v] = ev.req0[v]
+        dv = self._by_kind.get(3)
+        if dv is not None:
+            p.n_dev = len(dv._obs_labels)
+            p.dev_act_low, p.dev_act_high = 0.99, 1.0
+            p.dev_hours_per_step = dv.minutes_per_step / 60.0
+            for j in range(p.n_dev):
+                p.dev_obs_high[j] = dv.obs_high[j]
+        p.max_grid_power = float(self.max_grid_power)
+        self.params = p
+
+        f64 = dict(dtype=torch.float64, device=dev)
+        self._obs_buf = torch.zeros((self._obs_dim, n), **f64)
+        self._act_buf = torch.zeros((len(self.envs), n), **f64)
+        for c, e in enumerate(self.envs):
+            e._adopt(self._obs_buf[p.obs_off[c]:p.obs_off[c] + dims[c]].t())
+        st_soc = st.soc if st is not None else torch.zeros(n, **f64)
+        st_cost = st.cost if st is not None else torch.zeros(n, **f64)
+        self._ev_req = torch.zeros((max(p.n_veh, 1), n), **f64)
+        self._ev_chg = torch.zeros(n, dtype=torch.int64, device=dev)
+        self._ev_cost = torch.zeros(n, **f64)
+        self._dev_cost = torch.zeros(n, **f64)
+        self._es_last = torch.zeros(n, **f64)       # meta_state es_power = 0.0 (base_hs.py:59)
+        self._reward = torch.zeros(n, **f64)
+        self._meta = torch.zeros((3, n), **f64)
+        self._init_soc = torch.zeros(n, **f64)
+        b = _lib.HSBuffers()
+        b.action = _lib.Mat(self._act_buf.data_ptr(), 1, n)
+        b.obs = _lib.Mat(self._obs_buf.data_ptr(), 1, n)
+        b.soc, b.soc_cost = st_soc.data_ptr(), st_cost.data_ptr()
+        b.ev_req, b.ev_charging = self._ev_req.data_ptr(), self._ev_chg.data_ptr()
+        b.ev_cost, b.dev_cost = self._ev_cost.data_ptr(), self._dev_cost.data_ptr()
+        b.es_power_last = self._es_last.data_ptr()
+        b.reward, b.real_power = self._reward.data_ptr(), self._real_power.data_ptr()
+        b.meta_out = self._meta.data_ptr()
+        self._bufs = b
+        self._keep = (st_soc, st_cost)
+
+    def _info(self, row, ev_time, ev_next_time):
+        """Shared per-step values: data rows of PV / devices, grid cost, EV times."""
+        s = _lib.HSStepInfo()
+        pv = self._by_kind.get(0)
+        if pv is not None:
+            s.pv_avail = float(pv.data[pv.index])
+        s.grid_cost = self._grid_cost_data[self.time_index]
+        dv = self._by_kind.get(3)
+        if dv is not None:
+            for j, c in enumerate(dv._obs_labels):
+                s.dev_obs[j] = float(dv.data[dv.index][j]) if np.ndim(dv.data) > 1 else float(dv.data[dv.index])
+                s.dev_power[j] = float(dv.data_pd.loc[dv.index, c])
+        ev = self._by_kind.get(2)
+        if ev is not None:
+            s.ev_time, s.ev_next_time = float(ev_time), float(ev_next_time)
+            s.ev_window = ev.window(ev_time)
+        return s
+
+    # ------------------------------------------------------------ API
+    def reset(self, **kwargs):
+        """base_hs.py:66-91: every component to row 0, the EV's action-less step."""
+        self.time_index = 0
+        self.meta_state["timestamp"] = self._timestamps[self.time_index]
+        self.meta_state["grid_cost"] = self._grid_cost_data[self.time_index]
+        self.meta_state["grid_power"] = self.max_grid_power
+        for k, e in self._by_kind.items():
+            if k in (0, 3):
+                e.index = 0
+        st = self._by_kind.get(1)
+        if st is not None:
+            st.simulation_step = 0
+            soc0 = st.initial_soc(kwargs.get("init_storage"))
+        else:
+            soc0 = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._init_soc.copy_(soc0)
+        ev = self._by_kind.get(2)
+        t0 = 0.0
+        if ev is not None:
+            ev.time_index = 0
+            ev.time = t0 = ev.simulation_times[0]
+        s = self._info(0, t0, t0)
+        _lib.check(_lib.lib().pgw_hs_reset(self.params, s, self.num_envs, _lib.dptr(self._init_soc),
+                                           self._bufs, self._stream()))
+        if ev is not None:
+            ev.time = ev.simulation_times[ev.time_index]
+            ev.time_index += 1
+        return self.get_obs(**kwargs)[0]
+
+    def get_obs(self, **kwargs):
+        return {e.name: e._obs for e in self.envs}, {}
+
+    def _pack(self, action):
+        if isinstance(action, torch.Tensor):
+            if tuple(action.shape) != (self.num_envs, len(self.envs)):
+                raise ValueError("packed HS action must be [N, %d]" % len(self.envs))
+            self._act_buf.copy_(action.t())
+            return
+        for c, e in enumerate(self.envs):
+            self._act_buf[c].copy_(as_action(action[e.name], self.num_envs, 1, self.device)[:, 0])
+
+    def step(self, action, **kwargs):
+        """base_hs.py:114-180.  `action`: {component: [N, 1]} or one packed [N, n_comp]."""
+        self._pack(action)
+        self.meta_state["timestamp"] = self._timestamps[self.time_index]
+        self.meta_state["grid_cost"] = self._grid_cost_data[self.time_index]
+        self.meta_state["grid_power"] = self.max_grid_power
+        ev = self._by_kind.get(2)
+        ev_time = ev_next = 0.0
+        if ev is not None:
+            ev_time, ev_next = ev.time, ev.simulation_times[ev.time_index]
+        s = self._info(None, ev_time, ev_next)
+        _lib.check(_lib.lib().pgw_hs_step(self.params, s, self.num_envs, self._bufs, self._stream()))
+        dones = []
+        for k, e in zip(self._kinds, self.envs):
+            if k == 0:
+                e.index += 1
+                dones.append(e.index == e.episode_length)
+            elif k == 1:
+                e.simulation_step += 1
+                dones.append(e.simulation_step == e.max_episode_steps)
+            elif k == 2:
+                dones.append(e.time_index == e.max_episode_steps)
+                e.time = ev_next
+                e.time_index += 1
+            else:
+                e.index += 1
+                dones.append(e.index == e.episode_length)
+        self.time_index += 1
+        meta = dict(self.meta_state)
+        meta.update(pv_power=self._meta[0], es_power=self._meta[1], grid_power=self._meta[2],
+                    es_cost=0)
+        obs = {e.name: e._obs for e in self.envs}
+        return obs, self._reward, any(dones), meta
+
+    def step_reward(self, **kwargs):
+        return self._reward, {}
+
+    def _current_reward(self):
+        return self._reward

@@ -348,3 +348,62 @@ def test_heterogeneous_scenario_golden():
         close(torch.stack([rew[nm] for nm in ("building", "pv", "ev-charging")], 1), g["reward"][t],
               1e-7, 1e-7)
         assert dones["__all__"] == bool(g["done"][t, 0])
+
+
+# ------------------------------------------------------------------ Home-Steward house
+def _hs_run(env, g, names, n_rep=1):
+    """Step `env` (batch K * n_rep, golden actions tiled) through the golden's
+    two episodes; compare obs, reward, real power, done, meta and SoC."""
+    A, O = g["actions"], g["obs"]
+    K = A.shape[1]
+    tile = lambda x: np.tile(x, (n_rep,) + (1,) * (x.ndim - 1))
+    dims = [env.env_dict[n]._observation_space.shape[0] for n in names]
+    flat = lambda o: torch.cat([o[n] for n in names], 1)
+    t_obs, t_act = 0, 0
+    for ep in range(int(g["episodes"])):
+        o = env.reset()
+        close(flat(o), tile(O[t_obs]), 1e-12, 1e-12)
+        close(env.env_dict["storage"].current_storage, tile(g["soc"][t_obs]), 0, 0)
+        t_obs += 1
+        while True:
+            a = tile(A[t_act])
+            o, r, d, m = env.step({n: T(a[:, i:i + 1]) for i, n in enumerate(names)})
+            close(flat(o), tile(O[t_obs]), 1e-12, 1e-12)
+            close(r, tile(g["reward"][t_act]), 1e-12, 1e-12)
+            close(env.real_power, tile(g["real_power"][t_act]), 1e-12, 1e-12)
+            close(torch.stack([m["pv_power"], m["es_power"], m["grid_power"]], 1), tile(g["meta"][t_obs]),
+                  1e-12, 1e-12)
+            close(env.env_dict["storage"].current_storage, tile(g["soc"][t_obs]), 1e-12, 1e-12)
+            assert d == bool(g["done"][t_act, 0])
+            t_obs += 1
+            t_act += 1
+            if d:
+                break
+    assert t_act == A.shape[0] and sum(dims) == O.shape[2]
+
+
+def test_hs_house_golden_two_episodes():
+    """The reference's Home-Steward house (HSMultiComponentEnv + the shipped
+    JSON scenario) against the reference's own run: 4 envs, two 288-step
+    episodes each (the battery's stored-energy cost and the meta_state es_power
+    carried across reset), actions partly outside [-1, 1] and exact zeros."""
+    from powergridworld_amd.base_hs import HSMultiComponentEnv
+    from powergridworld_amd.scenarios.heterogeneous_hs import make_env_config
+    g = load("hs_scenario")
+    names = [str(x) for x in g["names"]]
+    K = g["actions"].shape[1]
+    env = HSMultiComponentEnv(**make_env_config(), num_envs=K, device=DEV)
+    assert [e.name for e in env.envs] == names
+    _hs_run(env, g, names)
+
+
+def test_hs_house_full_batch_tiled():
+    """Size-independent property at 65 536 envs: envs are independent, so the
+    golden's 4 trajectories tiled over the batch reproduce it everywhere."""
+    from powergridworld_amd.base_hs import HSMultiComponentEnv
+    from powergridworld_amd.scenarios.heterogeneous_hs import make_env_config
+    g = load("hs_scenario")
+    names = [str(x) for x in g["names"]]
+    K = g["actions"].shape[1]
+    env = HSMultiComponentEnv(**make_env_config(), num_envs=65536, device=DEV)
+    _hs_run(env, g, names, n_rep=65536 // K)

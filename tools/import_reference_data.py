@@ -10,6 +10,7 @@ the GPU box.  Only data is converted -- no reference source is copied.
                                                                          -> loadshape_8760.npy
 * 5-zone ROM state-space model (``gridworld/agents/buildings/data/state_space_model.p``)
                                                                          -> state_space_model.json
+* Home-Steward scenario, vehicles, device profiles, grid cost   -> hs_data.json
 
 The pickle is NOT unpickled: it is walked opcode-by-opcode with
 ``pickletools.genops`` (which executes nothing) and the raw little-endian
@@ -115,6 +116,20 @@ def main():
         zones, os.path.join(REF, "agents/buildings/data/state_space_model.json"))
     with open(os.path.join(OUT, "state_space_model.json"), "w") as f:
         json.dump({"zones": zones}, f, indent=1)
+    # Home-Steward data: the shipped house scenario (scenarios/data/env_config.json,
+    # read by heterogeneous_hs.py:45-57), its grid-cost series, and the default
+    # vehicle / device profiles the HS components fall back to.
+    with open(os.path.join(REF, "scenarios/data/env_config.json")) as f:
+        hs_cfg = json.load(f)
+    veh = pd.read_csv(os.path.join(REF, "agents/vehicles/vehicles_hs.csv"))
+    dev = pd.read_csv(os.path.join(REF, "agents/devices/data/devices_profile_hs.csv"))
+    gc = pd.read_csv(os.path.join(REF, "scenarios/data/grid_cost.csv"))
+    hs = {"env_config": hs_cfg,
+          "vehicles_hs": json.loads(veh.to_json(orient="split")),
+          "devices_profile_hs": {c: dev[c].astype(float).tolist() for c in dev.columns},
+          "grid_cost": {"time": gc["time"].tolist(), "grid_cost": gc["grid_cost"].astype(float).tolist()}}
+    with open(os.path.join(OUT, "hs_data.json"), "w") as f:
+        json.dump(hs, f)
     print("wrote", sorted(os.listdir(OUT)))
 
 
