@@ -133,9 +133,29 @@ class HSMultiComponentEnv(MultiComponentEnv):
         b.meta_out = self._meta.data_ptr()
         self._bufs = b
         self._keep = (st_soc, st_cost)
+        self._act_key = None
+        self._info_cache = {}
+        if dv is not None:
+            self._dev_power = self._dev_rows(dv)
 
-    def _info(self, row, ev_time, ev_next_time):
-        """Shared per-step values: data rows of PV / devices, grid cost, EV times."""
+    @staticmethod
+    def _dev_rows(dv):
+        return np.stack([dv.data_pd[c].to_numpy(np.float64) for c in dv._obs_labels], 1)
+
+    def _info(self, ev_time, ev_next_time):
+        """Shared per-step values: data rows of PV / devices, grid cost, EV times
+        (cached per (row indices, time): every env shares them)."""
+        pv, dv = self._by_kind.get(0), self._by_kind.get(3)
+        key = (pv.index if pv is not None else -1, dv.index if dv is not None else -1, self.time_index,
+               ev_time, ev_next_time)
+        s = self._info_cache.get(key)
+        if s is None:
+            if len(self._info_cache) > 4096:
+                self._info_cache.clear()
+            s = self._info_cache[key] = self._make_info(ev_time, ev_next_time)
+        return s
+
+    def _make_info(self, ev_time, ev_next_time):
         s = _lib.HSStepInfo()
         pv = self._by_kind.get(0)
         if pv is not None:
@@ -145,7 +165,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
         if dv is not None:
             for j, c in enumerate(dv._obs_labels):
                 s.dev_obs[j] = float(dv.data[dv.index][j]) if np.ndim(dv.data) > 1 else float(dv.data[dv.index])
-                s.dev_power[j] = float(dv.data_pd.loc[dv.index, c])
+                s.dev_power[j] = float(self._dev_power[dv.index, j])
         ev = self._by_kind.get(2)
         if ev is not None:
             s.ev_time, s.ev_next_time = float(ev_time), float(ev_next_time)
@@ -174,7 +194,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
         if ev is not None:
             ev.time_index = 0
             ev.time = t0 = ev.simulation_times[0]
-        s = self._info(0, t0, t0)
+        s = self._info(t0, t0)
         _lib.check(_lib.lib().pgw_hs_reset(self.params, s, self.num_envs, _lib.dptr(self._init_soc),
                                            self._bufs, self._stream()))
         if ev is not None:
@@ -186,13 +206,22 @@ class HSMultiComponentEnv(MultiComponentEnv):
         return {e.name: e._obs for e in self.envs}, {}
 
     def _pack(self, action):
+        """A packed [N, n_comp] tensor is read in place (any strides); a
+        {component: [N, 1]} dict is gathered into the house's action buffer."""
         if isinstance(action, torch.Tensor):
             if tuple(action.shape) != (self.num_envs, len(self.envs)):
                 raise ValueError("packed HS action must be [N, %d]" % len(self.envs))
-            self._act_buf.copy_(action.t())
-            return
-        for c, e in enumerate(self.envs):
-            self._act_buf[c].copy_(as_action(action[e.name], self.num_envs, 1, self.device)[:, 0])
+            if action.dtype != torch.float64 or action.device != self.device:
+                action = action.to(device=self.device, dtype=torch.float64)
+            key = (action.data_ptr(), action.stride(0), action.stride(1))
+            self._act_hold = action
+        else:
+            for c, e in enumerate(self.envs):
+                self._act_buf[c].copy_(as_action(action[e.name], self.num_envs, 1, self.device)[:, 0])
+            key = (self._act_buf.data_ptr(), 1, self.num_envs)
+        if key != self._act_key:
+            self._bufs.action = _lib.Mat(*key)
+            self._act_key = key
 
     def step(self, action, **kwargs):
         """base_hs.py:114-180.  `action`: {component: [N, 1]} or one packed [N, n_comp]."""
@@ -204,7 +233,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
         ev_time = ev_next = 0.0
         if ev is not None:
             ev_time, ev_next = ev.time, ev.simulation_times[ev.time_index]
-        s = self._info(None, ev_time, ev_next)
+        s = self._info(ev_time, ev_next)
         _lib.check(_lib.lib().pgw_hs_step(self.params, s, self.num_envs, self._bufs, self._stream()))
         dones = []
         for k, e in zip(self._kinds, self.envs):
