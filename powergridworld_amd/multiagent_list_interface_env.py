@@ -1,5 +1,9 @@
 """dict -> list interface wrapper (reference: gridworld/multiagent_list_interface_env.py:8-111).
-Per-agent observations are concatenated along the feature axis ([N, obs_dim])."""
+Per-agent observations are [N, obs_dim] (components concatenated along the
+feature axis, in config order).  On the fused path they are zero-copy views of
+the engine's packed observation buffer, and a list of [N, act_dim] actions is
+written once into its packed action buffer (the
+observations stay on the device for a torch policy)."""
 from collections import OrderedDict
 
 import numpy as np
@@ -28,16 +32,40 @@ class MultiAgentListInterfaceEnv(spaces.Env):
             seq[item['name']] = [x['name'] for x in item['config']['components']]
         return seq
 
+    def _packed(self):
+        """Fused engine whose agent order and component order match the list
+        order: then obs / actions map to its packed buffers directly."""
+        ma = self.ma_env
+        if getattr(ma, "_fused", None) is None:
+            return False
+        names = [a.name for a in ma.agents]
+        if names != list(self.nested_sequence):
+            return False
+        return all([e.name for e in a.envs] == self.nested_sequence[a.name] for a in ma.agents)
+
     def reset(self):
         return self.convert_to_list_obs(self.ma_env.reset())
 
     def step(self, action):
-        action = self.convert_from_list_act(action)
-        next_obs, reward, done, info = self.ma_env.step(action)
+        if self._packed():
+            packed, _ = self.ma_env.action_buffer()
+            if isinstance(action, torch.Tensor) and action.dim() == 3:
+                act = action                          # already [n_agents, N, act_dim]
+            else:
+                for i, a in enumerate(action):
+                    packed[i].copy_(torch.as_tensor(a, dtype=torch.float64).to(packed.device)
+                                    .reshape(packed.shape[1:]))
+                act = packed
+            next_obs, reward, done, info = self.ma_env.step(act)
+        else:
+            next_obs, reward, done, info = self.ma_env.step(self.convert_from_list_act(action))
         return (self.convert_to_list_obs(next_obs), [reward[k] for k in self.nested_sequence],
                 [done[k] for k in self.nested_sequence], info)
 
     def convert_to_list_obs(self, obs):
+        if self._packed():
+            packed = self.ma_env.packed_obs()         # [n_agents, N, obs_dim] view
+            return [packed[i] for i in range(self.n)]
         return [torch.cat([obs[k][x] for x in v], dim=1) for k, v in self.nested_sequence.items()]
 
     def convert_from_list_act(self, action):
