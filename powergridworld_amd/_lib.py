@@ -223,7 +223,16 @@ def check(rc):
         raise PgwError(lib().pgw_last_error().decode() or ("libpgw error %d" % rc))
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None):
+    """hipStream_t of torch's current stream on `device` (the raw accessor skips
+    building a torch Stream object: this runs several times per env step)."""
+    if _raw_stream is not None:
+        idx = device.index if isinstance(device, torch.device) and device.index is not None else \
+            (device if isinstance(device, int) else torch.cuda.current_device())
+        return C.c_void_p(_raw_stream(idx))
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -76,6 +76,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self.tol, self.max_iter = float(tol), int(max_iter)
         self.bus_voltages = {}
         self.iterations = None
+        self._extrema = None
         self._hour_memo = {}
         self._ctrl_names = []
         self.use_predictor = bool(predictor)
@@ -285,10 +286,19 @@ class OpenDSSSolver(PowerFlowSolver):
         p = self.step_params(current_time)
         cp = cq = None
         if self._ctrl_names and p_controllable_consumed is not None:
-            zeros = torch.zeros(n, dtype=torch.float64, device=self.device)
-            get = lambda d, k: as_env_tensor(d[k], n, self.device, k) if (d and k in d) else zeros
-            cp = torch.stack([get(p_controllable_consumed, k) for k in self._ctrl_names])
-            cq = torch.stack([get(q_controllable_consumed, k) for k in self._ctrl_names])
+            zeros = None
+            get = lambda d, k: as_env_tensor(d[k], n, self.device, k) if (d and k in d) else None
+            ps = [get(p_controllable_consumed, k) for k in self._ctrl_names]
+            qs = [get(q_controllable_consumed, k) for k in self._ctrl_names]
+            if len(ps) == 1:                       # one load: a [1, N] view, no copy
+                cp = ps[0].reshape(1, n) if ps[0] is not None else None
+                cq = qs[0].reshape(1, n) if qs[0] is not None else None
+                if cp is None:
+                    cp = torch.zeros((1, n), dtype=torch.float64, device=self.device)
+            else:
+                zeros = torch.zeros(n, dtype=torch.float64, device=self.device)
+                cp = torch.stack([x if x is not None else zeros for x in ps])
+                cq = torch.stack([x if x is not None else zeros for x in qs])
         tables = self.step_tables(current_time) if cp is not None else self.tables
         _lib.check(_lib.lib().pgw_pf_solve(p, tables, n, _lib.dptr(cp), _lib.dptr(cq),
                                            _lib.dptr(self.v_out), _lib.dptr(self._iters),
@@ -297,7 +307,19 @@ class OpenDSSSolver(PowerFlowSolver):
         self._prepare_bus_voltages()
 
     def _prepare_bus_voltages(self):
-        self.bus_voltages = {name: self.v_out[i] for i, name in enumerate(self.output_names)}
+        """{node: [N] view of its v_out row}; the views stay valid across solves."""
+        key = (self.v_out.data_ptr(), tuple(self.output_names))
+        if getattr(self, "_bv_key", None) != key:
+            self.bus_voltages = {name: self.v_out[i] for i, name in enumerate(self.output_names)}
+            self._bv_key = key
+        self._extrema = None
+
+    def voltage_extrema(self):
+        """(min, max) over all output nodes per env, once per solve (multiagent_env.py:107-113)."""
+        if self._extrema is None:
+            v = self.v_out[:len(self.output_names)]
+            self._extrema = (v.min(0).values, v.max(0).values)
+        return self._extrema
 
     def get_bus_voltages(self) -> dict:
         return self.bus_voltages

@@ -116,10 +116,17 @@ class MultiAgentEnv(Env):
         if "bus_voltage" in agent.obs_labels:
             kwargs["bus_voltage"] = self.pf_solver.get_bus_voltage_by_name(
                 self.agent_name_bus_map[agent.name])
-        if "max_voltage" in agent.obs_labels:
-            kwargs["max_voltage"] = torch.stack(list(self.voltages.values())).max(0).values
-        if "min_voltage" in agent.obs_labels:
-            kwargs["min_voltage"] = torch.stack(list(self.voltages.values())).min(0).values
+        if "max_voltage" in agent.obs_labels or "min_voltage" in agent.obs_labels:
+            solver = self.pf_solver
+            if self.voltages is getattr(solver, "bus_voltages", None) and hasattr(solver, "voltage_extrema"):
+                vmin, vmax = solver.voltage_extrema()          # one reduction per solve
+            else:
+                stacked = torch.stack(list(self.voltages.values()))
+                vmin, vmax = stacked.min(0).values, stacked.max(0).values
+            if "max_voltage" in agent.obs_labels:
+                kwargs["max_voltage"] = vmax
+            if "min_voltage" in agent.obs_labels:
+                kwargs["min_voltage"] = vmin
         return kwargs
 
     def reward_transform(self, rew_dict) -> dict:
