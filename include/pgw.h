@@ -40,8 +40,9 @@ const char* pgw_last_error(void);
 /* sizeof() of every ABI struct, in the order pgw_mat, battery_params, pv_params,
  * building_params, building_exo, building_ext, ev_params, ev_step_info,
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
- * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers -- lets a
- * binding verify its layouts.  Writes min(n, 19) values, returns 19. */
+ * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
+ * mc_step_args -- lets a binding verify its layouts.  Writes min(n, 20)
+ * values, returns 20. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -413,6 +414,48 @@ typedef struct pgw_coord_step_info {
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf,
                        const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                        pgw_coord_buffers b, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused MultiComponentEnv step (SURVEY 8(b) pgw_mc_agent_step): one agent of
+ * building / PV / storage / EV components (each at most once, any order) --
+ * MultiComponentEnv.step + step_reward (gridworld/base.py:114-156) with every
+ * component's step (the entries above) and the in-order sums in ONE launch.
+ * Same arithmetic as the separate kernels + pgw_agent_reduce (bit-identical).
+ * The building's reward is the fresh one (MC semantics, base.py:137).
+ * ---------------------------------------------------------------------- */
+enum { PGW_MC_BUILDING = 0, PGW_MC_PV = 1, PGW_MC_STORAGE = 2, PGW_MC_EV = 3 };
+
+typedef struct pgw_mc_component {
+  int32_t kind, pad_;
+  pgw_mat action;         /* the component's [N, act_dim] action            */
+  pgw_mat obs;            /* its [N, obs_dim] observation                   */
+  double* real_power;     /* its real power (building: p_consumed)          */
+} pgw_mc_component;
+
+typedef struct pgw_mc_step_args {
+  int32_t n_comp, pad_;
+  pgw_mc_component comp[4];
+  pgw_building_params bld;
+  pgw_building_exo bld_ex_t, bld_ex_next;
+  pgw_building_ext bld_ext;
+  double* bld_x;
+  double* bld_reward_state;
+  pgw_pv_params pv;
+  double pv_pmax;
+  const double* pv_min_voltage;
+  pgw_battery_params bat;
+  double* bat_soc;
+  pgw_ev_params ev;
+  pgw_ev_step_info ev_step;
+  const double* ev_endp;
+  double* ev_req;
+  uint64_t* ev_charging;
+  double* ev_reward;
+  double* real_power;     /* agent sums (n)                                 */
+  double* reward;
+} pgw_mc_step_args;
+
+int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream);
 
 /* ------------------------------------------------------------------------
  * Home-Steward house: HSMultiComponentEnv.reset/step

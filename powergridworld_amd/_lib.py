@@ -125,6 +125,20 @@ class CoordStepInfo(C.Structure):
 HS_MAX_VEHICLES, HS_MAX_DEV = 64, 4
 
 
+class MCComponent(C.Structure):
+    _fields_ = [("kind", i32), ("pad_", i32), ("action", Mat), ("obs", Mat), ("real_power", vp)]
+
+
+class MCStepArgs(C.Structure):
+    _fields_ = [("n_comp", i32), ("pad_", i32), ("comp", MCComponent * 4),
+                ("bld", BuildingParams), ("bld_ex_t", BuildingExo), ("bld_ex_next", BuildingExo),
+                ("bld_ext", BuildingExt), ("bld_x", vp), ("bld_reward_state", vp),
+                ("pv", PVParams), ("pv_pmax", f64), ("pv_min_voltage", vp),
+                ("bat", BatteryParams), ("bat_soc", vp),
+                ("ev", EVParams), ("ev_step", EVStepInfo), ("ev_endp", vp), ("ev_req", vp),
+                ("ev_charging", vp), ("ev_reward", vp), ("real_power", vp), ("reward", vp)]
+
+
 class HSParams(C.Structure):
     _fields_ = [("n_comp", i32), ("kind", i32 * 4), ("obs_off", i32 * 4), ("rescale", i32 * 4),
                 ("n_veh", i32), ("n_dev", i32),
@@ -181,6 +195,7 @@ _SIGS = {
     "pgw_coord_step": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
                              CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
+    "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
     "pgw_hs_step": (i32, [P(HSParams), P(HSStepInfo), i64, HSBuffers, vp]),
 }
 
@@ -188,7 +203,7 @@ EXPORTED = sorted(_SIGS)
 
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
-           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers]
+           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs]
 
 _lib = None
 

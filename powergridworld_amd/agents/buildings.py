@@ -308,6 +308,23 @@ class FiveZoneROMEnv(ComponentEnv):
     def get_obs(self, **obs_kwargs):
         return self._obs, {"p_consumed": self.p_consumed}
 
+    # ---- fused MultiComponentEnv step (pgw_mc_agent_step): same as step() in an MC
+    def _mc_prepare(self, args, slot, action, obs_kwargs):
+        a = as_action(action, self.num_envs, 6, self.device)
+        t = self.time_index
+        if t + 1 >= len(self._exo):
+            raise IndexError("building stepped past the end of its exogenous data")
+        ext, keep = self._ext(obs_kwargs)
+        args.bld, args.bld_ex_t, args.bld_ex_next, args.bld_ext = self.params, self._exo[t], self._exo[t + 1], ext
+        args.bld_x, args.bld_reward_state = self.x.data_ptr(), self._reward_state.data_ptr()
+        c = args.comp[slot]
+        c.kind, c.action, c.obs, c.real_power = 0, _lib.mat(a), _lib.mat(self._obs), self.p_consumed.data_ptr()
+        return a, keep
+
+    def _mc_finish(self, obs_kwargs):
+        self.time_index += 1
+        return self._obs, self._reward_state, self.is_terminal(), {"p_consumed": self.p_consumed}
+
     def step_reward(self):
         if self.reward_kind == "viol":
             return self._viol_reward(), {}
@@ -333,3 +350,4 @@ class FiveZoneROMThermalEnergyEnv(FiveZoneROMEnv):
 
     fused_kind = "building"
     reward_kind = "thermal_energy"
+    mc_kind = 0

@@ -111,6 +111,20 @@ class EnergyStorageEnv(ComponentEnv):
     def step_reward(self, **kwargs):
         return self._zero_reward, {}
 
+    mc_kind = 2
+
+    def _mc_prepare(self, args, slot, action, kwargs):
+        a = as_action(action, self.num_envs, 1, self.device)
+        args.bat, args.bat_soc = self.params, self.soc.data_ptr()
+        c = args.comp[slot]
+        c.kind, c.action, c.obs, c.real_power = 2, _lib.mat(a), _lib.mat(self._obs), self._real_power.data_ptr()
+        return a
+
+    def _mc_finish(self, kwargs):
+        obs, meta = self.get_obs()
+        self.simulation_step += 1
+        return obs, self._zero_reward, self.is_terminal(), meta
+
     def _current_reward(self):
         return None
 

@@ -78,6 +78,21 @@ class PVEnv(ComponentEnv):
                                          _lib.dptr(vmin), _lib.mat(self._obs), self._stream()))
         return self._obs, {"real_power": float(-self.data[self.index])}
 
+    mc_kind = 1
+
+    def _mc_prepare(self, args, slot, action, kwargs):
+        a = as_action(action, self.num_envs, 1, self.device)
+        vmin = self._min_voltage(kwargs)
+        self._mc_pmax = float(self.data[self.index])
+        args.pv, args.pv_pmax, args.pv_min_voltage = self.params, self._mc_pmax, _lib.dptr(vmin)
+        c = args.comp[slot]
+        c.kind, c.action, c.obs, c.real_power = 1, _lib.mat(a), _lib.mat(self._obs), self._real_power.data_ptr()
+        return a, vmin
+
+    def _mc_finish(self, kwargs):
+        self.index += 1
+        return self._obs, None, self.is_terminal(), {"real_power": -self._mc_pmax}
+
     def is_terminal(self):
         return self.index == (self.episode_length - 1)                     # :117-119
 

@@ -145,6 +145,23 @@ class EVChargingEnv(ComponentEnv):
         self.time_index += 1
         self.time = self.simulation_times[self.time_index]
 
+    mc_kind = 3
+
+    def _mc_prepare(self, args, slot, action, kwargs):
+        s = self._step_info(action is not None)
+        a = as_action(action, self.num_envs, 1, self.device)
+        args.ev, args.ev_step = self.params, s
+        args.ev_endp, args.ev_req = self._endp_dev.data_ptr(), self.req.data_ptr()
+        args.ev_charging, args.ev_reward = self.charging.data_ptr(), self._reward.data_ptr()
+        c = args.comp[slot]
+        c.kind, c.action, c.obs, c.real_power = 3, _lib.mat(a), _lib.mat(self._obs), self._real_power.data_ptr()
+        return a
+
+    def _mc_finish(self, kwargs):
+        self.time_index += 1
+        self.time = self.simulation_times[self.time_index]
+        return self._obs, self._reward, self.is_terminal(), {}
+
     def reset(self, **kwargs):
         """(:145-168): fresh vehicle table, then one step with no action."""
         self.time_index = 0

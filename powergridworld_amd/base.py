@@ -184,8 +184,39 @@ class MultiComponentEnv(ComponentEnv):
         _lib.check(_lib.lib().pgw_agent_reduce(a, self.num_envs, _lib.dptr(self._real_power),
                                                _lib.dptr(self._reward), self._stream()))
 
+    def _mc_fusable(self):
+        """Every component is one of the kinds pgw_mc_agent_step implements
+        (building with the thermal-energy reward, PV, storage, EV), each once,
+        and none overrides its step."""
+        if getattr(self, "_mc_fuse", None) is None:
+            def own_step(e):
+                # the class that declares mc_kind must also provide the step that runs
+                owner = next(c for c in type(e).__mro__ if "mc_kind" in c.__dict__)
+                return type(e).step is owner.step
+            kinds = [getattr(type(e), "mc_kind", None) for e in self.envs]
+            ok = all(k is not None for k in kinds) and len(set(kinds)) == len(kinds) and len(kinds) <= 4
+            self._mc_fuse = ok and all(own_step(e) for e in self.envs)
+        return self._mc_fuse
+
     def step(self, action: dict, **kwargs):
         obs, dones, metas = {}, [], {}
+        if self._mc_fusable():
+            # the whole agent in one launch (pgw_mc_agent_step), same arithmetic
+            args = _lib.MCStepArgs()
+            args.n_comp = len(self.envs)
+            keep, kws = [], []
+            for c, env in enumerate(self.envs):
+                env_kwargs = {k: v for k, v in kwargs.items() if k in env.obs_labels}
+                kws.append(env_kwargs)
+                keep.append(env._mc_prepare(args, c, action[env.name], env_kwargs))
+            args.real_power, args.reward = self._real_power.data_ptr(), self._reward.data_ptr()
+            _lib.check(_lib.lib().pgw_mc_agent_step(args, self.num_envs, self._stream()))
+            for env, env_kwargs in zip(self.envs, kws):
+                ob, _, done, meta = env._mc_finish(env_kwargs)
+                obs[env.name] = ob
+                dones.append(done)
+                metas[env.name] = meta
+            return obs, self._reward, any(dones), metas
         for env in self.envs:
             env_kwargs = {k: v for k, v in kwargs.items() if k in env.obs_labels}
             ob, _, done, meta = env.step(action[env.name], **env_kwargs)

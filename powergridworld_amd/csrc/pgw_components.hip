@@ -38,30 +38,43 @@ __global__ void __launch_bounds__(kBlock) k_battery_reset(pgw_battery_params p, 
   st(obs, e, 0, battery_obs(p, s));
 }
 
+// One env's EnergyStorageEnv.step; returns its real power (-power, :150).
+__device__ __forceinline__ double battery_step_env(const pgw_battery_params& p, int64_t e, const pgw_mat& act,
+                                                   double* __restrict__ soc, const pgw_mat& obs) {
+  double s = soc[e];
+  double power = battery_step(p, ld(act, e, 0), s);
+  soc[e] = s;
+  st(obs, e, 0, battery_obs(p, s));
+  return -power;
+}
+
 __global__ void __launch_bounds__(kBlock) k_battery_step(pgw_battery_params p, int64_t n,
                                                          pgw_mat act, double* __restrict__ soc,
                                                          pgw_mat obs, double* __restrict__ rp) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  double s = soc[e];
-  double power = battery_step(p, ld(act, e, 0), s);
-  soc[e] = s;
-  rp[e] = -power;                                     // :150
-  st(obs, e, 0, battery_obs(p, s));
+  rp[e] = battery_step_env(p, e, act, soc, obs);
 }
 
 // ====================================================================== PV
-__global__ void __launch_bounds__(kBlock) k_pv(pgw_pv_params p, int64_t n, double pmax, pgw_mat act,
-                                               const double* __restrict__ vmin, pgw_mat obs,
-                                               double* __restrict__ rp) {
-  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= n) return;
+// One env's PVEnv obs (+ step when act.ptr): obs first (pre-advance, :143).
+__device__ __forceinline__ double pv_step_env(const pgw_pv_params& p, int64_t e, double pmax, const pgw_mat& act,
+                                              const double* __restrict__ vmin, const pgw_mat& obs) {
   st(obs, e, 0, pv_obs(p, pmax));
   if (p.grid_aware) {
     double v = vmin[e];
     st(obs, e, 1, p.rescale ? to_scaled(v, p.vmin_low, p.vmin_high) : v);
   }
-  if (rp) rp[e] = pv_real_power(p, ld(act, e, 0), pmax);
+  return act.ptr ? pv_real_power(p, ld(act, e, 0), pmax) : 0.0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_pv(pgw_pv_params p, int64_t n, double pmax, pgw_mat act,
+                                               const double* __restrict__ vmin, pgw_mat obs,
+                                               double* __restrict__ rp) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  const double r = pv_step_env(p, e, pmax, act, vmin, obs);
+  if (rp) rp[e] = r;
 }
 
 // ====================================================================== building
@@ -99,15 +112,13 @@ __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p
   if (rstate) rstate[e] = building_reward(p, T, ex0.comfort_lb, ex0.comfort_ub, 0.0);
 }
 
-__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p, pgw_building_exo ex,
-                                                          pgw_building_exo exn, int64_t n, pgw_mat act,
-                                                          double* __restrict__ x,
-                                                          double* __restrict__ pcons,
-                                                          double* __restrict__ rout,
-                                                          double* __restrict__ rstate, int32_t lagged,
-                                                          pgw_building_ext ext, pgw_mat obs) {
-  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= n) return;
+// One env's FiveZoneROMEnv.step_ (:183-225); returns p_consumed (its real power).
+__device__ __forceinline__ double building_step_env(const pgw_building_params& p, const pgw_building_exo& ex,
+                                                    const pgw_building_exo& exn, int64_t n, int64_t e,
+                                                    const pgw_mat& act, double* __restrict__ x,
+                                                    double* __restrict__ pcons, double* __restrict__ rout,
+                                                    double* __restrict__ rstate, int32_t lagged,
+                                                    const pgw_building_ext& ext, const pgw_mat& obs) {
   double a[6], xs[5], T[5];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -132,6 +143,19 @@ __global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p,
   if (rstate) rstate[e] = fresh;
   BuildingExt xv = building_ext(ext, e);
   building_write_obs(p, T, exn, pc, xv, [&](int j, double v) { st(obs, e, j, v); });
+  return pc;
+}
+
+__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p, pgw_building_exo ex,
+                                                          pgw_building_exo exn, int64_t n, pgw_mat act,
+                                                          double* __restrict__ x,
+                                                          double* __restrict__ pcons,
+                                                          double* __restrict__ rout,
+                                                          double* __restrict__ rstate, int32_t lagged,
+                                                          pgw_building_ext ext, pgw_mat obs) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  (void)building_step_env(p, ex, exn, n, e, act, x, pcons, rout, rstate, lagged, ext, obs);
 }
 
 // ====================================================================== EV
@@ -148,14 +172,12 @@ __global__ void __launch_bounds__(kBlock) k_ev_reset(int64_t n, int32_t V, int32
 // ev_charging_env.py:171-264.  Vehicles are visited in ascending index order
 // (the reference iterates a Python set of small ints); only vehicles parked now
 // or at the previous step can contribute (`scan`, uniform across the wave).
-__global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step_info s, int64_t n,
-                                                    pgw_mat act, const double* __restrict__ endp,
-                                                    double* __restrict__ req,
-                                                    uint64_t* __restrict__ chg, pgw_mat obs,
-                                                    double* __restrict__ rp,
-                                                    double* __restrict__ rew) {
-  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= n) return;
+// One env's EVChargingEnv.step (:171-264); writes rp[e] and rew[e].
+__device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+                                            int64_t e, const pgw_mat& act, const double* __restrict__ endp,
+                                            double* __restrict__ req, uint64_t* __restrict__ chg,
+                                            const pgw_mat& obs, double* __restrict__ rp,
+                                            double* __restrict__ rew) {
   double a = act.ptr ? ld(act, e, 0) : s.action_default;
   if (p.rescale) a = to_raw(a, 0.0, 1.0);
   double kwh = a * p.rate * p.hours_per_step;
@@ -206,6 +228,57 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
 #pragma unroll
   for (int j = 0; j < 6; ++j)
     st(obs, e, j, p.rescale ? to_scaled(st_[j], p.obs_low[j], p.obs_high[j]) : st_[j]);
+}
+
+__global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step_info s, int64_t n,
+                                                    pgw_mat act, const double* __restrict__ endp,
+                                                    double* __restrict__ req,
+                                                    uint64_t* __restrict__ chg, pgw_mat obs,
+                                                    double* __restrict__ rp,
+                                                    double* __restrict__ rew) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  ev_step_env(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+}
+
+// ====================================================================== fused MC step
+// MultiComponentEnv.step (base.py:114-139) of an agent made of building / PV /
+// storage / EV components (each at most once, any order): every component's
+// step in order, then real power and reward summed in order from 0 -- the
+// generic path's kernels and k_agent_reduce in one launch.
+__global__ void __launch_bounds__(kBlock) k_mc_step(pgw_mc_step_args a, int64_t n) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double rp_sum = 0.0, rew_sum = 0.0;
+  for (int c = 0; c < a.n_comp; ++c) {
+    const pgw_mc_component& C = a.comp[c];
+    double rp = 0.0, rew = 0.0;
+    switch (C.kind) {
+      case PGW_MC_BUILDING:
+        rp = building_step_env(a.bld, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x, C.real_power,
+                               nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
+        rew = a.bld_reward_state[e];
+        break;
+      case PGW_MC_PV:
+        rp = pv_step_env(a.pv, e, a.pv_pmax, C.action, a.pv_min_voltage, C.obs);
+        C.real_power[e] = rp;
+        break;
+      case PGW_MC_STORAGE:
+        rp = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
+        C.real_power[e] = rp;
+        break;
+      default:
+        ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
+                    C.real_power, a.ev_reward);
+        rp = C.real_power[e];
+        rew = a.ev_reward[e];
+        break;
+    }
+    rp_sum = rp_sum + rp;
+    rew_sum = rew_sum + rew;
+  }
+  a.real_power[e] = rp_sum;
+  a.reward[e] = rew_sum;
 }
 
 // ====================================================================== MC reduce
@@ -305,6 +378,28 @@ int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n
   PGW_REQUIRE(s->n_words == (p->n_vehicles + 63) / 64 && s->n_words <= PGW_EV_MAX_WORDS,
               "pgw_ev_step: n_words does not match n_vehicles");
   PGW_LAUNCH(k_ev_step, n, stream, *p, *s, n, action, endp, req, charging, obs, real_power, reward);
+}
+
+int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
+  PGW_REQUIRE(a && n >= 0 && a->n_comp >= 1 && a->n_comp <= 4, "pgw_mc_agent_step: bad args");
+  PGW_REQUIRE(a->real_power && a->reward, "pgw_mc_agent_step: null output");
+  int seen = 0;
+  for (int c = 0; c < a->n_comp; ++c) {
+    const pgw_mc_component& C = a->comp[c];
+    PGW_REQUIRE(C.kind >= 0 && C.kind <= 3 && !(seen & (1 << C.kind)),
+                "pgw_mc_agent_step: component kinds must be distinct PGW_MC_* values");
+    seen |= 1 << C.kind;
+    PGW_REQUIRE(C.action.ptr && C.obs.ptr && C.real_power, "pgw_mc_agent_step: component %d buffers", c);
+    if (C.kind == PGW_MC_BUILDING)
+      PGW_REQUIRE(a->bld_x && a->bld_reward_state && a->bld.n_obs <= PGW_BLD_MAX_OBS,
+                  "pgw_mc_agent_step: building buffers");
+    if (C.kind == PGW_MC_PV) PGW_REQUIRE(!a->pv.grid_aware || a->pv_min_voltage, "pgw_mc_agent_step: min_voltage");
+    if (C.kind == PGW_MC_STORAGE) PGW_REQUIRE(a->bat_soc, "pgw_mc_agent_step: storage buffers");
+    if (C.kind == PGW_MC_EV)
+      PGW_REQUIRE(a->ev_endp && a->ev_req && a->ev_charging && a->ev_reward &&
+                  a->ev_step.n_words <= PGW_EV_MAX_WORDS, "pgw_mc_agent_step: EV buffers");
+  }
+  PGW_LAUNCH(k_mc_step, n, stream, *a, n);
 }
 
 int32_t pgw_agent_reduce(const pgw_reduce_args* a, int64_t n, double* real_power, double* reward,
