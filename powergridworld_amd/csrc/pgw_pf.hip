@@ -622,7 +622,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
   std_agent_compute<1>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
     if (slot < kSlotSoc) xp[slot * n] = v[0];
     else if (slot == kSlotSoc) *socp = v[0];
-    else if (slot < kSlotPower) op[(slot - kSlotObs) * b.obs.s_dim] = v[0];
+    else if (slot < kSlotPower) st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
     else if (slot == kSlotPower) b.agent_power[(int64_t)a * n + e] = v[0];
     else b.reward[(int64_t)a * n + e] = v[0];
   });
