@@ -34,6 +34,7 @@ FP64_PEAK_TFS = 78.6         # MI355X spec, FP64 vector (= FP64 matrix); tools/m
 #   reads  actions 8x8 + x_k 5x8 + soc 8                       = 112
 #   writes x_k 5x8 + soc 8 + obs 17x8 + reward 8 + power 8     = 200
 AGENT_BYTES = 112 + 200
+AGENT_BYTES_F32 = AGENT_BYTES // 2       # the same items in fp32 (pgw_coord_step_f32)
 # k_coord_pf -- per env: reads 5 agent powers + 5 rewards, writes 5 rewards + v + vv + iters
 PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
 # k_coord_pf -- algorithmic fp64 FLOPs (m = 14 load phase elements): per fixed-point
@@ -58,7 +59,57 @@ def parse():
     ap.add_argument("--cpu-sample-steps", type=int, default=286)
     ap.add_argument("--time-every", type=int, default=16,
                     help="HIP-event-time every k-th launch of each kernel in the timed region")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the fp32-storage variant line (N=1 only; never the headline)")
     return ap.parse_args()
+
+
+def f32_variant(n, steps, warmup, pool_size, seed, dev):
+    """The same C4 workload on the fp32-storage fused path (pgw_coord_step_f32:
+    fp32 state/actions/outputs, fp64 arithmetic).  Reported beside
+    the fp64 headline, never as it: the reference computes in fp64."""
+    from powergridworld_amd import _lib
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=dev,
+                                             dtype=torch.float32)
+    gen = torch.Generator(dev).manual_seed(seed)
+    pool = torch.empty((pool_size, N_AGENTS, ACT_DIM, n), dtype=torch.float32, device=dev)
+    pool.uniform_(-1.0, 1.0, generator=gen)
+    packed = pool.transpose(2, 3)
+    env.reset()
+    k = [0]
+
+    def run(m):
+        for _ in range(m):
+            _, _, dones, _ = env.step(packed[k[0] % pool_size])
+            k[0] += 1
+            if dones["__all__"]:
+                env.reset()
+    run(warmup)
+    torch.cuda.synchronize()
+    _lib.check(_lib.lib().pgw_timing_start(16))
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tot = (_lib.C.c_double * len(KERNELS))()
+    cnt = (_lib.C.c_int64 * len(KERNELS))()
+    _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
+    a_us = tot[0] / cnt[0] * 1e3 if cnt[0] else None
+    p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
+    out = {"dtype": "f32 storage, f64 arithmetic", "value": N_AGENTS * n * steps / dt,
+           "unit": "agent-env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+           "parity": "tests/test_gpu_f32.py: one step = fp64 result rounded once; episode within "
+                     "1e-3 rel of fp64",
+           "k_coord_agents_std": {"avg_us": a_us, "bytes_per_launch": AGENT_BYTES_F32 * N_AGENTS * n,
+                                  "achieved": (AGENT_BYTES_F32 * N_AGENTS * n / (a_us * 1e-6) / 1e9
+                                               if a_us else None),
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s"},
+           "k_coord_pf_avg_us": p_us}
+    if a_us:
+        out["k_coord_agents_std"]["frac"] = out["k_coord_agents_std"]["achieved"] / HBM_PEAK_GBS
+    return out
 
 
 def cpu_baseline(envs, steps):
@@ -201,6 +252,9 @@ def main():
             "kernels": kernels,
             "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist},
         }
+        if world == 1 and not args.no_variants:
+            out["variants"] = {"f32": f32_variant(n, min(args.steps, 286), args.warmup, P,
+                                                  pgd.rank_seed(0, rank), dev)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
         print(json.dumps(out))

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 7
+#define PGW_ABI_VERSION 8
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -41,8 +41,8 @@ const char* pgw_last_error(void);
  * building_params, building_exo, building_ext, ev_params, ev_step_info,
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
  * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
- * mc_step_args -- lets a binding verify its layouts.  Writes min(n, 20)
- * values, returns 20. */
+ * mc_step_args, matf, coord_buffers_f32 -- lets a binding verify its
+ * layouts.  Writes min(n, 22) values, returns 22. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -54,6 +54,17 @@ typedef struct pgw_mat {
   int64_t s_env;
   int64_t s_dim;
 } pgw_mat;
+
+/* fp32 variant of pgw_mat, for the *_f32 entries.  The f32 entries store state,
+ * actions and outputs as fp32 (half the HBM bytes) but compute in fp64
+ * registers: each value is widened on load and rounded once at its store, so
+ * the only deviation from the fp64 path is the storage rounding (~6e-8 rel per
+ * step; the north-star bound for fp32 is 1e-3 rel). */
+typedef struct pgw_matf {
+  float* ptr;
+  int64_t s_env;
+  int64_t s_dim;
+} pgw_matf;
 
 /* ------------------------------------------------------------------------
  * Energy storage.  Replaces EnergyStorageEnv.reset/step/get_obs
@@ -75,6 +86,11 @@ int32_t pgw_battery_reset(const pgw_battery_params* p, int64_t n, const double* 
  * Reward is identically 0 (:159-164).  (:100-157) */
 int32_t pgw_battery_step(const pgw_battery_params* p, int64_t n, pgw_mat action,
                          double* soc, pgw_mat obs, double* real_power, void* stream);
+/* fp32-storage variants of the two entries above (fp64 arithmetic). */
+int32_t pgw_battery_reset_f32(const pgw_battery_params* p, int64_t n, const float* init_soc,
+                              float* soc, pgw_matf obs, void* stream);
+int32_t pgw_battery_step_f32(const pgw_battery_params* p, int64_t n, pgw_matf action,
+                             float* soc, pgw_matf obs, float* real_power, void* stream);
 
 /* ------------------------------------------------------------------------
  * PV curtailment.  Replaces PVEnv.get_obs/step
@@ -414,6 +430,27 @@ typedef struct pgw_coord_step_info {
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf,
                        const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                        pgw_coord_buffers b, void* stream);
+
+/* fp32-storage variant: every per-env buffer fp32, arithmetic in fp64 (the
+ * power flow included: the agent powers are widened and summed in fp64, the
+ * solve is the fp64 one).  Standard C4 agent layout only ([building, pv,
+ * storage] at action offsets 0/6/7, default building obs) -- PGW_ERR_ARG
+ * otherwise. */
+typedef struct pgw_coord_buffers_f32 {
+  pgw_matf action; int64_t act_stride_agent;
+  pgw_matf obs;    int64_t obs_stride_agent;
+  float* x;
+  float* soc;
+  float* reward;
+  float* agent_power;
+  float* v_out;
+  float* vv;
+  int32_t* iters;
+} pgw_coord_buffers_f32;
+
+int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
+                           const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                           pgw_coord_buffers_f32 b, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused MultiComponentEnv step (SURVEY 8(b) pgw_mc_agent_step): one agent of

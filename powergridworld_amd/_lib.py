@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -29,6 +29,11 @@ class PgwError(RuntimeError):
 
 
 class Mat(C.Structure):
+    _fields_ = [("ptr", vp), ("s_env", i64), ("s_dim", i64)]
+
+
+class Matf(C.Structure):
+    """pgw_matf: the fp32-storage variant of Mat (the *_f32 entries)."""
     _fields_ = [("ptr", vp), ("s_env", i64), ("s_dim", i64)]
 
 
@@ -118,6 +123,12 @@ class CoordBuffers(C.Structure):
                 ("vv", vp), ("iters", vp)]
 
 
+class CoordBuffersF32(C.Structure):
+    _fields_ = [("action", Matf), ("act_stride_agent", i64), ("obs", Matf), ("obs_stride_agent", i64),
+                ("x", vp), ("soc", vp), ("reward", vp), ("agent_power", vp), ("v_out", vp),
+                ("vv", vp), ("iters", vp)]
+
+
 class CoordStepInfo(C.Structure):
     _fields_ = [("ex_t", BuildingExo), ("ex_next", BuildingExo), ("pv_pmax", f64)]
 
@@ -172,6 +183,8 @@ _SIGS = {
     "pgw_last_error": (C.c_char_p, []),
     "pgw_battery_reset": (i32, [P(BatteryParams), i64, vp, vp, Mat, vp]),
     "pgw_battery_step": (i32, [P(BatteryParams), i64, Mat, vp, Mat, vp, vp]),
+    "pgw_battery_reset_f32": (i32, [P(BatteryParams), i64, vp, vp, Matf, vp]),
+    "pgw_battery_step_f32": (i32, [P(BatteryParams), i64, Matf, vp, Matf, vp, vp]),
     "pgw_pv_obs": (i32, [P(PVParams), i64, f64, vp, Mat, vp]),
     "pgw_pv_step": (i32, [P(PVParams), i64, f64, Mat, vp, Mat, vp, vp]),
     "pgw_building_reset": (i32, [P(BuildingParams), P(BuildingExo), i64, vp, vp, vp, BuildingExt,
@@ -194,6 +207,8 @@ _SIGS = {
     "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
     "pgw_coord_step": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
                              CoordBuffers, vp]),
+    "pgw_coord_step_f32": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
+                                 CoordBuffersF32, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
     "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
     "pgw_hs_step": (i32, [P(HSParams), P(HSStepInfo), i64, HSBuffers, vp]),
@@ -203,7 +218,7 @@ EXPORTED = sorted(_SIGS)
 
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
-           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs]
+           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32]
 
 _lib = None
 
@@ -262,6 +277,25 @@ def mat(t2d):
         return Mat(None, 0, 0)
     assert t2d.dim() == 2 and t2d.dtype == torch.float64, (t2d.shape, t2d.dtype)
     return Mat(t2d.data_ptr(), t2d.stride(0), t2d.stride(1))
+
+
+def matf(t2d):
+    """pgw_matf for a 2-D [n_envs, dim] fp32 device tensor (any strides)."""
+    if t2d is None:
+        return Matf(None, 0, 0)
+    assert t2d.dim() == 2 and t2d.dtype == torch.float32, (t2d.shape, t2d.dtype)
+    return Matf(t2d.data_ptr(), t2d.stride(0), t2d.stride(1))
+
+
+STORAGE_DTYPES = (torch.float64, torch.float32)
+
+
+def storage_dtype(dtype):
+    """The storage dtype of an env (fp64 = the reference's; fp32 = the _f32 entries)."""
+    dtype = torch.float64 if dtype is None else dtype
+    if dtype not in STORAGE_DTYPES:
+        raise PgwError("storage dtype must be torch.float64 or torch.float32, got %s" % (dtype,))
+    return dtype
 
 
 def require_device(device):

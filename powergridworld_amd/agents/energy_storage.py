@@ -16,14 +16,16 @@ class EnergyStorageEnv(ComponentEnv):
     [-1, 1] (discharge > 0), reward 0.  Step kernel: pgw_battery_step."""
 
     fused_kind = "storage"
+    supported_dtypes = (torch.float64, torch.float32)    # fp32: pgw_battery_*_f32
 
     def __init__(self, name: str = None, storage_range: tuple = (3.0, 50.0),
                  initial_storage_mean: float = 30.0, initial_storage_std: float = 5.0,
                  charge_efficiency: float = 0.95, discharge_efficiency: float = 0.9,
                  max_power: float = 15.0, max_episode_steps: int = 288,
                  control_timedelta: pd.Timedelta = pd.Timedelta(300, "s"),
-                 rescale_spaces: bool = True, num_envs: int = 1, device=None, seed=None, **kwargs):
-        super().__init__(name=name, num_envs=num_envs, device=device)
+                 rescale_spaces: bool = True, num_envs: int = 1, device=None, seed=None, dtype=None,
+                 **kwargs):
+        super().__init__(name=name, num_envs=num_envs, device=device, dtype=dtype)
         self.storage_range = storage_range
         self.initial_storage_mean = initial_storage_mean
         self.initial_storage_std = initial_storage_std
@@ -45,7 +47,11 @@ class EnergyStorageEnv(ComponentEnv):
             eta_c=float(charge_efficiency), eta_d=float(discharge_efficiency),
             max_power=float(max_power), dt_h=float(self.control_interval_in_hr),
             rescale=int(bool(rescale_spaces)))
-        self.soc = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self.soc = torch.zeros(self.num_envs, dtype=self.dtype, device=self.device)
+        f32 = self.dtype == torch.float32
+        self._k_reset = "pgw_battery_reset_f32" if f32 else "pgw_battery_reset"
+        self._k_step = "pgw_battery_step_f32" if f32 else "pgw_battery_step"
+        self._mat = _lib.matf if f32 else _lib.mat
         self._obs = self._new_obs(1)
         self._gen = torch.Generator(device=self.device)
         self.seed(seed)
@@ -92,18 +98,18 @@ class EnergyStorageEnv(ComponentEnv):
                 print(e)
                 print("init_storage value needs to be a float, use default value instead")
                 init = self.initial_storage_mean
-        init = as_env_tensor(init, n, self.device, "init_storage")
-        _lib.check(_lib.lib().pgw_battery_reset(self.params, n, _lib.dptr(init), _lib.dptr(self.soc),
-                                                _lib.mat(self._obs), self._stream()))
+        init = as_env_tensor(init, n, self.device, "init_storage").to(self.dtype)
+        _lib.check(getattr(_lib.lib(), self._k_reset)(self.params, n, _lib.dptr(init), _lib.dptr(self.soc),
+                                                      self._mat(self._obs), self._stream()))
         self._real_power.zero_()
         return self.get_obs(**kwargs)
 
     def step(self, action, **kwargs):
         """(:131-157)"""
-        a = as_action(action, self.num_envs, 1, self.device)
-        _lib.check(_lib.lib().pgw_battery_step(self.params, self.num_envs, _lib.mat(a),
-                                               _lib.dptr(self.soc), _lib.mat(self._obs),
-                                               _lib.dptr(self._real_power), self._stream()))
+        a = as_action(action, self.num_envs, 1, self.device, self.dtype)
+        _lib.check(getattr(_lib.lib(), self._k_step)(self.params, self.num_envs, self._mat(a),
+                                                     _lib.dptr(self.soc), self._mat(self._obs),
+                                                     _lib.dptr(self._real_power), self._stream()))
         obs, meta = self.get_obs()
         self.simulation_step += 1
         return obs, self._zero_reward, self.is_terminal(), meta

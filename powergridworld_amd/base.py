@@ -39,13 +39,13 @@ def as_env_tensor(x, n, device, what="value"):
     return t.contiguous()
 
 
-def as_action(a, n, dim, device):
-    """Normalise an action to a [n, dim] fp64 device tensor (views where possible)."""
+def as_action(a, n, dim, device, dtype=torch.float64):
+    """Normalise an action to a [n, dim] device tensor of `dtype` (views where possible)."""
     if a is None:
         return None
     t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a, dtype=np.float64))
-    if t.dtype != torch.float64 or t.device != device:
-        t = t.to(device=device, dtype=torch.float64)
+    if t.dtype != dtype or t.device != device:
+        t = t.to(device=device, dtype=dtype)
     if t.dim() == 0:
         return t.reshape(1, 1).expand(n, dim)
     if t.dim() == 1:
@@ -63,17 +63,30 @@ class ComponentEnv(spaces.Env, ABC):
     """Base class for any environment used in the multiagent simulation
     (gridworld/base.py:12-71), batched over ``num_envs`` copies."""
 
-    def __init__(self, name: str = None, num_envs: int = 1, device=None, **kwargs):
+    # storage dtypes the subclass's kernels implement (fp32 = the _f32 entries)
+    supported_dtypes = (torch.float64,)
+
+    def __new__(cls, *args, **kwargs):
+        # checked here, before any subclass __init__ could swallow `dtype` in **kwargs
+        dt = kwargs.get("dtype")
+        if dt is not None and _lib.storage_dtype(dt) not in cls.supported_dtypes:
+            raise NotImplementedError("%s has no %s storage variant" % (cls.__name__, dt))
+        return super().__new__(cls)
+
+    def __init__(self, name: str = None, num_envs: int = 1, device=None, dtype=None, **kwargs):
         super().__init__()
         self.name = name
         self.num_envs = int(num_envs)
         if self.num_envs < 1:
             raise ValueError("num_envs must be >= 1")
         self.device = _lib.require_device(device)
+        self.dtype = _lib.storage_dtype(dtype)
+        if self.dtype not in self.supported_dtypes:
+            raise NotImplementedError("%s has no %s storage variant" % (type(self).__name__, self.dtype))
         n = self.num_envs
-        self._real_power = torch.zeros(n, dtype=torch.float64, device=self.device)
-        self._reactive_power = torch.zeros(n, dtype=torch.float64, device=self.device)
-        self._zero_reward = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self._real_power = torch.zeros(n, dtype=self.dtype, device=self.device)
+        self._reactive_power = torch.zeros(n, dtype=self.dtype, device=self.device)
+        self._zero_reward = torch.zeros(n, dtype=self.dtype, device=self.device)
         self._obs_labels = []
         self._in_multicomponent = False
 
@@ -81,7 +94,7 @@ class ComponentEnv(spaces.Env, ABC):
     def _new_obs(self, dim):
         """Env-minor obs buffer [dim, N]; the returned [N, dim] view is what
         step()/reset() hand out (coalesced device writes, zero-copy for the caller)."""
-        buf = torch.zeros((dim, self.num_envs), dtype=torch.float64, device=self.device)
+        buf = torch.zeros((dim, self.num_envs), dtype=self.dtype, device=self.device)
         return buf.t()
 
     def _stream(self):
@@ -155,6 +168,9 @@ class MultiComponentEnv(ComponentEnv):
             cls = resolve_env_class(c["cls"])
             env = cls(name=c["name"], num_envs=self.num_envs, device=self.device, **c["config"])
             env._in_multicomponent = True
+            if env.dtype != self.dtype:
+                raise NotImplementedError("MultiComponentEnv steps fp64 components only "
+                                          "(component %s is %s)" % (env.name, env.dtype))
             self.envs.append(env)
         self.observation_space = spaces.Dict({e.name: e.observation_space for e in self.envs})
         self.action_space = spaces.Dict({e.name: e.action_space for e in self.envs})

@@ -93,14 +93,19 @@ __device__ __forceinline__ double to_raw(double y, double lo, double hi) {
 __device__ __forceinline__ double pymax(double a, double b) { return (b > a) ? b : a; }
 __device__ __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
 
-__device__ __forceinline__ double ld(const pgw_mat& m, int64_t e, int j) {
-  return m.ptr[e * m.s_env + (int64_t)j * m.s_dim];
+// pgw_mat or pgw_matf; fp32 values are widened to fp64 (exactly).
+template <class Mt>
+__device__ __forceinline__ double ld(const Mt& m, int64_t e, int j) {
+  return (double)m.ptr[e * m.s_env + (int64_t)j * m.s_dim];
 }
 // Observation stores are write-once streams for the policy: nontemporal, so
 // they do not evict the state the next step re-reads (k_coord_agents_std
 // 21.4 -> 19.6 us at C4, profiles/r01/nt_stores.txt).
+// fp32 storage (the *_f32 entries): the fp64 value is rounded once, here.
 __device__ __forceinline__ void st_obs(double* p, double v) { __builtin_nontemporal_store(v, p); }
-__device__ __forceinline__ void st(const pgw_mat& m, int64_t e, int j, double v) {
+__device__ __forceinline__ void st_obs(float* p, double v) { __builtin_nontemporal_store((float)v, p); }
+template <class Mt>
+__device__ __forceinline__ void st(const Mt& m, int64_t e, int j, double v) {
   st_obs(m.ptr + e * m.s_env + (int64_t)j * m.s_dim, v);
 }
 

@@ -28,32 +28,37 @@ int32_t check_launch(const char* what) {
 }
 
 // ====================================================================== battery
+// S = double (pgw_mat) or float (pgw_matf, the _f32 entries: fp32 storage,
+// fp64 arithmetic).
+template <class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_battery_reset(pgw_battery_params p, int64_t n,
-                                                          const double* __restrict__ init,
-                                                          double* __restrict__ soc, pgw_mat obs) {
+                                                          const S* __restrict__ init,
+                                                          S* __restrict__ soc, Mt obs) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  double s = clip(init[e], p.soc_min, p.soc_max);   // energy_storage_env.py:86-95
-  soc[e] = s;
+  double s = clip((double)init[e], p.soc_min, p.soc_max);   // energy_storage_env.py:86-95
+  soc[e] = (S)s;
   st(obs, e, 0, battery_obs(p, s));
 }
 
 // One env's EnergyStorageEnv.step; returns its real power (-power, :150).
-__device__ __forceinline__ double battery_step_env(const pgw_battery_params& p, int64_t e, const pgw_mat& act,
-                                                   double* __restrict__ soc, const pgw_mat& obs) {
+template <class S, class Mt>
+__device__ __forceinline__ double battery_step_env(const pgw_battery_params& p, int64_t e, const Mt& act,
+                                                   S* __restrict__ soc, const Mt& obs) {
   double s = soc[e];
   double power = battery_step(p, ld(act, e, 0), s);
-  soc[e] = s;
+  soc[e] = (S)s;
   st(obs, e, 0, battery_obs(p, s));
   return -power;
 }
 
+template <class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_battery_step(pgw_battery_params p, int64_t n,
-                                                         pgw_mat act, double* __restrict__ soc,
-                                                         pgw_mat obs, double* __restrict__ rp) {
+                                                         Mt act, S* __restrict__ soc,
+                                                         Mt obs, S* __restrict__ rp) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  rp[e] = battery_step_env(p, e, act, soc, obs);
+  rp[e] = (S)battery_step_env(p, e, act, soc, obs);
 }
 
 // ====================================================================== PV
@@ -316,14 +321,27 @@ const char* pgw_last_error(void) { return g_err; }
 int32_t pgw_battery_reset(const pgw_battery_params* p, int64_t n, const double* init, double* soc,
                           pgw_mat obs, void* stream) {
   PGW_REQUIRE(p && init && soc && obs.ptr && n >= 0, "pgw_battery_reset: null argument");
-  PGW_LAUNCH(k_battery_reset, n, stream, *p, n, init, soc, obs);
+  PGW_LAUNCH((k_battery_reset<double, pgw_mat>), n, stream, *p, n, init, soc, obs);
+}
+
+int32_t pgw_battery_reset_f32(const pgw_battery_params* p, int64_t n, const float* init, float* soc,
+                              pgw_matf obs, void* stream) {
+  PGW_REQUIRE(p && init && soc && obs.ptr && n >= 0, "pgw_battery_reset_f32: null argument");
+  PGW_LAUNCH((k_battery_reset<float, pgw_matf>), n, stream, *p, n, init, soc, obs);
 }
 
 int32_t pgw_battery_step(const pgw_battery_params* p, int64_t n, pgw_mat action, double* soc,
                          pgw_mat obs, double* real_power, void* stream) {
   PGW_REQUIRE(p && action.ptr && soc && obs.ptr && real_power && n >= 0,
               "pgw_battery_step: null argument");
-  PGW_LAUNCH(k_battery_step, n, stream, *p, n, action, soc, obs, real_power);
+  PGW_LAUNCH((k_battery_step<double, pgw_mat>), n, stream, *p, n, action, soc, obs, real_power);
+}
+
+int32_t pgw_battery_step_f32(const pgw_battery_params* p, int64_t n, pgw_matf action, float* soc,
+                             pgw_matf obs, float* real_power, void* stream) {
+  PGW_REQUIRE(p && action.ptr && soc && obs.ptr && real_power && n >= 0,
+              "pgw_battery_step_f32: null argument");
+  PGW_LAUNCH((k_battery_step<float, pgw_matf>), n, stream, *p, n, action, soc, obs, real_power);
 }
 
 int32_t pgw_pv_obs(const pgw_pv_params* p, int64_t n, double pmax, const double* min_voltage,

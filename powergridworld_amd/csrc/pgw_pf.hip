@@ -601,30 +601,34 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p, con
   store(kSlotReward, v);
 }
 
-// Scalar variant: one thread per (env, agent), any action layout.
+// Scalar variant: one thread per (env, agent), any action layout.  Bufs =
+// pgw_coord_buffers (fp64) or pgw_coord_buffers_f32 (fp32 storage: loads are
+// widened, every store rounds the fp64 result once).
+template <class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
                                                              pgw_coord_step_info s, int64_t n,
-                                                             pgw_coord_buffers b, double pv_ob,
+                                                             Bufs b, double pv_ob,
                                                              StdDerived dv) {
+  using S = std::remove_pointer_t<decltype(b.soc)>;
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int a = blockIdx.y;
   if (e >= n) return;
   StdAgentIn in[1];
-  const double* ap = b.action.ptr + a * b.act_stride_agent + e * b.action.s_env;
+  const S* ap = b.action.ptr + a * b.act_stride_agent + e * b.action.s_env;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) in[0].av[j] = ap[j * b.action.s_dim];
-  double* xp = b.x + (int64_t)a * 5 * n + e;
+  for (int j = 0; j < 8; ++j) in[0].av[j] = (double)ap[j * b.action.s_dim];
+  S* xp = b.x + (int64_t)a * 5 * n + e;
 #pragma unroll
-  for (int z = 0; z < 5; ++z) in[0].xs[z] = xp[z * n];
-  double* socp = b.soc + (int64_t)a * n + e;
-  in[0].soc = *socp;
-  double* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;
+  for (int z = 0; z < 5; ++z) in[0].xs[z] = (double)xp[z * n];
+  S* socp = b.soc + (int64_t)a * n + e;
+  in[0].soc = (double)*socp;
+  S* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;
   std_agent_compute<1>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
-    if (slot < kSlotSoc) xp[slot * n] = v[0];
-    else if (slot == kSlotSoc) *socp = v[0];
+    if (slot < kSlotSoc) xp[slot * n] = (S)v[0];
+    else if (slot == kSlotSoc) *socp = (S)v[0];
     else if (slot < kSlotPower) st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
-    else if (slot == kSlotPower) b.agent_power[(int64_t)a * n + e] = v[0];
-    else b.reward[(int64_t)a * n + e] = v[0];
+    else if (slot == kSlotPower) b.agent_power[(int64_t)a * n + e] = (S)v[0];
+    else b.reward[(int64_t)a * n + e] = (S)v[0];
   });
 }
 
@@ -653,9 +657,10 @@ struct CoordPFArgs {
   double vv_lo, vv_hi, vv_penalty;
 };
 
-template <int M, bool UB, bool GC, bool KEEP>
+template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
-                                                     int64_t n, pgw_coord_buffers b) {
+                                                     int64_t n, Bufs b) {
+  using Sto = std::remove_pointer_t<decltype(b.reward)>;   // double, or float (_f32)
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   // read once: a reload per phase would put an L2 round trip on the chain
@@ -671,7 +676,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   const int64_t ec = valid ? e : 0;
 #pragma unroll
   for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-    rp[ag] = b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
+    rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
              ((valid && ag < c.n_agents) ? 1.0 : 0.0);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
@@ -700,26 +705,27 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   pf_trace(trace, 4);
   if (!valid) return;
   double vsel = v0;
-  if (b.v_out) b.v_out[e] = v0;
+  if (b.v_out) b.v_out[e] = (Sto)v0;
   if constexpr (kKeep)
     for (int o = 1; o < a.n_out; ++o) {
       const double v = pf_node_pu<M>(t, o, ir, ii);
-      if (b.v_out) b.v_out[(int64_t)o * n + e] = v;
+      if (b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
       vsel = (o == c.vv_row) ? v : vsel;
     }
   if (b.iters) b.iters[e] = it;
   pf_trace(trace, 5);
   if (c.coordinated) {
     const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
-    if (b.vv) b.vv[e] = vv;
+    if (b.vv) b.vv[e] = (Sto)vv;
     const double share = (vv * c.vv_penalty) / (double)c.n_agents;
     // reward -= share as a no-return atomic add of -share: one IEEE add per
     // address (bit-identical to the subtraction, deterministic), no load
-    // round trip at the end of the kernel
+    // round trip at the end of the kernel.  fp32 storage: the share is rounded
+    // to fp32 first, so the add is RN32(r - RN32(share)).
 #pragma unroll
     for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
       if (ag < c.n_agents)
-        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, -share, __ATOMIC_RELAXED,
+        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -876,11 +882,11 @@ static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t 
   return check_launch("k_pf_solve");
 }
 
-template <int M, bool UB, bool GC, bool KEEP>
+template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_pf_tables& t,
-                               int64_t n, const pgw_coord_buffers& b, hipStream_t st) {
-  launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP>, dim3(grid_for(n)), dim3(kBlock), st, c, a, t,
-               n, b);
+                               int64_t n, const Bufs& b, hipStream_t st) {
+  launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP, Bufs>, dim3(grid_for(n)), dim3(kBlock), st, c, a,
+               t, n, b);
   return check_launch("k_coord_pf");
 }
 
@@ -906,6 +912,63 @@ static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_
 }  // namespace pgw
 
 using namespace pgw;
+
+// pgw_coord_step / pgw_coord_step_f32
+template <class Bufs>
+static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
+                          const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream) {
+  constexpr bool kF32 = std::is_same<Bufs, pgw_coord_buffers_f32>::value;
+  PGW_REQUIRE(p && pf && pft && s && n >= 0, "pgw_coord_step: null argument");
+  PGW_REQUIRE(p->n_agents >= 1 && p->n_agents <= PGW_MAX_AGENTS, "pgw_coord_step: bad n_agents");
+  PGW_REQUIRE(p->n_comp >= 1 && p->n_comp <= 3, "pgw_coord_step: bad n_comp");
+  PGW_REQUIRE(b.action.ptr && b.obs.ptr && b.reward && b.agent_power,
+              "pgw_coord_step: null buffer");
+  PGW_REQUIRE(pft->block, "pgw_coord_step: null PF block");
+  PGW_REQUIRE(!pft->load_scale && !pft->U_init, "pgw_coord_step: load_scale / U_init not supported");
+  PGW_REQUIRE(pf->m >= 1 && pf->m <= PGW_PF_MAX_M && pf->m == padded_m(pf->m),
+              "pgw_coord_step: pf m=%d not padded", pf->m);
+  PGW_REQUIRE(pf->n_out >= 1 && p->vv_row >= 0 && p->vv_row < pf->n_out,
+              "pgw_coord_step: bad vv_row");
+  PGW_REQUIRE(pft->G && pft->V0, "pgw_coord_step: missing G/V0");
+  PGW_REQUIRE(pf->max_iter >= 1, "pgw_coord_step: max_iter < 1");
+  PGW_REQUIRE(pf->n_ctrl >= 0 && pf->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_coord_step: bad n_ctrl");
+  for (int a = 0; a < p->n_agents; ++a)
+    PGW_REQUIRE(p->agent_ctrl[a] < pf->n_ctrl, "pgw_coord_step: agent_ctrl out of range");
+  for (int c = 0; c < p->n_comp; ++c) {
+    int k = p->comp_order[c];
+    PGW_REQUIRE(k >= 0 && k <= 2, "pgw_coord_step: bad comp_order");
+    if (k == 0) PGW_REQUIRE(b.x && p->act_bld >= 0 && p->bld.n_obs <= PGW_BLD_MAX_OBS, "pgw_coord_step: building");
+    if (k == 2) PGW_REQUIRE(b.soc && p->act_bat >= 0, "pgw_coord_step: storage");
+  }
+  if (n == 0) return PGW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const bool std_layout = coord_is_std(*p);
+  PGW_REQUIRE(std_layout || !kF32,
+              "pgw_coord_step_f32: needs the standard C4 agent layout (building/pv/storage at 0/6/7)");
+  // PVEnv.get_obs is the same for every env: evaluate it once here
+  const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
+                                        - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
+                                     : -s->pv_pmax;
+  CoordPFArgs c = {};
+  c.n_agents = p->n_agents;
+  c.coordinated = p->coordinated;
+  c.vv_row = p->vv_row;
+  for (int a = 0; a < p->n_agents; ++a) c.agent_ctrl[a] = p->agent_ctrl[a];
+  c.vv_lo = p->vv_lo;
+  c.vv_hi = p->vv_hi;
+  c.vv_penalty = p->vv_penalty;
+  const PFArgs a = make_pf_args(*pf, *pft);
+  if (std_layout) {
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std<Bufs>, dim3(grid_for(n), p->n_agents),
+                 dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
+  } else if constexpr (!kF32) {
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
+                 st, *p, *s, n, b);
+  }
+  int32_t rc = check_launch("k_coord_agents");
+  if (rc) return rc;
+  PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
+}
 
 extern "C" {
 
@@ -1014,54 +1077,13 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
                        const pgw_coord_step_info* s, int64_t n, pgw_coord_buffers b, void* stream) {
-  PGW_REQUIRE(p && pf && pft && s && n >= 0, "pgw_coord_step: null argument");
-  PGW_REQUIRE(p->n_agents >= 1 && p->n_agents <= PGW_MAX_AGENTS, "pgw_coord_step: bad n_agents");
-  PGW_REQUIRE(p->n_comp >= 1 && p->n_comp <= 3, "pgw_coord_step: bad n_comp");
-  PGW_REQUIRE(b.action.ptr && b.obs.ptr && b.reward && b.agent_power,
-              "pgw_coord_step: null buffer");
-  PGW_REQUIRE(pft->block, "pgw_coord_step: null PF block");
-  PGW_REQUIRE(!pft->load_scale && !pft->U_init, "pgw_coord_step: load_scale / U_init not supported");
-  PGW_REQUIRE(pf->m >= 1 && pf->m <= PGW_PF_MAX_M && pf->m == padded_m(pf->m),
-              "pgw_coord_step: pf m=%d not padded", pf->m);
-  PGW_REQUIRE(pf->n_out >= 1 && p->vv_row >= 0 && p->vv_row < pf->n_out,
-              "pgw_coord_step: bad vv_row");
-  PGW_REQUIRE(pft->G && pft->V0, "pgw_coord_step: missing G/V0");
-  PGW_REQUIRE(pf->max_iter >= 1, "pgw_coord_step: max_iter < 1");
-  PGW_REQUIRE(pf->n_ctrl >= 0 && pf->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_coord_step: bad n_ctrl");
-  for (int a = 0; a < p->n_agents; ++a)
-    PGW_REQUIRE(p->agent_ctrl[a] < pf->n_ctrl, "pgw_coord_step: agent_ctrl out of range");
-  for (int c = 0; c < p->n_comp; ++c) {
-    int k = p->comp_order[c];
-    PGW_REQUIRE(k >= 0 && k <= 2, "pgw_coord_step: bad comp_order");
-    if (k == 0) PGW_REQUIRE(b.x && p->act_bld >= 0 && p->bld.n_obs <= PGW_BLD_MAX_OBS, "pgw_coord_step: building");
-    if (k == 2) PGW_REQUIRE(b.soc && p->act_bat >= 0, "pgw_coord_step: storage");
-  }
-  if (n == 0) return PGW_OK;
-  hipStream_t st = (hipStream_t)stream;
-  const bool std_layout = coord_is_std(*p);
-  // PVEnv.get_obs is the same for every env: evaluate it once here
-  const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
-                                        - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
-                                     : -s->pv_pmax;
-  CoordPFArgs c = {};
-  c.n_agents = p->n_agents;
-  c.coordinated = p->coordinated;
-  c.vv_row = p->vv_row;
-  for (int a = 0; a < p->n_agents; ++a) c.agent_ctrl[a] = p->agent_ctrl[a];
-  c.vv_lo = p->vv_lo;
-  c.vv_hi = p->vv_hi;
-  c.vv_penalty = p->vv_penalty;
-  const PFArgs a = make_pf_args(*pf, *pft);
-  if (std_layout) {
-    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std, dim3(grid_for(n), p->n_agents),
-                 dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
-  } else {
-    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
-                 st, *p, *s, n, b);
-  }
-  int32_t rc = check_launch("k_coord_agents");
-  if (rc) return rc;
-  PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
+  return coord_step(p, pf, pft, s, n, b, stream);
+}
+
+int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
+                           const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                           pgw_coord_buffers_f32 b, void* stream) {
+  return coord_step(p, pf, pft, s, n, b, stream);
 }
 
 }  // extern "C"

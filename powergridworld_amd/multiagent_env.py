@@ -54,12 +54,17 @@ class MultiAgentEnv(Env):
     def __init__(self, common_config: dict = {}, pf_config: dict = {}, agents: list = None,
                  max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
                  device=None, fused: Union[bool, str] = "auto", record_history: bool = False,
-                 **kwargs):
+                 dtype=None, **kwargs):
         self.common_config = common_config
         self.rescale_spaces = rescale_spaces
         assert len(agents) > 0, "need at least one agent!"
         self.num_envs = int(num_envs)
         self.device = _lib.require_device(device)
+        # storage dtype of the per-env buffers: fp64 (the reference's), or fp32 on
+        # the fused path (pgw_coord_step_f32: fp32 storage, fp64 arithmetic)
+        self.dtype = _lib.storage_dtype(dtype)
+        if self.dtype != torch.float64 and fused is False:
+            raise ValueError("dtype=%s needs the fused path" % self.dtype)
         self.start_time = pd.Timestamp(common_config["start_time"])
         self.end_time = pd.Timestamp(common_config["end_time"])
         self.control_timedelta = common_config["control_timedelta"]
@@ -97,6 +102,10 @@ class MultiAgentEnv(Env):
         self._fused = None
         if fused:
             why = self._fusable()
+            if why is None and self.dtype != torch.float64:
+                why = self._f32_fusable()
+                if why is not None:
+                    raise ValueError("dtype=%s: %s" % (self.dtype, why))
             if why is None:
                 self._setup_fused()
             elif fused is True:
@@ -155,9 +164,15 @@ class MultiAgentEnv(Env):
         self.history = {"timestamp": [], "voltage": [], "agent_power_p": []}
         self.pf_solver.calculate_power_flow(current_time=self.time)
         self.voltages = self.pf_solver.get_bus_voltages()
+        f32 = self._fused is not None and self.dtype != torch.float64
+        if f32:
+            self._f32_sync(up=True)
         for agent in self.agents:
             kwargs = self.get_external_obs_vars(agent)
             _ = agent.reset(**kwargs)
+        if f32:
+            self._f32_sync(up=False)
+            return self._fused["obs_dict"]
         return self.get_obs()
 
     def get_obs(self) -> Dict[str, any]:
@@ -276,9 +291,53 @@ class MultiAgentEnv(Env):
             return "coordinated reward needs all agents on one bus"
         return None
 
+    def _f32_fusable(self):
+        """pgw_coord_step_f32 implements the standard C4 agent only."""
+        a0 = self.agents[0]
+        kinds = [type(e).fused_kind for e in a0.envs]
+        if kinds != ["building", "pv", "storage"]:
+            return "the fp32 fused step needs agents of [building, pv, storage] in that order"
+        if [e.action_space.shape[0] for e in a0.envs] != [6, 1, 1] or \
+                [e.observation_space.shape[0] for e in a0.envs] != [15, 1, 1]:
+            return "the fp32 fused step needs the default building action / observation layout"
+        return None
+
+    def _f32_sync(self, up):
+        """fp32 fused path: the component envs keep fp64 state for their reset
+        (it runs once per episode); the step state lives in the fp32 buffers.
+        up: fp32 -> components (x_k persists across resets, as in the
+        reference); down: components -> fp32 after their reset."""
+        F = self._fused
+        for ai, agent in enumerate(self.agents):
+            bld, pv, bat = agent.envs
+            if up:
+                bld.x.copy_(F["x"][ai])
+                bat.soc.copy_(F["soc"][ai])
+            else:
+                F["x"][ai].copy_(bld.x)
+                F["soc"][ai].copy_(bat.soc)
+                for i, e in enumerate(agent.envs):
+                    o = int(F["obs_off"][i])
+                    F["obs"][ai, o:o + F["obs_dims"][i]].copy_(e._obs.t())
+                F["reward"][ai].zero_()
+                F["agent_power"][ai].zero_()
+        if not up:
+            F["v_out"][: self.pf_solver.v_out.shape[0]].copy_(self.pf_solver.v_out)
+            self.voltages = F["voltages"]
+
+    def load_component_state(self):
+        """fp32 fused path: re-read the component envs' state and observations
+        into the fp32 step buffers, after a component was reset directly (e.g.
+        ``agent.env_dict["storage"].reset(init_storage=...)``).  No-op otherwise."""
+        if self._fused is not None and self.dtype != torch.float64:
+            self._f32_sync(up=False)
+        return self.packed_obs() if self._fused is not None else None
+
     def _setup_fused(self):
         n, na = self.num_envs, len(self.agents)
         dev = self.device
+        dt = self.dtype
+        f32 = dt != torch.float64
         a0 = self.agents[0]
         kinds = [type(e).fused_kind for e in a0.envs]
         act_dims = [e.action_space.shape[0] for e in a0.envs]
@@ -324,15 +383,24 @@ class MultiAgentEnv(Env):
 
         F = dict(params=p, kinds=kinds, act_off=act_off, obs_off=obs_off, act_dims=act_dims,
                  obs_dims=obs_dims, act_dim=act_dim, obs_dim=obs_dim)
-        F["obs"] = torch.zeros((na, obs_dim, n), dtype=torch.float64, device=dev)
-        F["act"] = torch.zeros((na, act_dim, n), dtype=torch.float64, device=dev)
-        F["x"] = torch.zeros((na, 5, n), dtype=torch.float64, device=dev)
-        F["soc"] = torch.zeros((na, n), dtype=torch.float64, device=dev)
-        F["reward"] = torch.zeros((na, n), dtype=torch.float64, device=dev)
-        F["agent_power"] = torch.zeros((na, n), dtype=torch.float64, device=dev)
-        F["vv"] = torch.zeros(n, dtype=torch.float64, device=dev)
+        F["obs"] = torch.zeros((na, obs_dim, n), dtype=dt, device=dev)
+        F["act"] = torch.zeros((na, act_dim, n), dtype=dt, device=dev)
+        F["x"] = torch.zeros((na, 5, n), dtype=dt, device=dev)
+        F["soc"] = torch.zeros((na, n), dtype=dt, device=dev)
+        F["reward"] = torch.zeros((na, n), dtype=dt, device=dev)
+        F["agent_power"] = torch.zeros((na, n), dtype=dt, device=dev)
+        F["vv"] = torch.zeros(n, dtype=dt, device=dev)
         F["iters"] = torch.zeros(n, dtype=torch.int32, device=dev)
+        # fp32: own voltage rows; fp64: the solver's v_out (its bus_voltages views)
+        F["v_out"] = torch.zeros_like(self.pf_solver.v_out, dtype=dt) if f32 else self.pf_solver.v_out
+        F["voltages"] = {name: F["v_out"][i] for i, name in enumerate(self.pf_solver.output_names)}
         for ai, agent in enumerate(self.agents):
+            if f32:       # the components keep their fp64 buffers (reset only, _f32_sync)
+                F["x"][ai].copy_(agent.envs[0].x)
+                F["soc"][ai].copy_(agent.envs[2].soc)
+                agent._real_power = F["agent_power"][ai]
+                agent._reward = F["reward"][ai]
+                continue
             for i, (k, e) in enumerate(zip(kinds, agent.envs)):
                 view = F["obs"][ai, int(obs_off[i]):int(obs_off[i]) + obs_dims[i]].t()
                 if k == "building":
@@ -344,13 +412,15 @@ class MultiAgentEnv(Env):
             agent._real_power = F["agent_power"][ai]
             agent._reward = F["reward"][ai]
         # ---- constant per-step launch state and return values (views)
-        bufs = _lib.CoordBuffers()
+        bufs = _lib.CoordBuffersF32() if f32 else _lib.CoordBuffers()
+        F["Mat"] = _lib.Matf if f32 else _lib.Mat
+        F["kernel"] = "pgw_coord_step_f32" if f32 else "pgw_coord_step"
         obs = F["obs"]
-        bufs.obs = _lib.Mat(obs.data_ptr(), 1, obs.stride(1))
+        bufs.obs = F["Mat"](obs.data_ptr(), 1, obs.stride(1))
         bufs.obs_stride_agent = obs.stride(0)
         bufs.x, bufs.soc = F["x"].data_ptr(), F["soc"].data_ptr()
         bufs.reward, bufs.agent_power = F["reward"].data_ptr(), F["agent_power"].data_ptr()
-        bufs.v_out = self.pf_solver.v_out.data_ptr()
+        bufs.v_out = F["v_out"].data_ptr()
         bufs.vv, bufs.iters = F["vv"].data_ptr(), F["iters"].data_ptr()
         F["bufs"], F["act_key"], F["step_cache"] = bufs, None, {}
         comps = [dict(zip(kinds, agent.envs)) for agent in self.agents]
@@ -359,7 +429,13 @@ class MultiAgentEnv(Env):
         F["pv_envs"] = [c["pv"] for c in comps if "pv" in c]
         F["bat_envs"] = [c["storage"] for c in comps if "storage" in c]
         F["agent0_envs"] = list(self.agents[0].envs)
-        F["obs_dict"] = {agent.name: {e.name: e._obs for e in agent.envs} for agent in self.agents}
+        if f32:
+            F["obs_dict"] = {agent.name: {e.name: F["obs"][ai, int(F["obs_off"][i]):int(F["obs_off"][i]) +
+                                                   F["obs_dims"][i]].t()
+                                          for i, e in enumerate(agent.envs)}
+                             for ai, agent in enumerate(self.agents)}
+        else:
+            F["obs_dict"] = {agent.name: {e.name: e._obs for e in agent.envs} for agent in self.agents}
         F["rew_dict"] = {agent.name: F["reward"][ai] for ai, agent in enumerate(self.agents)}
         F["done_true"] = {agent.name: True for agent in self.agents}
         F["done_false"] = {agent.name: False for agent in self.agents}
@@ -388,13 +464,14 @@ class MultiAgentEnv(Env):
             if action.dim() != 3 or tuple(action.shape) != (na, n, F["act_dim"]):
                 raise ValueError("packed action must be [n_agents=%d, N=%d, act_dim=%d], got %s"
                                  % (na, n, F["act_dim"], tuple(action.shape)))
-            if action.dtype != torch.float64 or action.device != self.device:
-                action = action.to(device=self.device, dtype=torch.float64)
+            if action.dtype != self.dtype or action.device != self.device:
+                action = action.to(device=self.device, dtype=self.dtype)
             return action
         packed, views = self.action_buffer()
         for ai, agent in enumerate(self.agents):
             for i, e in enumerate(agent.envs):
-                src = as_action(action[agent.name][e.name], self.num_envs, F["act_dims"][i], self.device)
+                src = as_action(action[agent.name][e.name], self.num_envs, F["act_dims"][i], self.device,
+                                self.dtype)
                 views[agent.name][e.name].copy_(src)
         return packed
 
@@ -404,7 +481,7 @@ class MultiAgentEnv(Env):
         key = (act.data_ptr(), act.stride(0), act.stride(1), act.stride(2))
         bufs = F["bufs"]
         if key != F["act_key"]:
-            bufs.action = _lib.Mat(key[0], key[2], key[3])
+            bufs.action = F["Mat"](key[0], key[2], key[3])
             bufs.act_stride_agent = key[1]
             F["act_key"] = key
         bld, pv = F["bld0"], F["pv0"]
@@ -430,12 +507,12 @@ class MultiAgentEnv(Env):
         if tv != solver.tables_version:    # the table solve above recycled the device tables
             F["step_cache"].clear()
             return self._step_fused(action)
-        rc = _lib.lib().pgw_coord_step(F["params"], pfp, pft, info,
-                                       self.num_envs, bufs, _lib.stream_ptr(self.device))
+        rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
+                                              self.num_envs, bufs, _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
         self.pf_solver.iterations = F["iters"]
-        self.voltages = self.pf_solver.bus_voltages
+        self.voltages = F["voltages"]
         # advance the component clocks (their is_terminal() drives `done`)
         for e in F["bld_envs"]:
             e.time_index += 1

@@ -1,0 +1,153 @@
+"""fp32-storage variants (pgw_*_f32): state, actions and outputs
+stored as fp32, arithmetic in fp64.  Needs an MI355X.
+
+Two kinds of check:
+* one-step parity (bit level): from the same fp32 state and fp32-representable
+  actions, every fp32 output equals the fp64 path's output rounded to fp32
+  (within 1 fp32 ulp where a second rounding is involved: the coordinated
+  reward is RN32(RN32(r) - RN32(share)));
+* a free-running episode against the fp64 path within the north-star fp32
+  bound, 1e-3 relative (BASELINE.json north_star).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+F32_ULP = 2.0 ** -23
+
+
+def rn32(t):
+    return t.to(torch.float32)
+
+
+def assert_f32(got, want64, ulps=1, atol=0.0):
+    """got (fp32) == RN32(want64) within `ulps` fp32 ulps."""
+    assert got.dtype == torch.float32
+    want = rn32(want64).double()
+    g = got.double()
+    tol = ulps * F32_ULP * want.abs() + atol
+    bad = (g - want).abs() > tol
+    assert not bad.any(), (int(bad.sum()), g[bad][:5].tolist(), want[bad][:5].tolist())
+
+
+def test_battery_f32_one_step_and_episode():
+    from powergridworld_amd.agents import EnergyStorageEnv
+    n = 4096
+    gen = torch.Generator(DEV).manual_seed(3)
+    init = (torch.rand(n, dtype=torch.float64, device=DEV, generator=gen) * 60.0).float()
+    e32 = EnergyStorageEnv(num_envs=n, device=DEV, dtype=torch.float32)
+    e64 = EnergyStorageEnv(num_envs=n, device=DEV)
+    free = EnergyStorageEnv(num_envs=n, device=DEV)
+    o32 = e32.reset(init_storage=init)[0]
+    o64 = e64.reset(init_storage=init.double())[0]
+    free.reset(init_storage=init.double())
+    assert o32.dtype == torch.float32 and e32.soc.dtype == torch.float32
+    assert_f32(o32, o64, ulps=0)
+    assert_f32(e32.soc, e64.soc, ulps=0)
+    for t in range(300):
+        a = (torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2.6 - 1.3).float()
+        e64.soc.copy_(e32.soc)                      # teacher forcing: same fp32 state
+        o32, r32, d32, _ = e32.step(a)
+        o64, _, d64, _ = e64.step(a.double())
+        _, _, _, _ = free.step(a.double())
+        assert_f32(o32, o64, ulps=0)
+        assert_f32(e32.soc, e64.soc, ulps=0)
+        assert_f32(e32.real_power, e64.real_power, ulps=0)
+        assert d32 == d64
+    # free-running fp64 vs fp32: SoC is continuous in the state (the clamps end at
+    # the bounds), so it stays within the fp32 bound over the whole episode
+    np.testing.assert_allclose(e32.soc.double().cpu().numpy(), free.soc.cpu().numpy(), rtol=1e-3, atol=1e-3)
+
+
+def _c4_pair(n, seed):
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    e32 = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV,
+                                             dtype=torch.float32)
+    e64 = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
+    assert e32._fused is not None and e32._fused["kernel"] == "pgw_coord_step_f32"
+    gen = torch.Generator(DEV).manual_seed(seed)
+    init = (torch.rand((5, n), dtype=torch.float64, device=DEV, generator=gen) * 50.0).float().double()
+    for e in (e32, e64):
+        e.reset()
+        for a, agent in enumerate(e.agents):
+            agent.env_dict["storage"].reset(init_storage=init[a])
+    e32.load_component_state()
+    return e32, e64, gen
+
+
+def test_c4_f32_one_step_parity():
+    """Teacher-forced: each step starts the fp64 fused env from the fp32 env's
+    state; every fp32 output is the fp64 output rounded once."""
+    n = 8192
+    e32, e64, gen = _c4_pair(n, 5)
+    assert_f32(e32.packed_obs(), e64.packed_obs(), ulps=0)
+    F32, F64 = e32._fused, e64._fused
+    names = [a.name for a in e32.agents]
+    for t in range(40):
+        F64["x"].copy_(F32["x"])
+        F64["soc"].copy_(F32["soc"])
+        act = (torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=gen) * 2.2 - 1.1).float()
+        _, r32, d32, m32 = e32.step(act)
+        _, r64, d64, m64 = e64.step(act.double())
+        assert_f32(e32.packed_obs(), e64.packed_obs(), ulps=0)
+        assert_f32(F32["x"], F64["x"], ulps=0)
+        assert_f32(F32["soc"], F64["soc"], ulps=0)
+        assert_f32(F32["agent_power"], F64["agent_power"], ulps=0)
+        # PF from the fp32-rounded agent powers (same values, summed in fp64)
+        assert_f32(F32["v_out"][0], F64["v_out"][0], ulps=1)
+        assert_f32(m32["voltage_violation"], m64["voltage_violation"], ulps=1, atol=1e-9)
+        for nm in names:
+            assert_f32(r32[nm], r64[nm], ulps=2, atol=1e-6)
+        assert d32["__all__"] == d64["__all__"]
+
+
+def test_c4_f32_episode_within_bound():
+    """Free-running full episode (286 steps + the next reset) at batch 4096
+    against the fp64 path: observations within 1e-3 relative (north star).
+    The reward contains the reference's discontinuous battery clamp
+    (energy_storage_env.py:117-126 omit the efficiency) via the agent power in
+    the voltage penalty, so a state 1 fp32 ulp from a clamp threshold can take
+    the other branch; rewards are held to the bound on all but a 1e-4 fraction."""
+    n = 4096
+    e32, e64, gen = _c4_pair(n, 9)
+    names = [a.name for a in e32.agents]
+    bad_r, tot_r = 0, 0
+    steps = 0
+    while True:
+        act = (torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=gen) * 2 - 1).float()
+        _, r32, d32, _ = e32.step(act)
+        _, r64, d64, _ = e64.step(act.double())
+        steps += 1
+        np.testing.assert_allclose(e32.packed_obs().double().cpu().numpy(),
+                                   e64.packed_obs().cpu().numpy(), rtol=1e-3, atol=1e-3)
+        for nm in names:
+            g, w = r32[nm].double(), r64[nm]
+            bad_r += int(((g - w).abs() > 1e-3 * w.abs() + 1e-3).sum())
+            tot_r += n
+        assert d32["__all__"] == d64["__all__"]
+        if d64["__all__"]:
+            break
+    assert steps == 286
+    assert bad_r <= 1e-4 * tot_r, (bad_r, tot_r)
+    o32, o64 = e32.reset(), e64.reset()      # x_k persists across the reset
+    for nm in names:
+        for c in ("building", "pv"):         # (storage: each env draws its own initial SoC)
+            np.testing.assert_allclose(o32[nm][c].double().cpu().numpy(), o64[nm][c].cpu().numpy(),
+                                       rtol=1e-3, atol=1e-3)
+
+
+def test_f32_refuses_non_standard_layout():
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    from powergridworld_amd.agents import EnergyStorageEnv
+    from powergridworld_amd.agents.pv import PVEnv
+    with pytest.raises(ValueError):
+        CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=8, device=DEV,
+                                           dtype=torch.float32, fused=False)
+    with pytest.raises(NotImplementedError):
+        PVEnv(profile_csv="pv_profile.csv", num_envs=8, device=DEV, dtype=torch.float32)
+    with pytest.raises(Exception):
+        EnergyStorageEnv(num_envs=8, device=DEV, dtype=torch.float16)
