@@ -113,6 +113,8 @@ class OpenDSSSolver(PowerFlowSolver):
         self.tables = _lib.PFTables(block=self._block.data_ptr(), G=self._G.data_ptr(),
                                     V0=self._V0.data_ptr())
         self.v_out = torch.zeros((max(len(names), 1), self.num_envs), dtype=torch.float64, device=dev)
+        self._own_v_out = self.v_out
+        self._bv_cache = {}
         self._iters = torch.zeros(self.num_envs, dtype=torch.int32, device=dev)
         n_pred = self.PREDICTOR_N
         self._pred_x = torch.tensor([[self.PREDICTOR_X0 + j * self.PREDICTOR_H for j in range(n_pred)]],
@@ -306,11 +308,30 @@ class OpenDSSSolver(PowerFlowSolver):
         self.iterations = self._iters
         self._prepare_bus_voltages()
 
+    def bind_output(self, v_out=None):
+        """Write the next solves' node voltages into `v_out` ([n_out, N] fp64, e.g.
+        a slot of MultiAgentEnv's on-device voltage history) instead of the
+        solver's own buffer; None restores the own buffer."""
+        if v_out is None:
+            v_out = self._own_v_out
+        elif (v_out.dtype != torch.float64 or v_out.device != self._own_v_out.device or
+              tuple(v_out.shape) != tuple(self._own_v_out.shape) or not v_out.is_contiguous()):
+            raise ValueError("bind_output: need a contiguous fp64 [%d, %d] tensor on %s"
+                             % (tuple(self._own_v_out.shape) + (self._own_v_out.device,)))
+        self.v_out = v_out
+
     def _prepare_bus_voltages(self):
-        """{node: [N] view of its v_out row}; the views stay valid across solves."""
+        """{node: [N] view of its v_out row}; the views stay valid across solves
+        (one dict per output buffer, cached)."""
         key = (self.v_out.data_ptr(), tuple(self.output_names))
         if getattr(self, "_bv_key", None) != key:
-            self.bus_voltages = {name: self.v_out[i] for i, name in enumerate(self.output_names)}
+            cache = self.__dict__.setdefault("_bv_cache", {})
+            bv = cache.get(key)
+            if bv is None:
+                if len(cache) > 8192:
+                    cache.clear()
+                bv = cache[key] = {name: self.v_out[i] for i, name in enumerate(self.output_names)}
+            self.bus_voltages = bv
             self._bv_key = key
         self._extrema = None
 

@@ -54,7 +54,7 @@ class MultiAgentEnv(Env):
     def __init__(self, common_config: dict = {}, pf_config: dict = {}, agents: list = None,
                  max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
                  device=None, fused: Union[bool, str] = "auto", record_history: bool = False,
-                 dtype=None, **kwargs):
+                 dtype=None, history_capacity: int = None, **kwargs):
         self.common_config = common_config
         self.rescale_spaces = rescale_spaces
         assert len(agents) > 0, "need at least one agent!"
@@ -115,6 +115,9 @@ class MultiAgentEnv(Env):
         if self._fused is None:
             buses = sorted(set(self.agent_name_bus_map.values()))
             self.pf_solver.set_controllable_loads(buses)
+        self._hist = None
+        if self.record_history:
+            self._init_history(history_capacity)
 
     # ================================================================ hooks
     @abstractmethod
@@ -162,6 +165,12 @@ class MultiAgentEnv(Env):
         self.episode_step = 0
         self.time = self._time_at(0)
         self.history = {"timestamp": [], "voltage": [], "agent_power_p": []}
+        if self._hist is not None:
+            self._hist["t"] = 0
+            self.pf_solver.bind_output(None)     # the reset solve is not recorded
+            if self._fused is not None:          # agents' real power back off the ring
+                for ai, agent in enumerate(self.agents):
+                    agent._real_power = self._fused["agent_power"][ai]
         self.pf_solver.calculate_power_flow(current_time=self.time)
         self.voltages = self.pf_solver.get_bus_voltages()
         f32 = self._fused is not None and self.dtype != torch.float64
@@ -213,6 +222,12 @@ class MultiAgentEnv(Env):
             load_bus = self.agent_name_bus_map[name]
             p, q = agent.real_power, agent.reactive_power
             agent_power_p.append(p)
+        if self._hist is not None:                     # this step's history slot
+            self.pf_solver.bind_output(self._hist["v"][self._hist["t"] % self._hist["cap"]])
+        for agent in self.agents:
+            name = agent.name
+            load_bus = self.agent_name_bus_map[name]
+            p, q = agent.real_power, agent.reactive_power
             if load_bus in load_p:
                 load_p[load_bus] = load_p[load_bus] + p
                 load_q[load_bus] = load_q[load_bus] + q
@@ -227,11 +242,59 @@ class MultiAgentEnv(Env):
         meta = self.meta_transform(meta)
         return obs, rew, done, meta
 
+    def _init_history(self, capacity):
+        """On-device voltage / agent-power history: a ring of
+        `capacity` step slots, [cap, n_nodes, N] voltages and [cap, n_agents, N]
+        agent powers, in place of the reference's per-step dict copies
+        (multiagent_env.py:129, 191-194).  On the fused path the kernels write
+        each step's outputs straight into its slot (no copy); the history lists
+        hold views of the slots, valid until the ring wraps (clone to keep)."""
+        if capacity is None:
+            capacity = int(min(self.max_episode_steps, self._end_step, 4096)) + 1
+        cap, n = int(capacity), self.num_envs
+        if cap < 1:
+            raise ValueError("history_capacity must be >= 1")
+        solver = self.pf_solver
+        rows = {name: i for i, name in enumerate(solver.output_names)}
+        names = [x for x in solver.feeder.node_names if x in rows]
+        dt = self.dtype if self._fused is not None else torch.float64
+        H = {"cap": cap, "t": 0,
+             "v": torch.zeros((cap, len(solver.output_names), n), dtype=dt, device=self.device),
+             "p": torch.zeros((cap, len(self.agents), n), dtype=dt, device=self.device)}
+        # per-slot views, built once: {node: [N]} in the reference's node order
+        H["vd"] = [{x: H["v"][s_, rows[x]] for x in names} for s_ in range(cap)]
+        H["pl"] = [[H["p"][s_, a] for a in range(len(self.agents))] for s_ in range(cap)]
+        self._hist = H
+
+    def voltage_history(self):
+        """(voltages [T, n_nodes, N], agent powers [T, n_agents, N], node names) of
+        the steps recorded this episode (the last `history_capacity` if more), as
+        views of the device ring in step order when it has not wrapped."""
+        H = self._hist
+        if H is None:
+            raise RuntimeError("record_history=False")
+        t, cap = H["t"], H["cap"]
+        order = list(range(t)) if t <= cap else [(t + i) % cap for i in range(cap)]
+        idx = torch.tensor(order, dtype=torch.long, device=self.device)
+        v, p = (H["v"][:t], H["p"][:t]) if t <= cap else (H["v"][idx], H["p"][idx])
+        rows = {name: i for i, name in enumerate(self.pf_solver.output_names)}
+        names = list(H["vd"][0].keys())
+        perm = [rows[x] for x in names]
+        if perm != list(range(len(perm))):
+            v = v[:, perm]
+        return v, p, names
+
     def _record(self, agent_power_p):
-        if self.record_history:
-            self.history["timestamp"].append(self.time)
-            self.history["voltage"].append({k: v.clone() for k, v in self.voltages.items()})
-            self.history["agent_power_p"].append([p.clone() for p in agent_power_p])
+        H = self._hist
+        if H is None:
+            return
+        s_ = H["t"] % H["cap"]
+        if self._fused is None:                # the fused kernels wrote the slot themselves
+            torch.stack(agent_power_p, out=H["p"][s_])
+        H["t"] += 1
+        self.history["timestamp"].append(self.time)
+        self.history["voltage"].append(H["vd"][s_])
+        self.history["agent_power_p"].append(H["pl"][s_])
 
     @property
     def agent_dict(self) -> Dict[str, ComponentEnv]:
@@ -358,6 +421,8 @@ class MultiAgentEnv(Env):
                     out_nodes.append(x)
         if not out_nodes:
             out_nodes = [self.pf_solver.feeder.node_names[0]]
+        if self.record_history:            # the history holds every node (AllBusMagPu)
+            out_nodes += [x for x in self.pf_solver.feeder.node_names if x not in out_nodes]
         self.pf_solver.set_output_nodes(out_nodes)
         if self.fused_reward_transform == "coordinated" and len(_bus_nodes(buses[0])) != 1:
             raise ValueError("coordinated reward needs a single-phase common bus (e.g. '675c')")
@@ -507,12 +572,24 @@ class MultiAgentEnv(Env):
         if tv != solver.tables_version:    # the table solve above recycled the device tables
             F["step_cache"].clear()
             return self._step_fused(action)
+        H = self._hist
+        if H is not None:            # outputs straight into this step's history slot
+            s_ = H["t"] % H["cap"]
+            bufs.v_out, bufs.agent_power = H["v"][s_].data_ptr(), H["p"][s_].data_ptr()
         rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
                                               self.num_envs, bufs, _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
         self.pf_solver.iterations = F["iters"]
-        self.voltages = F["voltages"]
+        if H is None:
+            self.voltages = F["voltages"]
+        else:
+            self.voltages = H["vd"][s_]
+            for ai, agent in enumerate(self.agents):
+                agent._real_power = H["pl"][s_][ai]
+            if self.dtype == torch.float64:       # keep the solver's views current
+                solver.bind_output(H["v"][s_])
+                solver._prepare_bus_voltages()
         # advance the component clocks (their is_terminal() drives `done`)
         for e in F["bld_envs"]:
             e.time_index += 1
@@ -521,8 +598,8 @@ class MultiAgentEnv(Env):
         for e in F["bat_envs"]:
             e.simulation_step += 1
         d = any(e.is_terminal() for e in F["agent0_envs"])
-        if self.record_history:
-            self._record([F["agent_power"][ai] for ai in range(len(self.agents))])
+        if H is not None:
+            self._record(None)
         return F["obs_dict"], F["rew_dict"], F["done_true"] if d else F["done_false"], F["meta"]
 
     def packed_obs(self):

@@ -482,3 +482,53 @@ def test_mc_fused_equals_generic_c3():
             assert torch.equal(fused.env_dict[c].real_power, generic.env_dict[c].real_power), c
         assert torch.equal(rf, rg) and torch.equal(fused.real_power, generic.real_power)
         assert df == dg
+
+
+# ------------------------------------------------------------------ voltage history
+def test_history_ring_fused_and_generic():
+    """record_history=True: the on-device ring holds every node's voltage and
+    every agent's power per step (the reference's self.history,
+    multiagent_env.py:129, 191-194).  Fused (kernels write the slot) and generic
+    (solver bound to the slot) agree bit for bit, recording does not change the
+    step results, and the ring wraps at its capacity."""
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    n, steps = 1000, 12
+    mk = lambda **kw: CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, **kw)
+    envs = [mk(fused=True, record_history=True), mk(fused=False, record_history=True),
+            mk(fused=True), mk(fused=True, record_history=True, history_capacity=5)]
+    init = torch.rand((5, n), dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(4)) * 50
+    for e in envs:
+        e.reset()
+        for a, agent in enumerate(e.agents):
+            agent.env_dict["storage"].reset(init_storage=init[a])
+    names = [a.name for a in envs[0].agents]
+    gen = torch.Generator(DEV).manual_seed(6)
+    nodes = envs[1].pf_solver.feeder.node_names
+    for t in range(steps):
+        act = torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=gen) * 2 - 1
+        dict_act = {nm: {"building": act[a, :, :6], "pv": act[a, :, 6:7], "storage": act[a, :, 7:8]}
+                    for a, nm in enumerate(names)}
+        outs = [e.step(act if e._fused is not None else dict_act) for e in envs]
+        for o in outs[1:]:
+            for nm in names:
+                assert torch.equal(outs[0][1][nm], o[1][nm])
+        hf, hg = envs[0].history, envs[1].history
+        assert list(hf["voltage"][t].keys()) == list(nodes) == list(hg["voltage"][t].keys())
+        for x in nodes:
+            assert torch.equal(hf["voltage"][t][x], hg["voltage"][t][x]), x
+        for a in range(5):
+            assert torch.equal(hf["agent_power_p"][t][a], hg["agent_power_p"][t][a])
+        # the solver and env views follow the newest slot
+        assert torch.equal(envs[0].pf_solver.get_bus_voltage_by_name("675c"),
+                           envs[2].pf_solver.get_bus_voltage_by_name("675c"))
+        assert torch.equal(envs[0].voltages["675.3"], hf["voltage"][t]["675.3"])
+    v, p, vn = envs[0].voltage_history()
+    assert tuple(v.shape) == (steps, len(nodes), n) and tuple(p.shape) == (steps, 5, n) and vn == list(nodes)
+    for t in (0, steps - 1):
+        assert torch.equal(v[t, vn.index("675.3")], envs[0].history["voltage"][t]["675.3"])
+    v5, p5, _ = envs[3].voltage_history()          # wrapped: the last 5 steps in order
+    assert tuple(v5.shape) == (5, len(nodes), n)
+    assert torch.equal(v5, v[-5:]) and torch.equal(p5, p[-5:])
+    vg, pg, _ = envs[1].voltage_history()
+    assert torch.equal(vg, v) and torch.equal(pg, p)
