@@ -146,9 +146,13 @@ def main():
     from powergridworld_amd import distributed as pgd
     rank, local, world = pgd.env_rank()
     dist = world > 1
-    dev = torch.device("cuda", local)
+    # PGW_BENCH_REHEARSE=1: rehearse N ranks on fewer GPUs (ranks share devices
+    # round-robin, collectives on gloo) -- a correctness check of the N>1 path,
+    # never a measurement
+    rehearse = os.environ.get("PGW_BENCH_REHEARSE") == "1"
+    dev = torch.device("cuda", local % torch.cuda.device_count() if rehearse else local)
     torch.cuda.set_device(dev)
-    pgd.init("nccl", dev)
+    pgd.init("gloo" if rehearse else "nccl", dev)
     if dist:
         import torch.distributed as tdist
 
