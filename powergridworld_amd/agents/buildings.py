@@ -244,6 +244,7 @@ class FiveZoneROMEnv(ComponentEnv):
             self.x = x
         if obs is not None:
             self._obs = obs
+        self._bufv += 1
 
     def _ext(self, kw):
         n = self.num_envs
@@ -309,16 +310,25 @@ class FiveZoneROMEnv(ComponentEnv):
         return self._obs, {"p_consumed": self.p_consumed}
 
     # ---- fused MultiComponentEnv step (pgw_mc_agent_step): same as step() in an MC
+    def _mc_static(self, args, slot):
+        args.bld, args.bld_ext = self.params, _lib.BuildingExt()
+        args.bld_x, args.bld_reward_state = self.x.data_ptr(), self._reward_state.data_ptr()
+        c = args.comp[slot]
+        c.kind, c.obs, c.real_power = 0, _lib.mat(self._obs), self.p_consumed.data_ptr()
+
     def _mc_prepare(self, args, slot, action, obs_kwargs):
         a = as_action(action, self.num_envs, 6, self.device)
         t = self.time_index
         if t + 1 >= len(self._exo):
             raise IndexError("building stepped past the end of its exogenous data")
-        ext, keep = self._ext(obs_kwargs)
-        args.bld, args.bld_ex_t, args.bld_ex_next, args.bld_ext = self.params, self._exo[t], self._exo[t + 1], ext
-        args.bld_x, args.bld_reward_state = self.x.data_ptr(), self._reward_state.data_ptr()
-        c = args.comp[slot]
-        c.kind, c.action, c.obs, c.real_power = 0, _lib.mat(a), _lib.mat(self._obs), self.p_consumed.data_ptr()
+        keep = None
+        if obs_kwargs:
+            args.bld_ext, keep = self._ext(obs_kwargs)
+        elif args.bld_ext.bus_voltage or args.bld_ext.min_voltage or args.bld_ext.max_voltage or \
+                args.bld_ext.p_setpoint:
+            args.bld_ext = _lib.BuildingExt()
+        args.bld_ex_t, args.bld_ex_next = self._exo[t], self._exo[t + 1]
+        args.comp[slot].action = self._act_mat(a)
         return a, keep
 
     def _mc_finish(self, obs_kwargs):

@@ -81,6 +81,8 @@ class EnergyStorageEnv(ComponentEnv):
             self.soc = soc
         if obs is not None:
             self._obs = obs
+        self._bufv += 1
+        self._step_c = None
 
     def reset(self, init_storage=None, **kwargs):
         """(:72-97) SoC ~ mean + std * truncnorm(-1, 1) unless init_storage is given
@@ -107,23 +109,28 @@ class EnergyStorageEnv(ComponentEnv):
     def step(self, action, **kwargs):
         """(:131-157)"""
         a = as_action(action, self.num_envs, 1, self.device, self.dtype)
-        _lib.check(getattr(_lib.lib(), self._k_step)(self.params, self.num_envs, self._mat(a),
-                                                     _lib.dptr(self.soc), self._mat(self._obs),
-                                                     _lib.dptr(self._real_power), self._stream()))
-        obs, meta = self.get_obs()
+        c = self.__dict__.get("_step_c")
+        if c is None or c[0] is not self._real_power:      # per-layout constants, built once
+            c = self._step_c = (self._real_power, getattr(_lib.lib(), self._k_step),
+                                _lib.dptr(self.soc), self._mat(self._obs), _lib.dptr(self._real_power),
+                                self._obs, {"state_of_charge": self.soc.unsqueeze(1)})
+        _lib.check(c[1](self.params, self.num_envs, self._act_mat(a), c[2], c[3], c[4], self._stream()))
         self.simulation_step += 1
-        return obs, self._zero_reward, self.is_terminal(), meta
+        return c[5], self._zero_reward, self.is_terminal(), c[6]
 
     def step_reward(self, **kwargs):
         return self._zero_reward, {}
 
     mc_kind = 2
 
-    def _mc_prepare(self, args, slot, action, kwargs):
-        a = as_action(action, self.num_envs, 1, self.device)
+    def _mc_static(self, args, slot):
         args.bat, args.bat_soc = self.params, self.soc.data_ptr()
         c = args.comp[slot]
-        c.kind, c.action, c.obs, c.real_power = 2, _lib.mat(a), _lib.mat(self._obs), self._real_power.data_ptr()
+        c.kind, c.obs, c.real_power = 2, _lib.mat(self._obs), self._real_power.data_ptr()
+
+    def _mc_prepare(self, args, slot, action, kwargs):
+        a = as_action(action, self.num_envs, 1, self.device)
+        args.comp[slot].action = self._act_mat(a)
         return a
 
     def _mc_finish(self, kwargs):

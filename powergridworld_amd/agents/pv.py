@@ -65,6 +65,7 @@ class PVEnv(ComponentEnv):
     def _adopt(self, obs=None):
         if obs is not None:
             self._obs = obs
+        self._bufv += 1
 
     def _min_voltage(self, kwargs):
         if not self.grid_aware:
@@ -80,13 +81,20 @@ class PVEnv(ComponentEnv):
 
     mc_kind = 1
 
+    def _mc_static(self, args, slot):
+        args.pv = self.params
+        c = args.comp[slot]
+        c.kind, c.obs, c.real_power = 1, _lib.mat(self._obs), self._real_power.data_ptr()
+
     def _mc_prepare(self, args, slot, action, kwargs):
         a = as_action(action, self.num_envs, 1, self.device)
-        vmin = self._min_voltage(kwargs)
         self._mc_pmax = float(self.data[self.index])
-        args.pv, args.pv_pmax, args.pv_min_voltage = self.params, self._mc_pmax, _lib.dptr(vmin)
-        c = args.comp[slot]
-        c.kind, c.action, c.obs, c.real_power = 1, _lib.mat(a), _lib.mat(self._obs), self._real_power.data_ptr()
+        args.pv_pmax = self._mc_pmax
+        vmin = None
+        if self.grid_aware:
+            vmin = self._min_voltage(kwargs)
+            args.pv_min_voltage = vmin.data_ptr()
+        args.comp[slot].action = self._act_mat(a)
         return a, vmin
 
     def _mc_finish(self, kwargs):

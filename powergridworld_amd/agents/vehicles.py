@@ -116,11 +116,22 @@ class EVChargingEnv(ComponentEnv):
         self.time_index = None
         self.time = None
         self._prev_window = None
+        self._info_cache = {}
 
     def _window(self, time):
         return (time >= self._start) & (time <= self._endp_floor)                      # :186-190
 
     def _step_info(self, action_given):
+        # a pure function of (time index, first step after reset): lockstep envs
+        # share the schedule, so it is built once per episode step and cached
+        key = (self.time_index, self._prev_window is None)
+        c = self._info_cache.get(key)
+        if c is None:
+            c = self._info_cache[key] = self._build_step_info()
+        self._prev_window = c[1]
+        return c[0]
+
+    def _build_step_info(self):
         s = _lib.EVStepInfo()
         s.time = float(self.time)
         s.next_time = float(self.simulation_times[self.time_index + 1])
@@ -131,8 +142,7 @@ class EVChargingEnv(ComponentEnv):
         for w, (a, b) in enumerate(zip(_pack_bits(win), _pack_bits(win | prev))):
             s.window[w] = a
             s.scan[w] = b
-        self._prev_window = win
-        return s
+        return s, win
 
     def _advance(self, action):
         s = self._step_info(action is not None)
@@ -147,14 +157,17 @@ class EVChargingEnv(ComponentEnv):
 
     mc_kind = 3
 
-    def _mc_prepare(self, args, slot, action, kwargs):
-        s = self._step_info(action is not None)
-        a = as_action(action, self.num_envs, 1, self.device)
-        args.ev, args.ev_step = self.params, s
+    def _mc_static(self, args, slot):
+        args.ev = self.params
         args.ev_endp, args.ev_req = self._endp_dev.data_ptr(), self.req.data_ptr()
         args.ev_charging, args.ev_reward = self.charging.data_ptr(), self._reward.data_ptr()
         c = args.comp[slot]
-        c.kind, c.action, c.obs, c.real_power = 3, _lib.mat(a), _lib.mat(self._obs), self._real_power.data_ptr()
+        c.kind, c.obs, c.real_power = 3, _lib.mat(self._obs), self._real_power.data_ptr()
+
+    def _mc_prepare(self, args, slot, action, kwargs):
+        args.ev_step = self._step_info(action is not None)
+        a = as_action(action, self.num_envs, 1, self.device)
+        args.comp[slot].action = self._act_mat(a)
         return a
 
     def _mc_finish(self, kwargs):
