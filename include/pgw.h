@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 8
+#define PGW_ABI_VERSION 9
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -206,6 +206,11 @@ typedef struct pgw_ev_step_info {
   double time;           /* minutes, before the step's advance        */
   double next_time;      /* simulation_times[time_index + 1]          */
   double action_default; /* raw action used when action.ptr == NULL (reset step) */
+  /* Optional (device, NULL = computed in the kernel): per vehicle v,
+   * tl_rcp[2v] = (end_park[v] - time) / 60 (time left in hours, the
+   * reference's expression, :199) and tl_rcp[2v+1] = 1 / tl_rcp[2v], so the
+   * per-vehicle division by it is exact_div (bit-identical, no IEEE divide). */
+  const double* tl_rcp;
   int32_t n_words, pad_;
   uint64_t window[PGW_EV_MAX_WORDS];
   uint64_t scan[PGW_EV_MAX_WORDS];

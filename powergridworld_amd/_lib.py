@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -72,7 +72,8 @@ class EVParams(C.Structure):
 
 
 class EVStepInfo(C.Structure):
-    _fields_ = [("time", f64), ("next_time", f64), ("action_default", f64), ("n_words", i32),
+    _fields_ = [("time", f64), ("next_time", f64), ("action_default", f64), ("tl_rcp", vp),
+                ("n_words", i32),
                 ("pad_", i32), ("window", u64 * EV_MAX_WORDS), ("scan", u64 * EV_MAX_WORDS)]
 
 

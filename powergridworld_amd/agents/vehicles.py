@@ -111,6 +111,12 @@ class EVChargingEnv(ComponentEnv):
         self.charging = torch.zeros((max(self._words, 1), n), dtype=torch.int64, device=self.device)
         self._req0_dev = torch.tensor(self._req0, dtype=torch.float64, device=self.device)
         self._endp_dev = torch.tensor(endp.astype(np.float64), dtype=torch.float64, device=self.device)
+        # per step t and vehicle v: time left in hours, (end_park[v] - time_t) / 60 with the
+        # reference's IEEE operations (:199), and its reciprocal for the kernel's exact_div
+        tl = (endp.astype(np.float64)[None, :] - self.simulation_times.astype(np.float64)[:, None]) / 60.0
+        rcp = np.divide(1.0, tl, out=np.zeros_like(tl), where=tl != 0.0)
+        self._tl_rcp = torch.tensor(np.ascontiguousarray(np.stack([tl, rcp], -1)), dtype=torch.float64,
+                                    device=self.device)
         self._reward = torch.zeros(n, dtype=torch.float64, device=self.device)
         self._obs = self._new_obs(6)
         self.time_index = None
@@ -136,6 +142,7 @@ class EVChargingEnv(ComponentEnv):
         s.time = float(self.time)
         s.next_time = float(self.simulation_times[self.time_index + 1])
         s.action_default = float(self._action_space.low[0])                           # :178
+        s.tl_rcp = self._tl_rcp[self.time_index].data_ptr() if self.num_vehicles else None
         s.n_words = self._words
         win = self._window(self.time)
         prev = self._prev_window if self._prev_window is not None else np.zeros_like(win)

@@ -299,4 +299,86 @@ __device__ __forceinline__ void building_write_obs(const pgw_building_params& p,
   }
 }
 
+// ---------------------------------------------------------------- std building
+// The reference's default 5-zone building (state_space_model.p input_sel_list
+// [1,8,7,2] / [1,8,6,2] and neighbours, defaults.py:2-10 observation config)
+// with the selections as compile-time indices and the divisions by host
+// reciprocals (exact_div): the same IEEE results as the generic functions
+// above, op for op, in far fewer instructions.  k_coord_agents_std
+// (pgw_pf.hip) is the same arithmetic for the C4 agent.
+struct BldDerived {
+  double act_rng[6], act_sum[6];                 // actions: hi - lo, hi + lo
+  double obs_sum[15], obs_rng[15], obs_rcp[15];  // obs: lo + hi, hi - lo, 1 / (hi - lo)
+};
+
+inline BldDerived make_bld_derived(const pgw_building_params& p) {
+  BldDerived d = {};
+  for (int j = 0; j < 6; ++j) {
+    d.act_rng[j] = p.act_high[j] - p.act_low[j];
+    d.act_sum[j] = p.act_high[j] + p.act_low[j];
+  }
+  for (int j = 0; j < 15; ++j) {
+    d.obs_sum[j] = p.obs_low[j] + p.obs_high[j];
+    d.obs_rng[j] = p.obs_high[j] - p.obs_low[j];
+    d.obs_rcp[j] = 1.0 / d.obs_rng[j];
+  }
+  return d;
+}
+
+inline bool bld_is_std(const pgw_building_params& p) {
+  static const int sel[5][4] = {{0, 7, 6, 1}, {0, 7, 6, 1}, {0, 7, 5, 1}, {0, 7, 5, 1}, {0, 7, 5, 1}};
+  static const int nbr[5][4] = {{1, 2, 3, 4}, {0, 2, 3, 4}, {0, 1, 3, 4}, {0, 1, 2, 4}, {0, 1, 2, 3}};
+  if (p.n_obs != 15) return false;
+  for (int z = 0; z < 5; ++z)
+    for (int j = 0; j < 4; ++j)
+      if (p.sel[z][j] != sel[z][j] || p.nbr[z][j] != nbr[z][j]) return false;
+  for (int j = 0; j < 15; ++j)
+    if (p.obs_var[j] != 5 + j) return false;
+  return true;
+}
+
+// One std building step (five_zone_rom_env.py:183-225 + the thermal-energy
+// reward :315-335): av = the 6 actions as given (rescaled if p.rescale), xs =
+// x_k in/out.  Returns p_consumed; `reward` = the fresh reward; obs slot j goes
+// to store(j, value).
+template <class Store>
+__device__ __forceinline__ double bld_std_step(const pgw_building_params& B, const BldDerived& d,
+                                               const pgw_building_exo& ex, const pgw_building_exo& exn,
+                                               double (&av)[6], double (&xs)[5], double& reward,
+                                               Store&& store) {
+  double T[5];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
+    av[j] = B.rescale ? (clip_fast(av[j], -1.0, 1.0) * d.act_rng[j] + d.act_sum[j]) * 0.5 : av[j];
+#pragma unroll
+  for (int z = 0; z < 5; ++z) T[z] = B.C[z] * xs[z] + B.mean[z];
+#pragma unroll
+  for (int z = 0; z < 5; ++z) {
+    const int nz = z < 2 ? 4 : (z == 2 ? 3 : 2);
+    const double u0 = ex.T_oa - T[z];
+    const double u1 = av[z] * (av[5] - T[z]);
+    const double u2 = T[nz] - T[z];
+    const double u3 = ex.q_solar[z];
+    double bu = B.B[z][0] * u0;
+    bu = bu + B.B[z][1] * u1;
+    bu = bu + B.B[z][2] * u2;
+    bu = bu + B.B[z][3] * u3;
+    xs[z] = B.A[z] * xs[z] + bu;   // T still holds the pre-step temps
+  }
+#pragma unroll
+  for (int z = 0; z < 5; ++z) T[z] = B.C[z] * xs[z] + B.mean[z];
+  const double pc = building_p_consumed(av, ex.T_oa);
+  reward = building_reward(B, T, exn.comfort_lb, exn.comfort_ub, pc, exact_div(-pc, 12.0, 1.0 / 12.0));
+  const double lb = exn.comfort_lb, ub = exn.comfort_ub;
+#pragma unroll
+  for (int j = 0; j < 15; ++j) {
+    const double o = j < 5 ? T[j] - ub : j < 10 ? lb - T[j - 5] : j == 10 ? lb
+                   : j == 11 ? ub : j == 12 ? exn.T_oa : j == 13 ? pc : exn.time_of_day;
+    double c = clip_fast(o, B.obs_low[j], B.obs_high[j]);
+    if (B.rescale) c = exact_div(2.0 * c - d.obs_sum[j], d.obs_rng[j], d.obs_rcp[j]);
+    store(j, c);
+  }
+  return pc;
+}
+
 }  // namespace pgw

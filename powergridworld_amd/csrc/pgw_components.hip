@@ -118,12 +118,29 @@ __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p
 }
 
 // One env's FiveZoneROMEnv.step_ (:183-225); returns p_consumed (its real power).
-__device__ __forceinline__ double building_step_env(const pgw_building_params& p, const pgw_building_exo& ex,
+// STD: the reference's default model/obs layout (bld_is_std), via bld_std_step.
+template <bool STD>
+__device__ __forceinline__ double building_step_env(const pgw_building_params& p, const BldDerived& d,
+                                                    const pgw_building_exo& ex,
                                                     const pgw_building_exo& exn, int64_t n, int64_t e,
                                                     const pgw_mat& act, double* __restrict__ x,
                                                     double* __restrict__ pcons, double* __restrict__ rout,
                                                     double* __restrict__ rstate, int32_t lagged,
                                                     const pgw_building_ext& ext, const pgw_mat& obs) {
+  if constexpr (STD) {
+    double av[6], xs[5], fresh;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) av[j] = ld(act, e, j);
+#pragma unroll
+    for (int z = 0; z < 5; ++z) xs[z] = x[z * n + e];
+    const double pc = bld_std_step(p, d, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); });
+#pragma unroll
+    for (int z = 0; z < 5; ++z) x[z * n + e] = xs[z];
+    pcons[e] = pc;
+    if (rout) rout[e] = lagged ? rstate[e] : fresh;
+    if (rstate) rstate[e] = fresh;
+    return pc;
+  }
   double a[6], xs[5], T[5];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -151,7 +168,9 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
   return pc;
 }
 
-__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p, pgw_building_exo ex,
+template <bool STD>
+__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p, BldDerived d,
+                                                          pgw_building_exo ex,
                                                           pgw_building_exo exn, int64_t n, pgw_mat act,
                                                           double* __restrict__ x,
                                                           double* __restrict__ pcons,
@@ -160,7 +179,7 @@ __global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p,
                                                           pgw_building_ext ext, pgw_mat obs) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  (void)building_step_env(p, ex, exn, n, e, act, x, pcons, rout, rstate, lagged, ext, obs);
+  (void)building_step_env<STD>(p, d, ex, exn, n, e, act, x, pcons, rout, rstate, lagged, ext, obs);
 }
 
 // ====================================================================== EV
@@ -188,31 +207,61 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
   double kwh = a * p.rate * p.hours_per_step;
   double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
   int dcnt = 0, nact = 0;
+  // The scan mask is wave-uniform (scalar), so the vehicle loop is too.  The
+  // vehicles go in chunks of kEvChunk: the chunk's requirements are loaded back
+  // to back (one memory round trip per chunk, not per vehicle), then processed
+  // in ascending order exactly as one at a time.  Both passes walk the same
+  // chunk mask, so no index array is needed.
+  constexpr int kEvChunk = 8;
   for (int w = 0; w < s.n_words; ++w) {
-    uint64_t scan = s.scan[w], win = s.window[w];
-    uint64_t prev = chg[(int64_t)w * n + e];
+    uint64_t scan = s.scan[w];
+    const uint64_t win = s.window[w];
+    const uint64_t prev = chg[(int64_t)w * n + e];
     uint64_t now_bits = 0ull;
     while (scan) {
-      int b = __builtin_ctzll(scan);
-      scan &= scan - 1;
-      int v = w * 64 + b;
-      double r = req[(int64_t)v * n + e];
-      bool active = ((win >> b) & 1ull) && (r > 0.0);
-      if (active) {
-        now_bits |= 1ull << b;
-        ++nact;
-        demand = demand + r;
-        double tl = (endp[v] - s.time) / 60.0;
-        if (tl > 0.0) {
-          double def = pymax(0.0, p.rate - r / tl);
-          dsum = dsum + def;
-          ++dcnt;
-          double ch = pymin(kwh, r);
-          req[(int64_t)v * n + e] = r - ch;
-          consumed = consumed + ch;
+      uint64_t chunk = scan;
+#pragma unroll
+      for (int i = 0; i < kEvChunk; ++i) scan &= scan - 1;   // the chunk: the next <= kEvChunk bits
+      chunk &= ~scan;
+      double rs[kEvChunk];
+      uint64_t m = chunk;
+#pragma unroll
+      for (int i = 0; i < kEvChunk; ++i) {
+        const int b = m ? __builtin_ctzll(m) : 0;    // past the chunk's end: a harmless reload
+        rs[i] = req[(int64_t)(w * 64 + b) * n + e];
+        m &= m - 1;
+      }
+      m = chunk;
+#pragma unroll
+      for (int i = 0; i < kEvChunk; ++i) {
+        if (m == 0) continue;          // uniform: the chunk's tail
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        const int v = w * 64 + b;
+        const double r = rs[i];
+        bool active = ((win >> b) & 1ull) && (r > 0.0);
+        if (active) {
+          now_bits |= 1ull << b;
+          ++nact;
+          demand = demand + r;
+          double tl, rc = 0.0;
+          if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
+            tl = s.tl_rcp[2 * v];
+            rc = s.tl_rcp[2 * v + 1];
+          } else {
+            tl = (endp[v] - s.time) / 60.0;
+          }
+          if (tl > 0.0) {
+            double def = pymax(0.0, p.rate - (s.tl_rcp ? exact_div(r, tl, rc) : r / tl));
+            dsum = dsum + def;
+            ++dcnt;
+            double ch = pymin(kwh, r);
+            req[(int64_t)v * n + e] = r - ch;
+            consumed = consumed + ch;
+          }
+        } else if ((prev >> b) & 1ull) {
+          unserved = unserved + r;          // departed: not charging now (:239-243)
         }
-      } else if ((prev >> b) & 1ull) {
-        unserved = unserved + r;          // departed: not charging now (:239-243)
       }
     }
     chg[(int64_t)w * n + e] = now_bits;
@@ -247,40 +296,51 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
 }
 
 // ====================================================================== fused MC step
+// One component of an MC agent for env e; writes its real power (and its
+// reward where it has one) to the component's own buffers.
+template <bool STD>
+__device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const pgw_mc_component& C,
+                                             const BldDerived& d, int64_t n, int64_t e) {
+  switch (C.kind) {
+    case PGW_MC_BUILDING:
+      (void)building_step_env<STD>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
+                                   C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
+      break;
+    case PGW_MC_PV:
+      C.real_power[e] = pv_step_env(a.pv, e, a.pv_pmax, C.action, a.pv_min_voltage, C.obs);
+      break;
+    case PGW_MC_STORAGE:
+      C.real_power[e] = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
+      break;
+    default:
+      ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
+                  C.real_power, a.ev_reward);
+      break;
+  }
+}
+
 // MultiComponentEnv.step (base.py:114-139) of an agent made of building / PV /
 // storage / EV components (each at most once, any order): every component's
 // step in order, then real power and reward summed in order from 0 -- the
-// generic path's kernels and k_agent_reduce in one launch.
-__global__ void __launch_bounds__(kBlock) k_mc_step(pgw_mc_step_args a, int64_t n) {
-  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// generic path's kernels and k_agent_reduce in one launch.  (Measured and
+// dropped: the components as parallel blocks with the last one per env block
+// forming the sums -- the device-scope release/acquire fences that make the
+// other blocks' outputs visible across XCDs write back L2 and cost more than
+// the overlap gains: C3 19.7 -> 34.6 us.)
+template <bool STD>
+__global__ void __launch_bounds__(kBlock) k_mc_step(pgw_mc_step_args a, BldDerived d, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
+  for (int c = 0; c < a.n_comp; ++c) mc_component<STD>(a, a.comp[c], d, n, e);
   double rp_sum = 0.0, rew_sum = 0.0;
-  for (int c = 0; c < a.n_comp; ++c) {
-    const pgw_mc_component& C = a.comp[c];
-    double rp = 0.0, rew = 0.0;
-    switch (C.kind) {
-      case PGW_MC_BUILDING:
-        rp = building_step_env(a.bld, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x, C.real_power,
-                               nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
-        rew = a.bld_reward_state[e];
-        break;
-      case PGW_MC_PV:
-        rp = pv_step_env(a.pv, e, a.pv_pmax, C.action, a.pv_min_voltage, C.obs);
-        C.real_power[e] = rp;
-        break;
-      case PGW_MC_STORAGE:
-        rp = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
-        C.real_power[e] = rp;
-        break;
-      default:
-        ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
-                    C.real_power, a.ev_reward);
-        rp = C.real_power[e];
-        rew = a.ev_reward[e];
-        break;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c < a.n_comp) {
+      const int kind = a.comp[c].kind;
+      rp_sum = rp_sum + a.comp[c].real_power[e];
+      rew_sum = rew_sum + (kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
+                           : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0);
     }
-    rp_sum = rp_sum + rp;
-    rew_sum = rew_sum + rew;
   }
   a.real_power[e] = rp_sum;
   a.reward[e] = rew_sum;
@@ -375,8 +435,12 @@ int32_t pgw_building_step(const pgw_building_params* p, const pgw_building_exo* 
               "pgw_building_step: null argument");
   PGW_REQUIRE(!lagged || reward_state, "pgw_building_step: lagged reward needs reward_state");
   PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_step: bad n_obs");
-  PGW_LAUNCH(k_building_step, n, stream, *p, *ex_t, *ex_next, n, action, x, p_consumed, reward_out,
-             reward_state, lagged, ext, obs);
+  const BldDerived d = make_bld_derived(*p);
+  if (bld_is_std(*p))
+    PGW_LAUNCH(k_building_step<true>, n, stream, *p, d, *ex_t, *ex_next, n, action, x, p_consumed,
+               reward_out, reward_state, lagged, ext, obs);
+  PGW_LAUNCH(k_building_step<false>, n, stream, *p, d, *ex_t, *ex_next, n, action, x, p_consumed,
+             reward_out, reward_state, lagged, ext, obs);
 }
 
 int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, double* req,
@@ -417,7 +481,12 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
       PGW_REQUIRE(a->ev_endp && a->ev_req && a->ev_charging && a->ev_reward &&
                   a->ev_step.n_words <= PGW_EV_MAX_WORDS, "pgw_mc_agent_step: EV buffers");
   }
-  PGW_LAUNCH(k_mc_step, n, stream, *a, n);
+  const BldDerived d = make_bld_derived(a->bld);
+  bool std_bld = false;
+  for (int c = 0; c < a->n_comp; ++c)
+    if (a->comp[c].kind == PGW_MC_BUILDING) std_bld = bld_is_std(a->bld);
+  if (std_bld) PGW_LAUNCH(k_mc_step<true>, n, stream, *a, d, n);
+  PGW_LAUNCH(k_mc_step<false>, n, stream, *a, d, n);
 }
 
 int32_t pgw_agent_reduce(const pgw_reduce_args* a, int64_t n, double* real_power, double* reward,

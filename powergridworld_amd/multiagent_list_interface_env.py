@@ -53,7 +53,7 @@ class MultiAgentListInterfaceEnv(spaces.Env):
                 act = action                          # already [n_agents, N, act_dim]
             else:
                 for i, a in enumerate(action):
-                    packed[i].copy_(torch.as_tensor(a, dtype=torch.float64).to(packed.device)
+                    packed[i].copy_(torch.as_tensor(a, dtype=packed.dtype).to(packed.device)
                                     .reshape(packed.shape[1:]))
                 act = packed
             next_obs, reward, done, info = self.ma_env.step(act)
