@@ -10,7 +10,7 @@ import os
 import sys
 
 NAMES = {"k_coord_agents_std": "k_coord_agents_std",
-         "k_coord_pf<14, true, false, false>": "k_coord_pf<14,true,false,false>",
+         "k_coord_pf<14, true, false, false": "k_coord_pf<14,true,false,false>",
          "k_pf_solve<14, true, false, false>": "k_pf_solve<14,true,false,false>"}
 
 
