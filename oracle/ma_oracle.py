@@ -65,3 +65,60 @@ class CoordinatedOracle:
         rew = np.stack(rew) - (vv * self.VV_UNIT_PENALTY) / self.n
         self.done = bool(np.any(dones) or self.t >= self.end)
         return np.stack(obs), rew, vv
+
+
+class MultiAgentOracle:
+    """MultiAgentEnv (gridworld/multiagent_env.py:24-212) with the base
+    pass-through reward / meta transforms, for agents that observe no grid
+    voltage (get_external_obs_vars :90-115 then passes nothing): each agent
+    steps in list order, its real power is added to its bus load (:171-181,
+    the first agent's value then ``+=``), the power flow runs at the advanced
+    time (:183-189), and the episode ends when any agent is done, at
+    max_episode_steps - 1, or when the time reaches end_time (:199-202).
+
+    agents: list of (name, bus, oracle) with oracle an MCOracle or a component
+    oracle.  A standalone building returns its lagged reward
+    (five_zone_rom_env.py:215); components in an MCOracle the fresh sum."""
+
+    def __init__(self, K, agents, sys_load, start, end, dt=DT, max_episode_steps=None):
+        self.K, self.agents = K, agents
+        self.pf = BatchedPF(system_load_rescale_factor=sys_load)
+        self.start, self.end, self.dt = pd.Timestamp(start), pd.Timestamp(end), dt
+        self.max_episode_steps = np.inf if max_episode_steps is None else max_episode_steps
+
+    def _obs(self, ag):
+        if isinstance(ag, MCOracle):
+            return {n: (c.get_obs() if isinstance(c, BuildingOracle) else c.obs()) for n, c in ag.comps}
+        return ag.get_obs() if isinstance(ag, BuildingOracle) else ag.obs()
+
+    def reset(self, init_storage=None):
+        """init_storage: {agent name: [K] initial SoC} for the agents holding a battery."""
+        init_storage = init_storage or {}
+        self.t = self.start
+        self.episode_step = 0
+        self.v = self.pf.calculate(self.t, K=self.K)                     # :131-133
+        for name, _, ag in self.agents:
+            if isinstance(ag, MCOracle):
+                ag.reset(init_storage=init_storage.get(name))
+            elif isinstance(ag, BatteryOracle):
+                ag.reset(init_storage[name])
+            else:
+                ag.reset()
+        return {name: self._obs(ag) for name, _, ag in self.agents}
+
+    def step(self, action):
+        self.episode_step += 1
+        self.t = self.t + self.dt
+        obs, rew, done, load = {}, {}, [], {}
+        for name, bus, ag in self.agents:
+            if isinstance(ag, BuildingOracle):
+                o, r, d, _ = ag.step(action[name], lagged_reward=True)
+            else:
+                o, r, d, _ = ag.step(action[name])
+            obs[name], rew[name] = o, r
+            done.append(np.any(d))
+            p = ag.real_power
+            load[bus] = load[bus] + p if bus in load else p
+        self.v = self.pf.calculate(self.t, load, K=self.K)
+        d = bool(any(done) or self.episode_step == self.max_episode_steps - 1 or self.t >= self.end)
+        return obs, rew, d

@@ -16,6 +16,7 @@ Two execution paths behind the reference API:
   through them.
 """
 from abc import abstractmethod
+from collections.abc import Mapping
 from typing import Dict, Tuple, Union
 
 import ctypes as C
@@ -100,6 +101,7 @@ class MultiAgentEnv(Env):
         self.action_space = {agent.name: agent.action_space for agent in self.agents}
 
         self._fused = None
+        self._fused_steps = 0
         if fused:
             why = self._fusable()
             if why is None and self.dtype != torch.float64:
@@ -173,6 +175,9 @@ class MultiAgentEnv(Env):
                     agent._real_power = self._fused["agent_power"][ai]
         self.pf_solver.calculate_power_flow(current_time=self.time)
         self.voltages = self.pf_solver.get_bus_voltages()
+        if self._fused is not None and len(self.pf_solver.output_names) < self.pf_solver.feeder.n:
+            lazy = _FusedVoltages(self, dict(self.voltages), self._fused_steps, reset=True)
+            self.voltages = self.pf_solver.bus_voltages = lazy
         f32 = self._fused is not None and self.dtype != torch.float64
         if f32:
             self._f32_sync(up=True)
@@ -387,6 +392,40 @@ class MultiAgentEnv(Env):
         if not up:
             F["v_out"][: self.pf_solver.v_out.shape[0]].copy_(self.pf_solver.v_out)
             self.voltages = F["voltages"]
+            if len(self.pf_solver.output_names) < self.pf_solver.feeder.n:
+                self.voltages = _FusedVoltages(self, F["voltages"], self._fused_steps, reset=True)
+
+    def _full_voltages(self, step_no, reset=False):
+        """Every node's voltage for the fused step `step_no` (_FusedVoltages): the
+        same snap solve as the kernel's -- the bus loads summed in agent order
+        from the step's agent powers, the same predictor first guess -- on a
+        second solver that outputs all nodes, so the values are the ones the
+        generic path reports (tests/test_gpu_parity.py checks fused == generic)."""
+        if step_no != self._fused_steps:
+            raise RuntimeError("voltages of an earlier step: the fused path solves the other nodes "
+                               "on demand from the step's agent powers, which a later step overwrote")
+        F, solver = self._fused, self.pf_solver
+        full = self.__dict__.get("_pf_full")
+        if full is None:
+            full = self._pf_full = type(solver)(**self.pf_config["config"], num_envs=self.num_envs,
+                                               device=self.device)
+        ctrl = solver._ctrl_names
+        full.set_controllable_loads(ctrl)
+        if reset:                                   # the reset solve: no controllable load
+            full.calculate_power_flow(current_time=self.time)
+        else:
+            sums, p = {}, F["params"]
+            for ai in range(len(self.agents)):
+                s_ = p.agent_ctrl[ai]
+                if s_ >= 0:
+                    x = F["agent_power"][ai].double()
+                    sums[s_] = sums[s_] + x if s_ in sums else x    # 0 + p0 + p1 ... (kernel order)
+            full.calculate_power_flow(p_controllable_consumed={ctrl[k]: v for k, v in sums.items()},
+                                      current_time=self.time)
+        out = full.get_bus_voltages()
+        if self.dtype != torch.float64:
+            out = {k: v.to(self.dtype) for k, v in out.items()}
+        return out
 
     def load_component_state(self):
         """fp32 fused path: re-read the component envs' state and observations
@@ -581,8 +620,12 @@ class MultiAgentEnv(Env):
         if rc:
             _lib.check(rc)
         self.pf_solver.iterations = F["iters"]
+        self._fused_steps += 1
         if H is None:
-            self.voltages = F["voltages"]
+            # the rows the kernel wrote, every other node solved on first access
+            lazy = _FusedVoltages(self, F["voltages"], self._fused_steps)
+            self.voltages = lazy
+            solver.bus_voltages = lazy
         else:
             self.voltages = H["vd"][s_]
             for ai, agent in enumerate(self.agents):
@@ -605,6 +648,35 @@ class MultiAgentEnv(Env):
     def packed_obs(self):
         """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""
         return self._fused["obs"].transpose(1, 2)
+
+
+class _FusedVoltages(Mapping):
+    """{node: [N] voltage} after a fused step, in the feeder's node order like
+    OpenDSS's AllBusMagPu (opendss.py:156-165).  The kernel writes only the rows
+    the step needs (the coordinated bus); the others are solved on first access
+    (MultiAgentEnv._full_voltages), so the hot path pays nothing for them."""
+    __slots__ = ("_env", "_fast", "_step", "_reset", "_full")
+
+    def __init__(self, env, fast, step_no, reset=False):
+        self._env, self._fast, self._step, self._reset, self._full = env, fast, step_no, reset, None
+
+    def _all(self):
+        if self._full is None:
+            self._full = self._env._full_voltages(self._step, self._reset)
+        return self._full
+
+    def __getitem__(self, node):
+        v = self._fast.get(node)
+        return v if v is not None else self._all()[node]
+
+    def __iter__(self):
+        return iter(self._env.pf_solver.feeder.node_names)
+
+    def __len__(self):
+        return len(self._env.pf_solver.feeder.node_names)
+
+    def copy(self):
+        return dict(self.items())
 
 
 def _bus_nodes(bus):
