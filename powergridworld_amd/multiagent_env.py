@@ -176,8 +176,9 @@ class MultiAgentEnv(Env):
         self.pf_solver.calculate_power_flow(current_time=self.time)
         self.voltages = self.pf_solver.get_bus_voltages()
         if self._fused is not None and len(self.pf_solver.output_names) < self.pf_solver.feeder.n:
-            lazy = _FusedVoltages(self, dict(self.voltages), self._fused_steps, reset=True)
-            self.voltages = self.pf_solver.bus_voltages = lazy
+            # the reset solve's rows, every other node solved on first access
+            self.voltages = self.pf_solver.bus_voltages = _FusedVoltages(
+                self, dict(self.voltages), self._fused_steps, reset=True)
         f32 = self._fused is not None and self.dtype != torch.float64
         if f32:
             self._f32_sync(up=True)
@@ -498,6 +499,7 @@ class MultiAgentEnv(Env):
         # fp32: own voltage rows; fp64: the solver's v_out (its bus_voltages views)
         F["v_out"] = torch.zeros_like(self.pf_solver.v_out, dtype=dt) if f32 else self.pf_solver.v_out
         F["voltages"] = {name: F["v_out"][i] for i, name in enumerate(self.pf_solver.output_names)}
+        F["lazy_v"] = _FusedVoltages(self, F["voltages"], 0)     # reused every step
         for ai, agent in enumerate(self.agents):
             if f32:       # the components keep their fp64 buffers (reset only, _f32_sync)
                 F["x"][ai].copy_(agent.envs[0].x)
@@ -623,9 +625,9 @@ class MultiAgentEnv(Env):
         self._fused_steps += 1
         if H is None:
             # the rows the kernel wrote, every other node solved on first access
-            lazy = _FusedVoltages(self, F["voltages"], self._fused_steps)
-            self.voltages = lazy
-            solver.bus_voltages = lazy
+            lazy = F["lazy_v"]
+            lazy._step, lazy._reset, lazy._full = self._fused_steps, False, None
+            self.voltages = solver.bus_voltages = lazy
         else:
             self.voltages = H["vd"][s_]
             for ai, agent in enumerate(self.agents):
@@ -654,7 +656,9 @@ class _FusedVoltages(Mapping):
     """{node: [N] voltage} after a fused step, in the feeder's node order like
     OpenDSS's AllBusMagPu (opendss.py:156-165).  The kernel writes only the rows
     the step needs (the coordinated bus); the others are solved on first access
-    (MultiAgentEnv._full_voltages), so the hot path pays nothing for them."""
+    (MultiAgentEnv._full_voltages), so the hot path pays nothing for them.  Like
+    every per-step output it describes the latest step (one object per env,
+    re-armed each step)."""
     __slots__ = ("_env", "_fast", "_step", "_reset", "_full")
 
     def __init__(self, env, fast, step_no, reset=False):
