@@ -331,8 +331,10 @@ class OpenDSSSolver(PowerFlowSolver):
                 if len(cache) > 8192:
                     cache.clear()
                 bv = cache[key] = {name: self.v_out[i] for i, name in enumerate(self.output_names)}
-            self.bus_voltages = bv
+            self._bv = bv
             self._bv_key = key
+        # (a fused MultiAgentEnv step replaces bus_voltages with its own mapping)
+        self.bus_voltages = self._bv
         self._extrema = None
 
     def voltage_extrema(self):

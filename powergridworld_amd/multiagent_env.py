@@ -178,7 +178,7 @@ class MultiAgentEnv(Env):
         if self._fused is not None and len(self.pf_solver.output_names) < self.pf_solver.feeder.n:
             # the reset solve's rows, every other node solved on first access
             self.voltages = self.pf_solver.bus_voltages = _FusedVoltages(
-                self, dict(self.voltages), self._fused_steps, reset=True)
+                self, self.pf_solver.bus_voltages, self._fused_steps, reset=True)
         f32 = self._fused is not None and self.dtype != torch.float64
         if f32:
             self._f32_sync(up=True)

@@ -1,0 +1,72 @@
+"""Host cost split of the fused C4 step at a tiny batch (GPU far ahead):
+the whole env.step, the bare ctypes pgw_coord_step call with the same cached
+arguments, and an empty torch launch for reference."""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
+from powergridworld_amd import _lib
+from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+
+n = 256
+env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=torch.device("cuda", 0), fused=True)
+act = torch.zeros((5, n, 8), dtype=torch.float64, device="cuda")
+env.reset()
+
+
+def run(k):
+    for _ in range(k):
+        _, _, d, _ = env.step(act)
+        if d["__all__"]:
+            env.reset()
+
+
+run(600)
+torch.cuda.synchronize()
+for rep in range(3):
+    t0 = time.perf_counter()
+    run(572)
+    torch.cuda.synchronize()
+    print("env.step: %.1f us/step" % ((time.perf_counter() - t0) / 572 * 1e6))
+F = env._fused
+info, pfp, pft, _ = next(iter(F["step_cache"].values()))
+lib, st = _lib.lib(), _lib.stream_ptr(env.device)
+fn = getattr(lib, F["kernel"])
+for rep in range(3):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        fn(F["params"], pfp, pft, info, n, F["bufs"], st)
+    torch.cuda.synchronize()
+    print("bare pgw_coord_step (2 launches): %.1f us/call" % ((time.perf_counter() - t0) / 2000 * 1e6))
+x = torch.zeros(16, device="cuda")
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        x.add_(1.0)
+    torch.cuda.synchronize()
+    print("torch add_ launch: %.1f us" % ((time.perf_counter() - t0) / 2000 * 1e6))
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(20000):
+        lib.pgw_pf_padded_m(14)
+    print("ctypes trivial call: %.2f us" % ((time.perf_counter() - t0) / 20000 * 1e6))
+ra = _lib.ReduceArgs()
+ra.n_comp = 1
+ra.real_power[0] = F["agent_power"].data_ptr()
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        lib.pgw_agent_reduce(ra, n, F["vv"].data_ptr(), None, st)
+    torch.cuda.synchronize()
+    print("pgw_agent_reduce (1 small launch): %.2f us" % ((time.perf_counter() - t0) / 2000 * 1e6))
+import ctypes
+p_ = ctypes.byref(F["params"])
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        fn(p_, ctypes.byref(pfp), ctypes.byref(pft), ctypes.byref(info), n, F["bufs"], st)
+    torch.cuda.synchronize()
+    print("pgw_coord_step with byref args: %.1f us/call" % ((time.perf_counter() - t0) / 2000 * 1e6))
