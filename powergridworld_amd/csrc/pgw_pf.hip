@@ -195,27 +195,45 @@ template <int M, bool UB, bool GC> struct PFSolver {
     return (int32_t)sg;
   }
 
-  // Quadratic of predictor record c (pgw_pf_pred_pack) at grid coordinate g:
-  // u = u_c + t (d1/2 + t d2/2), t = g - c.
-  __device__ __forceinline__ void pred_quad(const double* rec, int c, double g) {
-    const double t = g - (double)c;
-    const double h1 = 0.5 * t, h2 = 0.5 * t * t;
+  // Predictor record c (pgw_pf_pred_pack): u_c (fp64) and d1, d2 (fp32).
+  struct Rec {
+    double2 u[M];
+    float2 d1[M], d2[M];
+  };
+  __device__ __forceinline__ static void pred_load(const double* rec, int c, Rec& R) {
     const char* r = reinterpret_cast<const char*>(rec) + (int64_t)c * (32 * M);
     const double2* v = reinterpret_cast<const double2*>(r);
     const float2* d1 = reinterpret_cast<const float2*>(r + 16 * M);
     const float2* d2 = reinterpret_cast<const float2*>(r + 24 * M);
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-      const double2 u = v[k];
-      const float2 a1 = d1[k], a2 = d2[k];
-      ur[k] = fma(h2, (double)a2.x, fma(h1, (double)a1.x, u.x));
-      ui[k] = fma(h2, (double)a2.y, fma(h1, (double)a1.y, u.y));
+      R.u[k] = v[k];
+      R.d1[k] = d1[k];
+      R.d2[k] = d2[k];
     }
+  }
+  // Its quadratic at grid coordinate g: u = u_c + t (d1/2 + t d2/2), t = g - c.
+  __device__ __forceinline__ void pred_eval(const Rec& R, int c, double g) {
+    const double t = g - (double)c;
+    const double h1 = 0.5 * t, h2 = 0.5 * t * t;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      ur[k] = fma(h2, (double)R.d2[k].x, fma(h1, (double)R.d1[k].x, R.u[k].x));
+      ui[k] = fma(h2, (double)R.d2[k].y, fma(h1, (double)R.d1[k].y, R.u[k].y));
+    }
+  }
+  __device__ __forceinline__ void pred_quad(const double* rec, int c, double g) {
+    Rec R;
+    pred_load(rec, c, R);
+    pred_eval(R, c, g);
   }
 
   // Initial guess: per-env U_init; or the predictor -- the quadratic through 3
   // grid solutions, the stencil chosen per grid segment by pgw_pf_pred_meta so
   // that it never straddles a load-band switch; or u0.
+  // SPEC: load the nearest record speculatively with the segment metadata (the
+  // fast kernel; the others keep the dependent loads, which need fewer VGPRs).
+  template <bool SPEC = false>
   __device__ __forceinline__ void initial(const PFArgs& a, const pgw_pf_tables& t, int64_t e,
                                           bool valid) {
     if (t.U_init) {
@@ -228,15 +246,27 @@ template <int M, bool UB, bool GC> struct PFSolver {
       }
     } else if (a.use_pred) {
       const double g = (pc - a.pred_x0) * a.pred_inv_h;
-      int c;
-      if (t.U_pred_meta) {
+      // the nearest record: what the segment's stencil choice is everywhere
+      // but next to a load-band switch
+      const int c0 = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
+      if (SPEC && t.U_pred_meta) {
+        // its loads go out together with the segment's metadata load (one L2
+        // round trip instead of two); a lane whose segment picks another
+        // centre reloads
         const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
         const pgw_pred_meta m = t.U_pred_meta[j];
-        c = (g - (double)j < m.tstar) ? m.left : m.right;
+        Rec R;
+        pred_load(t.U_pred, c0, R);
+        const int c = (g - (double)j < m.tstar) ? m.left : m.right;
+        if (c != c0) pred_load(t.U_pred, c, R);
+        pred_eval(R, c, g);
+      } else if (t.U_pred_meta) {
+        const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
+        const pgw_pred_meta m = t.U_pred_meta[j];
+        pred_quad(t.U_pred, (g - (double)j < m.tstar) ? m.left : m.right, g);
       } else {
-        c = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
+        pred_quad(t.U_pred, c0, g);
       }
-      pred_quad(t.U_pred, c, g);
     } else {
       pf_u0<M>(ur, ui, w);
     }
@@ -695,7 +725,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   }
   S.powers(a, cp, cq, 1.0);
   pf_trace(trace, 1);
-  S.initial(a, t, e, valid);
+  S.template initial<!(KEEP || !UB || GC)>(a, t, e, valid);
   pf_trace(trace, 2);
   constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
   double v0r, v0i, ir[M], ii[M];

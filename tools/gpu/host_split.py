@@ -70,3 +70,25 @@ for rep in range(2):
         fn(p_, ctypes.byref(pfp), ctypes.byref(pft), ctypes.byref(info), n, F["bufs"], st)
     torch.cuda.synchronize()
     print("pgw_coord_step with byref args: %.1f us/call" % ((time.perf_counter() - t0) / 2000 * 1e6))
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(20000):
+        fn(F["params"], pfp, pft, info, 0, F["bufs"], st)
+    print("pgw_coord_step n=0 (ctypes + checks, no launch): %.2f us" % ((time.perf_counter() - t0) / 20000 * 1e6))
+print("torch current stream handle:", st)
+s2 = torch.cuda.Stream()
+st2 = _lib.C.c_void_p(s2.cuda_stream)
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        fn(F["params"], pfp, pft, info, n, F["bufs"], st2)
+    torch.cuda.synchronize()
+    print("pgw_coord_step on a torch side stream: %.1f us/call" % ((time.perf_counter() - t0) / 2000 * 1e6))
+ra2 = _lib.ReduceArgs()
+for rep in range(2):
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        lib.pgw_agent_reduce(ra2, n, F["vv"].data_ptr(), None, st)
+        lib.pgw_agent_reduce(ra2, n, F["vv"].data_ptr(), None, st)
+    torch.cuda.synchronize()
+    print("2 x pgw_agent_reduce: %.1f us" % ((time.perf_counter() - t0) / 2000 * 1e6))
