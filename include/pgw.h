@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 9
+#define PGW_ABI_VERSION 10
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -305,6 +305,11 @@ typedef struct pgw_pf_tables {
    * several load levels (e.g. the loadshape hours of an episode) in one launch.
    * NULL = 1. */
   const double* load_scale;
+  /* Optional outputs of pgw_pf_solve (n doubles each): the minimum / maximum
+   * over the n_out output rows, taken in row order as Python's min()/max() do
+   * over the voltage dict (multiagent_env.py:107-113).  NULL = not written. */
+  double* v_min_out;
+  double* v_max_out;
 } pgw_pf_tables;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)
@@ -329,6 +334,12 @@ int32_t pgw_pf_pred_pack(const pgw_pf_params* p, int32_t n_tables, int32_t n_poi
 int32_t pgw_pf_pred_meta(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,
                          const double* U_pred, const int32_t* sig, pgw_pred_meta* meta,
                          void* stream);
+
+/* Voltage-band penalty of the heterogeneous scenario's PV farm
+ * (gridworld/scenarios/heterogeneous.py:47-52, ThisPVEnv.step_reward):
+ * out[e] = -(scale * (min(0, v[e] - lo) + min(0, hi - v[e])))^2. */
+int32_t pgw_voltage_band_penalty(int64_t n, const double* v, double lo, double hi, double scale,
+                                 double* out, void* stream);
 
 /* Element count the kernels are instantiated for (8, 14 or 16): pad the
  * feeder's m load phase elements to it with inert elements (zero power). */

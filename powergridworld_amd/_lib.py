@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -94,7 +94,7 @@ class PFParams(C.Structure):
 class PFTables(C.Structure):
     _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("U_pred", vp),
                 ("U_pred_meta", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp),
-                ("load_scale", vp)]
+                ("load_scale", vp), ("v_min_out", vp), ("v_max_out", vp)]
 
 
 class PredMeta(C.Structure):
@@ -197,6 +197,7 @@ _SIGS = {
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_padded_m": (i32, [i32]),
+    "pgw_voltage_band_penalty": (i32, [i64, vp, f64, f64, f64, vp, vp]),
     "pgw_pf_pack_size": (i64, [i32]),
     "pgw_timing_start": (i32, [i32]),
     "pgw_debug_pf_trace": (i32, [vp]),

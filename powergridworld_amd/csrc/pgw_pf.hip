@@ -413,8 +413,18 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
   if (a.n_out > 0) v_out[e] = v0;
+  double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
   if constexpr (kKeep)
-    for (int o = 1; o < a.n_out; ++o) v_out[(int64_t)o * n + e] = pf_node_pu<M>(t, o, ir, ii);
+    for (int o = 1; o < a.n_out; ++o) {
+      const double v = pf_node_pu<M>(t, o, ir, ii);
+      v_out[(int64_t)o * n + e] = v;
+      vmn = (v < vmn) ? v : vmn;
+      vmx = (v > vmx) ? v : vmx;
+    }
+  if (a.n_out > 0) {
+    if (t.v_min_out) t.v_min_out[e] = vmn;
+    if (t.v_max_out) t.v_max_out[e] = vmx;
+  }
   if (t.U_out) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
@@ -920,6 +930,20 @@ static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_
   return check_launch("k_coord_pf");
 }
 
+// ThisPVEnv.step_reward (scenarios/heterogeneous.py:47-52) on [n]: Python's
+// min(0, x) keeps 0 unless x < 0; (1000 viol)**2 as the square.
+__global__ void __launch_bounds__(kBlock) k_band_penalty(int64_t n, const double* __restrict__ v,
+                                                         double lo, double hi, double scale,
+                                                         double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  const double x = v[e];
+  const double l = x - lo, u = hi - x;
+  const double viol = ((l < 0.0) ? l : 0.0) + ((u < 0.0) ? u : 0.0);
+  const double y = scale * viol;
+  out[e] = -(y * y);
+}
+
 // Instantiated variants: IEEE-13 (m = 14) with a uniform band, at most one
 // controllable slot and no per-env load scale is the fast path (with one
 // output row accumulated inside the loop, or the last currents kept for any
@@ -1003,6 +1027,15 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
 extern "C" {
 
 int32_t pgw_pf_padded_m(int32_t m) { return padded_m(m); }
+
+int32_t pgw_voltage_band_penalty(int64_t n, const double* v, double lo, double hi, double scale,
+                                 double* out, void* stream) {
+  PGW_REQUIRE(v && out && n >= 0, "pgw_voltage_band_penalty: null argument");
+  if (n == 0) return PGW_OK;
+  hipLaunchKernelGGL(k_band_penalty, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, v, lo,
+                     hi, scale, out);
+  return check_launch("k_band_penalty");
+}
 
 int32_t pgw_pf_pred_meta(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,
                          const double* U_pred, const int32_t* sig, pgw_pred_meta* meta,

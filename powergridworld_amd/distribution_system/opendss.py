@@ -110,8 +110,14 @@ class OpenDSSSolver(PowerFlowSolver):
         _lib.check(_lib.lib().pgw_pf_pack(self.params, cp(Wf), cp(U0f), cp(G0), cp(V00), cp(block)))
         self._block = torch.tensor(block, dtype=torch.float64, device=dev)
         self._G, self._V0 = as_dev(Gs), as_dev(V0s)
+        # per-env min / max over the output rows, written by the solve's epilogue
+        # (multiagent_env.py:107-113 reads them when an agent observes them)
+        self._vmin = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
+        self._vmax = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
+        self._all_nodes = len(names) == f.n
         self.tables = _lib.PFTables(block=self._block.data_ptr(), G=self._G.data_ptr(),
-                                    V0=self._V0.data_ptr())
+                                    V0=self._V0.data_ptr(), v_min_out=self._vmin.data_ptr(),
+                                    v_max_out=self._vmax.data_ptr())
         self.v_out = torch.zeros((max(len(names), 1), self.num_envs), dtype=torch.float64, device=dev)
         self._own_v_out = self.v_out
         self._bv_cache = {}
@@ -267,6 +273,7 @@ class OpenDSSSolver(PowerFlowSolver):
         tb.U_out = grid.data_ptr()
         tb.sig_out = self._pred_sig[idx0].data_ptr()
         tb.load_scale = scale.data_ptr()
+        tb.v_min_out = tb.v_max_out = None         # (grid solves: H * P lanes, no output rows)
         st = _lib.stream_ptr(dev)
         lib = _lib.lib()
         _lib.check(lib.pgw_pf_solve(sp, tb, H * P, _lib.dptr(cp), _lib.dptr(cq), None, None, st))
@@ -307,6 +314,8 @@ class OpenDSSSolver(PowerFlowSolver):
                                            _lib.stream_ptr(self.device)))
         self.iterations = self._iters
         self._prepare_bus_voltages()
+        if self._all_nodes:                        # the epilogue's min / max over every node
+            self._extrema = (self._vmin, self._vmax)
 
     def bind_output(self, v_out=None):
         """Write the next solves' node voltages into `v_out` ([n_out, N] fp64, e.g.
@@ -340,7 +349,10 @@ class OpenDSSSolver(PowerFlowSolver):
     def voltage_extrema(self):
         """(min, max) over all output nodes per env, once per solve (multiagent_env.py:107-113)."""
         if self._extrema is None:
-            v = self.v_out[:len(self.output_names)]
+            if self._all_nodes and self.bus_voltages is self._bv:
+                v = self.v_out[:len(self.output_names)]
+            else:     # a subset of rows, or a fused step's mapping (every node, on demand)
+                v = torch.stack(list(self.bus_voltages.values()))
             self._extrema = (v.min(0).values, v.max(0).values)
         return self._extrema
 

@@ -102,6 +102,8 @@ class MultiAgentEnv(Env):
 
         self._fused = None
         self._fused_steps = 0
+        # every agent reports the base class's reactive power (its zero buffer)
+        self._q_zero = all(type(a).reactive_power is ComponentEnv.reactive_power for a in self.agents)
         if fused:
             why = self._fusable()
             if why is None and self.dtype != torch.float64:
@@ -223,25 +225,28 @@ class MultiAgentEnv(Env):
         for agent in self.agents:
             name = agent.name
             kwargs = self.get_external_obs_vars(agent)
-            obs[name], r, done[name], meta[name] = agent.step(action=action[name], **kwargs)
-            rew[name] = r.clone()
-            load_bus = self.agent_name_bus_map[name]
-            p, q = agent.real_power, agent.reactive_power
-            agent_power_p.append(p)
+            # (a view of the agent's reward buffer, like the observations: the next
+            # step overwrites it; reward_transform hooks build new tensors)
+            obs[name], rew[name], done[name], meta[name] = agent.step(action=action[name], **kwargs)
+            agent_power_p.append(agent.real_power)
         if self._hist is not None:                     # this step's history slot
             self.pf_solver.bind_output(self._hist["v"][self._hist["t"] % self._hist["cap"]])
+        # No agent class here sets a reactive power (every component's stays the
+        # zero buffer), so the q sums would add zeros: the solve takes q = 0.
+        q_zero = self._q_zero
         for agent in self.agents:
-            name = agent.name
-            load_bus = self.agent_name_bus_map[name]
-            p, q = agent.real_power, agent.reactive_power
+            load_bus = self.agent_name_bus_map[agent.name]
+            p = agent.real_power
             if load_bus in load_p:
                 load_p[load_bus] = load_p[load_bus] + p
-                load_q[load_bus] = load_q[load_bus] + q
+                if not q_zero:
+                    load_q[load_bus] = load_q[load_bus] + agent.reactive_power
             else:
                 load_p[load_bus] = p
-                load_q[load_bus] = q
+                if not q_zero:
+                    load_q[load_bus] = agent.reactive_power
         self.pf_solver.calculate_power_flow(current_time=self.time, p_controllable_consumed=load_p,
-                                            q_controllable_consumed=load_q)
+                                            q_controllable_consumed=None if q_zero else load_q)
         self.voltages = self.pf_solver.get_bus_voltages()
         self._record(agent_power_p)
         rew = self.reward_transform(rew)
@@ -628,6 +633,7 @@ class MultiAgentEnv(Env):
             lazy = F["lazy_v"]
             lazy._step, lazy._reset, lazy._full = self._fused_steps, False, None
             self.voltages = solver.bus_voltages = lazy
+            solver._extrema = None
         else:
             self.voltages = H["vd"][s_]
             for ai, agent in enumerate(self.agents):
