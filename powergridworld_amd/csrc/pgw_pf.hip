@@ -386,6 +386,36 @@ __device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, cons
   return sqrt(fma(vi, vi, vr * vr));
 }
 
+// The general kernels' output rows staged in LDS by the block, G then V0
+// (n_out (2M + 2) doubles), so a row's wave-uniform operands are LDS broadcasts
+// rather than one scalar-cache round trip per row (41 rows at IEEE-13).
+// Copied before the solve, so the loads overlap it.  Same values, same
+// operations: pf_node_pu_lds == pf_node_pu bit for bit.
+constexpr int kRowsLds = 4096;   // doubles (32 KB); more rows use pf_node_pu
+template <int M>
+__device__ __forceinline__ bool pf_rows_stage(const pgw_pf_tables& t, int n_out, double* s) {
+  if (n_out * (2 * M + 2) > kRowsLds || n_out <= 1) return false;   // uniform
+  for (int i = threadIdx.x; i < 2 * M * n_out; i += kBlock) s[i] = t.G[i];
+  for (int i = threadIdx.x; i < 2 * n_out; i += kBlock) s[2 * M * n_out + i] = t.V0[i];
+  return true;
+}
+template <int M>
+__device__ __forceinline__ double pf_node_pu_lds(const double* s, int n_out, int o, const double* ir,
+                                                 const double* ii) {
+  const double* G = s + 2 * M * o;
+  const double* V0 = s + 2 * M * n_out;
+  double vr = V0[2 * o], vi = V0[2 * o + 1];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double gr = G[2 * k], gi = G[2 * k + 1];
+    vr = fma(gr, ir[k], vr);
+    vr = fma(-gi, ii[k], vr);
+    vi = fma(gr, ii[k], vi);
+    vi = fma(gi, ir[k], vi);
+  }
+  return sqrt(fma(vi, vi, vr * vr));
+}
+
 template <int M, bool UB, bool GC, bool KEEP>
 __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, int64_t n,
                                                      const double* __restrict__ ctrl_p,
@@ -394,6 +424,10 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
                                                      int32_t* __restrict__ iters) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
+  constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
+  __shared__ double s_rows[kKeep ? kRowsLds : 1];
+  bool rows_lds = false;
+  if constexpr (kKeep) rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
   S.load(a, t.block);
@@ -405,18 +439,18 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   }
   S.powers(a, cp, cq, (t.load_scale && valid) ? t.load_scale[e] : 1.0);
   S.initial(a, t, e, valid);
-  constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
   double v0r, v0i, ir[M], ii[M];
   const int it = S.template iterate<kKeep>(a.max_iter, valid, v0r, v0i, ir, ii);
   const int32_t sig = t.sig_out ? S.signature() : 0;
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  if constexpr (kKeep) __syncthreads();       // the staged rows (every lane is still here)
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
   if (a.n_out > 0) v_out[e] = v0;
   double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
   if constexpr (kKeep)
     for (int o = 1; o < a.n_out; ++o) {
-      const double v = pf_node_pu<M>(t, o, ir, ii);
+      const double v = rows_lds ? pf_node_pu_lds<M>(s_rows, a.n_out, o, ir, ii) : pf_node_pu<M>(t, o, ir, ii);
       v_out[(int64_t)o * n + e] = v;
       vmn = (v < vmn) ? v : vmn;
       vmx = (v > vmx) ? v : vmx;
@@ -718,6 +752,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
     rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
              ((valid && ag < c.n_agents) ? 1.0 : 0.0);
+  constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
+  __shared__ double s_rows[kKeep ? kRowsLds : 1];
+  bool rows_lds = false;
+  if constexpr (kKeep) rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
   S.load(a, t.block);
@@ -737,18 +775,18 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   pf_trace(trace, 1);
   S.template initial<!(KEEP || !UB || GC)>(a, t, e, valid);
   pf_trace(trace, 2);
-  constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
   double v0r, v0i, ir[M], ii[M];
   const int it = S.template iterate<kKeep>(a.max_iter, valid, v0r, v0i, ir, ii);
   pf_trace(trace, 3);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   pf_trace(trace, 4);
+  if constexpr (kKeep) __syncthreads();       // the staged rows (every lane is still here)
   if (!valid) return;
   double vsel = v0;
   if (b.v_out) b.v_out[e] = (Sto)v0;
   if constexpr (kKeep)
     for (int o = 1; o < a.n_out; ++o) {
-      const double v = pf_node_pu<M>(t, o, ir, ii);
+      const double v = rows_lds ? pf_node_pu_lds<M>(s_rows, a.n_out, o, ir, ii) : pf_node_pu<M>(t, o, ir, ii);
       if (b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
       vsel = (o == c.vv_row) ? v : vsel;
     }
