@@ -327,20 +327,34 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const pg
 // forming the sums -- the device-scope release/acquire fences that make the
 // other blocks' outputs visible across XCDs write back L2 and cost more than
 // the overlap gains: C3 19.7 -> 34.6 us.)
+//
+// Layout: a block of n_comp waves serves 64 envs, wave w running component slot
+// w for all of them.  The components of an agent are independent within a step
+// (each reads only its own action and state), so they run side by side on the
+// block's SIMDs instead of one after another in each lane; each wave leaves its
+// component's real power and reward in LDS and, after the block barrier, wave 0
+// forms the sums in component order -- the same values and the same operation
+// order as one lane doing everything, without any cross-block synchronisation.
 template <bool STD>
-__global__ void __launch_bounds__(kBlock) k_mc_step(pgw_mc_step_args a, BldDerived d, int64_t n) {
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= n) return;
-  for (int c = 0; c < a.n_comp; ++c) mc_component<STD>(a, a.comp[c], d, n, e);
+__global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a, BldDerived d, int64_t n) {
+  __shared__ double s_rp[4][64], s_rew[4][64];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  if (e < n) {
+    const pgw_mc_component& C = a.comp[w];
+    mc_component<STD>(a, C, d, n, e);
+    const int kind = C.kind;
+    s_rp[w][lane] = C.real_power[e];                 // this thread's own writes
+    s_rew[w][lane] = kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
+                     : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
+  }
+  __syncthreads();
+  if (w != 0 || e >= n) return;
   double rp_sum = 0.0, rew_sum = 0.0;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    if (c < a.n_comp) {
-      const int kind = a.comp[c].kind;
-      rp_sum = rp_sum + a.comp[c].real_power[e];
-      rew_sum = rew_sum + (kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
-                           : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0);
-    }
+  for (int c = 0; c < a.n_comp; ++c) {
+    rp_sum = rp_sum + s_rp[c][lane];
+    rew_sum = rew_sum + s_rew[c][lane];
   }
   a.real_power[e] = rp_sum;
   a.reward[e] = rew_sum;
@@ -485,8 +499,13 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   bool std_bld = false;
   for (int c = 0; c < a->n_comp; ++c)
     if (a->comp[c].kind == PGW_MC_BUILDING) std_bld = bld_is_std(a->bld);
-  if (std_bld) PGW_LAUNCH(k_mc_step<true>, n, stream, *a, d, n);
-  PGW_LAUNCH(k_mc_step<false>, n, stream, *a, d, n);
+  if (n == 0) return PGW_OK;
+  const dim3 grid((unsigned)((n + 63) / 64)), block(64u * (unsigned)a->n_comp);
+  if (std_bld)
+    hipLaunchKernelGGL(k_mc_step<true>, grid, block, 0, (hipStream_t)stream, *a, d, n);
+  else
+    hipLaunchKernelGGL(k_mc_step<false>, grid, block, 0, (hipStream_t)stream, *a, d, n);
+  return check_launch("k_mc_step");
 }
 
 int32_t pgw_agent_reduce(const pgw_reduce_args* a, int64_t n, double* real_power, double* reward,
