@@ -706,63 +706,63 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
   });
 }
 
-// fp32 pair variant: one thread per (env pair, agent), every access a float2
-// (8 B a lane -- the fp64 kernel's request count at half its bytes; with one
-// env per lane the fp32 kernel issues as many memory instructions as the fp64
-// one and gains little).  The two envs' chains are computed interleaved
+// Pair variant: one thread per (env pair, agent), every access a 2-vector
+// (fp32: 8 B a lane -- the fp64 kernel's request count at half its bytes; with
+// one env per lane the fp32 kernel issues as many memory instructions as the
+// fp64 one and gains little).  The two envs' chains are computed interleaved
 // (std_agent_compute<2>), each exactly as alone.  Needs env-minor action / obs
-// views (s_env == 1), an even n and even strides (f32_pairs_ok).
-__global__ void __launch_bounds__(kBlock) k_coord_agents_std_f32x2(pgw_coord_params p,
-                                                                   pgw_coord_step_info s, int64_t n,
-                                                                   pgw_coord_buffers_f32 b,
-                                                                   double pv_ob, StdDerived dv) {
+// views (s_env == 1), an even n and even strides (pairs_ok).
+template <class Bufs>
+__global__ void __launch_bounds__(kBlock) k_coord_agents_std_x2(pgw_coord_params p,
+                                                                pgw_coord_step_info s, int64_t n,
+                                                                Bufs b, double pv_ob, StdDerived dv) {
+  using S = std::remove_pointer_t<decltype(b.soc)>;
+  typedef S S2 __attribute__((ext_vector_type(2)));
   const int64_t e = 2 * ((int64_t)blockIdx.x * kBlock + threadIdx.x);
   const int a = blockIdx.y;
   if (e >= n) return;
   StdAgentIn in[2];
-  const float* ap = b.action.ptr + a * b.act_stride_agent + e;
+  const S* ap = b.action.ptr + a * b.act_stride_agent + e;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float2 v = *reinterpret_cast<const float2*>(ap + j * b.action.s_dim);
+    const S2 v = *reinterpret_cast<const S2*>(ap + j * b.action.s_dim);
     in[0].av[j] = (double)v.x;
     in[1].av[j] = (double)v.y;
   }
-  float* xp = b.x + (int64_t)a * 5 * n + e;
+  S* xp = b.x + (int64_t)a * 5 * n + e;
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
-    const float2 v = *reinterpret_cast<const float2*>(xp + z * n);
+    const S2 v = *reinterpret_cast<const S2*>(xp + z * n);
     in[0].xs[z] = (double)v.x;
     in[1].xs[z] = (double)v.y;
   }
-  float* socp = b.soc + (int64_t)a * n + e;
+  S* socp = b.soc + (int64_t)a * n + e;
   {
-    const float2 v = *reinterpret_cast<const float2*>(socp);
+    const S2 v = *reinterpret_cast<const S2*>(socp);
     in[0].soc = (double)v.x;
     in[1].soc = (double)v.y;
   }
-  float* op = b.obs.ptr + a * b.obs_stride_agent + e;
+  S* op = b.obs.ptr + a * b.obs_stride_agent + e;
   std_agent_compute<2>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[2]) {
-    const float2 w = make_float2((float)v[0], (float)v[1]);
-    if (slot < kSlotSoc) *reinterpret_cast<float2*>(xp + slot * n) = w;
-    else if (slot == kSlotSoc) *reinterpret_cast<float2*>(socp) = w;
-    else if (slot < kSlotPower) {
-      typedef float f2v __attribute__((ext_vector_type(2)));
-      const f2v nv = {w.x, w.y};
-      __builtin_nontemporal_store(nv, reinterpret_cast<f2v*>(op + (slot - kSlotObs) * b.obs.s_dim));
-    }
-    else if (slot == kSlotPower) *reinterpret_cast<float2*>(b.agent_power + (int64_t)a * n + e) = w;
-    else *reinterpret_cast<float2*>(b.reward + (int64_t)a * n + e) = w;
+    const S2 w = {(S)v[0], (S)v[1]};
+    if (slot < kSlotSoc) *reinterpret_cast<S2*>(xp + slot * n) = w;
+    else if (slot == kSlotSoc) *reinterpret_cast<S2*>(socp) = w;
+    else if (slot < kSlotPower)
+      __builtin_nontemporal_store(w, reinterpret_cast<S2*>(op + (slot - kSlotObs) * b.obs.s_dim));
+    else if (slot == kSlotPower) *reinterpret_cast<S2*>(b.agent_power + (int64_t)a * n + e) = w;
+    else *reinterpret_cast<S2*>(b.reward + (int64_t)a * n + e) = w;
   });
 }
 
-static bool f32_pairs_ok(const pgw_coord_buffers_f32& b, int64_t n) {
-  const auto al8 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0; };
+template <class Bufs>
+static bool pairs_ok(const Bufs& b, int64_t n) {
+  using S = std::remove_pointer_t<decltype(b.soc)>;
+  const auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & (2 * sizeof(S) - 1)) == 0; };
   return n % 2 == 0 && b.action.s_env == 1 && b.obs.s_env == 1 && b.action.s_dim % 2 == 0 &&
          b.obs.s_dim % 2 == 0 && b.act_stride_agent % 2 == 0 && b.obs_stride_agent % 2 == 0 &&
-         al8(b.action.ptr) && al8(b.obs.ptr) && al8(b.x) && al8(b.soc) && al8(b.agent_power) &&
-         al8(b.reward);
+         al(b.action.ptr) && al(b.obs.ptr) && al(b.x) && al(b.soc) && al(b.agent_power) &&
+         al(b.reward);
 }
-static bool f32_pairs_ok(const pgw_coord_buffers&, int64_t) { return false; }
 
 static bool coord_is_std(const pgw_coord_params& p) {
   static const int sel[5][4] = {{0, 7, 6, 1}, {0, 7, 6, 1}, {0, 7, 5, 1}, {0, 7, 5, 1}, {0, 7, 5, 1}};
@@ -1108,18 +1108,14 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   c.vv_hi = p->vv_hi;
   c.vv_penalty = p->vv_penalty;
   const PFArgs a = make_pf_args(*pf, *pft);
-  if constexpr (kF32) {
-    if (f32_pairs_ok(b, n)) {
-      launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std_f32x2, dim3(grid_for(n / 2), p->n_agents),
-                   dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
-    } else {
-      launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std<Bufs>, dim3(grid_for(n), p->n_agents),
-                   dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
-    }
+  // (the pair layout measured for fp64 too: 19.5 -> 20.2 us, so fp32 only)
+  if (std_layout && kF32 && pairs_ok(b, n)) {
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std_x2<Bufs>, dim3(grid_for(n / 2), p->n_agents),
+                 dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
   } else if (std_layout) {
     launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std<Bufs>, dim3(grid_for(n), p->n_agents),
                  dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
-  } else {
+  } else if constexpr (!kF32) {
     launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p->n_agents), dim3(kBlock),
                  st, *p, *s, n, b);
   }
