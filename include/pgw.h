@@ -360,7 +360,7 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
  * the summed duration (ms) and the number of timed launches.
  * ---------------------------------------------------------------------- */
 enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COUNT = 3 };
-/* Debug: device buffer of 8 int64 per k_coord_pf wave (NULL = off); lane 0 of
+/* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
 int32_t pgw_debug_pf_trace(long long* buf);
 int32_t pgw_timing_start(int32_t every);

@@ -352,18 +352,22 @@ template <int M, bool UB, bool GC> struct PFSolver {
 
 };
 
-// |V| pu of output node o: V0 + sum_k G[o][k] I_k (wave-uniform G, V0 rows
-// through the scalar cache).
 // Debug phase trace (pgw_debug_pf_trace): when set, lane 0 of every k_coord_pf
-// wave records wall_clock64() (100 MHz) at each phase boundary.
+// or k_pf_solve wave records wall_clock64() (100 MHz) at each phase boundary
+// (the buffer holds 8 slots per wave of the launch).  Global, not flat, stores:
+// a pending flat store counts against lgkmcnt too and would make the LDS waits
+// after it conservative.
 __device__ long long* g_pf_trace = nullptr;
 __device__ __forceinline__ void pf_trace(long long* tr, int phase) {
   if (tr && (threadIdx.x & 63) == 0) {
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    tr[wave * 8 + phase] = wall_clock64();
+    typedef __attribute__((address_space(1))) long long* gptr;
+    ((gptr)tr)[wave * 8 + phase] = wall_clock64();
   }
 }
 
+// |V| pu of output node o: V0 + sum_k G[o][k] I_k (wave-uniform G, V0 rows
+// through the scalar cache).
 typedef const __attribute__((address_space(4))) double* sdptr;
 __device__ __forceinline__ sdptr scalar_ptr(const double* p) { return (sdptr)p; }
 
@@ -389,8 +393,8 @@ __device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, cons
 // The general kernels' output rows staged in LDS by the block, G then V0
 // (n_out (2M + 2) doubles), so a row's wave-uniform operands are LDS broadcasts
 // rather than one scalar-cache round trip per row (41 rows at IEEE-13).
-// Copied before the solve, so the loads overlap it.  Same values, same
-// operations: pf_node_pu_lds == pf_node_pu bit for bit.
+// Copied before the solve, so the loads overlap it.  Read as 16-byte pairs
+// (s_rows is 16-byte aligned; a row is 2M doubles).
 constexpr int kRowsLds = 4096;   // doubles (32 KB); more rows use pf_node_pu
 template <int M>
 __device__ __forceinline__ bool pf_rows_stage(const pgw_pf_tables& t, int n_out, double* s) {
@@ -399,21 +403,53 @@ __device__ __forceinline__ bool pf_rows_stage(const pgw_pf_tables& t, int n_out,
   for (int i = threadIdx.x; i < 2 * n_out; i += kBlock) s[2 * M * n_out + i] = t.V0[i];
   return true;
 }
+
+// Output rows 1 .. n_out-1, f(o, |V_o|) called in row order.  From LDS the
+// rows are software-pipelined: the next row's operands (one row of G and V0,
+// 2M + 2 doubles) are in flight while the current row's FMA chains run.  Left
+// to itself the scheduler issued two 16-byte LDS reads at a time and waited on
+// each pair (7 waits per row at one wave per SIMD, 0.45 us per row).  Same
+// operations in the same order as pf_node_pu, so the values are bit-identical.
 template <int M>
-__device__ __forceinline__ double pf_node_pu_lds(const double* s, int n_out, int o, const double* ir,
-                                                 const double* ii) {
-  const double* G = s + 2 * M * o;
-  const double* V0 = s + 2 * M * n_out;
-  double vr = V0[2 * o], vi = V0[2 * o + 1];
+__device__ __forceinline__ void pf_row_fetch(const double* s, int n_out, int o, double2 (&g)[M], double2& v0) {
+  const double2* G = reinterpret_cast<const double2*>(s) + M * o;
+#pragma unroll
+  for (int k = 0; k < M; ++k) g[k] = G[k];
+  v0 = reinterpret_cast<const double2*>(s + 2 * M * n_out)[o];
+}
+template <int M>
+__device__ __forceinline__ double pf_row_eval(const double2 (&g)[M], double2 v0, const double* ir,
+                                              const double* ii) {
+  double vr = v0.x, vi = v0.y;
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    const double gr = G[2 * k], gi = G[2 * k + 1];
+    const double gr = g[k].x, gi = g[k].y;
     vr = fma(gr, ir[k], vr);
     vr = fma(-gi, ii[k], vr);
     vi = fma(gr, ii[k], vi);
     vi = fma(gi, ir[k], vi);
   }
   return sqrt(fma(vi, vi, vr * vr));
+}
+template <int M, class F>
+__device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_lds, const double* s,
+                                            int n_out, const double* ir, const double* ii, F&& f) {
+  if (!rows_lds) {
+    for (int o = 1; o < n_out; ++o) f(o, pf_node_pu<M>(t, o, ir, ii));
+    return;
+  }
+  if (n_out <= 1) return;
+  double2 ga[M], gb[M], va, vb;
+  pf_row_fetch<M>(s, n_out, 1, ga, va);
+  for (int o = 1; o < n_out; o += 2) {
+    pf_row_fetch<M>(s, n_out, min(o + 1, n_out - 1), gb, vb);
+    __builtin_amdgcn_sched_barrier(0);
+    f(o, pf_row_eval<M>(ga, va, ir, ii));
+    if (o + 1 >= n_out) break;
+    pf_row_fetch<M>(s, n_out, min(o + 2, n_out - 1), ga, va);
+    __builtin_amdgcn_sched_barrier(0);
+    f(o + 1, pf_row_eval<M>(gb, vb, ir, ii));
+  }
 }
 
 template <int M, bool UB, bool GC, bool KEEP>
@@ -424,8 +460,10 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
                                                      int32_t* __restrict__ iters) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
+  long long* const trace = g_pf_trace;
+  pf_trace(trace, 0);
   constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
-  __shared__ double s_rows[kKeep ? kRowsLds : 1];
+  __shared__ __attribute__((aligned(16))) double s_rows[kKeep ? kRowsLds : 1];
   bool rows_lds = false;
   if constexpr (kKeep) rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
@@ -438,33 +476,39 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
     cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
   S.powers(a, cp, cq, (t.load_scale && valid) ? t.load_scale[e] : 1.0);
+  pf_trace(trace, 1);
   S.initial(a, t, e, valid);
+  pf_trace(trace, 2);
   double v0r, v0i, ir[M], ii[M];
   const int it = S.template iterate<kKeep>(a.max_iter, valid, v0r, v0i, ir, ii);
+  pf_trace(trace, 3);
   const int32_t sig = t.sig_out ? S.signature() : 0;
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if constexpr (kKeep) __syncthreads();       // the staged rows (every lane is still here)
+  pf_trace(trace, 4);
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
-  if (a.n_out > 0) v_out[e] = v0;
-  double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
-  if constexpr (kKeep)
-    for (int o = 1; o < a.n_out; ++o) {
-      const double v = rows_lds ? pf_node_pu_lds<M>(s_rows, a.n_out, o, ir, ii) : pf_node_pu<M>(t, o, ir, ii);
-      v_out[(int64_t)o * n + e] = v;
-      vmn = (v < vmn) ? v : vmn;
-      vmx = (v > vmx) ? v : vmx;
-    }
-  if (a.n_out > 0) {
-    if (t.v_min_out) t.v_min_out[e] = vmn;
-    if (t.v_max_out) t.v_max_out[e] = vmx;
-  }
+  // element voltages first: they are dead during the output rows, whose LDS
+  // operand loads then have the registers to go out together
   if (t.U_out) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
       t.U_out[2 * (e * M + k)] = S.ur[k];
       t.U_out[2 * (e * M + k) + 1] = S.ui[k];
     }
+  }
+  if (a.n_out > 0) v_out[e] = v0;
+  double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
+  if constexpr (kKeep)
+    pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
+      v_out[(int64_t)o * n + e] = v;
+      vmn = (v < vmn) ? v : vmn;
+      vmx = (v > vmx) ? v : vmx;
+    });
+  pf_trace(trace, 5);
+  if (a.n_out > 0) {
+    if (t.v_min_out) t.v_min_out[e] = vmn;
+    if (t.v_max_out) t.v_max_out[e] = vmx;
   }
   if (iters) iters[e] = it;
 }
@@ -811,7 +855,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
              ((valid && ag < c.n_agents) ? 1.0 : 0.0);
   constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
-  __shared__ double s_rows[kKeep ? kRowsLds : 1];
+  __shared__ __attribute__((aligned(16))) double s_rows[kKeep ? kRowsLds : 1];
   bool rows_lds = false;
   if constexpr (kKeep) rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
@@ -843,11 +887,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   double vsel = v0;
   if (b.v_out) b.v_out[e] = (Sto)v0;
   if constexpr (kKeep)
-    for (int o = 1; o < a.n_out; ++o) {
-      const double v = rows_lds ? pf_node_pu_lds<M>(s_rows, a.n_out, o, ir, ii) : pf_node_pu<M>(t, o, ir, ii);
+    pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
       if (b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
       vsel = (o == c.vv_row) ? v : vsel;
-    }
+    });
   if (b.iters) b.iters[e] = it;
   pf_trace(trace, 5);
   if (c.coordinated) {
