@@ -314,7 +314,8 @@ typedef struct pgw_pf_tables {
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)
  * (opendss.py:107-129 then OpenDSS's per-phase WNominal).
- * ctrl_p / ctrl_q: n_ctrl x n (kW / kvar, NULL = 0).  v_out: n_out x n (pu).
+ * ctrl_p / ctrl_q: n_ctrl x n (kW / kvar, NULL = 0).  v_out: n_out x n (pu); NULL
+ * when only the extrema (pgw_pf_tables.v_min_out / v_max_out) are wanted.
  * iters: n (int32, nullable) iteration count per env. */
 int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out,

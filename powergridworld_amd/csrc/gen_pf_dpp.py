@@ -58,11 +58,11 @@ def gen_node0(M, nr):
     ii = lambda k: "%%%d" % (2 + len(ps) + M + k)
     lines = ["v_mov_b64_dpp %%0, %s row_newbcast:%d %s" % (w(L["v0re"]), L["v0re"] % 16, DPP),
              "v_mov_b64_dpp %%1, %s row_newbcast:%d %s" % (w(L["v0im"]), L["v0im"] % 16, DPP)]
-    for k in range(M):
+    for k in range(M):             # vr and vi chains alternate (in order per chain)
         gr, gi = L["g0re"] + k, L["g0im"] + k
         lines += ["v_fmac_f64_dpp %%0, %s, %s row_newbcast:%d %s" % (w(gr), ir(k), gr % 16, DPP),
-                  "v_fmac_f64_dpp %%0, -%s, %s row_newbcast:%d %s" % (w(gi), ii(k), gi % 16, DPP),
                   "v_fmac_f64_dpp %%1, %s, %s row_newbcast:%d %s" % (w(gr), ii(k), gr % 16, DPP),
+                  "v_fmac_f64_dpp %%0, -%s, %s row_newbcast:%d %s" % (w(gi), ii(k), gi % 16, DPP),
                   "v_fmac_f64_dpp %%1, %s, %s row_newbcast:%d %s" % (w(gi), ir(k), gi % 16, DPP)]
     outs = ['"=&v"(vr)', '"=&v"(vi)']
     ins = ['"v"(w[%d])' % p for p in ps] + ['"v"(ir[%d])' % k for k in range(M)] + \
@@ -114,10 +114,15 @@ def gen_column_v(M, k):
             lines.append("v_fmac_f64_dpp %%%d, %s, %%%d row_newbcast:%d %s"
                          % (c * M + i, w(e), xs + c, e % 16, DPP))
     vr, vi, ir, ii = "%%%d" % (3 * M), "%%%d" % (3 * M + 1), "%%%d" % xs, "%%%d" % (xs + 1)
-    lines += ["v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vr, w(gr), ir, gr % 16, DPP),
-              "v_fmac_f64_dpp %s, -%s, %s row_newbcast:%d %s" % (vr, w(gi), ii, gi % 16, DPP),
-              "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gr), ii, gr % 16, DPP),
-              "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gi), ir, gi % 16, DPP)]
+    node = ["v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vr, w(gr), ir, gr % 16, DPP),
+            "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gr), ii, gr % 16, DPP),
+            "v_fmac_f64_dpp %s, -%s, %s row_newbcast:%d %s" % (vr, w(gi), ii, gi % 16, DPP),
+            "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gi), ir, gi % 16, DPP)]
+    # the node-0 FMAs spread through the independent accumulations (in order
+    # per chain), so no dependent FMA issues right behind its producer
+    step = len(lines) // 4
+    for j in reversed(range(4)):
+        lines.insert(step * j + step // 2, node[j])
     outs = ['"+v"(A[%d])' % i for i in range(M)] + ['"+v"(B[%d])' % i for i in range(M)] + \
            ['"+v"(C[%d])' % i for i in range(M)] + ['"+v"(vr)', '"+v"(vi)']
     ins = ['"v"(w[%d])' % p for p in ps] + ['"v"(ir)', '"v"(ii)', '"v"(is)']
@@ -189,6 +194,56 @@ def gen_band(M, k, nr):
             % (M, k, nr, asm_stmt(lines, outs, ins)))
 
 
+def gen_rows(M):
+    """Output rows from resident row pairs (pf_rows_out): one row's operands --
+    V0 re, im, then G re and G im of every element, slot j of the row in lane
+    j % 16 of pair j // 16 -- fed by row_newbcast.  Two rows interleaved (four
+    independent FMA chains), and a single row; per row the operations and their
+    order are pf_node_pu's: vr = V0r, then per element fma(gr, ir), fma(-gi, ii)
+    into vr and fma(gr, ii), fma(gi, ir) into vi."""
+    npr = (2 * M + 2 + 15) // 16
+    res = []
+    for rows in (2, 1):
+        names = "ab"[:rows]
+        w = lambda r, j: "%%%d" % (2 * rows + r * npr + j // 16)
+        base = 2 * rows + rows * npr
+        ir = lambda k: "%%%d" % (base + k)
+        ii = lambda k: "%%%d" % (base + M + k)
+        vr = lambda r: "%%%d" % (2 * r)
+        vi = lambda r: "%%%d" % (2 * r + 1)
+        lines = []
+        for r in range(rows):
+            lines += ["v_mov_b64_dpp %s, %s row_newbcast:0 %s" % (vr(r), w(r, 0), DPP),
+                      "v_mov_b64_dpp %s, %s row_newbcast:1 %s" % (vi(r), w(r, 1), DPP)]
+        # one wave per SIMD issues in order: a chain's next FMA sits 2 * rows
+        # instructions behind its previous one (never back to back), so the
+        # fp64 FMA latency overlaps the other chains' issue
+        for k in range(M):
+            gr, gi = 2 + k, 2 + M + k
+            for r in range(rows):
+                lines += ["v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vr(r), w(r, gr), ir(k), gr % 16, DPP),
+                          "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi(r), w(r, gr), ii(k), gr % 16, DPP)]
+            for r in range(rows):
+                lines += ["v_fmac_f64_dpp %s, -%s, %s row_newbcast:%d %s" % (vr(r), w(r, gi), ii(k), gi % 16, DPP),
+                          "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi(r), w(r, gi), ir(k), gi % 16, DPP)]
+        outs = []
+        for r in names:
+            outs += ['"=&v"(%sr)' % r, '"=&v"(%si)' % r]
+        ins = ['"v"(w%s[%d])' % (r, p) for r in names for p in range(npr)] + \
+              ['"v"(ir[%d])' % k for k in range(M)] + ['"v"(ii[%d])' % k for k in range(M)]
+        if rows == 2:
+            sig = ("template <> __device__ __forceinline__ void pf_row2_dpp<%d>(\n"
+                   "    double& ar, double& ai, double& br, double& bi, const double (&wa)[%d],\n"
+                   "    const double (&wb)[%d], const double (&ir)[%d], const double (&ii)[%d]) {\n"
+                   % (M, npr, npr, M, M))
+        else:
+            sig = ("template <> __device__ __forceinline__ void pf_row1_dpp<%d>(\n"
+                   "    double& ar, double& ai, const double (&wa)[%d], const double (&ir)[%d],\n"
+                   "    const double (&ii)[%d]) {\n" % (M, npr, M, M))
+        res.append(sig + asm_stmt(lines, outs, ins) + "}\n")
+    return "\n".join(res)
+
+
 def main():
     ns = (4 * 16 + 15) // 16          # resident s tables: 4 x PGW_PF_MAX_M entries
     out = ["// GENERATED by gen_pf_dpp.py -- do not edit.  DPP-broadcast asm groups of",
@@ -212,6 +267,12 @@ def main():
            "    const double (&w)[PFBlock<M>::kPairs], double ir, double ii, double is);",
            "template <int M> __device__ __forceinline__ void pf_v0(",
            "    double& vr, double& vi, const double (&w)[PFBlock<M>::kPairs]);",
+           "template <int M> __device__ __forceinline__ void pf_row2_dpp(",
+           "    double& ar, double& ai, double& br, double& bi, const double (&wa)[PFRow<M>::kPairs],",
+           "    const double (&wb)[PFRow<M>::kPairs], const double (&ir)[M], const double (&ii)[M]);",
+           "template <int M> __device__ __forceinline__ void pf_row1_dpp(",
+           "    double& ar, double& ai, const double (&wa)[PFRow<M>::kPairs], const double (&ir)[M],",
+           "    const double (&ii)[M]);",
            ""]
     for M in SIZES:
         L = block_layout(M)
@@ -221,6 +282,7 @@ def main():
         out.append(gen_bcast_group("pf_u0", M, [L["u0re"], L["u0im"]], nr))
         out.append(gen_node0(M, nr))
         out.append(gen_v0(M, nr))
+        out.append(gen_rows(M))
         for k in range(M):
             out.append(gen_column(M, k))
             out.append(gen_column_v(M, k))

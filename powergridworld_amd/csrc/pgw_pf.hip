@@ -79,6 +79,12 @@ constexpr int kSPairs = (4 * PGW_PF_MAX_M + 15) / 16;   // resident s0 / f entri
 // The DPP-broadcast groups (generated: gen_pf_dpp.py).  Entry e of a resident
 // table lives in lane e % 16 of every 16-lane row of register pair e / 16 and is
 // fed to its instruction with row_newbcast:(e % 16).
+// Output-row operands in resident form (pf_rows_out): slot j of a row (V0 re,
+// V0 im, G re of every element, G im of every element) in lane j % 16 of pair
+// j / 16.
+template <int M> struct PFRow {
+  static constexpr int kPairs = (2 * M + 2 + 15) / 16;
+};
 #include "pgw_pf_dpp.inc"
 
 __device__ __forceinline__ double fast_rcp(double m) {
@@ -390,65 +396,73 @@ __device__ __forceinline__ double pf_node_pu(const pgw_pf_tables& t, int o, cons
   return sqrt(fma(vi, vi, vr * vr));
 }
 
-// The general kernels' output rows staged in LDS by the block, G then V0
-// (n_out (2M + 2) doubles), so a row's wave-uniform operands are LDS broadcasts
-// rather than one scalar-cache round trip per row (41 rows at IEEE-13).
-// Copied before the solve, so the loads overlap it.  Read as 16-byte pairs
-// (s_rows is 16-byte aligned; a row is 2M doubles).
+// The general kernels' output rows, staged in LDS by the block in the resident
+// row layout (PFRow: 16 kPairs doubles per row), copied before the solve so the
+// loads overlap it.  A lane then loads slot (16 p + lane % 16) of each pair of
+// a row: 2 x 512 B of LDS data per row and wave, where broadcast reads of the
+// whole row (every lane all 2M + 2 operands) moved 15 KB and were bound by the
+// LDS return bandwidth (0.26 us per row).
 constexpr int kRowsLds = 4096;   // doubles (32 KB); more rows use pf_node_pu
 template <int M>
 __device__ __forceinline__ bool pf_rows_stage(const pgw_pf_tables& t, int n_out, double* s) {
-  if (n_out * (2 * M + 2) > kRowsLds || n_out <= 1) return false;   // uniform
-  for (int i = threadIdx.x; i < 2 * M * n_out; i += kBlock) s[i] = t.G[i];
-  for (int i = threadIdx.x; i < 2 * n_out; i += kBlock) s[2 * M * n_out + i] = t.V0[i];
+  constexpr int S = 16 * PFRow<M>::kPairs;
+  if (n_out * S > kRowsLds || n_out <= 1) return false;   // uniform
+  for (int i = threadIdx.x; i < n_out * S; i += kBlock) {
+    const int o = i / S, j = i - o * S;
+    double v = 0.0;
+    if (j < 2) v = t.V0[2 * o + j];
+    else if (j < 2 + M) v = t.G[2 * M * o + 2 * (j - 2)];
+    else if (j < 2 + 2 * M) v = t.G[2 * M * o + 2 * (j - 2 - M) + 1];
+    s[i] = v;
+  }
   return true;
 }
 
-// Output rows 1 .. n_out-1, f(o, |V_o|) called in row order.  From LDS the
-// rows are software-pipelined: the next row's operands (one row of G and V0,
-// 2M + 2 doubles) are in flight while the current row's FMA chains run.  Left
-// to itself the scheduler issued two 16-byte LDS reads at a time and waited on
-// each pair (7 waits per row at one wave per SIMD, 0.45 us per row).  Same
-// operations in the same order as pf_node_pu, so the values are bit-identical.
+// Output rows 1 .. n_out-1, f(o, |V_o|) called in row order.  From LDS: each
+// row's operands are loaded into resident pairs (one 8-byte LDS read per pair)
+// two rows ahead of use, and the rows are evaluated two at a time by DPP
+// broadcast FMAs (pf_row2_dpp: four independent chains; at 65 536 envs the
+// kernel runs one wave per SIMD).  Per row the operations and their order are
+// pf_node_pu's, so the values are bit-identical.
 template <int M>
-__device__ __forceinline__ void pf_row_fetch(const double* s, int n_out, int o, double2 (&g)[M], double2& v0) {
-  const double2* G = reinterpret_cast<const double2*>(s) + M * o;
+__device__ __forceinline__ void pf_row_load(const double* s, int o, double (&w)[PFRow<M>::kPairs]) {
+  const double* r = s + 16 * PFRow<M>::kPairs * o + (threadIdx.x & 15);
 #pragma unroll
-  for (int k = 0; k < M; ++k) g[k] = G[k];
-  v0 = reinterpret_cast<const double2*>(s + 2 * M * n_out)[o];
-}
-template <int M>
-__device__ __forceinline__ double pf_row_eval(const double2 (&g)[M], double2 v0, const double* ir,
-                                              const double* ii) {
-  double vr = v0.x, vi = v0.y;
-#pragma unroll
-  for (int k = 0; k < M; ++k) {
-    const double gr = g[k].x, gi = g[k].y;
-    vr = fma(gr, ir[k], vr);
-    vr = fma(-gi, ii[k], vr);
-    vi = fma(gr, ii[k], vi);
-    vi = fma(gi, ir[k], vi);
-  }
-  return sqrt(fma(vi, vi, vr * vr));
+  for (int p = 0; p < PFRow<M>::kPairs; ++p) w[p] = r[16 * p];
 }
 template <int M, class F>
 __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_lds, const double* s,
-                                            int n_out, const double* ir, const double* ii, F&& f) {
+                                            int n_out, const double (&ir)[M], const double (&ii)[M],
+                                            F&& f) {
   if (!rows_lds) {
     for (int o = 1; o < n_out; ++o) f(o, pf_node_pu<M>(t, o, ir, ii));
     return;
   }
-  if (n_out <= 1) return;
-  double2 ga[M], gb[M], va, vb;
-  pf_row_fetch<M>(s, n_out, 1, ga, va);
-  for (int o = 1; o < n_out; o += 2) {
-    pf_row_fetch<M>(s, n_out, min(o + 1, n_out - 1), gb, vb);
+  constexpr int P = PFRow<M>::kPairs;
+  double wa[P], wb[P], na[P], nb[P];
+  const int last = n_out - 1;
+  pf_row_load<M>(s, 1, wa);
+  pf_row_load<M>(s, min(2, last), wb);
+  int o = 1;
+  for (; o + 2 <= n_out; o += 2) {
+    pf_row_load<M>(s, min(o + 2, last), na);     // the next pair of rows in flight
+    pf_row_load<M>(s, min(o + 3, last), nb);
     __builtin_amdgcn_sched_barrier(0);
-    f(o, pf_row_eval<M>(ga, va, ir, ii));
-    if (o + 1 >= n_out) break;
-    pf_row_fetch<M>(s, n_out, min(o + 2, n_out - 1), ga, va);
-    __builtin_amdgcn_sched_barrier(0);
-    f(o + 1, pf_row_eval<M>(gb, vb, ir, ii));
+    double ar, ai, br, bi;
+    pf_row2_dpp<M>(ar, ai, br, bi, wa, wb, ir, ii);
+    const double ua = sqrt(fma(ai, ai, ar * ar)), ub = sqrt(fma(bi, bi, br * br));
+    f(o, ua);
+    f(o + 1, ub);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      wa[p] = na[p];
+      wb[p] = nb[p];
+    }
+  }
+  if (o < n_out) {
+    double ar, ai;
+    pf_row1_dpp<M>(ar, ai, wa, ir, ii);
+    f(o, sqrt(fma(ai, ai, ar * ar)));
   }
 }
 
@@ -463,7 +477,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   long long* const trace = g_pf_trace;
   pf_trace(trace, 0);
   constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
-  __shared__ __attribute__((aligned(16))) double s_rows[kKeep ? kRowsLds : 1];
+  __shared__ double s_rows[kKeep ? kRowsLds : 1];
   bool rows_lds = false;
   if constexpr (kKeep) rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
@@ -486,27 +500,28 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if constexpr (kKeep) __syncthreads();       // the staged rows (every lane is still here)
   pf_trace(trace, 4);
-  if (!valid) return;
-  if (t.sig_out) t.sig_out[e] = sig;
-  // element voltages first: they are dead during the output rows, whose LDS
-  // operand loads then have the registers to go out together
-  if (t.U_out) {
+  // element voltages first: they are dead during the output rows
+  if (valid && t.U_out) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
       t.U_out[2 * (e * M + k)] = S.ur[k];
       t.U_out[2 * (e * M + k) + 1] = S.ui[k];
     }
   }
-  if (a.n_out > 0) v_out[e] = v0;
+  // the output rows with every lane still here (their DPP broadcasts read all
+  // lanes); lanes past n store nothing
   double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
   if constexpr (kKeep)
     pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
-      v_out[(int64_t)o * n + e] = v;
+      if (valid && v_out) v_out[(int64_t)o * n + e] = v;
       vmn = (v < vmn) ? v : vmn;
       vmx = (v > vmx) ? v : vmx;
     });
   pf_trace(trace, 5);
+  if (!valid) return;
+  if (t.sig_out) t.sig_out[e] = sig;
   if (a.n_out > 0) {
+    if (v_out) v_out[e] = v0;
     if (t.v_min_out) t.v_min_out[e] = vmn;
     if (t.v_max_out) t.v_max_out[e] = vmx;
   }
@@ -855,7 +870,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
              ((valid && ag < c.n_agents) ? 1.0 : 0.0);
   constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
-  __shared__ __attribute__((aligned(16))) double s_rows[kKeep ? kRowsLds : 1];
+  __shared__ double s_rows[kKeep ? kRowsLds : 1];
   bool rows_lds = false;
   if constexpr (kKeep) rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
@@ -883,14 +898,16 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   pf_trace(trace, 4);
   if constexpr (kKeep) __syncthreads();       // the staged rows (every lane is still here)
-  if (!valid) return;
+  // the output rows with every lane still here (their DPP broadcasts read all
+  // lanes); lanes past n store nothing
   double vsel = v0;
-  if (b.v_out) b.v_out[e] = (Sto)v0;
   if constexpr (kKeep)
     pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
-      if (b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
+      if (valid && b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
       vsel = (o == c.vv_row) ? v : vsel;
     });
+  if (!valid) return;
+  if (b.v_out) b.v_out[e] = (Sto)v0;
   if (b.iters) b.iters[e] = it;
   pf_trace(trace, 5);
   if (c.coordinated) {
@@ -1273,8 +1290,9 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M && p->m == padded_m(p->m),
               "pgw_pf_solve: m=%d not padded (pgw_pf_padded_m)", p->m);
   PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve: bad n_ctrl");
-  PGW_REQUIRE(p->n_out == 0 || (v_out && t->G && t->V0),
-              "pgw_pf_solve: missing v_out/G/V0");
+  PGW_REQUIRE(p->n_out == 0 || (t->G && t->V0), "pgw_pf_solve: missing G/V0");
+  PGW_REQUIRE(p->n_out == 0 || v_out || t->v_min_out || t->v_max_out,
+              "pgw_pf_solve: n_out > 0 but no output (v_out, v_min_out, v_max_out all NULL)");
   PGW_REQUIRE(p->max_iter >= 1, "pgw_pf_solve: max_iter < 1");
   if (n == 0) return PGW_OK;
   const PFArgs a = make_pf_args(*p, *t);
