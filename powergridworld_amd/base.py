@@ -106,13 +106,19 @@ class ComponentEnv(spaces.Env, ABC):
     _bufv = 0
 
     def _act_mat(self, a):
-        """pgw_mat of an action tensor, reused while the caller passes the same
-        buffer (the usual case: a policy output or a preallocated action view)."""
-        key = (a.data_ptr(), a.stride(0), a.stride(1))
+        """pgw_mat of an action tensor, cached per (pointer, strides): a policy
+        writes its actions into a few buffers that the caching allocator hands
+        out in turn, or the caller cycles a preallocated pool."""
+        key = (a.data_ptr(), a.stride(0), a.stride(1), a.dtype)
         c = self.__dict__.get("_act_mat_c")
-        if c is None or c[0] != key:
-            c = self._act_mat_c = (key, (_lib.matf if a.dtype == torch.float32 else _lib.mat)(a))
-        return c[1]
+        if c is None:
+            c = self._act_mat_c = {}
+        m = c.get(key)
+        if m is None:
+            if len(c) >= 64:
+                c.clear()
+            m = c[key] = (_lib.matf if a.dtype == torch.float32 else _lib.mat)(a)
+        return m
 
     @abstractmethod
     def reset(self, **kwargs):

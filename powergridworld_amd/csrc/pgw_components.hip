@@ -209,9 +209,13 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
   int dcnt = 0, nact = 0;
   // The scan mask is wave-uniform (scalar), so the vehicle loop is too.  The
   // vehicles go in chunks of kEvChunk: the chunk's requirements are loaded back
-  // to back (one memory round trip per chunk, not per vehicle), then processed
-  // in ascending order exactly as one at a time.  Both passes walk the same
-  // chunk mask, so no index array is needed.
+  // to back (one memory round trip per chunk, not per vehicle); then every
+  // vehicle's quantities (deficit, charge, the new requirement) are computed
+  // with no branch -- independent chains the scheduler interleaves, where one
+  // vehicle at a time was a single dependent chain per wave (~0.2 us per
+  // vehicle at one wave per SIMD) -- and last the sums run over the chunk in
+  // ascending vehicle order, by selects, exactly as one vehicle at a time.
+  // Both passes walk the same chunk mask, so no index array is needed.
   constexpr int kEvChunk = 8;
   for (int w = 0; w < s.n_words; ++w) {
     uint64_t scan = s.scan[w];
@@ -223,45 +227,56 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) scan &= scan - 1;   // the chunk: the next <= kEvChunk bits
       chunk &= ~scan;
-      double rs[kEvChunk];
+      double rs[kEvChunk], df[kEvChunk], cv[kEvChunk];
+      double tls[kEvChunk], rcs[kEvChunk];
+      bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk];
       uint64_t m = chunk;
+      // the chunk's loads all go out before any is used: the requirements
+      // (vector) and the vehicles' time left (uniform: scalar loads, which
+      // complete out of order, so one wait for the chunk instead of one per
+      // vehicle)
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) {
         const int b = m ? __builtin_ctzll(m) : 0;    // past the chunk's end: a harmless reload
-        rs[i] = req[(int64_t)(w * 64 + b) * n + e];
+        const int v = w * 64 + b;
+        rs[i] = req[(int64_t)v * n + e];
+        if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
+          const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[v];
+          tls[i] = q.x;
+          rcs[i] = q.y;
+        } else {
+          tls[i] = (endp[v] - s.time) / 60.0;
+          rcs[i] = 0.0;
+        }
         m &= m - 1;
       }
       m = chunk;
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) {
-        if (m == 0) continue;          // uniform: the chunk's tail
-        const int b = __builtin_ctzll(m);
+        const bool in = m != 0;                      // uniform: the chunk's tail is not
+        const int b = in ? __builtin_ctzll(m) : 0;
         m &= m - 1;
         const int v = w * 64 + b;
-        const double r = rs[i];
-        bool active = ((win >> b) & 1ull) && (r > 0.0);
-        if (active) {
-          now_bits |= 1ull << b;
-          ++nact;
-          demand = demand + r;
-          double tl, rc = 0.0;
-          if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
-            tl = s.tl_rcp[2 * v];
-            rc = s.tl_rcp[2 * v + 1];
-          } else {
-            tl = (endp[v] - s.time) / 60.0;
-          }
-          if (tl > 0.0) {
-            double def = pymax(0.0, p.rate - (s.tl_rcp ? exact_div(r, tl, rc) : r / tl));
-            dsum = dsum + def;
-            ++dcnt;
-            double ch = pymin(kwh, r);
-            req[(int64_t)v * n + e] = r - ch;
-            consumed = consumed + ch;
-          }
-        } else if ((prev >> b) & 1ull) {
-          unserved = unserved + r;          // departed: not charging now (:239-243)
-        }
+        const double r = rs[i], tl = tls[i], rc = rcs[i];
+        act[i] = in && ((win >> b) & 1ull) && (r > 0.0);
+        chg_now[i] = act[i] && (tl > 0.0);
+        dep[i] = in && !act[i] && ((prev >> b) & 1ull);   // departed: not charging now (:239-243)
+        df[i] = pymax(0.0, p.rate - (s.tl_rcp ? exact_div(r, tl, rc) : r / tl));
+        cv[i] = pymin(kwh, r);
+        if (chg_now[i]) req[(int64_t)v * n + e] = r - cv[i];
+      }
+      m = chunk;
+#pragma unroll
+      for (int i = 0; i < kEvChunk; ++i) {
+        const uint64_t lo = m & (0ull - m);          // the chunk's i-th vehicle bit (0 past its end)
+        m &= m - 1;
+        demand = act[i] ? demand + rs[i] : demand;
+        nact += act[i] ? 1 : 0;
+        now_bits |= act[i] ? lo : 0ull;
+        dsum = chg_now[i] ? dsum + df[i] : dsum;
+        consumed = chg_now[i] ? consumed + cv[i] : consumed;
+        dcnt += chg_now[i] ? 1 : 0;
+        unserved = dep[i] ? unserved + rs[i] : unserved;
       }
     }
     chg[(int64_t)w * n + e] = now_bits;
