@@ -119,10 +119,13 @@ class PVEnv(ComponentEnv):
         """Obs of the current row, then curtailment, then advance (:133-148)."""
         a = as_action(action, self.num_envs, 1, self.device)
         vmin = self._min_voltage(kwargs)
-        pmax = float(self.data[self.index])
-        _lib.check(_lib.lib().pgw_pv_step(self.params, self.num_envs, pmax, _lib.mat(a),
-                                          _lib.dptr(vmin), _lib.mat(self._obs),
-                                          _lib.dptr(self._real_power), self._stream()))
+        c = self.__dict__.get("_step_c")
+        if c is None or c[0] != self._bufv:           # per-layout constants, built once
+            c = self._step_c = (self._bufv, _lib.lib().pgw_pv_step, _lib.mat(self._obs),
+                                _lib.dptr(self._real_power), [float(x) for x in self.data])
+        pmax = c[4][self.index]
+        _lib.check(c[1](self.params, self.num_envs, pmax, self._act_mat(a), _lib.dptr(vmin), c[2], c[3],
+                        self._stream()))
         self.index += 1
         rew, _ = self.step_reward(**kwargs)
         return self._obs, rew, self.is_terminal(), {"real_power": -pmax}

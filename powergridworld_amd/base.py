@@ -28,6 +28,9 @@ def as_env_tensor(x, n, device, what="value"):
     """Scalar / [N] / [N,1] input -> fp64 [N] device tensor (broadcast allowed)."""
     if x is None:
         return None
+    if (type(x) is torch.Tensor and x.dtype == torch.float64 and x.dim() == 1 and x.shape[0] == n
+            and x.device == device and x.is_contiguous()):
+        return x                                   # already an [N] fp64 device vector
     t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x, dtype=np.float64))
     if t.dtype != torch.float64 or t.device != device:
         t = t.to(device=device, dtype=torch.float64)

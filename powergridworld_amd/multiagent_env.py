@@ -234,16 +234,17 @@ class MultiAgentEnv(Env):
         # No agent class here sets a reactive power (every component's stays the
         # zero buffer), so the q sums would add zeros: the solve takes q = 0.
         q_zero = self._q_zero
-        for agent in self.agents:
-            load_bus = self.agent_name_bus_map[agent.name]
-            p = agent.real_power
-            if load_bus in load_p:
-                load_p[load_bus] = load_p[load_bus] + p
-                if not q_zero:
+        if q_zero:
+            load_p = self._bus_loads()
+        else:
+            for agent in self.agents:
+                load_bus = self.agent_name_bus_map[agent.name]
+                p = agent.real_power
+                if load_bus in load_p:
+                    load_p[load_bus] = load_p[load_bus] + p
                     load_q[load_bus] = load_q[load_bus] + agent.reactive_power
-            else:
-                load_p[load_bus] = p
-                if not q_zero:
+                else:
+                    load_p[load_bus] = p
                     load_q[load_bus] = agent.reactive_power
         self.pf_solver.calculate_power_flow(current_time=self.time, p_controllable_consumed=load_p,
                                             q_controllable_consumed=None if q_zero else load_q)
@@ -252,6 +253,44 @@ class MultiAgentEnv(Env):
         rew = self.reward_transform(rew)
         meta = self.meta_transform(meta)
         return obs, rew, done, meta
+
+    def _bus_loads(self):
+        """{bus: [N] real power}: the agents' powers summed per bus in agent order
+        (multiagent_env.py:171-181).  A bus with one agent takes its tensor as
+        is; several agents go through one pgw_agent_reduce launch (0 + p0 + p1
+        + ..., the reference's left-to-right sum) into a per-bus buffer, where
+        the reference's `+` made a new tensor per agent."""
+        key = tuple(a.real_power.data_ptr() for a in self.agents)
+        c = self.__dict__.get("_bus_c")
+        if c is None or c[0] != key:
+            groups = {}
+            for agent in self.agents:
+                groups.setdefault(self.agent_name_bus_map[agent.name], []).append(agent.real_power)
+            plan = []
+            for bus, ps in groups.items():
+                if len(ps) == 1 or len(ps) > _lib.MAX_COMP:
+                    plan.append((bus, ps, None, None))
+                    continue
+                ra = _lib.ReduceArgs()
+                ra.n_comp = len(ps)
+                for i, p in enumerate(ps):
+                    ra.real_power[i] = p.data_ptr()
+                    ra.reward[i] = None
+                out = torch.empty(self.num_envs, dtype=torch.float64, device=self.device)
+                plan.append((bus, ps, ra, out))
+            c = self._bus_c = (key, plan)
+        load_p = {}
+        lib, st = _lib.lib(), _lib.stream_ptr(self.device)
+        for bus, ps, ra, out in c[1]:
+            if ra is not None:
+                _lib.check(lib.pgw_agent_reduce(ra, self.num_envs, out.data_ptr(), None, st))
+                load_p[bus] = out
+            else:
+                acc = ps[0]
+                for p in ps[1:]:
+                    acc = acc + p
+                load_p[bus] = acc
+        return load_p
 
     def _init_history(self, capacity):
         """On-device voltage / agent-power history: a ring of
