@@ -89,6 +89,7 @@ class OpenDSSSolver(PowerFlowSolver):
         f = self.feeder
         names = f.node_names if nodes is None else [n.lower() for n in nodes]
         self.output_names = names
+        self._names_ver = getattr(self, "_names_ver", 0) + 1
         idx = [f.node_index[n] for n in names]
         M, W, U0, G, V0o = f.reduce(idx)
         self.M = M
@@ -143,6 +144,7 @@ class OpenDSSSolver(PowerFlowSolver):
             raise ValueError("at most %d controllable loads" % _lib.PF_MAX_CTRL)
         if names != self._ctrl_names:
             self._ctrl_names = names
+            self._seen_keys = None
             self._base_params()
 
     def _base_params(self):
@@ -287,11 +289,14 @@ class OpenDSSSolver(PowerFlowSolver):
                              q_controllable_consumed: dict = None, current_time: str = None) -> None:
         n = self.num_envs
         if p_controllable_consumed is not None:
-            keys = [k for k in self.load_bus_name
-                    if k in p_controllable_consumed or k in (q_controllable_consumed or {})]
-            if not set(keys) <= set(self._ctrl_names):     # the controllable set only grows
-                grown = set(keys) | set(self._ctrl_names)
-                self.set_controllable_loads([k for k in self.load_bus_name if k in grown])
+            kt = (tuple(p_controllable_consumed), tuple(q_controllable_consumed or ()))
+            if kt != self.__dict__.get("_seen_keys"):     # (checked once per key set)
+                keys = [k for k in self.load_bus_name
+                        if k in p_controllable_consumed or k in (q_controllable_consumed or {})]
+                if not set(keys) <= set(self._ctrl_names):     # the controllable set only grows
+                    grown = set(keys) | set(self._ctrl_names)
+                    self.set_controllable_loads([k for k in self.load_bus_name if k in grown])
+                self._seen_keys = kt
         p = self.step_params(current_time)
         cp = cq = None
         if self._ctrl_names and p_controllable_consumed is not None:
@@ -332,7 +337,7 @@ class OpenDSSSolver(PowerFlowSolver):
     def _prepare_bus_voltages(self):
         """{node: [N] view of its v_out row}; the views stay valid across solves
         (one dict per output buffer, cached)."""
-        key = (self.v_out.data_ptr(), tuple(self.output_names))
+        key = (self.v_out.data_ptr(), self._names_ver)
         if getattr(self, "_bv_key", None) != key:
             cache = self.__dict__.setdefault("_bv_cache", {})
             bv = cache.get(key)
