@@ -197,6 +197,45 @@ def test_pf_vs_oracle():
         assert (N(pf.iterations) == orc.last_iters).mean() > 0.99
 
 
+@pytest.mark.parametrize("loads", [("675c",), ("675c", "671")])
+def test_pf_all_rows_ragged_and_extrema_only(loads):
+    """All output rows at a ragged batch (the last wave part-empty: the rows'
+    DPP broadcasts read every lane, past-n lanes included, and store nothing);
+    the epilogue's min/max equal Python's min/max over the rows in order; an
+    extrema-only solve (v_out = NULL) gives the same extrema."""
+    from oracle.pf_oracle import BatchedPF
+    from powergridworld_amd import _lib
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    n = 1000
+    rng = np.random.default_rng(21)
+    pf = OpenDSSSolver("ieee_13_dss/IEEE13Nodeckt.dss", "ieee_13_dss/annual_hourly_load_profile.csv",
+                       system_load_rescale_factor=0.65, num_envs=n, device=DEV)
+    orc = BatchedPF(system_load_rescale_factor=0.65)
+    ts = "2020-08-12 13:00"
+    p_np = {k: rng.uniform(-400, 300, n) for k in loads}
+    pf.calculate_power_flow({k: T(v) for k, v in p_np.items()}, None, current_time=ts)
+    want = orc.calculate(ts, p_np, K=n)
+    v = pf.get_bus_voltages()
+    got = np.stack([N(v[name]) for name in orc.feeder.node_names], 1)
+    np.testing.assert_allclose(got, want, rtol=1e-8, atol=0)
+    rows = [N(v[name]) for name in pf.output_names]
+    vmn, vmx = rows[0].copy(), rows[0].copy()
+    for r in rows[1:]:
+        vmn = np.where(r < vmn, r, vmn)
+        vmx = np.where(r > vmx, r, vmx)
+    lo, hi = pf.voltage_extrema()
+    assert np.array_equal(N(lo), vmn) and np.array_equal(N(hi), vmx)
+    # the same solve with the extrema only
+    p = pf.step_params(ts)
+    t = _lib.PFTables.from_buffer_copy(pf.step_tables(ts))
+    mn = torch.full((n,), -1.0, dtype=torch.float64, device=DEV)
+    mx = torch.full((n,), -1.0, dtype=torch.float64, device=DEV)
+    t.v_min_out, t.v_max_out = mn.data_ptr(), mx.data_ptr()
+    cp = torch.stack([T(p_np[k]) for k in pf._ctrl_names])
+    _lib.check(_lib.lib().pgw_pf_solve(p, t, n, cp.data_ptr(), None, None, None, _lib.stream_ptr(DEV)))
+    assert torch.equal(mn, lo) and torch.equal(mx, hi)
+
+
 def test_pf_predictor_vs_oracle_and_cold_start():
     """Single controllable load: the per-hour predictor grid (warm start) must
     converge to the oracle's fixed point -- inside the grid, across band kinks and
