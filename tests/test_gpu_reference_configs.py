@@ -37,6 +37,9 @@ def _engine(case, exo):
     if case == "ev3":
         agents = [{"name": "ev-charging-%d" % i, "bus": "675c", "cls": EVChargingEnv, "config": EV_CFG}
                   for i in range(3)]
+    elif case == "buses":      # two buses, one of them with two agents (a per-bus sum)
+        agents = [{"name": "ev-charging-%d" % i, "bus": b, "cls": EVChargingEnv, "config": EV_CFG}
+                  for i, b in enumerate(("675c", "671", "675c"))]
     elif case == "mc3":
         agents = [{"name": "building-%d" % i, "bus": "675c", "cls": MultiComponentEnv,
                    "config": {"components": mc}} for i in range(3)]
@@ -62,6 +65,8 @@ def _oracle(case, exo):
                          ("storage", BatteryOracle(K, rescale_spaces=False))])
     if case == "ev3":
         agents = [("ev-charging-%d" % i, "675c", EVOracle(K, **EV_CFG)) for i in range(3)]
+    elif case == "buses":
+        agents = [("ev-charging-%d" % i, b, EVOracle(K, **EV_CFG)) for i, b in enumerate(("675c", "671", "675c"))]
     elif case == "mc3":
         agents = [("building-%d" % i, "675c", mc()) for i in range(3)]
     else:
@@ -96,7 +101,7 @@ def _cmp_obs(obs, want, t):
             _close(obs[name], o, 1e-9, 1e-9, "obs %s step %d" % (name, t))
 
 
-@pytest.mark.parametrize("case", ["ev3", "mc3", "het"])
+@pytest.mark.parametrize("case", ["ev3", "mc3", "het", "buses"])
 def test_reference_multiagent_configs(case, exo_frame):
     env, orc = _engine(case, exo_frame), _oracle(case, exo_frame)
     rng = np.random.default_rng(3)
