@@ -219,8 +219,14 @@ class HSMultiComponentEnv(MultiComponentEnv):
             for c, e in enumerate(self.envs):
                 self._act_buf[c].copy_(as_action(action[e.name], self.num_envs, 1, self.device)[:, 0])
             key = (self._act_buf.data_ptr(), 1, self.num_envs)
-        if key != self._act_key:
-            self._bufs.action = _lib.Mat(*key)
+        if key != self._act_key:                  # (Mats cached per buffer: callers cycle a few)
+            mats = self.__dict__.setdefault("_act_mats", {})
+            m = mats.get(key)
+            if m is None:
+                if len(mats) >= 64:
+                    mats.clear()
+                m = mats[key] = _lib.Mat(*key)
+            self._bufs.action = m
             self._act_key = key
 
     def step(self, action, **kwargs):
