@@ -115,3 +115,30 @@ def test_exact_division(tmp_path):
     r = subprocess.run([exe, "2000000"] + divisors, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]
     assert "mismatches: 0" in r.stdout
+
+
+def test_env_tensor_and_action_normalisation():
+    """as_env_tensor / as_action (the host side of every step): an [N] fp64
+    vector on the device passes through as the same object (the per-step fast
+    path), other shapes and dtypes are converted or broadcast, and a shape that
+    fits neither raises ValueError as the reference's numpy code would fail."""
+    import torch
+    from powergridworld_amd.base import as_action, as_env_tensor
+    dev = torch.device("cpu")
+    v = torch.arange(4, dtype=torch.float64)
+    assert as_env_tensor(v, 4, dev) is v
+    col = v.reshape(4, 1)
+    assert torch.equal(as_env_tensor(col, 4, dev), v)
+    assert torch.equal(as_env_tensor(2.5, 4, dev), torch.full((4,), 2.5, dtype=torch.float64))
+    assert as_env_tensor(v.float(), 4, dev).dtype == torch.float64
+    strided = torch.arange(8, dtype=torch.float64)[::2]
+    got = as_env_tensor(strided, 4, dev)
+    assert got.is_contiguous() and torch.equal(got, strided)
+    with pytest.raises(ValueError):
+        as_env_tensor(torch.zeros(3, dtype=torch.float64), 4, dev)
+    a = torch.zeros((4, 2), dtype=torch.float64)
+    assert as_action(a, 4, 2, dev) is a
+    assert tuple(as_action([0.5, -0.5], 4, 2, dev).shape) == (4, 2)       # one action for all envs
+    assert tuple(as_action(v, 4, 1, dev).shape) == (4, 1)
+    with pytest.raises(ValueError):
+        as_action(torch.zeros((3, 2)), 4, 2, dev)
