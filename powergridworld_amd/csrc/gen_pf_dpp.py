@@ -197,14 +197,15 @@ def gen_band(M, k, nr):
 def gen_rows(M):
     """Output rows from resident row pairs (pf_rows_out): one row's operands --
     V0 re, im, then G re and G im of every element, slot j of the row in lane
-    j % 16 of pair j // 16 -- fed by row_newbcast.  Two rows interleaved (four
-    independent FMA chains), and a single row; per row the operations and their
+    j % 16 of pair j // 16 -- fed by row_newbcast.  Four rows interleaved (eight
+    independent FMA chains: one DPP wave per SIMD needs about eight to approach
+    the fp64 issue rate, tools/micro/fp64_issue.hip), and a single row; per row the operations and their
     order are pf_node_pu's: vr = V0r, then per element fma(gr, ir), fma(-gi, ii)
     into vr and fma(gr, ii), fma(gi, ir) into vi."""
     npr = (2 * M + 2 + 15) // 16
     res = []
-    for rows in (2, 1):
-        names = "ab"[:rows]
+    for rows in (4, 1):
+        names = "abcd"[:rows]
         w = lambda r, j: "%%%d" % (2 * rows + r * npr + j // 16)
         base = 2 * rows + rows * npr
         ir = lambda k: "%%%d" % (base + k)
@@ -231,11 +232,12 @@ def gen_rows(M):
             outs += ['"=&v"(%sr)' % r, '"=&v"(%si)' % r]
         ins = ['"v"(w%s[%d])' % (r, p) for r in names for p in range(npr)] + \
               ['"v"(ir[%d])' % k for k in range(M)] + ['"v"(ii[%d])' % k for k in range(M)]
-        if rows == 2:
-            sig = ("template <> __device__ __forceinline__ void pf_row2_dpp<%d>(\n"
-                   "    double& ar, double& ai, double& br, double& bi, const double (&wa)[%d],\n"
-                   "    const double (&wb)[%d], const double (&ir)[%d], const double (&ii)[%d]) {\n"
-                   % (M, npr, npr, M, M))
+        if rows == 4:
+            sig = ("template <> __device__ __forceinline__ void pf_row4_dpp<%d>(\n"
+                   "    double& ar, double& ai, double& br, double& bi, double& cr, double& ci,\n"
+                   "    double& dr, double& di, const double (&wa)[%d], const double (&wb)[%d],\n"
+                   "    const double (&wc)[%d], const double (&wd)[%d], const double (&ir)[%d],\n"
+                   "    const double (&ii)[%d]) {\n" % (M, npr, npr, npr, npr, M, M))
         else:
             sig = ("template <> __device__ __forceinline__ void pf_row1_dpp<%d>(\n"
                    "    double& ar, double& ai, const double (&wa)[%d], const double (&ir)[%d],\n"
@@ -267,9 +269,11 @@ def main():
            "    const double (&w)[PFBlock<M>::kPairs], double ir, double ii, double is);",
            "template <int M> __device__ __forceinline__ void pf_v0(",
            "    double& vr, double& vi, const double (&w)[PFBlock<M>::kPairs]);",
-           "template <int M> __device__ __forceinline__ void pf_row2_dpp(",
-           "    double& ar, double& ai, double& br, double& bi, const double (&wa)[PFRow<M>::kPairs],",
-           "    const double (&wb)[PFRow<M>::kPairs], const double (&ir)[M], const double (&ii)[M]);",
+           "template <int M> __device__ __forceinline__ void pf_row4_dpp(",
+           "    double& ar, double& ai, double& br, double& bi, double& cr, double& ci, double& dr,",
+           "    double& di, const double (&wa)[PFRow<M>::kPairs], const double (&wb)[PFRow<M>::kPairs],",
+           "    const double (&wc)[PFRow<M>::kPairs], const double (&wd)[PFRow<M>::kPairs],",
+           "    const double (&ir)[M], const double (&ii)[M]);",
            "template <int M> __device__ __forceinline__ void pf_row1_dpp(",
            "    double& ar, double& ai, const double (&wa)[PFRow<M>::kPairs], const double (&ir)[M],",
            "    const double (&ii)[M]);",

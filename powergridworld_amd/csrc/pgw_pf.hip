@@ -420,9 +420,10 @@ __device__ __forceinline__ bool pf_rows_stage(const pgw_pf_tables& t, int n_out,
 
 // Output rows 1 .. n_out-1, f(o, |V_o|) called in row order.  From LDS: each
 // row's operands are loaded into resident pairs (one 8-byte LDS read per pair)
-// two rows ahead of use, and the rows are evaluated two at a time by DPP
-// broadcast FMAs (pf_row2_dpp: four independent chains; at 65 536 envs the
-// kernel runs one wave per SIMD).  Per row the operations and their order are
+// four rows ahead of use, and the rows are evaluated four at a time by DPP
+// broadcast FMAs (pf_row4_dpp: eight independent chains; at 65 536 envs the
+// kernel runs one wave per SIMD, which needs about eight DPP chains to
+// approach the fp64 issue rate, tools/micro/fp64_issue.hip).  Per row the operations and their order are
 // pf_node_pu's, so the values are bit-identical.
 template <int M>
 __device__ __forceinline__ void pf_row_load(const double* s, int o, double (&w)[PFRow<M>::kPairs]) {
@@ -439,29 +440,51 @@ __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_ld
     return;
   }
   constexpr int P = PFRow<M>::kPairs;
-  double wa[P], wb[P], na[P], nb[P];
+  double wa[P], wb[P], wc[P], wd[P], na[P], nb[P], nc[P], nd[P];
   const int last = n_out - 1;
   pf_row_load<M>(s, 1, wa);
   pf_row_load<M>(s, min(2, last), wb);
+  pf_row_load<M>(s, min(3, last), wc);
+  pf_row_load<M>(s, min(4, last), wd);
   int o = 1;
-  for (; o + 2 <= n_out; o += 2) {
-    pf_row_load<M>(s, min(o + 2, last), na);     // the next pair of rows in flight
-    pf_row_load<M>(s, min(o + 3, last), nb);
+  for (; o + 4 <= n_out; o += 4) {
+    pf_row_load<M>(s, min(o + 4, last), na);     // the next four rows in flight
+    pf_row_load<M>(s, min(o + 5, last), nb);
+    pf_row_load<M>(s, min(o + 6, last), nc);
+    pf_row_load<M>(s, min(o + 7, last), nd);
     __builtin_amdgcn_sched_barrier(0);
-    double ar, ai, br, bi;
-    pf_row2_dpp<M>(ar, ai, br, bi, wa, wb, ir, ii);
+    double ar, ai, br, bi, cr, ci, dr, di;
+    pf_row4_dpp<M>(ar, ai, br, bi, cr, ci, dr, di, wa, wb, wc, wd, ir, ii);
     const double ua = sqrt(fma(ai, ai, ar * ar)), ub = sqrt(fma(bi, bi, br * br));
+    const double uc = sqrt(fma(ci, ci, cr * cr)), ud = sqrt(fma(di, di, dr * dr));
     f(o, ua);
     f(o + 1, ub);
+    f(o + 2, uc);
+    f(o + 3, ud);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       wa[p] = na[p];
       wb[p] = nb[p];
+      wc[p] = nc[p];
+      wd[p] = nd[p];
     }
   }
+  // the last n_out - 1 mod 4 rows one at a time (wa, wb, wc hold them)
   if (o < n_out) {
     double ar, ai;
     pf_row1_dpp<M>(ar, ai, wa, ir, ii);
+    f(o, sqrt(fma(ai, ai, ar * ar)));
+    ++o;
+  }
+  if (o < n_out) {
+    double ar, ai;
+    pf_row1_dpp<M>(ar, ai, wb, ir, ii);
+    f(o, sqrt(fma(ai, ai, ar * ar)));
+    ++o;
+  }
+  if (o < n_out) {
+    double ar, ai;
+    pf_row1_dpp<M>(ar, ai, wc, ir, ii);
     f(o, sqrt(fma(ai, ai, ar * ar)));
   }
 }
