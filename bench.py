@@ -10,12 +10,23 @@ is inside the timed region.  Kernel durations come from HIP events the library
 records around every --time-every-th launch, on the launch's stream.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
-         (N>1 via torch.distributed.run: one rank per GPU, weak scaling,
-          no collective on the step path; barrier + max-over-ranks timing.)
+         N>1: under torch.distributed.run (one rank per GPU, WORLD_SIZE must
+         equal N), or started directly, in which case bench.py runs
+         torch.distributed.run --nproc-per-node N as a child process before
+         any GPU call and exits with its return code (rank 0 prints the line).
+         Weak scaling, no collective on the step path; barrier +
+         max-over-ranks timing.
+
+The CPU baseline (N=1 only) runs first, before the GPU is touched: the oracle
+on 1 process and on 8 forked processes; the reference's own loop cannot run on
+the GPU host, so its figures (tools/ref_cpu_loop.py, build container) are
+copied in from profiles/ref_cpu_loop.json as a labelled row.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -56,9 +67,11 @@ def parse():
                     help="distinct pre-generated action batches cycled through (HBM resident)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-envs", type=int, default=8192)
-    ap.add_argument("--cpu-sample-steps", type=int, default=286)
+    ap.add_argument("--cpu-sample-steps", type=int, default=143)
+    ap.add_argument("--cpu-procs", type=int, default=8)
     ap.add_argument("--time-every", type=int, default=16,
-                    help="HIP-event-time every k-th launch of each kernel in the timed region")
+                    help="HIP-event-time every k-th launch of each kernel in the timed region "
+                         "(lowered so that at least 8 launches per kernel are timed)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the fp32-storage variant line (N=1 only; never the headline)")
     return ap.parse_args()
@@ -112,11 +125,12 @@ def f32_variant(n, steps, warmup, pool_size, seed, dev):
     return out
 
 
-def cpu_baseline(envs, steps):
-    """The oracle (NumPy port of the reference step path) on the host, 1 thread."""
+def _oracle_leg(job):
+    """One process of the CPU baseline: the oracle, 1 thread, on its own envs."""
+    envs, steps, seed = job
     from threadpoolctl import threadpool_limits
     from oracle.ma_oracle import CoordinatedOracle
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     with threadpool_limits(limits=1):
         orc = CoordinatedOracle(envs)
         orc.reset(rng.uniform(3, 50, (N_AGENTS, envs)))
@@ -124,12 +138,56 @@ def cpu_baseline(envs, steps):
         t0 = time.perf_counter()
         for a in acts:
             orc.step(a)
-        dt = time.perf_counter() - t0
-    return {"value": N_AGENTS * envs * steps / dt, "unit": "agent-env-steps/s", "cores": 1,
-            "kind": "port",
-            "sample": "oracle/ma_oracle.CoordinatedOracle (batched NumPy fp64 port of the "
-                      "reference step path + PF), %d envs x %d steps, 1 thread, %.1f s"
-                      % (envs, steps, dt)}
+        return time.perf_counter() - t0
+
+
+def cpu_baseline(envs, steps, procs):
+    """The oracle (batched NumPy port of the reference step path + PF) on the
+    host: 1 process, then `procs` forked processes on independent env shards
+    (k = 1 and k = 8).  Runs before any GPU call, so the forks
+    never copy a GPU context.  value = the k-process aggregate."""
+    import multiprocessing as mp
+    units = N_AGENTS * envs * steps
+    t1 = _oracle_leg((envs, steps, 0))
+    with mp.get_context("fork").Pool(procs) as pool:
+        tk = pool.map(_oracle_leg, [(envs, steps, 1 + r) for r in range(procs)])
+    out = {"value": procs * units / max(tk), "unit": "agent-env-steps/s", "cores": procs,
+           "kind": "port",
+           "sample": "oracle/ma_oracle.CoordinatedOracle (batched NumPy fp64 port of the reference "
+                     "step path + PF), %d processes x %d envs x %d steps, 1 thread each, slowest "
+                     "%.1f s" % (procs, envs, steps, max(tk)),
+           "per_core": {"value": units / t1, "cores": 1, "sample": "1 process, %d envs x %d steps, "
+                                                                  "%.1f s" % (envs, steps, t1)}}
+    p = os.path.join(REPO, "profiles", "ref_cpu_loop.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            ref = json.load(f)
+        out["reference_loop"] = {
+            "note": "the reference's own Python loop (stub PF), timed by tools/ref_cpu_loop.py in the "
+                    "build container; it cannot run on the GPU host",
+            "host": ref.get("host"),
+            "rows": [{"cores": r["cores"], "value": r["value"]} for r in ref.get("rows", [])],
+            "survey_probe": [{"cores": 1, "value": 781.0}, {"cores": 8, "value": 5948.0}]}
+    return out
+
+
+def stream_copy_gbs(dev, nbytes=1 << 30, reps=20):
+    """Measured HBM ceiling of this run: a device-to-device copy of `nbytes`
+    (read + write = 2 x nbytes per copy), timed with events on the current stream."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def load_traffic():
@@ -141,11 +199,42 @@ def load_traffic():
     return {}
 
 
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N started without torchrun: run torch.distributed.run with N ranks
+    as a CHILD process (never exec: nothing here has touched the GPU yet) and
+    return its exit code.  Under torchrun, WORLD_SIZE must equal --gpus."""
+    under = "WORLD_SIZE" in os.environ or "LOCAL_RANK" in os.environ
+    if under:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world != args.gpus:
+            sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (one rank per GPU)" % (args.gpus, world))
+        return None
+    if args.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     from powergridworld_amd import distributed as pgd
     rank, local, world = pgd.env_rank()
     dist = world > 1
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:      # before the GPU is touched (fork-safe)
+        cpu = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps, args.cpu_procs)
     # PGW_BENCH_REHEARSE=1: rehearse N ranks on fewer GPUs (ranks share devices
     # round-robin, collectives on gloo) -- a correctness check of the N>1 path,
     # never a measurement
@@ -185,7 +274,8 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
-    _lib.check(_lib.lib().pgw_timing_start(args.time_every))
+    time_every = max(1, min(args.time_every, args.steps // 8))     # >= 8 timed launches per kernel
+    _lib.check(_lib.lib().pgw_timing_start(time_every))
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
@@ -200,11 +290,12 @@ def main():
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
         avg_us = {KERNELS[k]: (tot[k] / cnt[k] * 1e3 if cnt[k] else None) for k in range(len(KERNELS))}
-        it = env.pf_solver.iterations.double()
+        unconverged = env.pf_solver.unconverged()
+        it = env.pf_solver.iterations.abs().double()
         mean_it, max_it = float(it.mean()), int(it.max())
         # the PF kernel runs one wave (64 envs) per SIMD: its time follows the
         # slowest wave, so report how many waves need 1, 2, ... iterations
-        wmax = env.pf_solver.iterations[: (n // 64) * 64].view(-1, 64).max(1).values
+        wmax = env.pf_solver.iterations.abs()[: (n // 64) * 64].view(-1, 64).max(1).values
         wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
         traffic = load_traffic()
         kernels = {}
@@ -229,11 +320,24 @@ def main():
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "
                                            "per launch), all k_pf_solve variants"}
+        copy_gbs = stream_copy_gbs(dev)
+        for k in kernels.values():
+            if k.get("unit") == "GB/s":
+                k["frac_measured_copy"] = k["achieved"] / copy_gbs
         dom = max((k for k in kernels if "achieved" in kernels[k]), key=lambda k: kernels[k]["avg_us"])
         d = kernels[dom]
         roof = {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"],
-                "avg_launch_us": d["avg_us"]}
+                "avg_launch_us": d["avg_us"], "timed_launches": d["timed_launches"]}
+        if d["unit"] == "GB/s":
+            roof["peak_measured_copy"] = copy_gbs
+            roof["frac_measured_copy"] = d["achieved"] / copy_gbs
+        step_bytes = (AGENT_BYTES * N_AGENTS + PF_BYTES) * n
+        step_gbs = step_bytes / (elapsed / args.steps) / 1e9
+        step = {"bytes_per_step": step_bytes, "achieved": step_gbs, "unit": "GB/s",
+                "frac": step_gbs / HBM_PEAK_GBS, "frac_measured_copy": step_gbs / copy_gbs,
+                "note": "algorithmic HBM bytes of the whole step (agents 312 B x 5 + PF 140 B per "
+                        "env) / ms_per_step, per GPU"}
         out = {
             "metric": "agent-env-steps/sec at batch 65536, 5-agent scenario, 1/2/4/8 MI355X",
             "value": value,
@@ -253,14 +357,18 @@ def main():
                        "batch_per_gpu": n, "global_batch": total_envs, "episode_steps": 286,
                        "parallelism": "env-sharded x%d (no collective on the step path)" % world},
             "roofline": roof,
+            "step_hbm": step,
+            "stream_copy_gbs": copy_gbs,
             "kernels": kernels,
-            "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist},
+            "time_every": time_every,
+            "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist,
+                              "unconverged_envs": unconverged},
         }
         if world == 1 and not args.no_variants:
             out["variants"] = {"f32": f32_variant(n, min(args.steps, 286), args.warmup, P,
                                                   pgd.rank_seed(0, rank), dev)}
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_sample_envs, args.cpu_sample_steps)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out))
     if dist:
         tdist.destroy_process_group()

@@ -76,10 +76,13 @@ typedef struct pgw_battery_params {
   double max_power;          /* kW                       (:28)  */
   double dt_h;               /* control_timedelta in h   (:49)  */
   int32_t rescale;           /* rescale_spaces           (:31)  */
-  int32_t pad_;
+  int32_t sampled_init;      /* reset only: 1 = init_soc was drawn (truncnorm, :80-84)
+                                and is taken as is; 0 = a given init_storage, clipped
+                                to storage_range (:86-95).  The step ignores it. */
 } pgw_battery_params;
 
-/* soc[e] = clip(init_soc[e], soc_min, soc_max); obs = SoC (scaled). (:72-97) */
+/* soc[e] = init_soc[e], clipped to [soc_min, soc_max] unless p->sampled_init;
+ * obs = SoC (scaled). (:72-97) */
 int32_t pgw_battery_reset(const pgw_battery_params* p, int64_t n, const double* init_soc,
                           double* soc, pgw_mat obs, void* stream);
 /* One control step: to_raw, validate_power, SoC update, real_power = -power.
@@ -316,7 +319,8 @@ typedef struct pgw_pf_tables {
  * (opendss.py:107-129 then OpenDSS's per-phase WNominal).
  * ctrl_p / ctrl_q: n_ctrl x n (kW / kvar, NULL = 0).  v_out: n_out x n (pu); NULL
  * when only the extrema (pgw_pf_tables.v_min_out / v_max_out) are wanted.
- * iters: n (int32, nullable) iteration count per env. */
+ * iters: n (int32, nullable) iteration count per env; -count when the env stopped
+ * at max_iter without passing the convergence test. */
 int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out,
                      int32_t* iters, void* stream);

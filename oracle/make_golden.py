@@ -402,6 +402,63 @@ def gen_c4():
           init_storage=soc0, v675=v675)
 
 
+def _c4_cfg():
+    cfg = make_env_config(building_config={},
+                          pv_config={"profile_csv": "pv_profile.csv", "scaling_factor": 40.},
+                          storage_config={"max_power": 15., "storage_range": (3., 50.)},
+                          system_load_rescale_factor=1.2, num_buildings=5)
+    cfg["pf_config"] = {"cls": OraclePowerFlowSolver, "config": {"system_load_rescale_factor": 1.2}}
+    return cfg
+
+
+def gen_c4_episodes():
+    """C4 across the episode boundary: two full episodes per env, with the SoC
+    the reference draws at each reset (energy_storage_env.py:80-95) and every
+    building's x_k (persists across reset, five_zone_rom_env.py:147-176;
+    MultiAgentEnv.reset, multiagent_env.py:125-140) recorded after the resets
+    and after every step."""
+    rng = np.random.default_rng(616)
+    K, NA, E, T = 2, 5, 2, 286
+    acts = rng.uniform(-1, 1, size=(E, T, NA, K, 8))
+    acts[rng.random(acts.shape) < 0.03] *= 1.2
+    obs = np.zeros((E, T + 1, NA, K, 17)); rew = np.zeros((E, T, NA, K)); vv = np.zeros((E, T, K))
+    done = np.zeros((E, T, K), bool); soc0 = np.zeros((E, NA, K)); v675 = np.zeros((E, T + 1, K))
+    xk = np.zeros((E, T + 1, NA, K, 5))
+    for k in range(K):
+        env = CoordinatedEnv(**copy.deepcopy(_c4_cfg()))
+        names = [a.name for a in env.agents]
+
+        def snap(e, t):
+            for a, nm in enumerate(names):
+                ag = env.agent_dict[nm]
+                xk[e, t, a, k] = [float(np.ravel(m["x_k"])[0])
+                                  for m in ag.env_dict["building"].models]
+            v675[e, t, k] = env.pf_solver.get_bus_voltage_by_name("675c")
+
+        for e in range(E):
+            with quiet():
+                o = env.reset()
+            for a, nm in enumerate(names):
+                soc0[e, a, k] = env.agent_dict[nm].env_dict["storage"].current_storage
+                obs[e, 0, a, k] = np.concatenate([o[nm]["building"], o[nm]["pv"], o[nm]["storage"]])
+            snap(e, 0)
+            for t in range(T):
+                action = {nm: {"building": acts[e, t, a, k, :6], "pv": acts[e, t, a, k, 6:7],
+                               "storage": acts[e, t, a, k, 7:8]} for a, nm in enumerate(names)}
+                with quiet():
+                    o, r, d, m = env.step(action)
+                for a, nm in enumerate(names):
+                    obs[e, t + 1, a, k] = np.concatenate([o[nm]["building"], o[nm]["pv"],
+                                                          o[nm]["storage"]])
+                    rew[e, t, a, k] = r[nm]
+                vv[e, t, k] = m["voltage_violation"]
+                done[e, t, k] = d["__all__"]
+                snap(e, t + 1)
+    assert done[:, -1].all() and not done[:, :-1].any()
+    _save("c4_two_episodes", actions=acts, obs=obs, reward=rew, voltage_violation=vv, done=done,
+          init_storage=soc0, v675=v675, x_k=xk)
+
+
 # --------------------------------------------------------------------------
 # Heterogeneous 3-agent scenario (gridworld/scenarios/heterogeneous.py:13-112):
 # MC building (alpha 0) + grid-aware PV farm rewarded on min_voltage + EV 25x40
@@ -503,7 +560,7 @@ def gen_hs():
 
 
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4, "het": gen_het, "hs": gen_hs}
+              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes, "het": gen_het, "hs": gen_hs}
 
 
 def main():

@@ -39,7 +39,7 @@ class Matf(C.Structure):
 
 class BatteryParams(C.Structure):
     _fields_ = [("soc_min", f64), ("soc_max", f64), ("eta_c", f64), ("eta_d", f64),
-                ("max_power", f64), ("dt_h", f64), ("rescale", i32), ("pad_", i32)]
+                ("max_power", f64), ("dt_h", f64), ("rescale", i32), ("sampled_init", i32)]
 
 
 class PVParams(C.Structure):

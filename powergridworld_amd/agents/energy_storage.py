@@ -101,8 +101,14 @@ class EnergyStorageEnv(ComponentEnv):
                 print("init_storage value needs to be a float, use default value instead")
                 init = self.initial_storage_mean
         init = as_env_tensor(init, n, self.device, "init_storage").to(self.dtype)
-        _lib.check(getattr(_lib.lib(), self._k_reset)(self.params, n, _lib.dptr(init), _lib.dptr(self.soc),
-                                                      self._mat(self._obs), self._stream()))
+        # only a given init_storage is clipped to storage_range (:86-95)
+        self.params.sampled_init = int(init_storage is None)
+        try:
+            _lib.check(getattr(_lib.lib(), self._k_reset)(self.params, n, _lib.dptr(init),
+                                                          _lib.dptr(self.soc), self._mat(self._obs),
+                                                          self._stream()))
+        finally:
+            self.params.sampled_init = 0
         self._real_power.zero_()
         return self.get_obs(**kwargs)
 

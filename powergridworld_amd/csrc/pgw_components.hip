@@ -36,7 +36,9 @@ __global__ void __launch_bounds__(kBlock) k_battery_reset(pgw_battery_params p, 
                                                           S* __restrict__ soc, Mt obs) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  double s = clip((double)init[e], p.soc_min, p.soc_max);   // energy_storage_env.py:86-95
+  // a given init_storage is clipped (energy_storage_env.py:86-95), a drawn one
+  // (truncnorm * std + mean, :80-84) is not
+  double s = p.sampled_init ? (double)init[e] : clip((double)init[e], p.soc_min, p.soc_max);
   soc[e] = (S)s;
   st(obs, e, 0, battery_obs(p, s));
 }

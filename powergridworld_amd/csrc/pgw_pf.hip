@@ -295,7 +295,7 @@ template <int M, bool UB, bool GC> struct PFSolver {
   __device__ __forceinline__ int iterate(int max_iter, bool valid, double& v0r, double& v0i,
                                          double (&lir)[M], double (&lii)[M]) {
     int it = 0, my_it = 0;
-    bool done = !valid;
+    bool done = !valid, conv_ok = !valid;
     v0r = v0i = 0.0;
     if constexpr (KEEP) {
 #pragma unroll
@@ -349,11 +349,13 @@ template <int M, bool UB, bool GC> struct PFSolver {
       }
       ++it;
       my_it = done ? my_it : it;
+      conv_ok = conv_ok || (!done && conv);
       done = done || conv || it >= max_iter;
       if (__ballot(!done) == 0ull) break;
     }
     if constexpr (KEEP) pf_node0<M>(v0r, v0i, w, lir, lii);
-    return my_it;
+    // an env stopped by max_iter before passing the test reports -iterations
+    return conv_ok ? my_it : -my_it;
   }
 
 };

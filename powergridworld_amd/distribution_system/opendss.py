@@ -75,7 +75,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self.base_load = np.stack([self.feeder.base_kw, self.feeder.base_kvar], 1)
         self.tol, self.max_iter = float(tol), int(max_iter)
         self.bus_voltages = {}
-        self.iterations = None
+        self.iterations = None       # [N] int32 per env; -max_iter = stopped unconverged
         self._extrema = None
         self._hour_memo = {}
         self._ctrl_names = []
@@ -321,6 +321,12 @@ class OpenDSSSolver(PowerFlowSolver):
         self._prepare_bus_voltages()
         if self._all_nodes:                        # the epilogue's min / max over every node
             self._extrema = (self._vmin, self._vmax)
+
+    def unconverged(self) -> int:
+        """Envs whose last solve stopped at max_iter without meeting tol (the
+        kernels report their count as -iterations).  Synchronises; never
+        called on the step path."""
+        return 0 if self.iterations is None else int((self.iterations < 0).sum())
 
     def bind_output(self, v_out=None):
         """Write the next solves' node voltages into `v_out` ([n_out, N] fp64, e.g.

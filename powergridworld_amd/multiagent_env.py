@@ -394,9 +394,15 @@ class MultiAgentEnv(Env):
                     return "agents have different component parameters"
                 if hasattr(e0, "data") and not np.array_equal(e0.data, e1.data):
                     return "agents have different PV profiles"
-                if hasattr(e0, "_exo") and (e0.df.index[0] != e1.df.index[0] or
-                                            not np.array_equal(e0._T_oa, e1._T_oa)):
-                    return "agents have different exogenous data"
+                # the fused step feeds every agent agent 0's per-step exogenous
+                # row (BuildingExo: T_oa, Q_solar/int/cool, comfort bounds,
+                # time_of_day), so the whole tables must agree, not just T_oa
+                if hasattr(e0, "_exo") and (
+                        len(e0._exo) != len(e1._exo) or e0.df.index[0] != e1.df.index[0] or
+                        e0.max_episode_steps != e1.max_episode_steps or
+                        any(not np.array_equal(getattr(e0, t), getattr(e1, t))
+                            for t in ("_T_oa", "_q_solar", "_q_int", "_q_cool", "_cb"))):
+                    return "agents have different exogenous data or comfort bounds"
         if self.fused_reward_transform not in (None, "coordinated"):
             return "unknown fused reward transform"
         if self.fused_reward_transform == "coordinated" and \

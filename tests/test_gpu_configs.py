@@ -1,0 +1,251 @@
+"""BASELINE configs C1 and C5 on the HIP path, and C4 across the episode
+boundary against the reference.  Needs an MI355X.
+
+C1 = a single battery env (batch 1, EnergyStorageEnv defaults,
+energy_storage_env.py:131-157) -- the reference goldens replayed one env at a
+time.  C5 = the C4 shape sharded 8 x 65,536: each shard, stepped
+as its own env with the per-rank seeds bench.py uses, is bit-identical to the
+same envs inside one unsharded batch, and sampled envs match the oracle.
+"""
+import copy
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import golden_path
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def load(name):
+    with np.load(golden_path(name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def T(x):
+    return torch.tensor(np.asarray(x), dtype=torch.float64, device=DEV)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def close(got, want, rtol=1e-12, atol=1e-12):
+    np.testing.assert_allclose(N(got) if isinstance(got, torch.Tensor) else got, want, rtol, atol)
+
+
+# ------------------------------------------------------------------ C1
+@pytest.mark.parametrize("case", ["default", "norescale", "big"])
+def test_c1_battery_batch_one(case):
+    """num_envs = 1: each golden env replayed alone (obs, SoC, real power, reward, done)."""
+    from powergridworld_amd.agents import EnergyStorageEnv
+    g = load("battery_" + case)
+    cfg = json.loads(str(g["config"]))
+    if "storage_range" in cfg:
+        cfg["storage_range"] = tuple(cfg["storage_range"])
+    K = g["init_storage"].shape[0]
+    env = EnergyStorageEnv(name="storage", num_envs=1, device=DEV, **cfg)
+    for k in range(K):
+        obs, _ = env.reset(init_storage=float(g["init_storage"][k]))
+        assert tuple(obs.shape) == (1, 1)
+        close(obs[0], g["obs"][0, k])
+        for t in range(g["actions"].shape[0]):
+            obs, rew, done, meta = env.step(T(g["actions"][t, k][None]))
+            close(obs[0], g["obs"][t + 1, k])
+            close(env.real_power[0], g["real_power"][t, k])
+            close(env.soc[0], g["soc"][t + 1, k])
+            assert float(rew[0]) == g["reward"][t, k]
+            assert done == bool(g["done"][t, k])
+
+
+def test_c1_battery_sampled_init_not_clipped():
+    """A drawn initial SoC (truncnorm * std + mean, :80-84) is taken as is; a
+    given init_storage is clipped to storage_range (:86-95)."""
+    from powergridworld_amd.agents import EnergyStorageEnv
+    # mean 48 +- std 5 reaches past storage_range[1] = 50 for part of the draws
+    env = EnergyStorageEnv(name="storage", num_envs=4096, device=DEV, initial_storage_mean=48.0,
+                           initial_storage_std=5.0)
+    env.seed(3)
+    env.reset()
+    soc = N(env.soc)
+    assert soc.max() > 50.0 and soc.min() >= 43.0 - 1e-9 and soc.max() <= 53.0 + 1e-9
+    env.reset(init_storage=60.0)
+    assert (N(env.soc) == 50.0).all()
+
+
+# ------------------------------------------------------------------ C4 across the episode boundary
+def _c4_obs(env, fused, obs):
+    if fused:
+        return env.packed_obs()
+    return torch.stack([torch.cat([obs[a.name][c] for c in ("building", "pv", "storage")], 1)
+                        for a in env.agents])
+
+
+def _c4_step(env, fused, act):
+    if fused:
+        return env.step(act)
+    return env.step({a.name: {"building": act[i, :, :6], "pv": act[i, :, 6:7],
+                              "storage": act[i, :, 7:8]} for i, a in enumerate(env.agents)})
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_c4_two_episodes_golden(fused):
+    """Two full episodes per env (reference run, tests/golden/c4_two_episodes.npz):
+    obs, x_k (carried over the reset), rewards, voltage violation and done
+    through 2 x 286 steps, with the SoC the reference drew at each reset."""
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    g = load("c4_two_episodes")
+    E, Tn, NA, K, _ = g["actions"].shape
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=K, device=DEV, fused=fused)
+    for e in range(E):
+        env.reset()
+        for a, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=T(g["init_storage"][e, a]))
+        obs0 = torch.stack([torch.cat([ag.get_obs()[0][c] for c in ("building", "pv", "storage")], 1)
+                            for ag in env.agents])
+        close(obs0, g["obs"][e, 0], 1e-10, 1e-10)
+        xk = torch.stack([ag.env_dict["building"].x.t() for ag in env.agents])
+        close(xk, g["x_k"][e, 0], 1e-11, 1e-11)
+        close(env.pf_solver.get_bus_voltage_by_name("675c"), g["v675"][e, 0], 1e-8, 0)
+        for t in range(Tn):
+            obs, rew, dones, meta = _c4_step(env, fused, T(g["actions"][e, t]))
+            close(_c4_obs(env, fused, obs), g["obs"][e, t + 1], 1e-10, 1e-10)
+            xk = torch.stack([ag.env_dict["building"].x.t() for ag in env.agents])
+            close(xk, g["x_k"][e, t + 1], 1e-11, 1e-11)
+            close(torch.stack([rew[a.name] for a in env.agents]), g["reward"][e, t], 1e-7, 1e-7)
+            close(meta["voltage_violation"], g["voltage_violation"][e, t], 1e-8, 1e-11)
+            assert dones["__all__"] == bool(g["done"][e, t, 0])
+        assert env.pf_solver.unconverged() == 0
+
+
+def test_c4_two_episodes_tiled_full_batch():
+    """The same reference run tiled to the BASELINE batch (65,536 envs, fused
+    path): every env equals its golden env through both episodes (max error
+    accumulated on the device, one check per episode)."""
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    g = load("c4_two_episodes")
+    E, Tn, NA, K, _ = g["actions"].shape
+    n = 65536
+    idx = torch.arange(n, device=DEV) % K
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
+    acts = T(g["actions"])[:, :, :, idx]                       # [E, T, NA, n, 8]
+    want_obs = T(g["obs"])[:, :, :, idx]
+    want_rew = T(g["reward"])[:, :, :, idx]
+    want_vv = T(g["voltage_violation"])[:, :, idx]
+    want_x = T(g["x_k"])[:, :, :, idx]
+
+    def rel(got, want, tol):
+        """max |got - want| / (tol + tol |want|): <= 1 is assert_allclose(rtol=atol=tol)."""
+        return ((got - want).abs() / (tol + tol * want.abs())).max()
+
+    for e in range(E):
+        err = torch.zeros(4, dtype=torch.float64, device=DEV)
+        env.reset()
+        for a, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=T(g["init_storage"][e, a])[idx])
+        for t in range(Tn):
+            _, rew, dones, meta = env.step(acts[e, t])
+            err[0] = torch.maximum(err[0], rel(env.packed_obs(), want_obs[e, t + 1], 1e-10))
+            err[1] = torch.maximum(err[1], rel(torch.stack([rew[a.name] for a in env.agents]),
+                                               want_rew[e, t], 1e-7))
+            err[2] = torch.maximum(err[2], (meta["voltage_violation"] - want_vv[e, t]).abs().max())
+            xk = torch.stack([ag.env_dict["building"].x.t() for ag in env.agents])
+            err[3] = torch.maximum(err[3], rel(xk, want_x[e, t + 1], 1e-11))
+            assert dones["__all__"] == bool(g["done"][e, t, 0])
+        err = N(err)
+        assert err[0] <= 1 and err[1] <= 1 and err[2] < 1e-8 and err[3] <= 1, (e, err)
+        assert env.pf_solver.unconverged() == 0
+
+
+# ------------------------------------------------------------------ C5 (sharded)
+def test_c5_shards_bit_identical_to_unsharded_batch():
+    """C5 = 8 x 65,536 envs.  Each rank's shard (shard_bounds, per-rank seeds as
+    in bench.py) stepped as its own env equals the same envs of one unsharded
+    524,288-env batch bit for bit, across an episode boundary; 16 sampled envs
+    per shard match the oracle."""
+    from oracle.ma_oracle import CoordinatedOracle
+    from powergridworld_amd.distributed import rank_seed, shard_bounds
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    world, per = 8, 65536
+    total = world * per
+    steps = 3
+    shards = [shard_bounds(total, r, world) for r in range(world)]
+    inits, acts = [], []
+    for r, sh in enumerate(shards):
+        gen = torch.Generator(DEV).manual_seed(rank_seed(0, r))
+        inits.append(torch.rand((5, sh.count), dtype=torch.float64, device=DEV, generator=gen) * 47 + 3)
+        acts.append(torch.rand((steps, 5, sh.count, 8), dtype=torch.float64, device=DEV,
+                               generator=gen) * 2.2 - 1.1)
+    init_all, act_all = torch.cat(inits, 1), torch.cat(acts, 2)
+
+    def run(env, init, act, hook):
+        env.reset()
+        for a, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=init[a])
+        for t in range(steps):
+            _, rew, _, meta = env.step(act[t])
+            hook(t, env.packed_obs(), torch.stack([rew[a.name] for a in env.agents]),
+                 meta["voltage_violation"], env.pf_solver.get_bus_voltage_by_name("675c"))
+
+    ref = {}
+    big = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=total, device=DEV, fused=True)
+    run(big, init_all, act_all,
+        lambda t, o, r, v, u: ref.__setitem__(t, (o.clone(), r.clone(), v.clone(), u.clone())))
+    assert big.pf_solver.unconverged() == 0
+    del big
+    torch.cuda.empty_cache()
+    rng = np.random.default_rng(5)
+    for r, sh in enumerate(shards):
+        env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=sh.count, device=DEV,
+                                                 fused=True)
+        got = {}
+        run(env, inits[r], acts[r],
+            lambda t, o, rw, v, u: got.__setitem__(t, (o.clone(), rw.clone(), v.clone(), u.clone())))
+        for t in range(steps):
+            o, rw, v, u = got[t]
+            ro, rr, rv, ru = ref[t]
+            assert torch.equal(o, ro[:, sh.start:sh.stop]), (r, t)
+            assert torch.equal(rw, rr[:, sh.start:sh.stop]), (r, t)
+            assert torch.equal(v, rv[sh.start:sh.stop]), (r, t)
+            assert torch.equal(u, ru[sh.start:sh.stop]), (r, t)
+        pick = np.sort(rng.choice(sh.count, 16, replace=False))
+        orc = CoordinatedOracle(16)
+        orc.reset(N(inits[r])[:, pick])
+        for t in range(steps):
+            oo, orw, ovv = orc.step(N(acts[r][t])[:, pick])
+            o, rw, v, _ = got[t]
+            close(o[:, pick], oo, 1e-10, 1e-10)
+            close(rw[:, pick], orw, 1e-7, 1e-7)
+            close(v[pick], ovv, 1e-8, 1e-11)
+        del env, got
+        torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------ fused-path eligibility
+def test_fused_auto_refuses_agents_with_different_comfort_bounds():
+    """The fused step feeds every agent agent 0's exogenous row, so agents whose
+    comfort bounds (or gains) differ must take the generic path -- whose
+    results follow each agent's own table (oracle-free check: the agent with
+    the wider band sees different violation observations)."""
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    cfg = make_c4_config()
+    cfg["agents"] = copy.deepcopy(cfg["agents"])
+    cfg["agents"][1]["config"]["components"][0]["config"] = {"comfort_bounds": (20.0, 30.0)}
+    env = CoordinatedMultiBuildingControlEnv(**cfg, num_envs=64, device=DEV, fused="auto")
+    assert env._fused is None
+    with pytest.raises(ValueError, match="comfort bounds"):
+        CoordinatedMultiBuildingControlEnv(**cfg, num_envs=64, device=DEV, fused=True)
+    env.reset()
+    act = torch.zeros((5, 64, 8), dtype=torch.float64, device=DEV)
+    obs, _, _, _ = _c4_step(env, False, act)
+    names = [a.name for a in env.agents]
+    b0, b1 = obs[names[0]]["building"], obs[names[1]]["building"]
+    lb = env.agents[0].env_dict["building"].obs_labels.index("comfort_lower")
+    assert not torch.equal(b0[:, lb], b1[:, lb])

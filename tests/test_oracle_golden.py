@@ -145,3 +145,25 @@ def test_c4_coordinated_oracle():
         np.testing.assert_allclose(vv, g["voltage_violation"][t], 1e-12, 1e-12)
         np.testing.assert_allclose(orc.v, g["v675"][t + 1], 1e-12, 1e-12)
         assert orc.done == bool(g["done"][t, 0])
+
+
+def test_c4_two_episodes_oracle():
+    """C4 across the episode boundary (reference run, two episodes per env): the
+    SoC the reference drew at each reset is injected; x_k carries over."""
+    from oracle.ma_oracle import CoordinatedOracle
+    g = load("c4_two_episodes")
+    E, T, NA, K, _ = g["actions"].shape
+    orc = CoordinatedOracle(K, n_agents=NA)
+    for e in range(E):
+        obs0 = orc.reset(g["init_storage"][e])
+        np.testing.assert_allclose(obs0, g["obs"][e, 0], 1e-10, 1e-10)
+        xk = np.stack([a.comps[0][1].x for a in orc.agents])          # [NA, K, 5]
+        np.testing.assert_allclose(xk, g["x_k"][e, 0], 1e-12, 1e-12)
+        for t in range(T):
+            obs, rew, vv = orc.step(g["actions"][e, t])
+            np.testing.assert_allclose(obs, g["obs"][e, t + 1], 1e-10, 1e-10)
+            np.testing.assert_allclose(rew, g["reward"][e, t], 1e-9, 1e-9)
+            np.testing.assert_allclose(vv, g["voltage_violation"][e, t], 1e-12, 1e-12)
+            xk = np.stack([a.comps[0][1].x for a in orc.agents])
+            np.testing.assert_allclose(xk, g["x_k"][e, t + 1], 1e-12, 1e-12)
+            assert orc.done == bool(g["done"][e, t, 0])
