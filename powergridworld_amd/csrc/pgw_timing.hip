@@ -20,6 +20,7 @@ int64_t g_calls[PGW_T_COUNT] = {};
 std::vector<hipEvent_t> g_pool;
 std::vector<Sample> g_samples;
 size_t g_pool_used = 0;
+constexpr size_t kPrealloc = 512;   // events ready before a session (256 samples)
 
 hipEvent_t next_event() {
   if (g_pool_used == g_pool.size()) {
@@ -58,6 +59,15 @@ int32_t pgw_timing_start(int32_t every) {
   for (auto& c : g_calls) c = 0;
   g_samples.clear();
   g_pool_used = 0;
+  // events are created here, not on the first timed launches: hipEventCreate
+  // inside the timed region costs host time per sample (the short bench's
+  // 10 samples x 2 kernels would otherwise create 40 events while timing)
+  while (g_pool.size() < kPrealloc) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) break;
+    g_pool.push_back(ev);
+  }
+  g_samples.reserve(kPrealloc / 2);
   return PGW_OK;
 }
 
