@@ -55,7 +55,9 @@ PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
 M_ELEM = 14
 PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
 PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
-KERNELS = ("k_coord_agents_std", "k_coord_pf<14,true,false,false>", "k_pf_solve")
+PF_KERNEL = ("k_coord_pf_split" if os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
+             else "k_coord_pf<14,true,false,false>")
+KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve")
 
 
 def parse():
@@ -73,9 +75,9 @@ def parse():
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="(internal) print the cpu_baseline JSON and exit; bench.py runs this as a "
                          "child process so the oracle's imports stay out of the timed process")
-    ap.add_argument("--time-every", type=int, default=16,
-                    help="HIP-event-time every k-th launch of each kernel in the timed region "
-                         "(lowered so that at least 8 launches per kernel are timed)")
+    ap.add_argument("--time-steps", type=int, default=64,
+                    help="steps of the kernel-timing pass after the timed region (every launch "
+                         "HIP-event-timed; at least 8, at most --steps)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the fp32-storage variant line (N=1 only; never the headline)")
     return ap.parse_args()
@@ -292,18 +294,24 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
-    time_every = max(1, min(args.time_every, args.steps // 8))     # >= 8 timed launches per kernel
-    _lib.check(_lib.lib().pgw_timing_start(time_every))
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed = pgd.max_over_ranks(elapsed, dev)
+    # kernel durations: a second pass right after the timed region, every launch
+    # bracketed by HIP events on its own stream.  Kept out of `value`'s region:
+    # an event-bracketed launch costs ~10 us of extra step time (measured: the
+    # driver-shaped 20-step run went 36 -> 44 us/step with every 2nd launch timed).
+    time_steps = max(8, min(args.steps, args.time_steps))
+    _lib.check(_lib.lib().pgw_timing_start(1))
+    run(time_steps)
+    torch.cuda.synchronize()
     tot = (_lib.C.c_double * len(KERNELS))()
     cnt = (_lib.C.c_int64 * len(KERNELS))()
     _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
-    elapsed = pgd.max_over_ranks(elapsed, dev)
     total_envs = n * world
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
@@ -313,7 +321,8 @@ def main():
         mean_it, max_it = float(it.mean()), int(it.max())
         # the PF kernel runs one wave (64 envs) per SIMD: its time follows the
         # slowest wave, so report how many waves need 1, 2, ... iterations
-        wmax = env.pf_solver.iterations.abs()[: (n // 64) * 64].view(-1, 64).max(1).values
+        wenv = 32 if PF_KERNEL == "k_coord_pf_split" else 64      # envs per PF wave
+        wmax = env.pf_solver.iterations.abs()[: (n // wenv) * wenv].view(-1, wenv).max(1).values
         wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
         traffic = load_traffic()
         kernels = {}
@@ -329,7 +338,7 @@ def main():
             tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (p_us * 1e-6) / 1e12
             kernels[KERNELS[1]] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
                                    "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); "
-                                           "one wave per SIMD, latency-bound",
+                                           "one wave per SIMD at 65,536 envs, latency-bound",
                                    "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                                    "frac": tfs / FP64_PEAK_TFS,
                                    "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
@@ -377,7 +386,9 @@ def main():
             "step_hbm": step,
             "stream_copy_gbs": copy_gbs,
             "kernels": kernels,
-            "time_every": time_every,
+            "kernel_timing": {"steps": time_steps, "every_launch": True,
+                              "note": "HIP events around every launch of a separate pass of "
+                                      "`steps` steps right after the timed region (not inside it)"},
             "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist,
                               "unconverged_envs": unconverged},
         }

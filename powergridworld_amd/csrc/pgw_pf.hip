@@ -85,6 +85,19 @@ constexpr int kSPairs = (4 * PGW_PF_MAX_M + 15) / 16;   // resident s0 / f entri
 template <int M> struct PFRow {
   static constexpr int kPairs = (2 * M + 2 + 15) / 16;
 };
+// Split solve (k_coord_pf_split): the M elements of an env over S lanes, part h
+// owning elements h P .. h P + P - 1 (P = M / S); the per-part resident layout
+// is gen_pf_dpp.py's split_layout.
+template <int M, int S> struct PFSplit {
+  static_assert(M % S == 0, "elements must split evenly");
+  static constexpr int P = M / S;
+  static constexpr int kW = 3 * P * M;                 // W''(c, i, k) at k 3P + c P + i
+  static constexpr int kU0re = kW, kU0im = kW + P, kU0sum = kW + 2 * P;
+  static constexpr int kG0re = kW + 3 * P, kG0im = kG0re + M, kV0re = kG0re + 2 * M;
+  static constexpr int kSize = kV0re + 2;
+  static constexpr int kPairs = (kSize + 15) / 16;
+  static constexpr int kSPairs = (4 * P + 15) / 16;    // s0 re, s0 im, d/d kW, d/d kvar of own j
+};
 #include "pgw_pf_dpp.inc"
 
 __device__ __forceinline__ double fast_rcp(double m) {
@@ -951,6 +964,205 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   }
 }
 
+// K2 split (the C4 fast path: m = 14, uniform band, one controllable slot, one
+// output row): the same step with each env's 14 load elements over TWO lanes,
+// lanes l and l + 32 of a wave (32 envs a wave), part h = l / 32 owning elements
+// 7h .. 7h + 6.  At 65 536 envs that is 2 048 waves, two per SIMD, where the
+// one-lane kernel had one wave per SIMD whose latency chain (agent-power loads
+// -> predictor gathers -> iteration) nothing else could hide.  Per part:
+//   - the resident operands of its own rows (PFSplit), in its own 16-lane
+//     rows, so one row_newbcast feeds each part its own W'' entry;
+//   - its own elements' predictor record slices and currents;
+//   - the other part's currents arrive by v_permlane32_swap, after which
+//     every row accumulates columns 0 .. 13 in order, i.e. the one-lane
+//     kernel's operations per accumulator: the result is bit-identical to
+//     k_coord_pf<14, true, false, false> (and so to the generic path).
+// An env is converged when both its parts are (ballot), so both parts leave
+// the loop together; part 0 writes the outputs.
+__device__ __forceinline__ void swap_halves(double x, double& p0, double& p1) {
+  // v_permlane32_swap of a value with itself: [p0 | p0] and [p1 | p1]
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  p0 = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
+  p1 = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
+}
+
+template <class Bufs>
+__global__ void __launch_bounds__(kBlock, 2) k_coord_pf_split(CoordPFArgs c, PFArgs a,
+                                                              pgw_pf_tables t, int64_t n, Bufs b) {
+  constexpr int M = 14, S = 2;
+  using L = PFSplit<M, S>;
+  using B = PFBlock<M>;
+  constexpr int P = L::P;
+  using Sto = std::remove_pointer_t<decltype(b.reward)>;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t e = wave * 32 + (lane & 31);
+  const bool valid = e < n;
+  long long* const trace = g_pf_trace;
+  pf_trace(trace, 0);
+  // agent powers first (both parts load the same addresses: one request)
+  double rp[PGW_MAX_AGENTS];
+  const int64_t ec = valid ? e : 0;
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+    rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
+             ((valid && ag < c.n_agents) ? 1.0 : 0.0);
+  // this part's resident operands, gathered from the packed block
+  const int l16 = lane & 15;
+  double w[L::kPairs], sres[L::kSPairs];
+#pragma unroll
+  for (int j = 0; j < L::kPairs; ++j) {
+    const int el = 16 * j + l16;
+    int src = -1;
+    if (el < L::kW) {
+      const int k = el / (3 * P), r = el - k * 3 * P, cc = r / P, i = h * P + (r - cc * P);
+      const int lo = min(i, k), hi = max(i, k);
+      src = cc * B::kTri + lo * M - lo * (lo - 1) / 2 + (hi - lo);
+    } else if (el < L::kG0re) {
+      const int r = el - L::kW, q = r / P;
+      src = B::kU0re + q * M + h * P + (r - q * P);
+    } else if (el < L::kSize) {
+      src = B::kG0re + (el - L::kG0re);
+    }
+    w[j] = src >= 0 ? t.block[src] : 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < L::kSPairs; ++j) {
+    const int el = 16 * j + l16, q = el / P;
+    const int k = q < 4 ? h * P + (el - q * P) : 0;
+    sres[j] = q == 0 ? a.sr0[k] : q == 1 ? a.si0[k] : q == 2 ? a.fr[k] : q == 3 ? a.fi[k] : 0.0;
+  }
+  double cp[PGW_PF_MAX_CTRL];
+#pragma unroll
+  for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = 0.0;
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag) {
+    const int slot = ag < c.n_agents ? c.agent_ctrl[ag] : -1;
+#pragma unroll
+    for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
+  }
+  const double pc = cp[0], qc = 0.0;
+  pf_trace(trace, 1);
+  // first guess: the own elements' slice of the predictor record
+  double ur[P], ui[P];
+  if (a.use_pred) {
+    const double g = (pc - a.pred_x0) * a.pred_inv_h;
+    const int c0 = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
+    auto load = [&](int cc, double2 (&u)[P], float2 (&d1)[P], float2 (&d2)[P]) {
+      const char* r = reinterpret_cast<const char*>(t.U_pred) + (int64_t)cc * (32 * M);
+      const double2* pu = reinterpret_cast<const double2*>(r) + h * P;
+      const float2* p1 = reinterpret_cast<const float2*>(r + 16 * M) + h * P;
+      const float2* p2 = reinterpret_cast<const float2*>(r + 24 * M) + h * P;
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        u[k] = pu[k];
+        d1[k] = p1[k];
+        d2[k] = p2[k];
+      }
+    };
+    double2 u[P];
+    float2 d1[P], d2[P];
+    int cc = c0;
+    if (t.U_pred_meta) {
+      const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
+      const pgw_pred_meta m = t.U_pred_meta[j];
+      load(c0, u, d1, d2);               // speculatively, with the metadata
+      cc = (g - (double)j < m.tstar) ? m.left : m.right;
+      if (cc != c0) load(cc, u, d1, d2);
+    } else {
+      load(c0, u, d1, d2);
+    }
+    const double tt = g - (double)cc;
+    const double h1 = 0.5 * tt, h2 = 0.5 * tt * tt;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      ur[k] = fma(h2, (double)d2[k].x, fma(h1, (double)d1[k].x, u[k].x));
+      ui[k] = fma(h2, (double)d2[k].y, fma(h1, (double)d1[k].y, u[k].y));
+    }
+  } else {
+    pfs_u0<M, S>(ur, ui, w);
+  }
+  pf_trace(trace, 2);
+  const double lo2 = a.lo2, mn2 = a.mn2, mx2 = a.mx2, tol2 = a.tol2;
+  int it = 0, my_it = 0;
+  bool done = !valid, conv_ok = !valid;
+  double v0r = 0.0, v0i = 0.0;
+  while (true) {
+    double A[P], Bs[P], C[P], vr, vi, IR[M], II[M];
+    pfs_acc_init<M, S>(A, C, w);
+    pfs_v0<M, S>(vr, vi, w);
+#pragma unroll
+    for (int i = 0; i < P; ++i) Bs[i] = 0.0;
+    // own currents (PFSolver::current's operations), then the exchange
+    static_for<0, P>([&](auto j) {
+      double s_r, s_i;
+      pfs_power<M, S, decltype(j)::value>(s_r, s_i, sres, pc, qc);
+      const double m2 = fma(ui[j], ui[j], ur[j] * ur[j]);
+      double mc = fmin(fmax(m2, mn2), mx2);
+      mc = (m2 <= lo2) ? 1.0 : mc;
+      const double gg = fast_rcp(mc);
+      const double gr = gg * ur[j], gi = gg * ui[j];
+      const double ir = fma(s_r, gr, -(s_i * gi));
+      const double ii = fma(s_r, gi, s_i * gr);
+      swap_halves(ir, IR[j], IR[P + j]);
+      swap_halves(ii, II[j], II[P + j]);
+    });
+    static_for<0, M>([&](auto k) {
+      const double is = IR[k] + II[k];
+      pfs_column_v<M, S, decltype(k)::value>(A, Bs, C, vr, vi, w, IR[k], II[k], is);
+    });
+    bool conv = true;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const double nr = A[i] - Bs[i];
+      const double ni = (C[i] - A[i]) - Bs[i];
+      const double dr = nr - ur[i], di = ni - ui[i];
+      conv &= fma(dr, dr, di * di) < tol2;
+      ur[i] = done ? ur[i] : nr;
+      ui[i] = done ? ui[i] : ni;
+    }
+    // the env has converged when both of its parts have
+    const uint64_t nc = __ballot(!conv);
+    const bool conv_env = ((nc >> lane) & 1ull) == 0 && ((nc >> (lane ^ 32)) & 1ull) == 0;
+    v0r = done ? v0r : vr;
+    v0i = done ? v0i : vi;
+    ++it;
+    my_it = done ? my_it : it;
+    conv_ok = conv_ok || (!done && conv_env);
+    done = done || conv_env || it >= a.max_iter;
+    if (__ballot(!done) == 0ull) break;
+  }
+  pf_trace(trace, 3);
+  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  pf_trace(trace, 4);
+  if (!valid || h != 0) return;
+  if (b.v_out) b.v_out[e] = (Sto)v0;
+  if (b.iters) b.iters[e] = conv_ok ? my_it : -my_it;
+  pf_trace(trace, 5);
+  if (c.coordinated) {
+    const double vv = pymax(pymax(0.0, c.vv_lo - v0), v0 - c.vv_hi);
+    if (b.vv) b.vv[e] = (Sto)vv;
+    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
+#pragma unroll
+    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+      if (ag < c.n_agents)
+        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// PGW_PF_SPLIT=1 selects the split kernel (read per call: the tests compare the
+// two in one process).  Off by default: measured slower at 65 536 envs
+// (13.1 vs 9.6 us).
+static bool pf_split_enabled() {
+  const char* v = getenv("PGW_PF_SPLIT");
+  return v && v[0] == '1';
+}
+
 // Stencil metadata of the predictor grid (one thread per segment): in a
 // segment whose two ends share the band signature the switch sits at t* = 1/2
 // (the nearest-point rule) and both sides use a 3-point stencil of that
@@ -1206,6 +1418,13 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
+  if (pf->m == 14 && uniform_band(*pf) && pf->n_ctrl <= 1 && !pft->load_scale && pf->n_out <= 1 &&
+      pf_split_enabled()) {
+    // two lanes per env, 32 envs per wave (k_coord_pf_split)
+    launch_timed(PGW_T_COORD_PF, k_coord_pf_split<Bufs>, dim3((unsigned)((n + 127) / 128)),
+                 dim3(kBlock), st, c, a, *pft, n, b);
+    return check_launch("k_coord_pf_split");
+  }
   PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
 }
 

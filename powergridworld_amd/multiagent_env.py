@@ -187,6 +187,8 @@ class MultiAgentEnv(Env):
         for agent in self.agents:
             kwargs = self.get_external_obs_vars(agent)
             _ = agent.reset(**kwargs)
+        if self._fused is not None:
+            self._prewarm_steps()
         if f32:
             self._f32_sync(up=False)
             return self._fused["obs_dict"]
@@ -646,19 +648,7 @@ class MultiAgentEnv(Env):
                 self.time, solver.tables_version)
         ent = F["step_cache"].get(skey)
         if ent is None:
-            info = _lib.CoordStepInfo()
-            if bld is not None:
-                t = bld.time_index
-                if t + 1 >= len(bld._exo):
-                    raise IndexError("building stepped past the end of its exogenous data")
-                info.ex_t, info.ex_next = bld._exo[t], bld._exo[t + 1]
-            if pv is not None:
-                info.pv_pmax = float(pv.data[pv.index])
-            pfp = solver.step_params(self.time)
-            pft = solver.step_tables(self.time)
-            if len(F["step_cache"]) > 1 << 14:
-                F["step_cache"].clear()
-            ent = F["step_cache"][skey] = (info, pfp, pft, solver.tables_version)
+            ent = self._step_entry(skey)
         info, pfp, pft, tv = ent
         if tv != solver.tables_version:    # the table solve above recycled the device tables
             F["step_cache"].clear()
@@ -697,6 +687,50 @@ class MultiAgentEnv(Env):
         if H is not None:
             self._record(None)
         return F["obs_dict"], F["rew_dict"], F["done_true"] if d else F["done_false"], F["meta"]
+
+    def _step_entry(self, skey):
+        """The fused step's per-step constants for skey = (building time index,
+        PV index, time, tables version): exogenous rows, PV value, PF parameters
+        and tables of the hour; cached per key (every episode repeats them)."""
+        F, solver = self._fused, self.pf_solver
+        t, p, time = skey[0], skey[1], skey[2]
+        bld, pv = F["bld0"], F["pv0"]
+        info = _lib.CoordStepInfo()
+        if bld is not None:
+            if t + 1 >= len(bld._exo):
+                raise IndexError("building stepped past the end of its exogenous data")
+            info.ex_t, info.ex_next = bld._exo[t], bld._exo[t + 1]
+        if pv is not None:
+            info.pv_pmax = float(pv.data[p])
+        pfp = solver.step_params(time)
+        pft = solver.step_tables(time)
+        if len(F["step_cache"]) > 1 << 14:
+            F["step_cache"].clear()
+        ent = F["step_cache"][(t, p, time, solver.tables_version)] = (info, pfp, pft, solver.tables_version)
+        return ent
+
+    def _prewarm_steps(self):
+        """Fill the step cache for the episode that reset() just started (host
+        work once per start state, so that the first episode's steps cost what
+        later episodes' do; the constants are the ones each step would build)."""
+        F = self._fused
+        bld, pv = F["bld0"], F["pv0"]
+        t0 = bld.time_index if bld is not None else -1
+        p0 = pv.index if pv is not None else -1
+        solver = self.pf_solver
+        horizon = int(min(self.max_episode_steps if self.max_episode_steps else 0, 1024))
+        if bld is not None:
+            horizon = min(horizon, len(bld._exo) - 1 - t0)
+        if pv is not None:
+            horizon = min(horizon, len(pv.data) - p0)
+        for k in range(1, horizon + 1):
+            time = self._time_at(k)
+            if k >= self._end_step + 1:
+                break
+            key = (t0 + k - 1 if bld is not None else -1, p0 + k - 1 if pv is not None else -1, time,
+                   solver.tables_version)
+            if key not in F["step_cache"]:
+                self._step_entry(key)
 
     def packed_obs(self):
         """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""

@@ -1,5 +1,5 @@
 """Phase timeline of k_coord_pf waves (debug trace): per-phase durations across
-the 1024 waves of one C4 step at N = 65536, and the waves' start/end spread."""
+the waves of one C4 step at N = 65536, and the waves' start/end spread."""
 import os
 import sys
 
@@ -18,7 +18,10 @@ env.reset()
 for _ in range(40):
     env.step(torch.empty((5, n, 8), dtype=torch.float64, device="cuda").uniform_(-1, 1, generator=gen))
 torch.cuda.synchronize()
-buf = torch.zeros((n // 64, 8), dtype=torch.int64, device="cuda")
+split = os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
+wenv = 32 if split else 64          # envs per PF wave (k_coord_pf_split: two lanes per env)
+print("kernel:", "k_coord_pf_split" if split else "k_coord_pf")
+buf = torch.zeros((n // wenv, 8), dtype=torch.int64, device="cuda")
 _lib.check(_lib.lib().pgw_debug_pf_trace(_lib.dptr(buf)))
 for rep in range(3):
     env.step(torch.empty((5, n, 8), dtype=torch.float64, device="cuda").uniform_(-1, 1, generator=gen))
@@ -32,7 +35,7 @@ for rep in range(3):
         d = t[:, k] - t[:, k - 1]
         print("   %-12s mean %6.2f  p50 %6.2f  p99 %6.2f  max %6.2f us" %
               (names[k], d.mean(), np.median(d), np.percentile(d, 99), d.max()))
-    it = env.pf_solver.iterations.view(-1, 64).max(1).values.cpu().numpy()
+    it = env.pf_solver.iterations.view(-1, wenv).max(1).values.cpu().numpy()
     slow = np.argmax(t[:, 5])
     print("   slowest wave %d: iterations %d, phases %s" % (slow, it[slow], np.round(np.diff(t[slow, :6]), 2)))
 _lib.check(_lib.lib().pgw_debug_pf_trace(None))

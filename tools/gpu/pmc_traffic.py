@@ -11,6 +11,7 @@ import sys
 
 NAMES = {"k_coord_agents_std": "k_coord_agents_std",
          "k_coord_pf<14, true, false, false": "k_coord_pf<14,true,false,false>",
+         "k_coord_pf_split": "k_coord_pf_split",
          "k_pf_solve<14, true, false, false>": "k_pf_solve<14,true,false,false>"}
 
 
