@@ -179,9 +179,16 @@ def cpu_baseline(envs, steps, procs):
 
 def stream_copy_gbs(dev, nbytes=1 << 30, reps=20):
     """Measured HBM ceiling of this run: a device-to-device copy of `nbytes`
-    (read + write = 2 x nbytes per copy), timed with events on the current stream."""
+    (read + write = 2 x nbytes per copy) -- the library's 16-B-per-lane
+    nontemporal copy kernel (pgw_stream_copy) and torch's copy_, each timed with
+    events on the current stream; returns both in GB/s."""
+    from powergridworld_amd import _lib
     a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
     b = torch.empty_like(a)
+    ms = _lib.C.c_float()
+    _lib.check(_lib.lib().pgw_stream_copy(a.data_ptr(), b.data_ptr(), nbytes, reps, _lib.C.byref(ms),
+                                          _lib.stream_ptr(dev)))
+    kernel_gbs = 2 * nbytes / (ms.value * 1e-3) / 1e9
     for _ in range(3):
         b.copy_(a)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -191,9 +198,9 @@ def stream_copy_gbs(dev, nbytes=1 << 30, reps=20):
         b.copy_(a)
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    torch_gbs = 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
     del a, b
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    return kernel_gbs, torch_gbs
 
 
 def load_traffic():
@@ -286,10 +293,14 @@ def main():
     from powergridworld_amd import _lib
     # the measured HBM ceiling of this box (device copy) -- also brings the GPU
     # out of its idle clocks after the host-only CPU baseline, before warmup
-    copy_gbs = stream_copy_gbs(dev, reps=100)
-    run(args.warmup)
-    gc.collect()                 # start the timed region with no garbage pending
+    copy_gbs, torch_copy_gbs = stream_copy_gbs(dev, reps=100)
+    # no garbage pending in the timed region -- collected BEFORE the warmup: the
+    # first env.step after a gc.collect() costs ~120 us more host time (cold
+    # caches), +6 us/step on a 20-step region (tools/gpu/short_region.py,
+    # profiles/r02/short_region.txt); the warmup steps absorb it
+    gc.collect()
     gc.freeze()
+    run(args.warmup)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
@@ -385,6 +396,9 @@ def main():
             "roofline": roof,
             "step_hbm": step,
             "stream_copy_gbs": copy_gbs,
+            "stream_copy": {"kernel_gbs": copy_gbs, "torch_copy_gbs": torch_copy_gbs,
+                            "note": "1 GiB device copy, 2 x bytes per copy; kernel = pgw_stream_copy "
+                                    "(16 B/lane, nontemporal), the measured peak used for frac_measured_copy"},
             "kernels": kernels,
             "kernel_timing": {"steps": time_steps, "every_launch": True,
                               "note": "HIP events around every launch of a separate pass of "

@@ -370,6 +370,12 @@ enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COU
 int32_t pgw_debug_pf_trace(long long* buf);
 int32_t pgw_timing_start(int32_t every);
 int32_t pgw_timing_stop(double* total_ms, int64_t* count);
+/* Measured HBM ceiling (benchmark instrumentation): copies `bytes` (a multiple
+ * of 16) from src to dst `reps` times with a 16-B-per-lane nontemporal copy
+ * kernel and writes the average milliseconds per copy (2 x bytes of HBM
+ * traffic).  Synchronizes. */
+int32_t pgw_stream_copy(const void* src, void* dst, int64_t bytes, int32_t reps, float* ms_out,
+                        void* stream);
 
 /* ------------------------------------------------------------------------
  * Host-side feeder construction (C++, no GPU): the native stand-in for the

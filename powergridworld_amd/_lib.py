@@ -204,6 +204,7 @@ _SIGS = {
     "pgw_pf_pred_meta": (i32, [P(PFParams), i32, i32, vp, vp, vp, vp]),
     "pgw_pf_pred_pack": (i32, [P(PFParams), i32, i32, vp, vp, vp]),
     "pgw_timing_stop": (i32, [vp, vp]),
+    "pgw_stream_copy": (i32, [vp, vp, i64, i32, P(C.c_float), vp]),
     "pgw_pf_pack": (i32, [P(PFParams), vp, vp, vp, vp, vp]),
     "pgw_feeder_build": (i32, [P(FeederElem), i32, i32, vp, vp, vp, vp]),
     "pgw_pf_reduce": (i32, [i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
