@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 10
+#define PGW_ABI_VERSION 11
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -214,6 +214,14 @@ typedef struct pgw_ev_step_info {
    * reference's expression, :199) and tl_rcp[2v+1] = 1 / tl_rcp[2v], so the
    * per-vehicle division by it is exact_div (bit-identical, no IEEE divide). */
   const double* tl_rcp;
+  /* Optional (device, NULL = the shared schedule above): per-env vehicle
+   * tables, V x n, for randomize=True (each env drew its own vehicle subset,
+   * ev_charging_env.py:154-156).  env_start = floor(rounded start_time_min),
+   * env_endp = rounded end_time_park_min.  Then `window` is ignored (parked =
+   * env_start <= time <= floor(env_endp), per env), `scan` must hold all
+   * n_vehicles bits and tl_rcp must be NULL (time left is divided in IEEE). */
+  const double* env_start;
+  const double* env_endp;
   int32_t n_words, pad_;
   uint64_t window[PGW_EV_MAX_WORDS];
   uint64_t scan[PGW_EV_MAX_WORDS];
@@ -222,6 +230,10 @@ typedef struct pgw_ev_step_info {
 /* req (V x n) := req0 (V) broadcast; charging bits := 0. */
 int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, double* req,
                      uint64_t* charging, void* stream);
+/* randomize=True reset (:154-156): req (V x n) := req0_env (V x n, each env's
+ * sampled vehicles' energy_required_kwh * multiplier); charging bits := 0. */
+int32_t pgw_ev_reset_tables(const pgw_ev_params* p, int64_t n, const double* req0_env, double* req,
+                            uint64_t* charging, void* stream);
 /* One step (reset's action-less step when action.ptr == NULL).  endp = rounded
  * end_time_park_min (V).  Writes obs (6), real_power, reward. */
 int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,

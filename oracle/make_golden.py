@@ -260,6 +260,39 @@ def gen_ev():
               reward=rew, real_power=rp, done=done)
 
 
+def gen_ev_random():
+    """randomize=True (ev_charging_env.py:154-156): each env's DataFrame.sample
+    draws its own vehicles from NumPy's global state.  Two episodes per env; the
+    sampled row ids (the 'index' column reset_index() keeps) are recorded so
+    the engine can inject the same subsets."""
+    rng = np.random.default_rng(606)
+    np.random.seed(606)
+    cases = {
+        "hetero25": dict(num_vehicles=25, minutes_per_step=5, max_charge_rate_kw=7.,
+                         peak_threshold=200., vehicle_multiplier=40., rescale_spaces=True,
+                         randomize=True),
+        "v100": dict(EV_NB_CONFIG, rescale_spaces=True, randomize=True),
+    }
+    for cname, cfg in cases.items():
+        K, EP = 4, 2
+        envs = [EVChargingEnv(**cfg) for _ in range(K)]
+        V = cfg["num_vehicles"]
+        T = int(envs[0].max_episode_steps) - 2
+        acts = _actions(rng, EP * T, K, 1, overshoot=0.2).reshape(EP, T, K, 1)
+        obs = np.zeros((EP, T + 1, K, 6)); rew = np.zeros((EP, T, K)); rp = np.zeros((EP, T, K))
+        ids = np.zeros((EP, K, V), np.int64)
+        for ep in range(EP):
+            for k, e in enumerate(envs):
+                obs[ep, 0, k], _ = e.reset()
+                ids[ep, k] = e.df["index"].values
+            for t in range(T):
+                for k, e in enumerate(envs):
+                    o, r, d, _ = e.step(acts[ep, t, k])
+                    obs[ep, t + 1, k] = o; rew[ep, t, k] = r; rp[ep, t, k] = e.real_power
+        _save("ev_random_" + cname, config=json.dumps(cfg), vehicle_ids=ids, actions=acts, obs=obs,
+              reward=rew, real_power=rp)
+
+
 # --------------------------------------------------------------------------
 # MultiComponentEnv C3: building + PV + battery + EV (base.py:74-182)
 # --------------------------------------------------------------------------
@@ -560,7 +593,7 @@ def gen_hs():
 
 
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes, "het": gen_het, "hs": gen_hs}
+              "ev": gen_ev, "evrand": gen_ev_random, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes, "het": gen_het, "hs": gen_hs}
 
 
 def main():

@@ -332,8 +332,12 @@ class EVOracle:
         veh = load_vehicles()
         req_all = veh["energy_required_kwh"] * self.mult                     # :72
         rnd = lambda x: x - x % minutes_per_step                             # :273-275
-        self.start = np.floor(rnd(veh["start_time_min"])[:self.V])
-        self.endp_int = rnd(veh["end_time_park_min"])[:self.V]
+        # whole table (randomize: per-env subsets of its rows, :154-156)
+        self.all_start = np.floor(rnd(veh["start_time_min"]))
+        self.all_endp_int = rnd(veh["end_time_park_min"])
+        self.all_req = req_all
+        self.start = self.all_start[:self.V]
+        self.endp_int = self.all_endp_int[:self.V]
         self.endp = np.floor(self.endp_int)
         self.req0 = req_all[:self.V].copy()
         emax = req_all.max()
@@ -346,11 +350,20 @@ class EVOracle:
     def obs(self):
         return to_scaled(self.state, self.obs_low, self.obs_high) if self.rescale else self.state.copy()
 
-    def reset(self):                                           # :145-168
+    def reset(self, vehicle_ids=None):                         # :145-168
+        """vehicle_ids [K, V]: each env's rows of the vehicle table in sampled
+        order (randomize=True, :154-156); None = the first V rows."""
         self.ti = 0
         self.time = self.sim_times[0]
         self.charging = np.zeros((self.K, self.V), bool)
-        self.req = np.tile(self.req0, (self.K, 1))
+        if vehicle_ids is None:
+            ids = np.tile(np.arange(self.V), (self.K, 1))
+        else:
+            ids = np.asarray(vehicle_ids, dtype=np.int64).reshape(self.K, self.V)
+        self.start = self.all_start[ids]
+        self.endp_int = self.all_endp_int[ids]
+        self.endp = np.floor(self.endp_int)
+        self.req = self.all_req[ids].copy()
         self.real_power = np.zeros(self.K)
         self.step(None)
         return self.obs()
@@ -374,10 +387,10 @@ class EVOracle:
                 continue
             req = self.req[:, i]
             demand = np.where(m, demand + req, demand)
-            tl = (self.endp_int[i] - t) / 60.
-            if tl <= 0:
-                continue
-            deficit = np.maximum(0, self.rate - req / tl)
+            tl = (self.endp_int[:, i] - t) / 60.
+            m = m & (tl > 0)                                    # :219-220 (continue)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                deficit = np.maximum(0, self.rate - req / tl)
             dsum = np.where(m, dsum + deficit, dsum); dcnt += m
             ch = np.minimum(kwh, req)
             self.req[:, i] = np.where(m, req - ch, req)

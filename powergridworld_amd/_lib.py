@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -73,7 +73,7 @@ class EVParams(C.Structure):
 
 class EVStepInfo(C.Structure):
     _fields_ = [("time", f64), ("next_time", f64), ("action_default", f64), ("tl_rcp", vp),
-                ("n_words", i32),
+                ("env_start", vp), ("env_endp", vp), ("n_words", i32),
                 ("pad_", i32), ("window", u64 * EV_MAX_WORDS), ("scan", u64 * EV_MAX_WORDS)]
 
 
@@ -193,6 +193,7 @@ _SIGS = {
     "pgw_building_step": (i32, [P(BuildingParams), P(BuildingExo), P(BuildingExo), i64, Mat, vp, vp,
                                 vp, vp, i32, BuildingExt, Mat, vp]),
     "pgw_ev_reset": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
+    "pgw_ev_reset_tables": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
     "pgw_ev_step": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),

@@ -1,9 +1,12 @@
 """Batched EVChargingEnv (reference: gridworld/agents/vehicles/ev_charging_env.py).
 
-All env copies share the vehicle schedule (the reference's non-randomised
-``df[:num_vehicles]``) and the clock, so the parked-vehicle window is computed
-once per step on the host and passed as a bitmask; per env the kernel keeps
-each vehicle's remaining energy ([V, N]) and a charging bitmask ([W, N]).
+With the reference's default ``randomize=False`` all env copies share the
+vehicle schedule (``df[:num_vehicles]``) and the clock, so the parked-vehicle
+window is computed once per step on the host and passed as a bitmask; per env
+the kernel keeps each vehicle's remaining energy ([V, N]) and a charging
+bitmask ([W, N]).  With ``randomize=True`` every env samples its own vehicles
+at reset (``df.sample``, :154-156) and the kernel reads per-env [V, N] start /
+end-of-park tables instead of the shared window.
 """
 import os
 from collections import OrderedDict
@@ -49,9 +52,6 @@ class EVChargingEnv(ComponentEnv):
                  vehicle_csv: str = None, vehicle_multiplier: int = 1, rescale_spaces: bool = True,
                  num_envs: int = 1, device=None, **kwargs):
         super().__init__(name=name, num_envs=num_envs, device=device)
-        if randomize:
-            raise NotImplementedError("randomize=True (per-episode vehicle resampling) is not "
-                                      "supported by the batched engine yet")
         self.num_vehicles = num_vehicles
         self.max_charge_rate_kw = max_charge_rate_kw
         self.minutes_per_step = minutes_per_step
@@ -117,6 +117,24 @@ class EVChargingEnv(ComponentEnv):
         rcp = np.divide(1.0, tl, out=np.zeros_like(tl), where=tl != 0.0)
         self._tl_rcp = torch.tensor(np.ascontiguousarray(np.stack([tl, rcp], -1)), dtype=torch.float64,
                                     device=self.device)
+        if randomize:
+            # randomize=True (:154-156): every reset draws each env its own subset of
+            # num_vehicles rows of the whole table, in sampled order (df.sample), so
+            # the schedule is per env: [V, N] tables instead of the shared bitmask
+            R = len(req_all)
+            if num_vehicles > R:
+                raise ValueError("randomize=True samples %d of %d vehicles" % (num_vehicles, R))
+            dv = lambda x: torch.tensor(np.asarray(x, dtype=np.float64), device=self.device)
+            self._all_start = dv(np.floor(rnd(np.asarray(veh["start_time_min"]))))
+            self._all_endp = dv(rnd(np.asarray(veh["end_time_park_min"])))
+            self._all_req = dv(req_all)
+            shape = (max(V, 1), n)
+            self._env_start = torch.zeros(shape, dtype=torch.float64, device=self.device)
+            self._env_endp = torch.zeros(shape, dtype=torch.float64, device=self.device)
+            self._req0_env = torch.zeros(shape, dtype=torch.float64, device=self.device)
+            self.vehicle_ids = torch.zeros((n, V), dtype=torch.int64, device=self.device)
+            self._gen = torch.Generator(device=self.device)
+            self.seed(None)
         self._reward = torch.zeros(n, dtype=torch.float64, device=self.device)
         self._obs = self._new_obs(6)
         self.time_index = None
@@ -142,8 +160,15 @@ class EVChargingEnv(ComponentEnv):
         s.time = float(self.time)
         s.next_time = float(self.simulation_times[self.time_index + 1])
         s.action_default = float(self._action_space.low[0])                           # :178
-        s.tl_rcp = self._tl_rcp[self.time_index].data_ptr() if self.num_vehicles else None
         s.n_words = self._words
+        if self.randomize:
+            # per-env tables: every vehicle slot is visited, parked-ness per env
+            s.env_start, s.env_endp = self._env_start.data_ptr(), self._env_endp.data_ptr()
+            allv = np.ones(self.num_vehicles, dtype=bool)
+            for w, a in enumerate(_pack_bits(allv)):
+                s.scan[w] = a
+            return s, allv
+        s.tl_rcp = self._tl_rcp[self.time_index].data_ptr() if self.num_vehicles else None
         win = self._window(self.time)
         prev = self._prev_window if self._prev_window is not None else np.zeros_like(win)
         for w, (a, b) in enumerate(zip(_pack_bits(win), _pack_bits(win | prev))):
@@ -182,14 +207,57 @@ class EVChargingEnv(ComponentEnv):
         self.time = self.simulation_times[self.time_index]
         return self._obs, self._reward, self.is_terminal(), {}
 
-    def reset(self, **kwargs):
-        """(:145-168): fresh vehicle table, then one step with no action."""
+    def seed(self, seed=None):
+        """Seed the per-env vehicle sampling of randomize=True (the reference draws
+        from NumPy's global state through DataFrame.sample)."""
+        if self.randomize:
+            self._gen.manual_seed(int(seed) if seed is not None else int(torch.seed() % (2 ** 63)))
+
+    def _sample_vehicles(self, vehicle_ids=None):
+        """This episode's vehicles per env: `vehicle_ids` ([N, V] or [V] row ids of
+        the vehicle table, in the order DataFrame.sample returned them), or a
+        uniform draw without replacement per env (random keys, top V)."""
+        n, V, R = self.num_envs, self.num_vehicles, len(self._all_req)
+        if vehicle_ids is not None:
+            ids = torch.as_tensor(np.asarray(vehicle_ids) if not torch.is_tensor(vehicle_ids) else vehicle_ids,
+                                  dtype=torch.int64).to(self.device)
+            if ids.dim() == 1:
+                ids = ids.unsqueeze(0).expand(n, V)
+            if tuple(ids.shape) != (n, V):
+                raise ValueError("vehicle_ids: expected [%d, %d] or [%d], got %s" % (n, V, V, tuple(ids.shape)))
+            if V and (int(ids.min()) < 0 or int(ids.max()) >= R):
+                raise ValueError("vehicle_ids: row ids must lie in [0, %d)" % R)
+            self.vehicle_ids.copy_(ids)
+        else:
+            chunk = max(1, (1 << 26) // max(R, 1))      # <= 256 MB of fp32 keys at a time
+            for a in range(0, n, chunk):
+                b = min(n, a + chunk)
+                keys = torch.rand((b - a, R), generator=self._gen, device=self.device, dtype=torch.float32)
+                self.vehicle_ids[a:b] = keys.topk(V, dim=1).indices
+        if V:
+            idt = self.vehicle_ids.t()
+            self._env_start.copy_(self._all_start[idt])
+            self._env_endp.copy_(self._all_endp[idt])
+            self._req0_env.copy_(self._all_req[idt])
+
+    def reset(self, vehicle_ids=None, **kwargs):
+        """(:145-168): fresh vehicle table, then one step with no action.  With
+        randomize=True every env draws its own vehicles (:154-156); `vehicle_ids`
+        injects them instead (see _sample_vehicles)."""
         self.time_index = 0
         self.time = self.simulation_times[0]
         self._prev_window = None
-        _lib.check(_lib.lib().pgw_ev_reset(self.params, self.num_envs, _lib.dptr(self._req0_dev),
-                                           _lib.dptr(self.req), _lib.dptr(self.charging),
-                                           self._stream()))
+        if self.randomize:
+            self._sample_vehicles(vehicle_ids)
+            _lib.check(_lib.lib().pgw_ev_reset_tables(self.params, self.num_envs, _lib.dptr(self._req0_env),
+                                                      _lib.dptr(self.req), _lib.dptr(self.charging),
+                                                      self._stream()))
+        else:
+            if vehicle_ids is not None:
+                raise ValueError("vehicle_ids needs randomize=True")
+            _lib.check(_lib.lib().pgw_ev_reset(self.params, self.num_envs, _lib.dptr(self._req0_dev),
+                                               _lib.dptr(self.req), _lib.dptr(self.charging),
+                                               self._stream()))
         self._advance(None)
         return self._obs, {}
 

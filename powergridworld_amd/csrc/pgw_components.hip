@@ -195,6 +195,18 @@ __global__ void __launch_bounds__(kBlock) k_ev_reset(int64_t n, int32_t V, int32
   for (int w = 0; w < W; ++w) chg[(int64_t)w * n + e] = 0ull;
 }
 
+// randomize=True (ev_charging_env.py:154-156): every env restores its own
+// sampled vehicles' requirements.
+__global__ void __launch_bounds__(kBlock) k_ev_reset_tables(int64_t n, int32_t V, int32_t W,
+                                                            const double* __restrict__ req0,
+                                                            double* __restrict__ req,
+                                                            uint64_t* __restrict__ chg) {
+  int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  for (int v = 0; v < V; ++v) req[(int64_t)v * n + e] = req0[(int64_t)v * n + e];
+  for (int w = 0; w < W; ++w) chg[(int64_t)w * n + e] = 0ull;
+}
+
 // ev_charging_env.py:171-264.  Vehicles are visited in ascending index order
 // (the reference iterates a Python set of small ints); only vehicles parked now
 // or at the previous step can contribute (`scan`, uniform across the wave).
@@ -231,7 +243,7 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
       chunk &= ~scan;
       double rs[kEvChunk], df[kEvChunk], cv[kEvChunk];
       double tls[kEvChunk], rcs[kEvChunk];
-      bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk];
+      bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk], wins[kEvChunk];
       uint64_t m = chunk;
       // the chunk's loads all go out before any is used: the requirements
       // (vector) and the vehicles' time left (uniform: scalar loads, which
@@ -242,7 +254,12 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
         const int b = m ? __builtin_ctzll(m) : 0;    // past the chunk's end: a harmless reload
         const int v = w * 64 + b;
         rs[i] = req[(int64_t)v * n + e];
-        if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
+        if (s.env_start) {       // randomize: this env's own vehicle table
+          const double en = s.env_endp[(int64_t)v * n + e];
+          tls[i] = (en - s.time) / 60.0;
+          rcs[i] = 0.0;
+          wins[i] = (s.time >= s.env_start[(int64_t)v * n + e]) && (s.time <= floor(en));
+        } else if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
           const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[v];
           tls[i] = q.x;
           rcs[i] = q.y;
@@ -250,6 +267,7 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
           tls[i] = (endp[v] - s.time) / 60.0;
           rcs[i] = 0.0;
         }
+        if (!s.env_start) wins[i] = (win >> b) & 1ull;
         m &= m - 1;
       }
       m = chunk;
@@ -260,7 +278,7 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
         m &= m - 1;
         const int v = w * 64 + b;
         const double r = rs[i], tl = tls[i], rc = rcs[i];
-        act[i] = in && ((win >> b) & 1ull) && (r > 0.0);
+        act[i] = in && wins[i] && (r > 0.0);
         chg_now[i] = act[i] && (tl > 0.0);
         dep[i] = in && !act[i] && ((prev >> b) & 1ull);   // departed: not charging now (:239-243)
         df[i] = pymax(0.0, p.rate - (s.tl_rcp ? exact_div(r, tl, rc) : r / tl));
@@ -483,6 +501,15 @@ int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, doub
   PGW_LAUNCH(k_ev_reset, n, stream, n, p->n_vehicles, W, req0, req, charging);
 }
 
+int32_t pgw_ev_reset_tables(const pgw_ev_params* p, int64_t n, const double* req0_env, double* req,
+                            uint64_t* charging, void* stream) {
+  PGW_REQUIRE(p && req0_env && req && charging && n >= 0, "pgw_ev_reset_tables: null argument");
+  PGW_REQUIRE(p->n_vehicles >= 0 && p->n_vehicles <= 64 * PGW_EV_MAX_WORDS,
+              "pgw_ev_reset_tables: too many vehicles");
+  const int32_t W = (p->n_vehicles + 63) / 64;
+  PGW_LAUNCH(k_ev_reset_tables, n, stream, n, p->n_vehicles, W, req0_env, req, charging);
+}
+
 int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
                     const double* endp, double* req, uint64_t* charging, pgw_mat obs,
                     double* real_power, double* reward, void* stream) {
@@ -490,6 +517,8 @@ int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n
               "pgw_ev_step: null argument");
   PGW_REQUIRE(s->n_words == (p->n_vehicles + 63) / 64 && s->n_words <= PGW_EV_MAX_WORDS,
               "pgw_ev_step: n_words does not match n_vehicles");
+  PGW_REQUIRE(!s->env_start == !s->env_endp && (!s->env_start || !s->tl_rcp),
+              "pgw_ev_step: per-env tables need env_start and env_endp, and no tl_rcp");
   PGW_LAUNCH(k_ev_step, n, stream, *p, *s, n, action, endp, req, charging, obs, real_power, reward);
 }
 
@@ -510,7 +539,9 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
     if (C.kind == PGW_MC_STORAGE) PGW_REQUIRE(a->bat_soc, "pgw_mc_agent_step: storage buffers");
     if (C.kind == PGW_MC_EV)
       PGW_REQUIRE(a->ev_endp && a->ev_req && a->ev_charging && a->ev_reward &&
-                  a->ev_step.n_words <= PGW_EV_MAX_WORDS, "pgw_mc_agent_step: EV buffers");
+                  a->ev_step.n_words <= PGW_EV_MAX_WORDS &&
+                  !a->ev_step.env_start == !a->ev_step.env_endp &&
+                  (!a->ev_step.env_start || !a->ev_step.tl_rcp), "pgw_mc_agent_step: EV buffers");
   }
   const BldDerived d = make_bld_derived(a->bld);
   bool std_bld = false;

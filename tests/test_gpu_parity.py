@@ -128,6 +128,57 @@ def test_ev_notebook_known_answers_batched():
                                                 -1161670.9270816303], rtol=1e-12)
 
 
+@pytest.mark.parametrize("case", ["hetero25", "v100"])
+def test_ev_randomize_golden(case):
+    """randomize=True (ev_charging_env.py:154-156): the reference's sampled
+    vehicle rows injected per env, two episodes against its outputs."""
+    from powergridworld_amd.agents import EVChargingEnv
+    g = load("ev_random_" + case)
+    cfg = json.loads(str(g["config"]))
+    EP, steps, K = g["reward"].shape
+    env = EVChargingEnv(num_envs=K, device=DEV, **cfg)
+    for ep in range(EP):
+        obs, _ = env.reset(vehicle_ids=g["vehicle_ids"][ep])
+        close(obs, g["obs"][ep, 0])
+        for t in range(steps):
+            obs, rew, done, _ = env.step(T(g["actions"][ep, t]))
+            close(obs, g["obs"][ep, t + 1])
+            close(rew, g["reward"][ep, t])
+            close(env.real_power, g["real_power"][ep, t])
+
+
+def test_ev_randomize_sampled_vs_oracle():
+    """randomize=True with the engine's own per-env draw (seeded): every env's
+    subset is V distinct rows, envs differ, reseeding repeats the draw, and a
+    full episode equals the oracle run on the drawn subsets."""
+    from oracle.pgw_oracle import EVOracle
+    from powergridworld_amd.agents import EVChargingEnv
+    n, V = 512, 25
+    cfg = dict(num_vehicles=V, minutes_per_step=5, max_charge_rate_kw=7., peak_threshold=200.,
+               vehicle_multiplier=40., rescale_spaces=True)
+    env = EVChargingEnv(num_envs=n, device=DEV, randomize=True, **cfg)
+    env.seed(3)
+    obs, _ = env.reset()
+    ids = N(env.vehicle_ids)
+    assert all(len(set(r)) == V for r in ids) and len({tuple(r) for r in ids}) == n
+    assert ids.min() >= 0 and ids.max() < len(env._all_req)
+    env.seed(3)
+    env.reset()
+    assert (N(env.vehicle_ids) == ids).all()
+    orc = EVOracle(n, **cfg)
+    close(obs, orc.reset(ids))
+    rng = np.random.default_rng(7)
+    done = False
+    while not done:
+        a = rng.uniform(-1.2, 1.2, (n, 1))
+        obs, rew, done, _ = env.step(T(a))
+        o, r, d, _ = orc.step(a)
+        close(obs, o)
+        close(rew, r)
+        close(env.real_power, orc.real_power)
+        assert done == bool(d[0])
+
+
 def test_mc_c3_golden(exo_frame):
     from powergridworld_amd import MultiComponentEnv
     from powergridworld_amd.agents import (EnergyStorageEnv, EVChargingEnv,
@@ -530,10 +581,12 @@ def test_list_interface_fused_zero_copy_equals_dict():
 
 
 # ------------------------------------------------------------------ fused MC agent step
-def test_mc_fused_equals_generic_c3():
+@pytest.mark.parametrize("randomize", [False, True])
+def test_mc_fused_equals_generic_c3(randomize):
     """pgw_mc_agent_step (the whole building + PV + storage + EV agent in one
     launch) against the per-component kernels + reduce, bit for bit, at the C3
-    batch; the golden test above already runs the fused path."""
+    batch; the golden test above already runs the fused path.  randomize: the
+    EV draws per-env vehicle subsets (both envs seeded alike)."""
     from powergridworld_amd import MultiComponentEnv
     from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv, FiveZoneROMThermalEnergyEnv, PVEnv
     n = 16384
@@ -543,14 +596,19 @@ def test_mc_fused_equals_generic_c3():
         {"name": "storage", "cls": EnergyStorageEnv, "config": {}},
         {"name": "ev", "cls": EVChargingEnv,
          "config": dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7.,
-                        peak_threshold=250., vehicle_multiplier=5., rescale_spaces=True)},
+                        peak_threshold=250., vehicle_multiplier=5., rescale_spaces=True,
+                        randomize=randomize)},
     ]
     fused, generic = [MultiComponentEnv(name="mc", components=comps, num_envs=n, device=DEV) for _ in range(2)]
     generic._mc_fuse = False
     assert fused._mc_fusable()
     init = torch.rand(n, dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(11)) * 60
     for e in (fused, generic):
+        if randomize:
+            e.env_dict["ev"].seed(5)
         e.reset(init_storage=init)
+    if randomize:
+        assert torch.equal(fused.env_dict["ev"].vehicle_ids, generic.env_dict["ev"].vehicle_ids)
     gen = torch.Generator(DEV).manual_seed(12)
     dims = {"building": 6, "pv": 1, "storage": 1, "ev": 1}
     for t in range(40):

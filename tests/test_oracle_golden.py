@@ -87,7 +87,27 @@ def test_ev(case):
         assert (d == g["done"][t]).all()
 
 
-EV_KNOWN = {"high": -934170.2851237846, "low": -2659771.95782906, "0.8": -1161670.9270816303}
+@pytest.mark.parametrize("case", ["hetero25", "v100"])
+def test_ev_randomize(case):
+    """randomize=True: each env's sampled vehicle rows (recorded from the
+    reference's DataFrame.sample) injected into the oracle, two episodes."""
+    g = load("ev_random_" + case)
+    cfg = json.loads(str(g["config"]))
+    assert cfg.pop("randomize") is True
+    EP, T, K = g["reward"].shape
+    e = O.EVOracle(K, **cfg)
+    for ep in range(EP):
+        ids = g["vehicle_ids"][ep]
+        assert len(set(ids[0])) == ids.shape[1] and not (ids == np.arange(ids.shape[1])).all()
+        np.testing.assert_allclose(e.reset(ids), g["obs"][ep, 0], RTOL, ATOL)
+        for t in range(T):
+            o, r, d, _ = e.step(g["actions"][ep, t])
+            np.testing.assert_allclose(o, g["obs"][ep, t + 1], RTOL, ATOL)
+            np.testing.assert_allclose(r, g["reward"][ep, t], RTOL, ATOL)
+            np.testing.assert_allclose(e.real_power, g["real_power"][ep, t], RTOL, ATOL)
+
+
+EV_KNOWN = {"high":-934170.2851237846, "low": -2659771.95782906, "0.8": -1161670.9270816303}
 
 
 @pytest.mark.parametrize("policy", list(EV_KNOWN))
