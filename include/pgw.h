@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 11
+#define PGW_ABI_VERSION 12
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -66,6 +66,15 @@ typedef struct pgw_matf {
   int64_t s_dim;
 } pgw_matf;
 
+/* PGW_OOB -- out-of-bounds actions.  The reference's to_raw warns when a
+ * rescaled action leaves [-1 - 1e-4, 1 + 1e-4] (or is NaN) and clips it
+ * (gridworld/utils.py:35-40).  The kernels clip the same way; when a
+ * component's params carry a non-NULL `oob` (device uint64), every to_raw
+ * call the reference would have warned on -- one per (env, component, step),
+ * whatever the number of offending elements -- adds 1 to it (a vector atomic,
+ * only on that rare path).  The caller reads it whenever it likes. */
+#define PGW_OOB_EPS 1e-4
+
 /* ------------------------------------------------------------------------
  * Energy storage.  Replaces EnergyStorageEnv.reset/step/get_obs
  * (gridworld/agents/energy_storage/energy_storage_env.py:72-178).
@@ -79,6 +88,7 @@ typedef struct pgw_battery_params {
   int32_t sampled_init;      /* reset only: 1 = init_soc was drawn (truncnorm, :80-84)
                                 and is taken as is; 0 = a given init_storage, clipped
                                 to storage_range (:86-95).  The step ignores it. */
+  uint64_t* oob;             /* nullable device counter, see PGW_OOB below */
 } pgw_battery_params;
 
 /* soc[e] = init_soc[e], clipped to [soc_min, soc_max] unless p->sampled_init;
@@ -103,6 +113,7 @@ typedef struct pgw_pv_params {
   double obs_low, obs_high;     /* (-max(data), 0)           (:86-96) */
   double vmin_low, vmin_high;   /* (0.9, 1.1) when grid_aware */
   int32_t rescale, grid_aware;
+  uint64_t* oob;                /* nullable device counter, see PGW_OOB */
 } pgw_pv_params;
 
 /* obs only (PVEnv.get_obs at the current index); `pmax` = data[index]. */
@@ -151,6 +162,7 @@ typedef struct pgw_building_params {
   int32_t obs_var[PGW_BLD_MAX_OBS];   /* PGW_BV_* per obs slot, state-dict order */
   int32_t n_obs;
   int32_t rescale;
+  uint64_t* oob;         /* nullable device counter, see PGW_OOB     */
 } pgw_building_params;
 
 /* Exogenous row (shared by all envs, host values) + the obs-time scalars. */
@@ -200,6 +212,7 @@ typedef struct pgw_ev_params {
   double u_pen, p_pen, thr, reward_scale;
   double obs_low[6], obs_high[6];
   int32_t n_vehicles, rescale;
+  uint64_t* oob;         /* nullable device counter, see PGW_OOB */
 } pgw_ev_params;
 
 /* Per-step schedule, shared by all envs (time is lockstep): bit v of `window`
@@ -567,6 +580,7 @@ typedef struct pgw_hs_params {
   double dev_act_low, dev_act_high, dev_hours_per_step;
   double dev_obs_high[PGW_HS_MAX_DEV];
   double max_grid_power;
+  uint64_t* oob;                  /* nullable device counter, see PGW_OOB     */
 } pgw_hs_params;
 
 /* Per-step values shared by all envs (the house steps in lockstep). */

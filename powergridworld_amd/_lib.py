@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -39,12 +39,13 @@ class Matf(C.Structure):
 
 class BatteryParams(C.Structure):
     _fields_ = [("soc_min", f64), ("soc_max", f64), ("eta_c", f64), ("eta_d", f64),
-                ("max_power", f64), ("dt_h", f64), ("rescale", i32), ("sampled_init", i32)]
+                ("max_power", f64), ("dt_h", f64), ("rescale", i32), ("sampled_init", i32),
+                ("oob", vp)]
 
 
 class PVParams(C.Structure):
     _fields_ = [("obs_low", f64), ("obs_high", f64), ("vmin_low", f64), ("vmin_high", f64),
-                ("rescale", i32), ("grid_aware", i32)]
+                ("rescale", i32), ("grid_aware", i32), ("oob", vp)]
 
 
 class BuildingParams(C.Structure):
@@ -53,7 +54,8 @@ class BuildingParams(C.Structure):
                 ("T_init", f64 * 5), ("obs_low", f64 * BLD_MAX_OBS),
                 ("obs_high", f64 * BLD_MAX_OBS), ("alpha", f64),
                 ("sel", (i32 * 4) * 5), ("nbr", (i32 * 4) * 5),
-                ("obs_var", i32 * BLD_MAX_OBS), ("n_obs", i32), ("rescale", i32)]
+                ("obs_var", i32 * BLD_MAX_OBS), ("n_obs", i32), ("rescale", i32),
+                ("oob", vp)]
 
 
 class BuildingExo(C.Structure):
@@ -68,7 +70,7 @@ class BuildingExt(C.Structure):
 class EVParams(C.Structure):
     _fields_ = [("rate", f64), ("hours_per_step", f64), ("mult", f64), ("u_pen", f64),
                 ("p_pen", f64), ("thr", f64), ("reward_scale", f64), ("obs_low", f64 * 6),
-                ("obs_high", f64 * 6), ("n_vehicles", i32), ("rescale", i32)]
+                ("obs_high", f64 * 6), ("n_vehicles", i32), ("rescale", i32), ("oob", vp)]
 
 
 class EVStepInfo(C.Structure):
@@ -161,7 +163,7 @@ class HSParams(C.Structure):
                 ("ev_unserved_penalty", f64), ("ev_obs_low", f64 * 7), ("ev_obs_high", f64 * 7),
                 ("ev_end_park", f64 * HS_MAX_VEHICLES), ("ev_req0", f64 * HS_MAX_VEHICLES),
                 ("dev_act_low", f64), ("dev_act_high", f64), ("dev_hours_per_step", f64),
-                ("dev_obs_high", f64 * HS_MAX_DEV), ("max_grid_power", f64)]
+                ("dev_obs_high", f64 * HS_MAX_DEV), ("max_grid_power", f64), ("oob", vp)]
 
 
 class HSStepInfo(C.Structure):

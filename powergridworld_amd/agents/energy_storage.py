@@ -6,7 +6,7 @@ import pandas as pd
 import torch
 
 from powergridworld_amd import _lib, spaces
-from powergridworld_amd.base import ComponentEnv, as_action, as_env_tensor, register_env
+from powergridworld_amd.base import ComponentEnv, as_action, as_env_tensor, oob_poll, register_env
 from powergridworld_amd.utils import maybe_rescale_box_space
 
 
@@ -47,6 +47,7 @@ class EnergyStorageEnv(ComponentEnv):
             eta_c=float(charge_efficiency), eta_d=float(discharge_efficiency),
             max_power=float(max_power), dt_h=float(self.control_interval_in_hr),
             rescale=int(bool(rescale_spaces)))
+        self._bind_oob(self.oob_count)
         self.soc = torch.zeros(self.num_envs, dtype=self.dtype, device=self.device)
         f32 = self.dtype == torch.float32
         self._k_reset = "pgw_battery_reset_f32" if f32 else "pgw_battery_reset"
@@ -88,6 +89,7 @@ class EnergyStorageEnv(ComponentEnv):
         """(:72-97) SoC ~ mean + std * truncnorm(-1, 1) unless init_storage is given
         (a scalar or one value per env)."""
         self.simulation_step = 0
+        oob_poll(self.oob_count)
         n = self.num_envs
         if init_storage is None:
             init = self._sample_initial_storage()

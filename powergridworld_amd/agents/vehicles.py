@@ -16,7 +16,7 @@ import pandas as pd
 import torch
 
 from powergridworld_amd import _lib, spaces
-from powergridworld_amd.base import ComponentEnv, as_action, register_env
+from powergridworld_amd.base import ComponentEnv, as_action, oob_poll, register_env
 from powergridworld_amd.utils import maybe_rescale_box_space
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
@@ -105,6 +105,7 @@ class EVChargingEnv(ComponentEnv):
         if num_vehicles > 64 * _lib.EV_MAX_WORDS:
             raise ValueError("at most %d vehicles" % (64 * _lib.EV_MAX_WORDS))
         self.params = p
+        self._bind_oob(self.oob_count)
         n, V = self.num_envs, self.num_vehicles
         self._words = (V + 63) // 64
         self.req = torch.zeros((max(V, 1), n), dtype=torch.float64, device=self.device)
@@ -247,6 +248,7 @@ class EVChargingEnv(ComponentEnv):
         self.time_index = 0
         self.time = self.simulation_times[0]
         self._prev_window = None
+        oob_poll(self.oob_count)
         if self.randomize:
             self._sample_vehicles(vehicle_ids)
             _lib.check(_lib.lib().pgw_ev_reset_tables(self.params, self.num_envs, _lib.dptr(self._req0_env),

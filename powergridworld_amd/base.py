@@ -62,6 +62,32 @@ def as_action(a, n, dim, device, dtype=torch.float64):
                      % (tuple(t.shape), n, dim))
 
 
+def oob_poll(counter):
+    """The reference warns on every out-of-bounds action (utils.py:35-37); the
+    kernels count them on the device instead (PGW_OOB).  Called at resets: logs
+    the count a previous call copied to pinned host memory, if that copy has
+    landed and the count grew, then starts the next asynchronous copy -- never
+    a synchronization, so a warning arrives one reset late."""
+    st = getattr(counter, "_pgw_oob", None)
+    if st is None:
+        st = {"host": torch.zeros(1, dtype=torch.int64).pin_memory(), "ev": None, "seen": 0}
+        counter._pgw_oob = st
+    ev = st["ev"]
+    if ev is not None:
+        if not ev.query():
+            return
+        st["ev"] = None
+        v = int(st["host"][0])
+        if v > st["seen"]:
+            logger.warning("argument out of bounds: %d action(s) outside [-1 - 1e-4, 1 + 1e-4] were "
+                           "clipped (counted on the device)", v - st["seen"])
+            st["seen"] = v
+    st["host"].copy_(counter, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(counter.device))
+    st["ev"] = ev
+
+
 class ComponentEnv(spaces.Env, ABC):
     """Base class for any environment used in the multiagent simulation
     (gridworld/base.py:12-71), batched over ``num_envs`` copies."""
@@ -92,6 +118,24 @@ class ComponentEnv(spaces.Env, ABC):
         self._zero_reward = torch.zeros(n, dtype=self.dtype, device=self.device)
         self._obs_labels = []
         self._in_multicomponent = False
+        # out-of-bounds actions (gridworld/utils.py:35-37; PGW_OOB in pgw.h): the
+        # kernels count every to_raw call the reference would have warned on
+        self.oob_count = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    # ---- out-of-bounds action counter -----------------------------------------
+    def _bind_oob(self, counter):
+        """Count this env's out-of-bounds actions into `counter` (a [1] int64
+        device tensor; a composite env hands its own to every component)."""
+        self.oob_count = counter
+        p = self.__dict__.get("params")
+        if p is not None and hasattr(p, "oob"):
+            p.oob = counter.data_ptr()
+
+    def oob_actions(self) -> torch.Tensor:
+        """Out-of-bounds actions clipped so far: the number of warnings the
+        reference's to_raw would have logged (one per env, component and step).
+        A device tensor -- reading its value synchronizes."""
+        return self.oob_count
 
     # ---- buffers ------------------------------------------------------------
     def _new_obs(self, dim):
@@ -195,6 +239,7 @@ class MultiComponentEnv(ComponentEnv):
                 raise NotImplementedError("MultiComponentEnv steps fp64 components only "
                                           "(component %s is %s)" % (env.name, env.dtype))
             self.envs.append(env)
+        self._bind_oob(self.oob_count)
         self.observation_space = spaces.Dict({e.name: e.observation_space for e in self.envs})
         self.action_space = spaces.Dict({e.name: e.action_space for e in self.envs})
         self._obs_labels_dict = {e.name: e.obs_labels for e in self.envs}
@@ -206,8 +251,14 @@ class MultiComponentEnv(ComponentEnv):
         if len(self.envs) > _lib.MAX_COMP:
             raise ValueError("at most %d components per agent" % _lib.MAX_COMP)
 
+    def _bind_oob(self, counter):
+        super()._bind_oob(counter)
+        for e in self.__dict__.get("envs", ()):
+            e._bind_oob(counter)
+
     def reset(self, **kwargs):
         """Resets each component and returns (obs dict, meta dict) (base.py:108-111)."""
+        oob_poll(self.oob_count)
         for e in self.envs:
             e.reset(**kwargs)
         self._real_power.zero_()

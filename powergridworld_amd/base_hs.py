@@ -23,7 +23,7 @@ import pandas as pd
 import torch
 
 from powergridworld_amd import _lib
-from powergridworld_amd.base import MultiComponentEnv, as_action, register_env
+from powergridworld_amd.base import MultiComponentEnv, as_action, oob_poll, register_env
 
 
 @register_env
@@ -106,6 +106,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
                 p.dev_obs_high[j] = dv.obs_high[j]
         p.max_grid_power = float(self.max_grid_power)
         self.params = p
+        self._bind_oob(self.oob_count)
 
         f64 = dict(dtype=torch.float64, device=dev)
         self._obs_buf = torch.zeros((self._obs_dim, n), **f64)
@@ -176,6 +177,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
     def reset(self, **kwargs):
         """base_hs.py:66-91: every component to row 0, the EV's action-less step."""
         self.time_index = 0
+        oob_poll(self.oob_count)
         self.meta_state["timestamp"] = self._timestamps[self.time_index]
         self.meta_state["grid_cost"] = self._grid_cost_data[self.time_index]
         self.meta_state["grid_power"] = self.max_grid_power

@@ -83,7 +83,17 @@ __device__ __forceinline__ double to_scaled(double x, double lo, double hi) {
   return (2.0 * x - (lo + hi)) / (hi - lo);
 }
 
-// gridworld/utils.py:27-43 (the out-of-range warning is not reproduced)
+// The reference's to_raw warning condition (utils.py:36): y outside
+// [-1 - eps, 1 + eps], NaN included.  oob_note counts one warning (PGW_OOB in
+// pgw.h): the atomic is taken only by the lanes that would have warned.
+__device__ __forceinline__ bool oob_bad(double y) {
+  return !(y >= -1.0 - PGW_OOB_EPS && y <= 1.0 + PGW_OOB_EPS);
+}
+__device__ __forceinline__ void oob_note(uint64_t* c, bool bad) {
+  if (c != nullptr && bad) atomicAdd(reinterpret_cast<unsigned long long*>(c), 1ull);
+}
+
+// gridworld/utils.py:27-43 (the warning: oob_bad / oob_note at the call sites)
 __device__ __forceinline__ double to_raw(double y, double lo, double hi) {
   y = clip(y, -1.0, 1.0);
   return (y * (hi - lo) + (hi + lo)) / 2.0;
@@ -115,7 +125,10 @@ __device__ __forceinline__ void st(const Mt& m, int64_t e, int j, double v) {
 template <class Div>
 __device__ __forceinline__ double battery_step_impl(const pgw_battery_params& p, double a, double& soc,
                                                     Div&& div) {
-  if (p.rescale) a = to_raw(a, -1.0, 1.0);
+  if (p.rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, -1.0, 1.0);
+  }
   double power = a * p.max_power;
   // validate_power :112-126 (the clamps omit the efficiencies, as in the reference)
   if (power > 0.0) {
@@ -159,7 +172,10 @@ __device__ __forceinline__ double pv_obs(const pgw_pv_params& p, double pmax) {
 }
 
 __device__ __forceinline__ double pv_real_power(const pgw_pv_params& p, double a, double pmax) {
-  if (p.rescale) a = to_raw(a, 0.0, 1.0);
+  if (p.rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, 0.0, 1.0);
+  }
   return a * (-pmax);
 }
 
@@ -347,9 +363,13 @@ __device__ __forceinline__ double bld_std_step(const pgw_building_params& B, con
                                                double (&av)[6], double (&xs)[5], double& reward,
                                                Store&& store) {
   double T[5];
+  bool bad = false;
 #pragma unroll
-  for (int j = 0; j < 6; ++j)   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
+  for (int j = 0; j < 6; ++j) {   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
+    bad = bad || oob_bad(av[j]);
     av[j] = B.rescale ? (clip_fast(av[j], -1.0, 1.0) * d.act_rng[j] + d.act_sum[j]) * 0.5 : av[j];
+  }
+  if (B.rescale) oob_note(B.oob, bad);
 #pragma unroll
   for (int z = 0; z < 5; ++z) T[z] = B.C[z] * xs[z] + B.mean[z];
 #pragma unroll

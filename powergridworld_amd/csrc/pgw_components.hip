@@ -144,11 +144,14 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
     return pc;
   }
   double a[6], xs[5], T[5];
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     double v = ld(act, e, j);
+    bad = bad || oob_bad(v);
     a[j] = p.rescale ? to_raw(v, p.act_low[j], p.act_high[j]) : v;
   }
+  if (p.rescale) oob_note(p.oob, bad);
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
     xs[z] = x[z * n + e];
@@ -217,7 +220,10 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
                                             const pgw_mat& obs, double* __restrict__ rp,
                                             double* __restrict__ rew) {
   double a = act.ptr ? ld(act, e, 0) : s.action_default;
-  if (p.rescale) a = to_raw(a, 0.0, 1.0);
+  if (p.rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, 0.0, 1.0);
+  }
   double kwh = a * p.rate * p.hours_per_step;
   double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
   int dcnt = 0, nact = 0;

@@ -32,7 +32,10 @@ __device__ __forceinline__ void hs_pv(const pgw_hs_params& p, const pgw_hs_step_
     M.pv = s.pv_avail;   // get_obs meta pv_power (:118-121)
     return;
   }
-  if (rescale) a = to_raw(a, p.pv_act_low, p.pv_act_high);
+  if (rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, p.pv_act_low, p.pv_act_high);
+  }
   rp = a * s.pv_avail;
   M.pv = rp;
 }
@@ -40,7 +43,10 @@ __device__ __forceinline__ void hs_pv(const pgw_hs_params& p, const pgw_hs_step_
 // HSEnergyStorageEnv.step (energy_storage_env_hs.py:189-270) incl. validate_power (:100-131)
 __device__ __forceinline__ void hs_storage(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
                                            double a, HSMeta& M, HSState& S, double& rp) {
-  if (rescale) a = to_raw(a, -1.0, 1.0);
+  if (rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, -1.0, 1.0);
+  }
   double power = a * p.max_power;
   if (power > 0.0) {
     double delta = power * p.dt_h / p.eta_d;
@@ -99,7 +105,10 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
                                       bool reset, double a, int64_t n, int64_t e, const pgw_hs_buffers& b,
                                       HSMeta& M, HSState& S, double& rp, double* ob) {
   if (reset) a = 0.0;                                   // _action_space.low
-  if (rescale) a = to_raw(a, 0.0, 1.0);
+  if (rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, 0.0, 1.0);
+  }
   const double kwh = a * p.ev_rate * p.ev_hours_per_step;
   uint64_t prev = reset ? 0ull : b.ev_charging[e], now = 0ull;
   double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
@@ -173,7 +182,10 @@ __device__ __forceinline__ void hs_devices(const pgw_hs_params& p, const pgw_hs_
                                            double* ob) {
   for (int c = 0; c < p.n_dev; ++c) ob[c] = rescale ? to_scaled(s.dev_obs[c], 0.0, p.dev_obs_high[c]) : s.dev_obs[c];
   if (reset) return;
-  if (rescale) a = to_raw(a, p.dev_act_low, p.dev_act_high);
+  if (rescale) {
+    oob_note(p.oob, oob_bad(a));
+    a = to_raw(a, p.dev_act_low, p.dev_act_high);
+  }
   double sum = 0.0;
   for (int c = 0; c < p.n_dev; ++c) sum = sum + s.dev_power[c];
   rp = a * sum;

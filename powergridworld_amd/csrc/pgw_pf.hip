@@ -585,11 +585,14 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents(pgw_coord_params p, pgw
     if (comp == 0) {
       // building: five_zone_rom_env.py:183-225
       double av[6], xs[5], T[5];
+      bool bad = false;
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const double v = ld(act, e, p.act_bld + j);
+        bad = bad || oob_bad(v);
         av[j] = p.bld.rescale ? to_raw(v, p.bld.act_low[j], p.bld.act_high[j]) : v;
       }
+      if (p.bld.rescale) oob_note(p.bld.oob, bad);
       double* xp = b.x + (int64_t)a * 5 * n;
 #pragma unroll
       for (int z = 0; z < 5; ++z) {
@@ -684,10 +687,14 @@ __device__ __forceinline__ void std_agent_compute(const pgw_coord_params& p, con
   // ---- building
 #pragma unroll
   for (int q = 0; q < E; ++q) {
+    bool bad = false;
 #pragma unroll
-    for (int j = 0; j < 6; ++j)   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
+    for (int j = 0; j < 6; ++j) {   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
+      bad = bad || oob_bad(in[q].av[j]);
       in[q].av[j] = B.rescale ? (clip_fast(in[q].av[j], -1.0, 1.0) * dv.act_rng[j] + dv.act_sum[j]) * 0.5
                               : in[q].av[j];
+    }
+    if (B.rescale) oob_note(B.oob, bad);
 #pragma unroll
     for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
   }
