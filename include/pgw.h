@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 12
+#define PGW_ABI_VERSION 13
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -594,10 +594,30 @@ typedef struct pgw_hs_step_info {
   uint64_t ev_window;              /* bit v: start_v <= ev_time <= end_park_v  */
 } pgw_hs_step_info;
 
+/* Per-device step_meta records (base_hs.py:133-164 collects one dict per
+ * chain slot: pv_profile_env_hs.py:151-170, energy_storage_env_hs.py:180-185,
+ * 257-265, ev_charging_env_hs.py:172-180, 316-320, devices_env_hs.py:129-137,
+ * 195-199).  Numeric fields, each an n-vector at
+ * step_meta[(slot * PGW_HS_META_FIELDS + field) * n + e]:
+ *   0 cost, 1 reward (the component's own, with the meta_state of its step),
+ *   2 action (raw, after to_raw), 3 solar_power_consumed,
+ *   4 es_power_consumed, 5 grid_power_consumed,
+ *   6.. device_custom_info in the reference's key order:
+ *     PV       pv_available_power, pv_actionable_power
+ *     storage  current_storage, power_ask, solar_power_available,
+ *              grid_power_available, es_power_available
+ *     EV       power_ask, power_unserved, charging_vehicle, vehicle_charged,
+ *              solar_power_available, es_power_available, grid_power_available
+ *     devices  power_ask, solar_power_available, es_power_available,
+ *              grid_power_available
+ * (device_id and timestamp are host strings).  Unused fields are not written. */
+#define PGW_HS_META_FIELDS 13
+
 /* Per-env state and outputs (device).  action: n x n_comp, column = chain
  * slot.  obs: n x obs_dim.  ev_req: n_veh x n.  es_power_last: the house's
  * meta_state es_power, which survives into the next reset's EV step.
- * meta_out (nullable): 3 x n final pv_power, es_power, grid_power. */
+ * meta_out (nullable): 3 x n final pv_power, es_power, grid_power.
+ * step_meta (nullable, step only): n_comp x PGW_HS_META_FIELDS x n records. */
 typedef struct pgw_hs_buffers {
   pgw_mat action;
   pgw_mat obs;
@@ -611,6 +631,7 @@ typedef struct pgw_hs_buffers {
   double* reward;
   double* real_power;
   double* meta_out;
+  double* step_meta;
 } pgw_hs_buffers;
 
 /* reset (base_hs.py:66-91): PV and devices at row 0, storage SoC := clip(

@@ -559,7 +559,7 @@ def gen_hs():
     runs = []
     for k in range(K):
         env = HSMultiComponentEnv(**copy.deepcopy(cfg))
-        rec = dict(obs=[], act=[], rew=[], rp=[], done=[], meta=[], soc=[])
+        rec = dict(obs=[], act=[], rew=[], rp=[], done=[], meta=[], soc=[], smeta=[], sts=[])
         for ep in range(EPISODES):
             with quiet():
                 o = env.reset()
@@ -580,6 +580,19 @@ def gen_hs():
                 rec["rp"].append(float(env.real_power))
                 rec["done"].append(bool(d))
                 rec["meta"].append([m["pv_power"], m["es_power"], m["grid_power"]])
+                # the per-device step_meta records (base_hs.py:133-164), numeric fields
+                # in the reference's key order, custom-info keys recorded once
+                sm = np.full((len(names), HS_META_FIELDS), np.nan)
+                assert [r["device_id"] for r in m["step_meta"]] == names
+                for c, r in enumerate(m["step_meta"]):
+                    assert r["timestamp"] == m["timestamp"]
+                    vals = [r["cost"], r["reward"], r["action"][0], r["solar_power_consumed"],
+                            r["es_power_consumed"], r["grid_power_consumed"]]
+                    vals += list(r["device_custom_info"].values())
+                    sm[c, :len(vals)] = vals
+                    HS_CUSTOM_KEYS[c] = list(r["device_custom_info"].keys())
+                rec["smeta"].append(sm)
+                rec["sts"].append(str(m["timestamp"]))
                 rec["soc"].append(env.env_dict["storage"].current_storage)
                 if d:
                     break
@@ -587,9 +600,16 @@ def gen_hs():
     T = len(runs[0]["rew"])
     assert all(len(r["rew"]) == T for r in runs)
     stack = lambda key: np.stack([np.asarray(r[key], dtype=np.float64) for r in runs], 1)
+    assert all(r["sts"] == runs[0]["sts"] for r in runs)
     _save("hs_scenario", names=np.array(names), actions=stack("act"), obs=stack("obs"),
           reward=stack("rew"), real_power=stack("rp"), done=stack("done").astype(bool),
-          meta=stack("meta"), soc=stack("soc"), episodes=np.array(EPISODES))
+          meta=stack("meta"), soc=stack("soc"), episodes=np.array(EPISODES),
+          step_meta=stack("smeta"), step_meta_timestamp=np.array(runs[0]["sts"]),
+          step_meta_custom_keys=np.array([",".join(HS_CUSTOM_KEYS[c]) for c in range(len(names))]))
+
+
+HS_META_FIELDS = 13
+HS_CUSTOM_KEYS = {}
 
 
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,

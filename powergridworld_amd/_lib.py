@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -175,7 +175,7 @@ class HSStepInfo(C.Structure):
 class HSBuffers(C.Structure):
     _fields_ = [("action", Mat), ("obs", Mat), ("soc", vp), ("soc_cost", vp), ("ev_req", vp),
                 ("ev_charging", vp), ("ev_cost", vp), ("dev_cost", vp), ("es_power_last", vp),
-                ("reward", vp), ("real_power", vp), ("meta_out", vp)]
+                ("reward", vp), ("real_power", vp), ("meta_out", vp), ("step_meta", vp)]
 
 
 PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE = 1, 2, 3

@@ -26,14 +26,35 @@ from powergridworld_amd import _lib
 from powergridworld_amd.base import MultiComponentEnv, as_action, oob_poll, register_env
 
 
+# device_custom_info keys of each HS kind's step_meta record, in the reference's
+# order (PGW_HS_META_FIELDS, include/pgw.h): fields 6.. of the record
+HS_CUSTOM_INFO = {
+    0: ("pv_available_power", "pv_actionable_power"),                         # pv_profile_env_hs.py:155
+    1: ("current_storage", "power_ask", "solar_power_available", "grid_power_available",
+        "es_power_available"),                                                # energy_storage_env_hs.py:261
+    2: ("power_ask", "power_unserved", "charging_vehicle", "vehicle_charged", "solar_power_available",
+        "es_power_available", "grid_power_available"),                        # ev_charging_env_hs.py:320
+    3: ("power_ask", "solar_power_available", "es_power_available", "grid_power_available"),  # devices :199
+}
+HS_META_FIELDS = 13
+HS_COMMON_FIELDS = ("cost", "reward", "action", "solar_power_consumed", "es_power_consumed",
+                    "grid_power_consumed")
+
+
 @register_env
 class HSMultiComponentEnv(MultiComponentEnv):
+    """step_meta=True (default, as the reference): meta["step_meta"] is the
+    per-device record list base_hs.py:133-164 builds, one dict per chain slot
+    with the reference's keys; every numeric entry is an [N] device tensor (a
+    view of the kernel's record buffer, overwritten by the next step; `action`
+    is the raw action, where the reference holds a one-element list)."""
 
     def __init__(self, name: str = None, components: List[dict] = None, start_time: str = "",
                  end_time: str = "", control_timedelta=pd.Timedelta(300, "s"), max_grid_power: float = 48,
                  max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
-                 device=None, **kwargs):
+                 device=None, step_meta: bool = True, **kwargs):
         self.max_grid_power = max_grid_power
+        self._want_step_meta = bool(step_meta)
         super().__init__(name=name, components=components, num_envs=num_envs, device=device)
         from powergridworld_amd.agents.hs import _HSComponent
         self.rescale_spaces = rescale_spaces
@@ -132,6 +153,16 @@ class HSMultiComponentEnv(MultiComponentEnv):
         b.es_power_last = self._es_last.data_ptr()
         b.reward, b.real_power = self._reward.data_ptr(), self._real_power.data_ptr()
         b.meta_out = self._meta.data_ptr()
+        self._step_meta = None
+        if self._want_step_meta:
+            self._rec_buf = torch.zeros((len(self.envs), HS_META_FIELDS, n), **f64)
+            b.step_meta = self._rec_buf.data_ptr()
+            self._step_meta = []
+            for c, (k, e) in enumerate(zip(self._kinds, self.envs)):
+                r = {"device_id": e.name, "timestamp": None}
+                r.update({f: self._rec_buf[c, j] for j, f in enumerate(HS_COMMON_FIELDS)})
+                r["device_custom_info"] = {f: self._rec_buf[c, 6 + j] for j, f in enumerate(HS_CUSTOM_INFO[k])}
+                self._step_meta.append(r)
         self._bufs = b
         self._keep = (st_soc, st_cost)
         self._act_key = None
@@ -262,6 +293,10 @@ class HSMultiComponentEnv(MultiComponentEnv):
         meta = dict(self.meta_state)
         meta.update(pv_power=self._meta[0], es_power=self._meta[1], grid_power=self._meta[2],
                     es_cost=0)
+        if self._step_meta is not None:
+            for r in self._step_meta:
+                r["timestamp"] = meta["timestamp"]
+            meta["step_meta"] = self._step_meta
         obs = {e.name: e._obs for e in self.envs}
         return obs, self._reward, any(dones), meta
 

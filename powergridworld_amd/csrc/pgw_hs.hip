@@ -23,10 +23,25 @@ struct HSState {
   double rew_ev, rew_dev;
 };
 
+// One chain slot's step_meta record (PGW_HS_META_FIELDS in pgw.h); off = NULL.
+struct HSRec {
+  double* p;
+  int64_t n, e;
+  __device__ __forceinline__ void put(int f, double v) const {
+    if (p) p[(int64_t)f * n + e] = v;
+  }
+  // cost, reward, action, solar / es / grid power consumed
+  __device__ __forceinline__ void common(double cost, double rew, double a, double sc, double bc,
+                                         double gc) const {
+    put(0, cost); put(1, rew); put(2, a); put(3, sc); put(4, bc); put(5, gc);
+  }
+};
+
 // HSPVEnv (pv_profile_env_hs.py:96-160): obs before the advance; the curtailed
 // power a * data[index] becomes meta_state pv_power (rew_meta, :146).
 __device__ __forceinline__ void hs_pv(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
-                                      bool reset, double a, HSMeta& M, double& rp, double* ob) {
+                                      bool reset, double a, HSMeta& M, double& rp, double* ob,
+                                      const HSRec& R) {
   ob[0] = rescale ? to_scaled(-s.pv_avail, p.pv_obs_low, 0.0) : -s.pv_avail;
   if (reset) {
     M.pv = s.pv_avail;   // get_obs meta pv_power (:118-121)
@@ -38,11 +53,19 @@ __device__ __forceinline__ void hs_pv(const pgw_hs_params& p, const pgw_hs_step_
   }
   rp = a * s.pv_avail;
   M.pv = rp;
+  R.common(0.0, 0.0, a, s.pv_avail, 0.0, 0.0);   // :151-155, 162-170
+  R.put(6, s.pv_avail);
+  R.put(7, rp);
 }
 
 // HSEnergyStorageEnv.step (energy_storage_env_hs.py:189-270) incl. validate_power (:100-131)
+__device__ __forceinline__ double hs_storage_reward(const pgw_hs_params& p, const HSMeta& M, const HSState& S,
+                                                    double rp, double* cost_out = nullptr);
+
 __device__ __forceinline__ void hs_storage(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
-                                           double a, HSMeta& M, HSState& S, double& rp) {
+                                           double a, HSMeta& M, HSState& S, double& rp, const HSRec& R) {
+  const double pv_cap = M.pv, grid_cap = M.grid;
+  double sc = 0.0, gc = 0.0;
   if (rescale) {
     oob_note(p.oob, oob_bad(a));
     a = to_raw(a, -1.0, 1.0);
@@ -71,8 +94,8 @@ __device__ __forceinline__ void hs_storage(const pgw_hs_params& p, const pgw_hs_
   } else if (power < 0.0) {
     // charging: PV first, then the grid; weighted cost of the charge (:213-236)
     const double dS = p.eta_c * power * p.dt_h;
-    const double sc = pymin(-power, M.pv);
-    const double gc = pymin(M.grid, -power - sc);
+    sc = pymin(-power, M.pv);
+    gc = pymin(M.grid, -power - sc);
     S.delta_cost = (0.0 * sc + s.grid_cost * gc) / (sc + gc);
     S.soc_cost = (S.soc * S.soc_cost - dS * S.delta_cost) / (S.soc - dS);
     S.soc = S.soc - dS;
@@ -86,13 +109,24 @@ __device__ __forceinline__ void hs_storage(const pgw_hs_params& p, const pgw_hs_
     M.es = power;
   }
   rp = -power;
+  if (R.p) {   // the step's own step_reward, with the meta_state it leaves (:254-265)
+    double cost;
+    const double rew = hs_storage_reward(p, M, S, rp, &cost);
+    R.common(cost, rew, a, sc, 0.0, gc);
+    R.put(6, S.soc);
+    R.put(7, power);
+    R.put(8, pv_cap - sc);
+    R.put(9, grid_cap - gc);
+    R.put(10, M.es);
+  }
 }
 
 // the storage's step_reward, evaluated by the house with the FINAL meta_state
 // (base_hs.py:163 -> energy_storage_env_hs.py:156-187)
 __device__ __forceinline__ double hs_storage_reward(const pgw_hs_params& p, const HSMeta& M, const HSState& S,
-                                                    double rp) {
+                                                    double rp, double* cost_out) {
   const double cost = (rp < 0.0) ? 0.0 : S.delta_cost * p.eta_c * rp * p.dt_h;
+  if (cost_out) *cost_out = cost;
   double r = -cost;
   if (M.pv > 0.0 && M.es > 0.0 && S.soc < p.soc_max) r = r - p.max_storage_cost * (p.soc_max - S.soc);
   return r;
@@ -103,7 +137,7 @@ __device__ __forceinline__ double hs_storage_reward(const pgw_hs_params& p, cons
 // the reference's set iteration of small ints.
 __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
                                       bool reset, double a, int64_t n, int64_t e, const pgw_hs_buffers& b,
-                                      HSMeta& M, HSState& S, double& rp, double* ob) {
+                                      HSMeta& M, HSState& S, double& rp, double* ob, const HSRec& R) {
   if (reset) a = 0.0;                                   // _action_space.low
   if (rescale) {
     oob_note(p.oob, oob_bad(a));
@@ -112,7 +146,7 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
   const double kwh = a * p.ev_rate * p.ev_hours_per_step;
   uint64_t prev = reset ? 0ull : b.ev_charging[e], now = 0ull;
   double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
-  int nact = 0, dcnt = 0;
+  int nact = 0, dcnt = 0, ndep = 0;
   for (int v = 0; v < p.n_veh; ++v) {
     double* rq = b.ev_req + (int64_t)v * n + e;
     const double r = reset ? p.ev_req0[v] : *rq;
@@ -132,6 +166,7 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
       }
     } else if ((prev >> v) & 1ull) {
       unserved = unserved + r;                          // departed (:260-263)
+      ++ndep;
     }
     *rq = r_new;
   }
@@ -145,12 +180,13 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
   st[5] = unserved;
   rp = p.ev_mult * consumed;
   const double power = rp * p.ev_steps_per_hour;
+  const double pv_cap = M.pv, es_cap = M.es, grid_cap = M.grid;
+  double sc = 0.0, bc = 0.0, gc = 0.0;
   if (power == 0.0 || a == 0.0) {
     S.ev_cost = 0.0;
   } else {
     // PV first, then the battery or the grid, whichever is cheaper (:285-313)
-    const double sc = pymin(power, M.pv);
-    double bc, gc;
+    sc = pymin(power, M.pv);
     if (0.0 < s.grid_cost) {
       bc = pymin(M.es, power - sc);
       gc = pymin(M.grid, power - sc - bc);
@@ -171,7 +207,16 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
 #pragma unroll
   for (int j = 0; j < 7; ++j) ob[j] = rescale ? to_scaled(st[j], p.ev_obs_low[j], p.ev_obs_high[j]) : st[j];
   // step_reward (:167-180)
-  S.rew_ev = -(S.ev_cost * rp + p.ev_unserved_penalty * (unserved * unserved));
+  const double cost = S.ev_cost * rp;
+  S.rew_ev = -(cost + p.ev_unserved_penalty * (unserved * unserved));
+  R.common(cost, S.rew_ev, a, sc, bc, gc);            // :316-320
+  R.put(6, power);
+  R.put(7, unserved);
+  R.put(8, (double)nact);
+  R.put(9, (double)ndep);
+  R.put(10, pv_cap - sc);
+  R.put(11, es_cap - bc);
+  R.put(12, grid_cap - gc);
 }
 
 // HSDevicesEnv.step (devices_env_hs.py:147-205).  Its draws on the resources
@@ -179,7 +224,7 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
 // never reach meta_state.
 __device__ __forceinline__ void hs_devices(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
                                            bool reset, double a, const HSMeta& M, HSState& S, double& rp,
-                                           double* ob) {
+                                           double* ob, const HSRec& R) {
   for (int c = 0; c < p.n_dev; ++c) ob[c] = rescale ? to_scaled(s.dev_obs[c], 0.0, p.dev_obs_high[c]) : s.dev_obs[c];
   if (reset) return;
   if (rescale) {
@@ -189,15 +234,22 @@ __device__ __forceinline__ void hs_devices(const pgw_hs_params& p, const pgw_hs_
   double sum = 0.0;
   for (int c = 0; c < p.n_dev; ++c) sum = sum + s.dev_power[c];
   rp = a * sum;
+  double sc = 0.0, bc = 0.0, gc = 0.0;
   if (fabs(rp) < 0.0005) {                 // round(rp, 3) == 0.0
     S.dev_cost = 0.0;
   } else {
-    const double sc = pymin(rp, M.pv);
-    const double bc = pymin(M.es, rp - sc);
-    const double gc = pymin(M.grid, rp - sc - bc);
+    sc = pymin(rp, M.pv);
+    bc = pymin(M.es, rp - sc);
+    gc = pymin(M.grid, rp - sc - bc);
     S.dev_cost = (0.0 * sc + s.grid_cost * gc + 0.0 * bc) / (sc + gc + bc);
   }
-  S.rew_dev = -(S.dev_cost * rp * p.dev_hours_per_step);
+  const double cost = S.dev_cost * rp * p.dev_hours_per_step;
+  S.rew_dev = -cost;
+  R.common(cost, S.rew_dev, a, sc, bc, gc);           // :194-199
+  R.put(6, rp);
+  R.put(7, M.pv - sc);
+  R.put(8, M.es - bc);
+  R.put(9, M.grid - gc);
 }
 
 __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p, pgw_hs_step_info s, int64_t n,
@@ -217,16 +269,17 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p, pgw_hs_step_info
   int slot_storage = -1;
   for (int c = 0; c < p.n_comp; ++c) {
     const double a = reset ? 0.0 : ld(b.action, e, c);
+    const HSRec R = {(!reset && b.step_meta) ? b.step_meta + (int64_t)c * PGW_HS_META_FIELDS * n : nullptr, n, e};
     double ob[8];
     int dim = 0;
     S.rp[c] = 0.0;
     switch (p.kind[c]) {
       case PGW_HS_PV:
-        hs_pv(p, s, p.rescale[c], reset, a, M, S.rp[c], ob);
+        hs_pv(p, s, p.rescale[c], reset, a, M, S.rp[c], ob, R);
         dim = 1;
         break;
       case PGW_HS_STORAGE:
-        if (!reset) hs_storage(p, s, p.rescale[c], a, M, S, S.rp[c]);
+        if (!reset) hs_storage(p, s, p.rescale[c], a, M, S, S.rp[c], R);
         slot_storage = c;
         ob[0] = S.soc;
         ob[1] = S.soc_cost;
@@ -237,11 +290,11 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p, pgw_hs_step_info
         dim = 2;
         break;
       case PGW_HS_EV:
-        hs_ev(p, s, p.rescale[c], reset, a, n, e, b, M, S, S.rp[c], ob);
+        hs_ev(p, s, p.rescale[c], reset, a, n, e, b, M, S, S.rp[c], ob, R);
         dim = 7;
         break;
       default:
-        hs_devices(p, s, p.rescale[c], reset, a, M, S, S.rp[c], ob);
+        hs_devices(p, s, p.rescale[c], reset, a, M, S, S.rp[c], ob, R);
         dim = p.n_dev;
         break;
     }

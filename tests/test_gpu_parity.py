@@ -483,7 +483,7 @@ def test_heterogeneous_scenario_golden():
 
 
 # ------------------------------------------------------------------ Home-Steward house
-def _hs_run(env, g, names, n_rep=1):
+def _hs_run(env, g, names, n_rep=1, meta_every=1):
     """Step `env` (batch K * n_rep, golden actions tiled) through the golden's
     two episodes; compare obs, reward, real power, done, meta and SoC."""
     A, O = g["actions"], g["obs"]
@@ -506,12 +506,30 @@ def _hs_run(env, g, names, n_rep=1):
             close(torch.stack([m["pv_power"], m["es_power"], m["grid_power"]], 1), tile(g["meta"][t_obs]),
                   1e-12, 1e-12)
             close(env.env_dict["storage"].current_storage, tile(g["soc"][t_obs]), 1e-12, 1e-12)
+            if t_act % meta_every == 0:
+                _hs_step_meta(m, g, t_act, names, tile)
             assert d == bool(g["done"][t_act, 0])
             t_obs += 1
             t_act += 1
             if d:
                 break
     assert t_act == A.shape[0] and sum(dims) == O.shape[2]
+
+
+def _hs_step_meta(m, g, t, names, tile):
+    """meta["step_meta"] (base_hs.py:133-164) against the reference's records:
+    device ids, timestamp, custom-info keys and every numeric field."""
+    from powergridworld_amd.base_hs import HS_COMMON_FIELDS
+    recs = m["step_meta"]
+    assert [r["device_id"] for r in recs] == names
+    want = tile(g["step_meta"][t])                    # [N, n_comp, 13]
+    for c, r in enumerate(recs):
+        assert r["timestamp"] == str(g["step_meta_timestamp"][t])
+        keys = str(g["step_meta_custom_keys"][c]).split(",")
+        assert list(r["device_custom_info"]) == keys
+        got = [r[f] for f in HS_COMMON_FIELDS] + [r["device_custom_info"][k] for k in keys]
+        close(torch.stack(got, 1), want[:, c, :len(got)], 1e-12, 1e-12)
+        assert np.isnan(want[:, c, len(got):]).all()
 
 
 def test_hs_house_golden_two_episodes():
@@ -538,7 +556,7 @@ def test_hs_house_full_batch_tiled():
     names = [str(x) for x in g["names"]]
     K = g["actions"].shape[1]
     env = HSMultiComponentEnv(**make_env_config(), num_envs=65536, device=DEV)
-    _hs_run(env, g, names, n_rep=65536 // K)
+    _hs_run(env, g, names, n_rep=65536 // K, meta_every=37)
 
 
 # ------------------------------------------------------------------ list interface
