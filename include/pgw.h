@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 13
+#define PGW_ABI_VERSION 14
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -406,7 +406,10 @@ int32_t pgw_stream_copy(const void* src, void* dst, int64_t bytes, int32_t reps,
  * Host-side feeder construction (C++, no GPU): the native stand-in for the
  * OpenDSS model build behind opendss.py:36-51.
  * ---------------------------------------------------------------------- */
-enum { PGW_ELEM_LINE = 1, PGW_ELEM_XFMR = 2, PGW_ELEM_VSOURCE = 3 };
+/* PGW_ELEM_SHUNT: a constant admittance per phase, y_p = r[p] + j x[p] (siemens),
+ * between node1[p] and node2[p] (-1 = ground): capacitors and constant-Z
+ * (model 2) loads. */
+enum { PGW_ELEM_LINE = 1, PGW_ELEM_XFMR = 2, PGW_ELEM_VSOURCE = 3, PGW_ELEM_SHUNT = 4 };
 
 typedef struct pgw_feeder_elem {
   int32_t kind;          /* PGW_ELEM_*                                     */
@@ -418,6 +421,7 @@ typedef struct pgw_feeder_elem {
   double length;         /* line: length in the matrices' unit            */
   double freq;           /* Hz                                            */
   double kv1, kv2, kva, pct_r1, pct_r2, xhl;       /* transformer          */
+  double tap1, tap2;     /* transformer winding taps (pu of kv, 0 = 1.0)  */
   double basekv, pu, angle, mvasc3, mvasc1, x1r1, x0r0;  /* vsource        */
 } pgw_feeder_elem;
 

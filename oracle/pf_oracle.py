@@ -12,9 +12,11 @@ models the reference's call sites rely on:
   looked up by LOAD NAME; snap solve; per-node |V| in pu (``:156-165``);
 * ``get_bus_voltage_by_name`` (``opendss.py:173-186``): 'xxxc' -> 'xxx.3';
 * OpenDSS element models: Vsource (Thevenin from MVAsc3/MVAsc1, X1/R1=4,
-  X0/R0=3), 2-winding transformers (leakage %r1+%r2 + jXHL, wye/delta),
-  lines (R/X/C matrices x length, C split half/half), PQ loads (model 1:
-  constant PQ inside [Vminpu, Vmaxpu], constant Z outside, Vlowpu floor).
+  X0/R0=3), 2-winding transformers (leakage %r1+%r2 + jXHL, wye/delta,
+  winding taps), lines (R/X/C matrices x length, C split half/half),
+  capacitors and constant-Z (model 2) loads as fixed shunt admittances, PQ
+  loads (model 1: constant PQ inside [Vminpu, Vmaxpu], constant Z outside,
+  Vlowpu floor).
 
 Solve: nodal admittance Y (no loads) -> Z = Y^-1, no-load voltages V0 =
 Z I_src; the load-element voltages U obey U = U0 + W f(U) with W = -C Z C^T
@@ -85,6 +87,9 @@ class Feeder:
         for ld in spec["loads"]:
             b, nds = _bus(ld["bus1"], [1, 2, 3][:ld["phases"]])
             touch(b, nds)
+        for cap in spec.get("capacitors", []):
+            b, nds = _bus(cap["bus1"], [1, 2, 3][:cap["phases"]])
+            touch(b, nds)
         for ln in spec["lines"]:
             for key in ("bus1", "bus2"):
                 b, nds = _bus(ln[key], [1, 2, 3][:ln["phases"]])
@@ -144,6 +149,7 @@ class Feeder:
             b2, n2 = _bus(w2["bus"], [1, 2, 3][:ph])
             vw1 = w1["kv"] * 1000 / (math.sqrt(3) if (w1["conn"] == "wye" and ph == 3) else 1.0)
             vw2 = w2["kv"] * 1000 / (math.sqrt(3) if (w2["conn"] == "wye" and ph == 3) else 1.0)
+            vw1, vw2 = vw1 * w1.get("tap", 1.0), vw2 * w2.get("tap", 1.0)      # taps: turns ratio
             kva_ph = w1["kva"] * 1000 / ph
             zpu = complex((w1["pct_r"] + w2["pct_r"]) / 100.0, t["xhl"] / 100.0)
             y = 1.0 / (zpu * vw1 * vw1 / kva_ph)
@@ -188,6 +194,20 @@ class Feeder:
             nodes = [self.node(b1, k) for k in n1] + [self.node(b2, k) for k in n2]
             yp = np.block([[Yser + Yc / 2, -Yser], [-Yser, Yser + Yc / 2]])
             self._stamp(nodes, yp)
+        # --- shunts: capacitors (+jQ/V^2) and constant-Z loads (model 2: (P - jQ)/V^2)
+        sh = [(c, 1j * c["kvar"] * 1000 / c["phases"]) for c in spec.get("capacitors", [])]
+        sh += [(ld, (ld["kw"] - 1j * ld["kvar"]) * 1000 / ld["phases"]) for ld in spec["loads"]
+               if ld.get("model", 1) == 2]
+        for obj, s in sh:
+            ph = obj["phases"]
+            b, nds = _bus(obj["bus1"], [1, 2, 3][:ph])
+            delta = obj.get("conn", "wye") == "delta"
+            v = obj["kv"] * 1000 / (math.sqrt(3) if (not delta and ph >= 2) else 1.0)
+            y = s / (v * v)
+            for p in range(ph):
+                hi = self.node(b, nds[p])
+                lo = (self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])) if delta else -1
+                self._stamp([hi, lo], np.array([[y, -y], [-y, y]]))
         self.Z = _accurate_inverse(self.Y)
         self.V0 = (self.Z.astype(np.clongdouble) @ self.I_src.astype(np.clongdouble)).astype(complex)
 
@@ -207,6 +227,9 @@ class Feeder:
         self.elem_p, self.elem_q, self.elem_vbase, self.elem_load, self.elem_nph = [], [], [], [], []
         self.load_vmin, self.load_vmax, self.load_vlow = [], [], []
         for li, ld in enumerate(self.spec["loads"]):
+            if ld.get("model", 1) != 1:    # model 2: a shunt in Y (the reference re-sets model 1 only)
+                self.load_vmin.append(0.95); self.load_vmax.append(1.05); self.load_vlow.append(0.5)
+                continue
             ph = ld["phases"]
             b, nds = _bus(ld["bus1"], [1, 2, 3][:ph])
             for p in range(ph):
@@ -216,7 +239,7 @@ class Feeder:
                     vb = ld["kv"] * 1000
                 else:
                     lo = -1
-                    vb = ld["kv"] * 1000 / (math.sqrt(3) if ph == 3 else 1.0)
+                    vb = ld["kv"] * 1000 / (math.sqrt(3) if ph >= 2 else 1.0)
                 self.elem_p.append(hi); self.elem_q.append(lo); self.elem_vbase.append(vb)
                 self.elem_load.append(li); self.elem_nph.append(ph)
             self.load_vmin.append(ld.get("vminpu", 0.95)); self.load_vmax.append(ld.get("vmaxpu", 1.05))

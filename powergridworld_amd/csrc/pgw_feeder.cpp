@@ -13,7 +13,10 @@
 //            on the kVA base, winding voltages kV/sqrt3 (3-phase wye) or kV
 //            (delta); per phase  Yw = y [[1, -t], [-t, t^2]], t = Vw1/Vw2;
 //            delta windings span phase p -> p+1.
+//            Taps scale the winding voltages: t = (Vw1 tap1)/(Vw2 tap2), and the
+//            leakage impedance is referred to winding 1 at Vw1 tap1.
 //   Line     Z = (R + jX) len,  Yc = j 2 pi f C 1e-9 len, split half/half.
+//   Shunt    a constant admittance per phase (capacitor, constant-Z load).
 #include <cmath>
 #include <complex>
 #include <cstdarg>
@@ -138,9 +141,10 @@ bool add_transformer(Builder& B, const pgw_feeder_elem& e) {
   const double vw1 = e.kv1 * 1000.0 / ((e.conn1 == 0 && ph == 3) ? s3 : 1.0);
   const double vw2 = e.kv2 * 1000.0 / ((e.conn2 == 0 && ph == 3) ? s3 : 1.0);
   const double kva_ph = e.kva * 1000.0 / ph;
+  const double v1 = vw1 * (e.tap1 != 0.0 ? e.tap1 : 1.0), v2 = vw2 * (e.tap2 != 0.0 ? e.tap2 : 1.0);
   const cplx zpu((e.pct_r1 + e.pct_r2) / 100.0, e.xhl / 100.0);
-  const cplx y = 1.0 / (zpu * (vw1 * vw1 / kva_ph));
-  const double t = vw1 / vw2;
+  const cplx y = 1.0 / (zpu * (v1 * v1 / kva_ph));
+  const double t = v1 / v2;
   const cplx yw[4] = {y, -t * y, -t * y, t * t * y};
   for (int p = 0; p < ph; ++p) {
     // terminal list: [w1 hi, w1 lo, w2 hi, w2 lo]; winding voltage = hi - lo
@@ -181,6 +185,15 @@ bool add_line(Builder& B, const pgw_feeder_elem& e) {
   for (int p = 0; p < ph; ++p) nodes.push_back(e.node1[p]);
   for (int p = 0; p < ph; ++p) nodes.push_back(e.node2[p]);
   return B.stamp(nodes, yp);
+}
+
+bool add_shunt(Builder& B, const pgw_feeder_elem& e) {
+  for (int p = 0; p < e.nphases; ++p) {
+    const cplx y(e.r[p], e.x[p]);
+    const Mat yp = {y, -y, -y, y};
+    if (!B.stamp({e.node1[p], e.node2[p]}, yp)) return false;
+  }
+  return true;
 }
 
 void put(double* dst, const cplx* src, size_t count) {
@@ -230,6 +243,7 @@ int32_t pgw_feeder_build(const pgw_feeder_elem* elems, int32_t n_elems, int32_t 
         case PGW_ELEM_VSOURCE: ok = add_vsource(B, e); break;
         case PGW_ELEM_XFMR: ok = add_transformer(B, e); break;
         case PGW_ELEM_LINE: ok = add_line(B, e); break;
+        case PGW_ELEM_SHUNT: ok = add_shunt(B, e); break;
         default: ok = false;
       }
       if (!ok) {

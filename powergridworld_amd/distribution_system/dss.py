@@ -8,11 +8,17 @@ admittance matrix natively (``csrc/pgw_feeder.cpp``).
 
 Supported: comments (``!``, ``//``, ``/* */``), ``~``/``more`` continuation,
 ``Clear``, ``Set``, ``New``/``Edit`` for ``circuit``/``vsource``,
-``transformer`` (2 windings, ``wdg=k`` positional blocks), ``linecode``,
-``line`` (linecode or r1/x1/r0/x0/c1/c0, ``Switch=y``) and ``load``;
-``Redirect`` of further files; in-line RPN ``(8 1000 /)``; lower-triangular
-matrices ``(a | b c | ...)``.  Other commands (``calcv``, ``Solve``,
-``BusCoords``, ``Show``) are ignored, ``Set Voltagebases`` is kept.
+``transformer`` (2 windings; ``wdg=k`` positional blocks or the array forms
+``buses= conns= kvs= kvas= taps= %rs=``, ``tap=``, ``%loadloss=``; 1-phase
+units, e.g. the IEEE-13 voltage regulators at fixed taps), ``linecode``,
+``line`` (linecode or r1/x1/r0/x0/c1/c0, ``Switch=y``), ``load`` and
+``capacitor``; ``RegControl`` is recorded (automatic tap control is not
+simulated: the feeder model refuses it unless ``Set Controlmode=OFF``);
+property assignments ``Class.Name.Prop=value`` (e.g.
+``Transformer.Reg1.Taps=[1.0 1.0625]``); ``Redirect`` of further files;
+in-line RPN ``(8 1000 /)``; lower-triangular matrices ``(a | b c | ...)``.
+Other commands (``calcv``, ``Solve``, ``BusCoords``, ``Show``) are ignored,
+``Set Voltagebases`` and ``Set Controlmode`` are kept.
 """
 import math
 import os
@@ -160,7 +166,7 @@ class FeederSpec(dict):
 def parse_dss(path, spec=None):
     spec = spec if spec is not None else FeederSpec(
         source=None, transformers=[], linecodes={}, lines=[], loads=[], voltagebases=[],
-        base_frequency=60.0)
+        base_frequency=60.0, capacitors=[], regcontrols=[], controlmode="static")
     base_dir = os.path.dirname(os.path.abspath(path))
     with open(path) as f:
         cmds = _join_continuations(_strip_comments(f.read()))
@@ -182,6 +188,14 @@ def parse_dss(path, spec=None):
                     spec["voltagebases"] = [parse_number(x) for x in _unwrap(v).replace(",", " ").split()]
                 elif k == "defaultbasefrequency":
                     spec["base_frequency"] = parse_number(v)
+                elif k == "controlmode":
+                    spec["controlmode"] = v.lower()
+            continue
+        if verb.count(".") >= 2 and "=" in verb:      # Class.Name.Prop=value
+            path, v = toks[0].split("=", 1)
+            cls, name, prop = path.rsplit(".", 2)
+            _assign(spec, cls.lower(), name.lower(), [(prop.lower(), v.strip())] +
+                    [tuple(x.split("=", 1)) for x in toks[1:] if "=" in x])
             continue
         if verb not in ("new", "edit"):
             continue                                  # calcv, solve, buscoords, clear, show ...
@@ -195,7 +209,9 @@ def parse_dss(path, spec=None):
             if "=" in t:
                 k, v = t.split("=", 1)
                 props.append((k.strip().lower(), v.strip()))
-        if cls in ("circuit", "vsource"):
+        if verb == "edit":
+            _assign(spec, cls, name.lower(), props)
+        elif cls in ("circuit", "vsource"):
             _new_source(spec, name, props)
         elif cls == "transformer":
             _new_transformer(spec, name, props)
@@ -205,7 +221,52 @@ def parse_dss(path, spec=None):
             _new_line(spec, name, props)
         elif cls == "load":
             _new_load(spec, name, props)
+        elif cls == "capacitor":
+            _new_capacitor(spec, name, props)
+        elif cls == "regcontrol":
+            spec["regcontrols"].append(dict(name=name.lower(), props=props))
     return spec
+
+
+def _assign(spec, cls, name, props):
+    """Edit / property assignment on an element defined earlier (transformers and
+    loads; other classes are ignored like the other unsimulated commands)."""
+    if cls == "transformer":
+        for t in spec["transformers"]:
+            if t["name"] == name:
+                _transformer_props(t, props)
+                return
+        raise ValueError("Edit of undefined transformer %r" % name)
+    if cls == "load":
+        for ld in spec["loads"]:
+            if ld["name"] == name:
+                _load_props(ld, props)
+                return
+        raise ValueError("Edit of undefined load %r" % name)
+
+
+def _array(v):
+    return [x for x in _unwrap(v).replace(",", " ").split() if x]
+
+
+def _new_capacitor(spec, name, props):
+    """OpenDSS Capacitor defaults: 3 phases, wye, 12.47 kV, 1200 kvar; a kvar
+    array (several steps) counts as its sum (all steps in)."""
+    c = dict(name=name.lower(), bus1=None, phases=3, conn="wye", kv=12.47, kvar=1200.0)
+    for k, v in props:
+        if k == "bus1":
+            c["bus1"] = v
+        elif k == "bus2":
+            raise NotImplementedError("capacitor %s: series (bus2) capacitors are not supported" % name)
+        elif k == "phases":
+            c["phases"] = int(parse_number(v))
+        elif k == "conn":
+            c["conn"] = "delta" if v.lower().startswith("d") or v.lower().startswith("l") else "wye"
+        elif k == "kv":
+            c["kv"] = parse_number(v)
+        elif k == "kvar":
+            c["kvar"] = sum(parse_number(x) for x in _array(v))
+    spec["capacitors"].append(c)
 
 
 def _new_source(spec, name, props):
@@ -222,8 +283,22 @@ def _new_source(spec, name, props):
 
 
 def _new_transformer(spec, name, props):
-    t = dict(name=name.lower(), phases=3, windings=[{}, {}], xhl=7.0)
-    w = 0
+    t = dict(name=name.lower(), phases=3, windings=[{}, {}], xhl=7.0, _w=0)
+    _transformer_props(t, props)
+    for wd in t["windings"]:
+        wd.setdefault("conn", "wye")
+        wd.setdefault("kva", 1000.0)
+        wd.setdefault("pct_r", 0.2)
+        wd.setdefault("tap", 1.0)
+    spec["transformers"].append(t)
+
+
+def _conn(v):
+    return "delta" if v.lower().startswith("d") or v.lower().startswith("l") else "wye"
+
+
+def _transformer_props(t, props):
+    w = t.get("_w", 0)
     for k, v in props:
         if k == "phases":
             t["phases"] = int(parse_number(v))
@@ -235,21 +310,27 @@ def _new_transformer(spec, name, props):
         elif k == "bus":
             t["windings"][w]["bus"] = v
         elif k == "conn":
-            t["windings"][w]["conn"] = "delta" if v.lower().startswith("d") or v.lower().startswith("l") else "wye"
+            t["windings"][w]["conn"] = _conn(v)
         elif k == "kv":
             t["windings"][w]["kv"] = parse_number(v)
         elif k == "kva":
             t["windings"][w]["kva"] = parse_number(v)
         elif k in ("%r", "%r1"):
             t["windings"][w]["pct_r"] = parse_number(v)
-        elif k == "xhl":
+        elif k == "tap":
+            t["windings"][w]["tap"] = parse_number(v)
+        elif k in ("xhl", "x12"):
             t["xhl"] = parse_number(v)
+        elif k in ("buses", "conns", "kvs", "kvas", "taps", "%rs"):
+            key = {"buses": "bus", "conns": "conn", "kvs": "kv", "kvas": "kva", "taps": "tap",
+                   "%rs": "pct_r"}[k]
+            for i, x in enumerate(_array(v)[:2]):
+                t["windings"][i][key] = x if key == "bus" else _conn(x) if key == "conn" else parse_number(x)
+        elif k == "%loadloss":
+            for wd in t["windings"]:
+                wd["pct_r"] = parse_number(v) / 2.0
         # XHT/XLT only matter for 3-winding units
-    for wd in t["windings"]:
-        wd.setdefault("conn", "wye")
-        wd.setdefault("kva", 1000.0)
-        wd.setdefault("pct_r", 0.2)
-    spec["transformers"].append(t)
+    t["_w"] = w
 
 
 def _new_linecode(spec, name, props):
@@ -299,6 +380,11 @@ def _new_line(spec, name, props):
 def _new_load(spec, name, props):
     ld = dict(name=name.lower(), bus1=None, phases=3, conn="wye", model=1, kv=12.47,
               kw=10.0, kvar=5.0, vminpu=0.95, vmaxpu=1.05, vlowpu=0.50)
+    _load_props(ld, props)
+    spec["loads"].append(ld)
+
+
+def _load_props(ld, props):
     for k, v in props:
         if k == "bus1":
             ld["bus1"] = v
@@ -310,4 +396,3 @@ def _new_load(spec, name, props):
             ld["model"] = int(parse_number(v))
         elif k in ("kv", "kw", "kvar", "vminpu", "vmaxpu", "vlowpu"):
             ld[k] = parse_number(v)
-    spec["loads"].append(ld)

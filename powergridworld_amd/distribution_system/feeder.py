@@ -42,6 +42,26 @@ def _bus(spec, default):
     return parts[0].lower(), ([int(p) for p in parts[1:]] if len(parts) > 1 else list(default))
 
 
+def _elem_vbase(ld_or_cap, ph):
+    """Voltage across one phase branch (V): kV is line-to-line for 2- and
+    3-phase wye elements, the branch voltage otherwise (OpenDSS Load / Capacitor)."""
+    kv = ld_or_cap["kv"] * 1000.0
+    return kv / math.sqrt(3) if (ld_or_cap.get("conn", "wye") == "wye" and ph >= 2) else kv
+
+
+def _branches(bus_spec, ph, conn):
+    """Per phase branch (bus, hi node, lo node or 0 = ground) of a wye / delta element."""
+    b, nds = _bus(bus_spec, [1, 2, 3][:ph])
+    out = []
+    for p in range(ph):
+        if conn == "delta":
+            lo = nds[(p + 1) % ph] if ph > 1 else (nds[1] if len(nds) > 1 else 0)
+        else:
+            lo = 0
+        out.append((b, nds[p], lo))
+    return out
+
+
 def _seq_matrix(v1, v0, ph):
     s, m = (2 * v1 + v0) / 3.0, (v0 - v1) / 3.0
     return [[s if i == j else m for j in range(ph)] for i in range(ph)]
@@ -59,12 +79,21 @@ class Feeder(object):
                 self._touch(*_bus(w["bus"], [1, 2, 3][:t["phases"]]))
         for ld in spec["loads"]:
             self._touch(*_bus(ld["bus1"], [1, 2, 3][:ld["phases"]]))
+        for cap in spec.get("capacitors", []):
+            self._touch(*_bus(cap["bus1"], [1, 2, 3][:cap["phases"]]))
         for ln in spec["lines"]:
             for key in ("bus1", "bus2"):
                 self._touch(*_bus(ln[key], [1, 2, 3][:ln["phases"]]))
         self.node_names = ["%s.%d" % (b, nd) for b in self.buses for nd in self.bus_nodes[b]]
         self.node_index = {nm: i for i, nm in enumerate(self.node_names)}
         self.n = len(self.node_names)
+        if spec.get("regcontrols") and spec.get("controlmode", "static") != "off":
+            raise NotImplementedError("RegControl (automatic regulator tap control) is not simulated: "
+                                      "fix the taps (Transformer.X.Taps=[...]) and Set Controlmode=OFF")
+        for ld in spec["loads"]:
+            if ld.get("model", 1) not in (1, 2):
+                raise NotImplementedError("load %s: model %d (only 1 = constant PQ and 2 = constant Z)"
+                                          % (ld["name"], ld["model"]))
         self._build()
         self._bases()
         self._loads()
@@ -97,7 +126,8 @@ class Feeder(object):
             e = _lib.FeederElem(kind=_lib.PGW_ELEM_XFMR, nphases=ph,
                                 conn1=int(w1["conn"] == "delta"), conn2=int(w2["conn"] == "delta"),
                                 kv1=w1["kv"], kv2=w2["kv"], kva=w1["kva"], pct_r1=w1["pct_r"],
-                                pct_r2=w2["pct_r"], xhl=t["xhl"], freq=self.freq)
+                                pct_r2=w2["pct_r"], xhl=t["xhl"], tap1=w1.get("tap", 1.0),
+                                tap2=w2.get("tap", 1.0), freq=self.freq)
             for p in range(ph):
                 e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
             els.append(e)
@@ -125,6 +155,20 @@ class Feeder(object):
             (b1, n1), (b2, n2) = _bus(ln["bus1"], [1, 2, 3][:ph]), _bus(ln["bus2"], [1, 2, 3][:ph])
             for p in range(ph):
                 e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
+            els.append(e)
+        # constant admittances: capacitors (y = j Q / V^2 per phase) and
+        # constant-Z loads (model 2: y = (P - j Q) / V^2 at their base kW / kvar;
+        # the reference only re-sets model-1 loads, opendss.py:71, 149)
+        shunts = [(c, complex(0.0, c["kvar"] * 1000.0 / c["phases"])) for c in spec.get("capacitors", [])]
+        shunts += [(ld, complex(ld["kw"], -ld["kvar"]) * 1000.0 / ld["phases"]) for ld in spec["loads"]
+                   if ld.get("model", 1) == 2]
+        for obj, s in shunts:
+            ph = obj["phases"]
+            y = s / _elem_vbase(obj, ph) ** 2
+            e = _lib.FeederElem(kind=_lib.PGW_ELEM_SHUNT, nphases=ph, freq=self.freq)
+            for p, (b, hi, lo) in enumerate(_branches(obj["bus1"], ph, obj.get("conn", "wye"))):
+                e.node1[p], e.node2[p] = self.node(b, hi), self.node(b, lo)
+                e.r[p], e.x[p] = y.real, y.imag
             els.append(e)
         return els
 
@@ -164,10 +208,9 @@ class Feeder(object):
                 ep.append(self.node(b, nds[p]))
                 if ld["conn"] == "delta":
                     eq.append(self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1]))
-                    vb.append(ld["kv"] * 1000.0)
                 else:
                     eq.append(-1)
-                    vb.append(ld["kv"] * 1000.0 / (math.sqrt(3) if ph == 3 else 1.0))
+                vb.append(_elem_vbase(ld, ph))
                 el.append(li)
                 nph.append(float(ph))
                 vmin.append(ld.get("vminpu", 0.95))

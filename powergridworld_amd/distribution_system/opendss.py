@@ -71,7 +71,10 @@ class OpenDSSSolver(PowerFlowSolver):
         if len(self.annual_hourly_load_profile) != 8760:
             print("Warning: The provided load shape file is not annual hourly ",
                   "profile. Error might occur later")
-        self.load_bus_name = list(self.feeder.load_names)
+        # the PQ (model-1) loads the reference manipulates, in circuit order
+        # (opendss.py:54-77); other loads stay at their base values
+        self.load_bus_name = [nm for nm, ld in zip(self.feeder.load_names, self.feeder.spec["loads"])
+                              if ld.get("model", 1) == 1]
         self.base_load = np.stack([self.feeder.base_kw, self.feeder.base_kvar], 1)
         self.tol, self.max_iter = float(tol), int(max_iter)
         self.bus_voltages = {}
@@ -157,7 +160,7 @@ class OpenDSSSolver(PowerFlowSolver):
             p.vmax[k] = f.elem_vmax[k] if real else 1.05
             p.vlow[k] = f.elem_vlow[k] if real else 0.50
             p.nph[k] = f.elem_nph[k] if real else 1.0
-            ln = self.load_bus_name[f.elem_load[k]] if real else None
+            ln = f.load_names[f.elem_load[k]] if real else None
             p.elem_ctrl[k] = self._ctrl_names.index(ln) if ln in self._ctrl_names else -1
         p.tol, p.m, p.n_ctrl = self.tol, M, len(self._ctrl_names)
         p.n_out, p.max_iter = len(self.output_names), self.max_iter

@@ -76,6 +76,61 @@ def test_pf_fixed_point_solves_nodal_equations():
     np.testing.assert_allclose(S.imag[band], var_ph[band], rtol=1e-9, atol=1e-6)
 
 
+REGCAP = os.path.join(REPO, "tests", "data", "regcap_feeder.dss")
+
+
+def test_dss_regulators_capacitors_model2_loads():
+    """The DSS subset beyond IEEE-13 (tests/data/regcap_feeder.dss): 1-phase
+    regulators in array form with fixed taps set by property assignment,
+    RegControl off, capacitors, model-2 loads.  Parity unpinned (no OpenDSS):
+    the native build is checked against the oracle's independent NumPy one and
+    the solve against the nodal equations, shunts included."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    spec = load_feeder_spec(REGCAP)
+    regs = {t["name"]: t for t in spec["transformers"]}
+    assert [w["tap"] for w in regs["reg3"]["windings"]] == [1.0, 1.06875]
+    assert regs["reg1"]["phases"] == 1 and regs["reg1"]["windings"][1]["bus"] == "RG60.1"
+    assert regs["reg1"]["windings"][0]["pct_r"] == pytest.approx(0.005)
+    assert spec["controlmode"] == "off" and len(spec["regcontrols"]) == 1
+    assert [c["kvar"] for c in spec["capacitors"]] == [600.0, 100.0]
+    f, o = Feeder(spec), OracleFeeder(spec)
+    assert f.node_names == o.node_names
+    assert f.m == 5                      # model-1 phase elements: delta 3 + 2 single-phase
+    assert np.abs(f.Y - o.Y).max() / np.abs(o.Y).max() < 1e-12
+    assert np.abs(f.Z - o.Z).max() / np.abs(o.Z).max() < 1e-10
+    M, W, U0, G, V0 = f.reduce([f.node_index["b4.3"]])
+    assert np.abs(W[:f.m, :f.m] - o.W).max() / np.abs(o.W).max() < 1e-10
+    # the taps set the no-load ratio of each regulator
+    i = f.node_index
+    for ph, tap in ((1, 1.0625), (2, 1.05), (3, 1.06875)):
+        r = abs(f.V0[i["rg60.%d" % ph]]) / abs(f.V0[i["650.%d" % ph]])
+        assert r == pytest.approx(tap, rel=1e-3)     # (line charging and capacitors load it slightly)
+    # nodal residual of a converged solve, with the shunts in Y
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float)
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float)
+    V, it = o.solve(kw[None], kvar[None], tol=1e-13)
+    W_ph = kw[o.elem_load] * 1000.0 / o.elem_nph
+    var_ph = kvar[o.elem_load] * 1000.0 / o.elem_nph
+    U = o.Cinc @ V[0]
+    I = o.load_currents(U[None], W_ph[None], var_ph[None])[0]
+    resid = np.abs(o.Y @ V[0] - (o.I_src - o.Cinc.T @ I)).max() / np.abs(o.I_src).max()
+    assert resid < 1e-8
+
+
+def test_dss_unsupported_control_and_models_refused(tmp_path):
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    text = open(REGCAP).read()
+    p = tmp_path / "ctl.dss"
+    p.write_text(text.replace("Set Controlmode=OFF", ""))
+    with pytest.raises(NotImplementedError, match="RegControl"):
+        Feeder(load_feeder_spec(str(p)))
+    p = tmp_path / "m5.dss"
+    p.write_text(text.replace("Model=2 kV=2.4", "Model=5 kV=2.4"))
+    with pytest.raises(NotImplementedError, match="model 5"):
+        Feeder(load_feeder_spec(str(p)))
+
+
 def test_product_synthetic_exogenous_matches_fixture(exo_frame):
     from powergridworld_amd.agents.buildings import synthetic_exogenous_data
     df = synthetic_exogenous_data()

@@ -248,6 +248,32 @@ def test_pf_vs_oracle():
         assert (N(pf.iterations) == orc.last_iters).mean() > 0.99
 
 
+def test_pf_regcap_feeder_vs_oracle():
+    """A feeder beyond IEEE-13 (tests/data/regcap_feeder.dss: fixed-tap
+    regulators, capacitors, model-2 loads; parity unpinned, no OpenDSS) through
+    the batched solver against the oracle, two controllable loads."""
+    import os
+    from oracle.pf_oracle import BatchedPF
+    from powergridworld_amd.distribution_system.dss import parse_dss
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    from tests.conftest import REPO
+    path = os.path.join(REPO, "tests", "data", "regcap_feeder.dss")
+    n = 512
+    rng = np.random.default_rng(12)
+    pf = OpenDSSSolver(path, "ieee_13_dss/annual_hourly_load_profile.csv", system_load_rescale_factor=1.1,
+                       num_envs=n, device=DEV)
+    assert pf.load_bus_name == ["d1", "a1", "c1"]        # model-1 loads only
+    orc = BatchedPF(spec=parse_dss(path), system_load_rescale_factor=1.1)
+    for ts in ["2021-08-12 15:00", "2021-01-01 05:00"]:
+        pa = rng.uniform(-100, 300, n)
+        pc = rng.uniform(-50, 200, n)
+        pf.calculate_power_flow({"a1": T(pa), "c1": T(pc)}, {}, current_time=ts)
+        v = pf.get_bus_voltages()
+        want = orc.calculate(ts, {"a1": pa, "c1": pc}, {}, K=n)
+        got = np.stack([N(v[name]) for name in orc.feeder.node_names], 1)
+        np.testing.assert_allclose(got, want, rtol=1e-8, atol=0)
+
+
 @pytest.mark.parametrize("loads", [("675c",), ("675c", "671")])
 def test_pf_all_rows_ragged_and_extrema_only(loads):
     """All output rows at a ragged batch (the last wave part-empty: the rows'
