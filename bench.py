@@ -49,6 +49,9 @@ AGENT_BYTES = 112 + 200
 AGENT_BYTES_F32 = AGENT_BYTES // 2       # the same items in fp32 (pgw_coord_step_f32)
 # k_coord_pf -- per env: reads 5 agent powers + 5 rewards, writes 5 rewards + v + vv + iters
 PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
+# k_coord_fused -- the whole C4 step per env: 5 agents (312 B each, reward and
+# power written once) + V675.3, vv (8 B each) and PF iterations (4 B)
+FUSED_BYTES = AGENT_BYTES * N_AGENTS + 8 + 8 + 4
 # k_coord_pf -- algorithmic fp64 FLOPs (m = 14 load phase elements): per fixed-point
 # iteration 8 m^2 (complex matvec) + 12 m (PQ current law) + 6 m (update, |du|^2 test);
 # per env once more the final currents (12 m), one node voltage (8 m + 4) and the reward.
@@ -57,7 +60,7 @@ PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
 PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 PF_KERNEL = ("k_coord_pf_split" if os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
              else "k_coord_pf<14,true,false,false>")
-KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve")
+KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_fused")     # PGW_T_* order
 
 
 def parse():
@@ -354,6 +357,16 @@ def main():
                                    "frac": tfs / FP64_PEAK_TFS,
                                    "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
                                    "traffic": traffic.get(KERNELS[1])}
+        f_us = avg_us[KERNELS[3]]
+        if f_us:
+            gbs = FUSED_BYTES * n / (f_us * 1e-6) / 1e9
+            tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (f_us * 1e-6) / 1e12
+            kernels[KERNELS[3]] = {"avg_us": f_us, "timed_launches": cnt[3], "bound": "hbm",
+                                   "note": "agents + power flow in one launch (C4 fast path); "
+                                           "PF fp64 TFLOP/s over the same launch in pf_tflops",
+                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": FUSED_BYTES * n,
+                                   "traffic": traffic.get(KERNELS[3]), "pf_tflops": tfs}
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "
@@ -369,12 +382,12 @@ def main():
         if d["unit"] == "GB/s":
             roof["peak_measured_copy"] = copy_gbs
             roof["frac_measured_copy"] = d["achieved"] / copy_gbs
-        step_bytes = (AGENT_BYTES * N_AGENTS + PF_BYTES) * n
+        step_bytes = (AGENT_BYTES * N_AGENTS + 8) * n      # 1,568 B per C4 env-step
         step_gbs = step_bytes / (elapsed / args.steps) / 1e9
         step = {"bytes_per_step": step_bytes, "achieved": step_gbs, "unit": "GB/s",
                 "frac": step_gbs / HBM_PEAK_GBS, "frac_measured_copy": step_gbs / copy_gbs,
-                "note": "algorithmic HBM bytes of the whole step (agents 312 B x 5 + PF 140 B per "
-                        "env) / ms_per_step, per GPU"}
+                "note": "algorithmic HBM bytes of the whole step (SURVEY 8(d): agents 312 B x 5 + "
+                        "V675.3 8 B per env) / ms_per_step, per GPU"}
         out = {
             "metric": "agent-env-steps/sec at batch 65536, 5-agent scenario, 1/2/4/8 MI355X",
             "value": value,

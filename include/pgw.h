@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 14
+#define PGW_ABI_VERSION 15
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -389,7 +389,8 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
  * pgw_timing_stop synchronizes the recorded events and returns, per kernel,
  * the summed duration (ms) and the number of timed launches.
  * ---------------------------------------------------------------------- */
-enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COUNT = 3 };
+enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COORD_FUSED = 3,
+       PGW_T_COUNT = 4 };
 /* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
 int32_t pgw_debug_pf_trace(long long* buf);

@@ -1165,6 +1165,234 @@ __global__ void __launch_bounds__(kBlock, 2) k_coord_pf_split(CoordPFArgs c, PFA
 // PGW_PF_SPLIT=1 selects the split kernel (read per call: the tests compare the
 // two in one process).  Off by default: measured slower at 65 536 envs
 // (13.1 vs 9.6 us).
+// ---- K1 + K2 fused (the C4 fast path, fp64): ONE launch per step -----------
+// A block is NW waves over the same 64 envs: wave a first runs agent a's step
+// for them (k_coord_agents_std's arithmetic), leaving the agent's power in LDS
+// and its reward in a register; after a barrier the block solves the 64 envs'
+// power flow together, the 14 load elements' rows spread over the waves (wave
+// w owns rows R w .. R w + R - 1, the last wave also the output row).  Per
+// iteration each wave evaluates the currents of its own elements into LDS;
+// after a barrier every wave accumulates its rows over columns 0 .. 13 in
+// order, reading the currents from LDS and W'' from the operand block through
+// the scalar cache -- per accumulator the one-lane kernel's operations in its
+// order, so the result is bit-identical to k_coord_agents_std +
+// k_coord_pf<14, true, false, false> (and so to the generic path).  The
+// per-env convergence test ANDs the waves' flags through LDS.  Finally the
+// reward is r + (-share), the same single IEEE add the two-launch path's
+// atomic performs, stored once.
+// The aim: in the two-launch step the PF kernel runs one latency-bound wave per
+// SIMD after the agents kernel, with HBM idle (PF ~10 us of a ~30 us step);
+// here the PF's arithmetic and L2 gathers were to overlap other blocks' HBM
+// streaming.  They do not (see coord_fused_enabled): kept as an option.
+constexpr int kFusedM = 14;
+
+template <int NW, int W>
+__device__ __forceinline__ void fused_pf_rows(const PFArgs& a, const pgw_pf_tables& t, const double* blk,
+                                              const CoordPFArgs& c, int64_t n, int64_t e, bool valid,
+                                              int l, double pc, double (*s_ir)[64], double (*s_ii)[64],
+                                              int (*s_flag)[64], double* s_v, double& vsel, int& it_out) {
+  constexpr int M = kFusedM, R = (M + NW - 1) / NW, K0 = R * W;
+  constexpr int NR = (K0 + R <= M) ? R : (K0 < M ? M - K0 : 0);   // rows this wave owns
+  constexpr bool OUT = (W == NW - 1);                             // and the output row
+  using Lo = PFBlock<M>;
+  constexpr int T = Lo::kTri;
+  auto tri = [](int i, int k) { return i <= k ? i * M - i * (i - 1) / 2 + (k - i) : k * M - k * (k - 1) / 2 + (i - k); };
+  const double qc = 0.0;
+  // ---- first guess of the own elements (PFSolver::initial, SPEC form)
+  double ur[R > 0 ? R : 1], ui[R > 0 ? R : 1];
+  if (a.use_pred) {
+    const double g = (pc - a.pred_x0) * a.pred_inv_h;
+    int cc = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
+    if (t.U_pred_meta) {
+      const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
+      const pgw_pred_meta m = t.U_pred_meta[j];
+      cc = (g - (double)j < m.tstar) ? m.left : m.right;
+    }
+    const char* r = reinterpret_cast<const char*>(t.U_pred) + (int64_t)cc * (32 * M);
+    const double2* v = reinterpret_cast<const double2*>(r);
+    const float2* d1 = reinterpret_cast<const float2*>(r + 16 * M);
+    const float2* d2 = reinterpret_cast<const float2*>(r + 24 * M);
+    const double tt = g - (double)cc;
+    const double h1 = 0.5 * tt, h2 = 0.5 * tt * tt;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const double2 u = v[K0 + q];
+      const float2 e1 = d1[K0 + q], e2 = d2[K0 + q];
+      ur[q] = fma(h2, (double)e2.x, fma(h1, (double)e1.x, u.x));
+      ui[q] = fma(h2, (double)e2.y, fma(h1, (double)e1.y, u.y));
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      ur[q] = blk[Lo::kU0re + K0 + q];
+      ui[q] = blk[Lo::kU0im + K0 + q];
+    }
+  }
+  // ---- fixed point (PFSolver::iterate<false>)
+  int it = 0, my_it = 0;
+  bool done = !valid, conv_ok = !valid;
+  double v0r = 0.0, v0i = 0.0;
+  while (true) {
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {       // currents of the own elements (PFSolver::current)
+      const int k = K0 + q;
+      const double s_r = fma(a.fr[k], pc, a.sr0[k]);
+      const double s_i = fma(a.fi[k], qc, a.si0[k]);
+      const double m2 = fma(ui[q], ui[q], ur[q] * ur[q]);
+      double mc = fmin(fmax(m2, a.mn2), a.mx2);
+      mc = (m2 <= a.lo2) ? 1.0 : mc;
+      const double gg = fast_rcp(mc);
+      const double gr = gg * ur[q], gi = gg * ui[q];
+      s_ir[k][l] = fma(s_r, gr, -(s_i * gi));
+      s_ii[k][l] = fma(s_r, gi, s_i * gr);
+    }
+    __syncthreads();
+    double A[R > 0 ? R : 1], Bs[R > 0 ? R : 1], C[R > 0 ? R : 1];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      A[q] = blk[Lo::kU0re + K0 + q];
+      C[q] = blk[Lo::kU0sum + K0 + q];
+      Bs[q] = 0.0;
+    }
+    double vr = 0.0, vi = 0.0;
+    if constexpr (OUT) {
+      vr = blk[Lo::kV0re];
+      vi = blk[Lo::kV0im];
+    }
+#pragma unroll 1
+    for (int k = 0; k < M; ++k) {
+      const double ir = s_ir[k][l], ii = s_ii[k][l];
+      const double is = ir + ii;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        const int e3 = tri(K0 + q, k);
+        A[q] = fma(blk[e3], ir, A[q]);
+        Bs[q] = fma(blk[T + e3], ii, Bs[q]);
+        C[q] = fma(blk[2 * T + e3], is, C[q]);
+      }
+      if constexpr (OUT) {
+        const double gr = blk[Lo::kG0re + k], gi = blk[Lo::kG0im + k];
+        vr = fma(gr, ir, vr);
+        vi = fma(gr, ii, vi);
+        vr = fma(-gi, ii, vr);
+        vi = fma(gi, ir, vi);
+      }
+    }
+    bool conv = true;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const double nr = A[q] - Bs[q];
+      const double ni = (C[q] - A[q]) - Bs[q];
+      const double dr = nr - ur[q], di = ni - ui[q];
+      conv &= fma(dr, dr, di * di) < a.tol2;
+      ur[q] = done ? ur[q] : nr;
+      ui[q] = done ? ui[q] : ni;
+    }
+    if constexpr (OUT) {
+      v0r = done ? v0r : vr;
+      v0i = done ? v0i : vi;
+    }
+    s_flag[W][l] = conv ? 1 : 0;
+    __syncthreads();
+    bool all = true;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) all = all && (s_flag[ww][l] != 0);
+    ++it;
+    my_it = done ? my_it : it;
+    conv_ok = conv_ok || (!done && all);
+    done = done || all || it >= a.max_iter;
+    // every wave saw the same flags, so every wave leaves on the same iteration
+    if (__syncthreads_or(!done) == 0) break;
+  }
+  it_out = conv_ok ? my_it : -my_it;
+  if constexpr (OUT) s_v[l] = sqrt(fma(v0i, v0i, v0r * v0r));
+  __syncthreads();
+  vsel = s_v[l];
+  (void)c; (void)n; (void)e;
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 5) k_coord_fused(pgw_coord_params p, pgw_coord_step_info s,
+                                                            int64_t n, pgw_coord_buffers b, double pv_ob,
+                                                            StdDerived dv, CoordPFArgs c, PFArgs a,
+                                                            pgw_pf_tables t, int dbg) {
+  __shared__ double s_pow[NW][64];
+  __shared__ double s_ir[kFusedM][64], s_ii[kFusedM][64];
+  __shared__ int s_flag[NW][64];
+  __shared__ double s_v[64];
+  __shared__ double s_blk[PFBlock<kFusedM>::kSize];   // the operand block, read by broadcast
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 64 + l;
+  const bool valid = e < n;
+  for (int i = threadIdx.x; i < PFBlock<kFusedM>::kSize; i += 64 * NW) s_blk[i] = t.block[i];
+  // ---- agent w of this env (k_coord_agents_std)
+  double my_rew = 0.0, my_pow = 0.0;
+  if (dbg & 1) {
+    if (valid) my_pow = b.agent_power[(int64_t)w * n + e];
+  } else if (valid) {
+    StdAgentIn in[1];
+    const double* ap = b.action.ptr + w * b.act_stride_agent + e * b.action.s_env;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) in[0].av[j] = ap[j * b.action.s_dim];
+    double* xp = b.x + (int64_t)w * 5 * n + e;
+#pragma unroll
+    for (int z = 0; z < 5; ++z) in[0].xs[z] = xp[z * n];
+    double* socp = b.soc + (int64_t)w * n + e;
+    in[0].soc = *socp;
+    double* op = b.obs.ptr + w * b.obs_stride_agent + e * b.obs.s_env;
+    std_agent_compute<1>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
+      if (slot < kSlotSoc) xp[slot * n] = v[0];
+      else if (slot == kSlotSoc) *socp = v[0];
+      else if (slot < kSlotPower) st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
+      else if (slot == kSlotPower) {
+        b.agent_power[(int64_t)w * n + e] = v[0];
+        my_pow = v[0];
+      } else my_rew = v[0];
+    });
+  }
+  s_pow[w][l] = my_pow;
+  __syncthreads();
+  // bus load of the controllable slot (multiagent_env.py:171-181), agents in order
+  double pc = 0.0;
+#pragma unroll
+  for (int ag = 0; ag < NW; ++ag) pc = (c.agent_ctrl[ag] == 0) ? pc + s_pow[ag][l] : pc;
+  double vsel = 0.0;
+  int it = 0;
+  const double* blk = s_blk;
+  if (!(dbg & 2)) static_for<0, NW>([&](auto W) {
+    if (w == decltype(W)::value)
+      fused_pf_rows<NW, decltype(W)::value>(a, t, blk, c, n, e, valid, l, pc, s_ir, s_ii, s_flag, s_v, vsel, it);
+  });
+  if (!valid) return;
+  if (w == 0) {
+    if (b.v_out) b.v_out[e] = vsel;
+    if (b.iters) b.iters[e] = it;
+  }
+  double r = my_rew;
+  if (c.coordinated) {
+    const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
+    if (w == 0 && b.vv) b.vv[e] = vv;
+    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
+    r = r + (-share);
+  }
+  b.reward[(int64_t)w * n + e] = r;
+}
+
+static int coord_fused_dbg() {   // measurement only: 1 = skip the agents' arithmetic, 2 = skip the PF
+  const char* v = getenv("PGW_COORD_FUSED_DBG");
+  return v ? atoi(v) : 0;
+}
+
+// Measured and not the default: with 65,536 envs every
+// block is resident at once, so all blocks run their agent phase together and
+// then their PF phase together -- nothing overlaps, and the block-shaped agent
+// phase itself ran slower (28.7 us alone vs 18 us for k_coord_agents_std).
+// PGW_COORD_FUSED=1 selects it (tests/test_gpu_parity.py checks it bit for bit).
+static bool coord_fused_enabled() {
+  const char* v = getenv("PGW_COORD_FUSED");
+  return v && v[0] == '1';
+}
+
 static bool pf_split_enabled() {
   const char* v = getenv("PGW_PF_SPLIT");
   return v && v[0] == '1';
@@ -1412,6 +1640,16 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   c.vv_hi = p->vv_hi;
   c.vv_penalty = p->vv_penalty;
   const PFArgs a = make_pf_args(*pf, *pft);
+  if constexpr (!kF32) {
+    bool one_slot = true;
+    for (int ag = 0; ag < p->n_agents; ++ag) one_slot = one_slot && p->agent_ctrl[ag] <= 0;
+    if (std_layout && p->n_agents == 5 && pf->m == 14 && uniform_band(*pf) && pf->n_ctrl <= 1 &&
+        pf->n_out <= 1 && p->vv_row == 0 && one_slot && coord_fused_enabled()) {
+      launch_timed(PGW_T_COORD_FUSED, k_coord_fused<5>, dim3((unsigned)((n + 63) / 64)), dim3(5 * 64), st,
+                   *p, *s, n, b, pv_ob, make_std_derived(*p), c, a, *pft, coord_fused_dbg());
+      return check_launch("k_coord_fused");
+    }
+  }
   // (the pair layout measured for fp64 too: 19.5 -> 20.2 us, so fp32 only)
   if (std_layout && kF32 && pairs_ok(b, n)) {
     launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std_x2<Bufs>, dim3(grid_for(n / 2), p->n_agents),

@@ -409,16 +409,22 @@ def test_c4_fused_equals_generic_full_batch():
 
 
 @pytest.mark.parametrize("n", [65536, 1000, 33])
-def test_c4_split_pf_equals_one_lane_pf(n, monkeypatch):
-    """k_coord_pf_split (two lanes per env, currents exchanged by permlane32
-    swap) against the one-lane k_coord_pf, bit for bit: obs, rewards, voltage
-    violation, V675.3 and PF iterations over an episode boundary, with bus
-    loads spread over the whole predictor grid (so lanes reload a second
-    record) and batches that leave a wave part-filled."""
+@pytest.mark.parametrize("variant", ["fused", "split"])
+def test_c4_split_pf_equals_one_lane_pf(n, variant, monkeypatch):
+    """The C4 step's alternative kernels against the two-launch path
+    (k_coord_agents_std + one-lane k_coord_pf), bit for bit: obs, rewards,
+    agent powers, voltage violation, V675.3 and PF iterations over an episode
+    boundary, with bus loads spread over the whole predictor grid (so lanes
+    reload a second record) and batches that leave a wave part-filled.
+    fused: k_coord_fused (agents + PF in one launch, the default);
+    split: k_coord_pf_split (two lanes per env, currents exchanged by
+    permlane32 swap)."""
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     out = []
-    for split in ("1", "0"):
+    modes = [("1", "0"), ("0", "0")] if variant == "fused" else [("0", "1"), ("0", "0")]
+    for fused_k, split in modes:
+        monkeypatch.setenv("PGW_COORD_FUSED", fused_k)
         monkeypatch.setenv("PGW_PF_SPLIT", split)
         env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
         gen = torch.Generator(DEV).manual_seed(7)
@@ -433,6 +439,7 @@ def test_c4_split_pf_equals_one_lane_pf(n, monkeypatch):
                 act = torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2
                 _, rew, _, meta = env.step(act)
                 rec.append((env.packed_obs().clone(), torch.stack([rew[a.name] for a in env.agents]),
+                            torch.stack([a.real_power for a in env.agents]).clone(),
                             meta["voltage_violation"].clone(),
                             env.pf_solver.get_bus_voltage_by_name("675c").clone(),
                             env.pf_solver.iterations.clone()))
@@ -446,7 +453,7 @@ def test_c4_split_pf_equals_one_lane_pf(n, monkeypatch):
     for a, b in zip(*out):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
-    its = out[0][-1][4]
+    its = out[0][-1][5]
     assert int(its.abs().max()) >= 1 and int((its < 0).sum()) == 0
 
 
