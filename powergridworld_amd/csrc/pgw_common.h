@@ -103,10 +103,12 @@ __device__ __forceinline__ double to_raw(double y, double lo, double hi) {
 __device__ __forceinline__ double pymax(double a, double b) { return (b > a) ? b : a; }
 __device__ __forceinline__ double pymin(double a, double b) { return (b < a) ? b : a; }
 
-// pgw_mat or pgw_matf; fp32 values are widened to fp64 (exactly).
+// Action element (e, j) of a pgw_mat or pgw_matf; fp32 values are widened to
+// fp64 (exactly).  Every caller loads actions: they are read once per step, so
+// the load is nontemporal (C4: profiles/r02/act_nt.txt).
 template <class Mt>
 __device__ __forceinline__ double ld(const Mt& m, int64_t e, int j) {
-  return (double)m.ptr[e * m.s_env + (int64_t)j * m.s_dim];
+  return (double)__builtin_nontemporal_load(m.ptr + e * m.s_env + (int64_t)j * m.s_dim);
 }
 // Observation stores are write-once streams for the policy: nontemporal, so
 // they do not evict the state the next step re-reads (k_coord_agents_std

@@ -81,7 +81,10 @@ int32_t pgw_stream_copy(const void* src, void* dst, int64_t bytes, int32_t reps,
               "pgw_stream_copy: bad argument");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t n16 = bytes / 16;
-  const unsigned grid = 2048;   // 8 blocks per CU, grid-stride
+  // 32 blocks per CU, grid-stride: the best of the grids and cache policies
+  // tools/micro/copy_peak.hip measured (profiles/r02/copy_peak.txt: 6.06 TB/s;
+  // read-only 6.2-6.4, write-only 4.1-4.6)
+  const unsigned grid = 8192;
   auto launch = [&] {
     hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(kBlock), 0, st,
                        static_cast<const dv2*>(src), static_cast<dv2*>(dst), n16);
