@@ -319,7 +319,7 @@ class FiveZoneROMEnv(ComponentEnv):
         c.kind, c.obs, c.real_power = 0, _lib.mat(self._obs), self.p_consumed.data_ptr()
 
     def _mc_prepare(self, args, slot, action, obs_kwargs):
-        a = as_action(action, self.num_envs, 6, self.device)
+        a, m = self._action_mat(action, 6)
         t = self.time_index
         if t + 1 >= len(self._exo):
             raise IndexError("building stepped past the end of its exogenous data")
@@ -330,7 +330,7 @@ class FiveZoneROMEnv(ComponentEnv):
                 args.bld_ext.p_setpoint:
             args.bld_ext = _lib.BuildingExt()
         args.bld_ex_t, args.bld_ex_next = self._exo[t], self._exo[t + 1]
-        args.comp[slot].action = self._act_mat(a)
+        args.comp[slot].action = m
         return a, keep
 
     def _mc_finish(self, obs_kwargs):

@@ -137,8 +137,7 @@ class EnergyStorageEnv(ComponentEnv):
         c.kind, c.obs, c.real_power = 2, _lib.mat(self._obs), self._real_power.data_ptr()
 
     def _mc_prepare(self, args, slot, action, kwargs):
-        a = as_action(action, self.num_envs, 1, self.device)
-        args.comp[slot].action = self._act_mat(a)
+        a, args.comp[slot].action = self._action_mat(action, 1)
         return a
 
     def _mc_finish(self, kwargs):
@@ -150,7 +149,10 @@ class EnergyStorageEnv(ComponentEnv):
         return None
 
     def get_obs(self, **kwargs):
-        return self._obs, {"state_of_charge": self.soc.unsqueeze(1)}
+        m = self.__dict__.get("_soc_meta")
+        if m is None or m[0] != self.soc.data_ptr():        # (a view per SoC buffer, not per step)
+            m = self._soc_meta = (self.soc.data_ptr(), {"state_of_charge": self.soc.unsqueeze(1)})
+        return self._obs, dict(m[1])
 
     def is_terminal(self):
         return self.simulation_step + 1 == self.max_episode_steps      # :180-181

@@ -88,14 +88,14 @@ class PVEnv(ComponentEnv):
         c.kind, c.obs, c.real_power = 1, _lib.mat(self._obs), self._real_power.data_ptr()
 
     def _mc_prepare(self, args, slot, action, kwargs):
-        a = as_action(action, self.num_envs, 1, self.device)
+        a, m = self._action_mat(action, 1)
         self._mc_pmax = float(self.data[self.index])
         args.pv_pmax = self._mc_pmax
         vmin = None
         if self.grid_aware:
             vmin = self._min_voltage(kwargs)
             args.pv_min_voltage = vmin.data_ptr()
-        args.comp[slot].action = self._act_mat(a)
+        args.comp[slot].action = m
         return a, vmin
 
     def _mc_finish(self, kwargs):

@@ -199,8 +199,7 @@ class EVChargingEnv(ComponentEnv):
 
     def _mc_prepare(self, args, slot, action, kwargs):
         args.ev_step = self._step_info(action is not None)
-        a = as_action(action, self.num_envs, 1, self.device)
-        args.comp[slot].action = self._act_mat(a)
+        a, args.comp[slot].action = self._action_mat(action, 1)
         return a
 
     def _mc_finish(self, kwargs):

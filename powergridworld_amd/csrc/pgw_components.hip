@@ -236,74 +236,94 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
   // vehicle at one wave per SIMD) -- and last the sums run over the chunk in
   // ascending vehicle order, by selects, exactly as one vehicle at a time.
   // Both passes walk the same chunk mask, so no index array is needed.
+  // Software-pipelined: the NEXT chunk's loads are issued before the current
+  // chunk is processed (the chunks hold different vehicles, so its stores
+  // cannot touch them), so a wave waits out one memory latency per word rather
+  // than one per chunk.
   constexpr int kEvChunk = 8;
+  struct Chunk {
+    uint64_t bits;
+    double rs[kEvChunk], tls[kEvChunk], rcs[kEvChunk];
+    bool wins[kEvChunk];
+  };
+  auto take = [](uint64_t& scan) {                   // the next <= kEvChunk vehicle bits
+    uint64_t c = scan;
+#pragma unroll
+    for (int i = 0; i < kEvChunk; ++i) scan &= scan - 1;
+    return c & ~scan;
+  };
   for (int w = 0; w < s.n_words; ++w) {
     uint64_t scan = s.scan[w];
     const uint64_t win = s.window[w];
     const uint64_t prev = chg[(int64_t)w * n + e];
     uint64_t now_bits = 0ull;
-    while (scan) {
-      uint64_t chunk = scan;
-#pragma unroll
-      for (int i = 0; i < kEvChunk; ++i) scan &= scan - 1;   // the chunk: the next <= kEvChunk bits
-      chunk &= ~scan;
-      double rs[kEvChunk], df[kEvChunk], cv[kEvChunk];
-      double tls[kEvChunk], rcs[kEvChunk];
-      bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk], wins[kEvChunk];
-      uint64_t m = chunk;
-      // the chunk's loads all go out before any is used: the requirements
-      // (vector) and the vehicles' time left (uniform: scalar loads, which
-      // complete out of order, so one wait for the chunk instead of one per
-      // vehicle)
+    // the chunk's loads all go out before any is used: the requirements
+    // (vector) and the vehicles' time left (uniform: scalar loads)
+    auto load = [&](Chunk& C) {
+      uint64_t m = C.bits;
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) {
         const int b = m ? __builtin_ctzll(m) : 0;    // past the chunk's end: a harmless reload
         const int v = w * 64 + b;
-        rs[i] = req[(int64_t)v * n + e];
+        C.rs[i] = req[(int64_t)v * n + e];
         if (s.env_start) {       // randomize: this env's own vehicle table
           const double en = s.env_endp[(int64_t)v * n + e];
-          tls[i] = (en - s.time) / 60.0;
-          rcs[i] = 0.0;
-          wins[i] = (s.time >= s.env_start[(int64_t)v * n + e]) && (s.time <= floor(en));
+          C.tls[i] = (en - s.time) / 60.0;
+          C.rcs[i] = 0.0;
+          C.wins[i] = (s.time >= s.env_start[(int64_t)v * n + e]) && (s.time <= floor(en));
         } else if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
           const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[v];
-          tls[i] = q.x;
-          rcs[i] = q.y;
+          C.tls[i] = q.x;
+          C.rcs[i] = q.y;
         } else {
-          tls[i] = (endp[v] - s.time) / 60.0;
-          rcs[i] = 0.0;
+          C.tls[i] = (endp[v] - s.time) / 60.0;
+          C.rcs[i] = 0.0;
         }
-        if (!s.env_start) wins[i] = (win >> b) & 1ull;
+        if (!s.env_start) C.wins[i] = (win >> b) & 1ull;
         m &= m - 1;
       }
-      m = chunk;
+    };
+    auto process = [&](const Chunk& C) {
+      double df[kEvChunk], cv[kEvChunk];
+      bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk];
+      uint64_t m = C.bits;
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) {
         const bool in = m != 0;                      // uniform: the chunk's tail is not
         const int b = in ? __builtin_ctzll(m) : 0;
         m &= m - 1;
         const int v = w * 64 + b;
-        const double r = rs[i], tl = tls[i], rc = rcs[i];
-        act[i] = in && wins[i] && (r > 0.0);
+        const double r = C.rs[i], tl = C.tls[i], rc = C.rcs[i];
+        act[i] = in && C.wins[i] && (r > 0.0);
         chg_now[i] = act[i] && (tl > 0.0);
         dep[i] = in && !act[i] && ((prev >> b) & 1ull);   // departed: not charging now (:239-243)
         df[i] = pymax(0.0, p.rate - (s.tl_rcp ? exact_div(r, tl, rc) : r / tl));
         cv[i] = pymin(kwh, r);
         if (chg_now[i]) req[(int64_t)v * n + e] = r - cv[i];
       }
-      m = chunk;
+      m = C.bits;
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) {
         const uint64_t lo = m & (0ull - m);          // the chunk's i-th vehicle bit (0 past its end)
         m &= m - 1;
-        demand = act[i] ? demand + rs[i] : demand;
+        demand = act[i] ? demand + C.rs[i] : demand;
         nact += act[i] ? 1 : 0;
         now_bits |= act[i] ? lo : 0ull;
         dsum = chg_now[i] ? dsum + df[i] : dsum;
         consumed = chg_now[i] ? consumed + cv[i] : consumed;
         dcnt += chg_now[i] ? 1 : 0;
-        unserved = dep[i] ? unserved + rs[i] : unserved;
+        unserved = dep[i] ? unserved + C.rs[i] : unserved;
       }
+    };
+    Chunk cur;
+    cur.bits = take(scan);
+    if (cur.bits) load(cur);
+    while (cur.bits) {
+      Chunk nxt;
+      nxt.bits = take(scan);
+      if (nxt.bits) load(nxt);
+      process(cur);
+      cur = nxt;
     }
     chg[(int64_t)w * n + e] = now_bits;
   }

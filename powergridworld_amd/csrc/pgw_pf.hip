@@ -806,7 +806,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
   for (int j = 0; j < 8; ++j) in[0].av[j] = (double)ld_act(ap + j * b.action.s_dim);
   S* xp = b.x + (int64_t)a * 5 * n + e;
 #pragma unroll
-  for (int z = 0; z < 5; ++z) in[0].xs[z] = (double)xp[z * n];
+  for (int z = 0; z < 5; ++z) in[0].xs[z] = (double)xp[z * n];   // state: cached (re-read next step)
   S* socp = b.soc + (int64_t)a * n + e;
   in[0].soc = (double)*socp;
   S* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;

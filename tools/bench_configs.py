@@ -53,7 +53,8 @@ def bench_c2(dev, steps, warmup, n=4096, pool=64):
     return dict(config="C2", workload="EnergyStorageEnv defaults", batch=n, agents=1, steps=steps, seconds=dt)
 
 
-def bench_c3(dev, steps, warmup, n=16384, pool=16):
+def c3_env(dev, n, pool=16):
+    """The C3 agent and a pool of pre-generated action dicts (HBM resident)."""
     from powergridworld_amd import MultiComponentEnv
     from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv, FiveZoneROMThermalEnergyEnv, PVEnv
     comps = [
@@ -69,6 +70,12 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16):
     dims = {"building": 6, "pv": 1, "storage": 1, "ev": 1}
     acts = [{c: torch.empty((n, d), dtype=torch.float64, device=dev).uniform_(-1, 1, generator=gen)
              for c, d in dims.items()} for _ in range(pool)]
+    return env, acts
+
+
+def bench_c3(dev, steps, warmup, n=16384, pool=16):
+    env, acts = c3_env(dev, n, pool)
+    gen = torch.Generator(dev).manual_seed(1)
     init = torch.empty(n, dtype=torch.float64, device=dev).uniform_(3.0, 50.0, generator=gen)
     k = [0]
 
