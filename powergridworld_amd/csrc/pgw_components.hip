@@ -214,11 +214,17 @@ __global__ void __launch_bounds__(kBlock) k_ev_reset_tables(int64_t n, int32_t V
 // (the reference iterates a Python set of small ints); only vehicles parked now
 // or at the previous step can contribute (`scan`, uniform across the wave).
 // One env's EVChargingEnv.step (:171-264); writes rp[e] and rew[e].
-__device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
-                                            int64_t e, const pgw_mat& act, const double* __restrict__ endp,
-                                            double* __restrict__ req, uint64_t* __restrict__ chg,
-                                            const pgw_mat& obs, double* __restrict__ rp,
-                                            double* __restrict__ rew) {
+// MODE (uniform, chosen once per call by ev_step_env): 0 = the host's
+// time-left table with reciprocals (exact_div), 1 = randomize's per-env tables,
+// 2 = time left divided in the kernel.  Instantiated per mode so the vehicle
+// loop carries no per-vehicle branch and no unused IEEE division.
+enum { kEvTable = 0, kEvPerEnv = 1, kEvDivide = 2 };
+template <int MODE>
+__device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+                                             int64_t e, const pgw_mat& act, const double* __restrict__ endp,
+                                             double* __restrict__ req, uint64_t* __restrict__ chg,
+                                             const pgw_mat& obs, double* __restrict__ rp,
+                                             double* __restrict__ rew) {
   double a = act.ptr ? ld(act, e, 0) : s.action_default;
   if (p.rescale) {
     oob_note(p.oob, oob_bad(a));
@@ -236,10 +242,6 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
   // vehicle at one wave per SIMD) -- and last the sums run over the chunk in
   // ascending vehicle order, by selects, exactly as one vehicle at a time.
   // Both passes walk the same chunk mask, so no index array is needed.
-  // Software-pipelined: the NEXT chunk's loads are issued before the current
-  // chunk is processed (the chunks hold different vehicles, so its stores
-  // cannot touch them), so a wave waits out one memory latency per word rather
-  // than one per chunk.
   constexpr int kEvChunk = 8;
   struct Chunk {
     uint64_t bits;
@@ -266,12 +268,12 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
         const int b = m ? __builtin_ctzll(m) : 0;    // past the chunk's end: a harmless reload
         const int v = w * 64 + b;
         C.rs[i] = req[(int64_t)v * n + e];
-        if (s.env_start) {       // randomize: this env's own vehicle table
+        if constexpr (MODE == kEvPerEnv) {       // randomize: this env's own vehicle table
           const double en = s.env_endp[(int64_t)v * n + e];
           C.tls[i] = (en - s.time) / 60.0;
           C.rcs[i] = 0.0;
           C.wins[i] = (s.time >= s.env_start[(int64_t)v * n + e]) && (s.time <= floor(en));
-        } else if (s.tl_rcp) {          // host table: the same IEEE quotient, and its reciprocal
+        } else if constexpr (MODE == kEvTable) { // host table: the same IEEE quotient, and its reciprocal
           const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[v];
           C.tls[i] = q.x;
           C.rcs[i] = q.y;
@@ -279,7 +281,7 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
           C.tls[i] = (endp[v] - s.time) / 60.0;
           C.rcs[i] = 0.0;
         }
-        if (!s.env_start) C.wins[i] = (win >> b) & 1ull;
+        if constexpr (MODE != kEvPerEnv) C.wins[i] = (win >> b) & 1ull;
         m &= m - 1;
       }
     };
@@ -297,9 +299,14 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
         act[i] = in && C.wins[i] && (r > 0.0);
         chg_now[i] = act[i] && (tl > 0.0);
         dep[i] = in && !act[i] && ((prev >> b) & 1ull);   // departed: not charging now (:239-243)
-        df[i] = pymax(0.0, p.rate - (s.tl_rcp ? exact_div(r, tl, rc) : r / tl));
+        if constexpr (MODE == kEvTable) df[i] = pymax(0.0, p.rate - exact_div(r, tl, rc));
+        else df[i] = pymax(0.0, p.rate - r / tl);
         cv[i] = pymin(kwh, r);
-        if (chg_now[i]) req[(int64_t)v * n + e] = r - cv[i];
+        // unconditional (the unchanged value where not charging): a store
+        // under a branch leaves the compiler no static count of outstanding
+        // memory operations, and it then waits for all of them (vmcnt(0)),
+        // stores included, before every later load's use
+        if (in) req[(int64_t)v * n + e] = chg_now[i] ? r - cv[i] : r;
       }
       m = C.bits;
 #pragma unroll
@@ -315,15 +322,19 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
         unserved = dep[i] ? unserved + C.rs[i] : unserved;
       }
     };
-    Chunk cur;
-    cur.bits = take(scan);
-    if (cur.bits) load(cur);
-    while (cur.bits) {
-      Chunk nxt;
-      nxt.bits = take(scan);
-      if (nxt.bits) load(nxt);
-      process(cur);
-      cur = nxt;
+    // two chunk buffers in turn: the next chunk's loads go out before the
+    // current chunk's stores (a copy `cur = next` would wait for them)
+    Chunk A, B;
+    A.bits = take(scan);
+    if (A.bits) load(A);
+    while (A.bits) {
+      B.bits = take(scan);
+      if (B.bits) load(B);
+      process(A);
+      if (!B.bits) break;
+      A.bits = take(scan);
+      if (A.bits) load(A);
+      process(B);
     }
     chg[(int64_t)w * n + e] = now_bits;
   }
@@ -343,6 +354,16 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
 #pragma unroll
   for (int j = 0; j < 6; ++j)
     st(obs, e, j, p.rescale ? to_scaled(st_[j], p.obs_low[j], p.obs_high[j]) : st_[j]);
+}
+
+__device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+                                            int64_t e, const pgw_mat& act, const double* __restrict__ endp,
+                                            double* __restrict__ req, uint64_t* __restrict__ chg,
+                                            const pgw_mat& obs, double* __restrict__ rp,
+                                            double* __restrict__ rew) {
+  if (s.env_start) ev_step_mode<kEvPerEnv>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  else if (s.tl_rcp) ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  else ev_step_mode<kEvDivide>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
 }
 
 __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step_info s, int64_t n,

@@ -1,0 +1,15 @@
+# PMC passes (each its own rocprofv3 run, --pmc only) over the C3 config bench:
+# where k_mc_step's waves spend their cycles.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/pmc
+export TMPDIR=/tmp
+TAG=${1:-c3}
+run_pass() {
+  name=$1; shift
+  cd /tmp && timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/$TAG/$name" -o run -- python3 "$GRAFT_REPO_ROOT/tools/bench_configs.py" --configs C3 --steps 100 --warmup 5 > "$GRAFT_REPO_ROOT/gpurun_out/pmc/${TAG}_$name.log" 2>&1
+  rc=$?; cd "$GRAFT_REPO_ROOT"; return $rc
+}
+run_pass p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA || exit $?
+run_pass p2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_WAIT_INST_LDS || exit $?
+python tools/gpu/pmc_summary.py $TAG
