@@ -60,6 +60,7 @@ PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
 PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 PF_KERNEL = ("k_coord_pf_split" if os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
              else "k_coord_pf<14,true,false,false>")
+PF_HALF = os.environ.get("PGW_PF_HALF", "0").startswith("1")   # 32 envs per PF wave (option, slower)
 KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_fused")     # PGW_T_* order
 
 
@@ -335,7 +336,7 @@ def main():
         mean_it, max_it = float(it.mean()), int(it.max())
         # the PF kernel runs one wave (64 envs) per SIMD: its time follows the
         # slowest wave, so report how many waves need 1, 2, ... iterations
-        wenv = 32 if PF_KERNEL == "k_coord_pf_split" else 64      # envs per PF wave
+        wenv = 32 if (PF_KERNEL == "k_coord_pf_split" or PF_HALF) else 64      # envs per PF wave
         wmax = env.pf_solver.iterations.abs()[: (n // wenv) * wenv].view(-1, wenv).max(1).values
         wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
         traffic = load_traffic()
@@ -352,7 +353,9 @@ def main():
             tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (p_us * 1e-6) / 1e12
             kernels[KERNELS[1]] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
                                    "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); "
-                                           "one wave per SIMD at 65,536 envs, latency-bound",
+                                           "latency-bound; %s" % ("32 envs per wave (each on two "
+                                           "lanes), two waves per SIMD at 65,536 envs" if PF_HALF else
+                                           "one wave per SIMD at 65,536 envs"),
                                    "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                                    "frac": tfs / FP64_PEAK_TFS,
                                    "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,

@@ -902,11 +902,19 @@ struct CoordPFArgs {
   double vv_lo, vv_hi, vv_penalty;
 };
 
-template <int M, bool UB, bool GC, bool KEEP, class Bufs>
+// EPW = envs per wave: 64 (one lane per env) or 32 (lanes l and l + 32 solve
+// the same env, and only the low half stores).  With 32 a launch has twice the
+// waves -- at 65,536 envs two per SIMD instead of one -- for the same
+// instructions per wave (the idea: a lone fp64 wave per SIMD issues its DPP
+// FMAs at about half the rate two waves reach, profiles/r01/fp64_issue.txt).
+// Slower in practice: see pf_half_waves.
+template <int M, bool UB, bool GC, bool KEEP, class Bufs, int EPW = 64>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
                                                      int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;   // double, or float (_f32)
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t e = EPW == 64 ? (int64_t)blockIdx.x * kBlock + threadIdx.x
+                              : ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * EPW + (threadIdx.x & (EPW - 1));
+  const bool owner = EPW == 64 || (threadIdx.x & 63) < EPW;   // the lane that stores env e
   const bool valid = e < n;
   // read once: a reload per phase would put an L2 round trip on the chain
   long long* const trace = g_pf_trace;
@@ -957,10 +965,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   double vsel = v0;
   if constexpr (kKeep)
     pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
-      if (valid && b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
+      if (valid && owner && b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
       vsel = (o == c.vv_row) ? v : vsel;
     });
-  if (!valid) return;
+  if (!valid || !owner) return;
   if (b.v_out) b.v_out[e] = (Sto)v0;
   if (b.iters) b.iters[e] = it;
   pf_trace(trace, 5);
@@ -1559,9 +1567,25 @@ static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t 
   return check_launch("k_pf_solve");
 }
 
+// Measured and not the default: 32 envs per wave ran 12.6 us against 9.2 us
+// (profiles/r02/pf_half_waves.txt) -- the iteration phase did not speed up
+// (3.6 vs 3.8 us per wave) and the waves' first loads and L2 gathers got
+// slower.  PGW_PF_HALF=1 selects it.
+static bool pf_half_waves() {
+  const char* v = getenv("PGW_PF_HALF");
+  return v && v[0] == '1';
+}
+
 template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_pf_tables& t,
                                int64_t n, const Bufs& b, hipStream_t st) {
+  if constexpr (M == 14 && UB && !GC && !KEEP) {
+    if (pf_half_waves()) {   // 32 envs per wave (the C4 fast path)
+      launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP, Bufs, 32>,
+                   dim3((unsigned)((n + 127) / 128)), dim3(kBlock), st, c, a, t, n, b);
+      return check_launch("k_coord_pf");
+    }
+  }
   launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP, Bufs>, dim3(grid_for(n)), dim3(kBlock), st, c, a,
                t, n, b);
   return check_launch("k_coord_pf");

@@ -19,8 +19,11 @@ for _ in range(40):
     env.step(torch.empty((5, n, 8), dtype=torch.float64, device="cuda").uniform_(-1, 1, generator=gen))
 torch.cuda.synchronize()
 split = os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
-wenv = 32 if split else 64          # envs per PF wave (k_coord_pf_split: two lanes per env)
-print("kernel:", "k_coord_pf_split" if split else "k_coord_pf")
+half = os.environ.get("PGW_PF_HALF", "0").startswith("1")
+# envs per PF wave (k_coord_pf_split: two lanes per env; k_coord_pf with half
+# waves: 32 envs, each on two lanes) -- the buffer needs 8 slots per wave
+wenv = 32 if (split or half) else 64
+print("kernel:", "k_coord_pf_split" if split else "k_coord_pf", "envs per wave", wenv)
 buf = torch.zeros((n // wenv, 8), dtype=torch.int64, device="cuda")
 _lib.check(_lib.lib().pgw_debug_pf_trace(_lib.dptr(buf)))
 for rep in range(3):
