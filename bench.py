@@ -61,7 +61,7 @@ PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 PF_KERNEL = ("k_coord_pf_split" if os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
              else "k_coord_pf<14,true,false,false>")
 PF_HALF = os.environ.get("PGW_PF_HALF", "0").startswith("1")   # 32 envs per PF wave (option, slower)
-KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_fused")     # PGW_T_* order
+KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_fused", "k_ma_step")   # PGW_T_* order
 
 
 def parse():

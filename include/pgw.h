@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 15
+#define PGW_ABI_VERSION 16
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -41,8 +41,8 @@ const char* pgw_last_error(void);
  * building_params, building_exo, building_ext, ev_params, ev_step_info,
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
  * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
- * mc_step_args, matf, coord_buffers_f32 -- lets a binding verify its
- * layouts.  Writes min(n, 22) values, returns 22. */
+ * mc_step_args, matf, coord_buffers_f32, ma_step_args -- lets a binding
+ * verify its layouts.  Writes min(n, 23) values, returns 23. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -387,10 +387,11 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
  * Kernel timing (benchmark instrumentation): while on, every `every`-th launch
  * of each kernel below is bracketed by HIP events on its own stream.
  * pgw_timing_stop synchronizes the recorded events and returns, per kernel,
- * the summed duration (ms) and the number of timed launches.
+ * the summed duration (ms) and the number of timed launches (PGW_T_COUNT
+ * entries each).
  * ---------------------------------------------------------------------- */
 enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COORD_FUSED = 3,
-       PGW_T_COUNT = 4 };
+       PGW_T_MA_STEP = 4, PGW_T_COUNT = 5 };
 /* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
 int32_t pgw_debug_pf_trace(long long* buf);
@@ -550,6 +551,77 @@ typedef struct pgw_mc_step_args {
 } pgw_mc_step_args;
 
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused multi-agent step over MC-kind components (the heterogeneous scenario,
+ * gridworld/scenarios/heterogeneous.py:13-112): MultiAgentEnv.step
+ * (gridworld/multiagent_env.py:151-212) for agents that are plain
+ * MultiComponentEnvs of the PGW_MC_* kinds or single PV / storage / EV envs,
+ * the per-bus load sums (:171-181) and the power flow -- two launches, one call.
+ * The component slots (at most PGW_MA_MAX_SLOTS over all agents, agents'
+ * slots contiguous and in component order) share ONE parameter set per kind,
+ * as in pgw_mc_step_args, except PV which has two (pv, pv2): at most one
+ * building, one storage and one EV component in total.
+ * A block of 64 envs runs n_waves waves, wave w stepping the slots
+ * wave_slot[wave_first[w] .. + wave_count[w]) one after another (e.g. one wave
+ * per building / EV slot, the light PV / storage slots together); after the
+ * block barrier wave 0 forms every agent's sums (0 + c0 + c1 ..., component
+ * order, base.py:125-156) and every bus's load (0 + a0 + a1 ..., agent order).
+ * ---------------------------------------------------------------------- */
+#define PGW_MA_MAX_SLOTS 8
+
+typedef struct pgw_ma_step_args {
+  int32_t n_comp, pad_;                     /* component slots                        */
+  pgw_mc_component comp[PGW_MA_MAX_SLOTS];  /* kind, action, obs, real_power per slot */
+  /* parameter sets, state and per-step values: the pgw_mc_step_args fields */
+  pgw_building_params bld;
+  pgw_building_exo bld_ex_t, bld_ex_next;
+  pgw_building_ext bld_ext;
+  double* bld_x;
+  double* bld_reward_state;
+  pgw_pv_params pv;
+  double pv_pmax;
+  const double* pv_min_voltage;
+  pgw_battery_params bat;
+  double* bat_soc;
+  pgw_ev_params ev;
+  pgw_ev_step_info ev_step;
+  const double* ev_endp;
+  double* ev_req;
+  uint64_t* ev_charging;
+  double* ev_reward;
+  /* second PV parameter set (slot_pv2[c] = 1) */
+  pgw_pv_params pv2;
+  double pv2_pmax;
+  const double* pv2_min_voltage;
+  /* per slot: owning agent; PV parameter set; PV band reward output (NULL =
+   * none): -(band_scale (min(0, v - band_lo) + min(0, band_hi - v)))^2 of the
+   * PV's min_voltage v (ThisPVEnv.step_reward, heterogeneous.py:47-52) */
+  int32_t slot_agent[PGW_MA_MAX_SLOTS];
+  int32_t slot_pv2[PGW_MA_MAX_SLOTS];
+  double* slot_reward[PGW_MA_MAX_SLOTS];
+  double band_lo, band_hi, band_scale;
+  /* agents: slots [first, first + count); bus = controllable-load slot of its
+   * bus (-1: none); sum = 1 for a MultiComponentEnv (real_power / reward get
+   * the in-order sums), 0 for a single component (its own buffers are the
+   * agent's) */
+  int32_t n_agents, n_bus;
+  int32_t agent_first[PGW_MAX_AGENTS], agent_count[PGW_MAX_AGENTS];
+  int32_t agent_bus[PGW_MAX_AGENTS], agent_sum[PGW_MAX_AGENTS];
+  double* agent_real_power[PGW_MAX_AGENTS];
+  double* agent_reward[PGW_MAX_AGENTS];
+  double* bus_p;                            /* n_bus x n bus loads (kW)               */
+  /* waves of a block: each slot listed once in wave_slot */
+  int32_t n_waves, pad2_;
+  int32_t wave_first[PGW_MA_MAX_SLOTS], wave_count[PGW_MA_MAX_SLOTS];
+  int32_t wave_slot[PGW_MA_MAX_SLOTS];
+} pgw_ma_step_args;
+
+/* The agents' step (k_ma_step), then -- pf != NULL -- pgw_pf_solve(pf, pft, n,
+ * a->bus_p, NULL, v_out, iters) on the same stream (pf->n_ctrl == a->n_bus).
+ * v_out may be NULL when pft carries v_min_out / v_max_out (extrema only). */
+int32_t pgw_ma_step(const pgw_ma_step_args* a, const pgw_pf_params* pf, const pgw_pf_tables* pft,
+                    int64_t n, double* v_out, int32_t* iters, void* stream);
 
 /* ------------------------------------------------------------------------
  * Home-Steward house: HSMultiComponentEnv.reset/step

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -154,6 +154,31 @@ class MCStepArgs(C.Structure):
                 ("ev_charging", vp), ("ev_reward", vp), ("real_power", vp), ("reward", vp)]
 
 
+MA_MAX_SLOTS = 8
+
+
+class MAStepArgs(C.Structure):
+    """pgw_ma_step_args: the pgw_mc_step_args fields (same names, so the
+    components' _mc_static / _mc_prepare fill it unchanged) with 8 slots, a
+    second PV parameter set and the agent / bus layout."""
+    _fields_ = [("n_comp", i32), ("pad_", i32), ("comp", MCComponent * MA_MAX_SLOTS),
+                ("bld", BuildingParams), ("bld_ex_t", BuildingExo), ("bld_ex_next", BuildingExo),
+                ("bld_ext", BuildingExt), ("bld_x", vp), ("bld_reward_state", vp),
+                ("pv", PVParams), ("pv_pmax", f64), ("pv_min_voltage", vp),
+                ("bat", BatteryParams), ("bat_soc", vp),
+                ("ev", EVParams), ("ev_step", EVStepInfo), ("ev_endp", vp), ("ev_req", vp),
+                ("ev_charging", vp), ("ev_reward", vp),
+                ("pv2", PVParams), ("pv2_pmax", f64), ("pv2_min_voltage", vp),
+                ("slot_agent", i32 * MA_MAX_SLOTS), ("slot_pv2", i32 * MA_MAX_SLOTS),
+                ("slot_reward", vp * MA_MAX_SLOTS), ("band_lo", f64), ("band_hi", f64), ("band_scale", f64),
+                ("n_agents", i32), ("n_bus", i32),
+                ("agent_first", i32 * MAX_AGENTS), ("agent_count", i32 * MAX_AGENTS),
+                ("agent_bus", i32 * MAX_AGENTS), ("agent_sum", i32 * MAX_AGENTS),
+                ("agent_real_power", vp * MAX_AGENTS), ("agent_reward", vp * MAX_AGENTS), ("bus_p", vp),
+                ("n_waves", i32), ("pad2_", i32), ("wave_first", i32 * MA_MAX_SLOTS),
+                ("wave_count", i32 * MA_MAX_SLOTS), ("wave_slot", i32 * MA_MAX_SLOTS)]
+
+
 class HSParams(C.Structure):
     _fields_ = [("n_comp", i32), ("kind", i32 * 4), ("obs_off", i32 * 4), ("rescale", i32 * 4),
                 ("n_veh", i32), ("n_dev", i32),
@@ -219,13 +244,15 @@ _SIGS = {
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
     "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
     "pgw_hs_step": (i32, [P(HSParams), P(HSStepInfo), i64, HSBuffers, vp]),
+    "pgw_ma_step": (i32, [P(MAStepArgs), P(PFParams), P(PFTables), i64, vp, vp, vp]),
 }
 
 EXPORTED = sorted(_SIGS)
 
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
-           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32]
+           CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32,
+           MAStepArgs]
 
 _lib = None
 

@@ -81,20 +81,25 @@ class PVEnv(ComponentEnv):
         return self._obs, {"real_power": float(-self.data[self.index])}
 
     mc_kind = 1
+    # the PV parameter set of the fused step's args this env fills: pgw_mc_step_args
+    # has one; pgw_ma_step_args a second one (pv2 ...) for a second PV env
+    _mc_pv_fields = ("pv", "pv_pmax", "pv_min_voltage")
 
     def _mc_static(self, args, slot):
-        args.pv = self.params
+        f = self._mc_pv_fields if hasattr(args, "pv2_pmax") else PVEnv._mc_pv_fields
+        setattr(args, f[0], self.params)
         c = args.comp[slot]
         c.kind, c.obs, c.real_power = 1, _lib.mat(self._obs), self._real_power.data_ptr()
 
     def _mc_prepare(self, args, slot, action, kwargs):
         a, m = self._action_mat(action, 1)
         self._mc_pmax = float(self.data[self.index])
-        args.pv_pmax = self._mc_pmax
+        f = self._mc_pv_fields if hasattr(args, "pv2_pmax") else PVEnv._mc_pv_fields
+        setattr(args, f[1], self._mc_pmax)
         vmin = None
         if self.grid_aware:
             vmin = self._min_voltage(kwargs)
-            args.pv_min_voltage = vmin.data_ptr()
+            setattr(args, f[2], vmin.data_ptr())
         args.comp[slot].action = m
         return a, vmin
 

@@ -309,7 +309,12 @@ template <typename Store>
 __device__ __forceinline__ void building_write_obs(const pgw_building_params& p, const double T[5],
                                                    const pgw_building_exo& ex, double p_cons,
                                                    const BuildingExt& xv, Store store) {
-  for (int j = 0; j < p.n_obs; ++j) {
+  // unrolled to constant indices: a loop bound by n_obs indexed the by-value
+  // params dynamically, which made the compiler copy the whole kernel-argument
+  // struct to scratch (k_ma_step<false>: 3.2 KB per lane)
+#pragma unroll
+  for (int j = 0; j < PGW_BLD_MAX_OBS; ++j) {
+    if (j >= p.n_obs) break;
     double v = building_obs_value(p.obs_var[j], T, ex, p_cons, xv);
     v = clip(v, p.obs_low[j], p.obs_high[j]);
     if (p.rescale) v = to_scaled(v, p.obs_low[j], p.obs_high[j]);

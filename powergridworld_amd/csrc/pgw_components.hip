@@ -442,6 +442,102 @@ __global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a, BldDerived 
   a.reward[e] = rew_sum;
 }
 
+// ====================================================================== fused multi-agent step
+// MultiAgentEnv.step (multiagent_env.py:151-212) of MC-kind agents, e.g. the
+// heterogeneous scenario (scenarios/heterogeneous.py:13-112): a block of
+// n_comp waves serves 64 envs, wave w running component slot w (k_mc_step's
+// layout, widened to every agent's components: the components of all agents
+// are independent within a step -- each reads only its own action and state
+// and the PREVIOUS power flow's voltages).  After the block barrier wave 0
+// forms each MultiComponentEnv agent's sums in component order (base.py:125-156)
+// and each bus's load in agent order (multiagent_env.py:171-181), the values and
+// operation order of pgw_agent_reduce.
+//
+// Waves: the building and the EV (the long per-env chains) get a wave each and
+// the light PV / storage slots share one (pgw_ma_step_args.wave_*): a wave per
+// slot made the heterogeneous scenario's blocks 5 waves, which at the kernel's
+// register count did not all fit at once.
+template <bool STD>
+__global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_args a, BldDerived d,
+                                                                   int64_t n) {
+  __shared__ double s_rp[PGW_MA_MAX_SLOTS][64], s_rew[PGW_MA_MAX_SLOTS][64];
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  // the wave's role, uniform: a building or an EV slot runs alone in its wave,
+  // the light PV / storage slots one after another (a loop over every kind let
+  // the compiler hoist all parameter loads of every path into one prologue,
+  // spilling SGPRs: 10 us for a PV-only step)
+  const int c0 = a.wave_slot[a.wave_first[wv]];
+  const int kind0 = a.comp[c0].kind;
+  if (e < n) {
+    if (kind0 == PGW_MC_BUILDING) {
+      const pgw_mc_component& C = a.comp[c0];
+      s_rp[c0][lane] = building_step_env<STD>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
+                                              C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
+      s_rew[c0][lane] = a.bld_reward_state[e];        // the fresh reward (MC semantics)
+    } else if (kind0 == PGW_MC_EV) {
+      const pgw_mc_component& C = a.comp[c0];
+      ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs, C.real_power,
+                  a.ev_reward);
+      s_rp[c0][lane] = C.real_power[e];               // this thread's own writes
+      s_rew[c0][lane] = a.ev_reward[e];
+    } else {
+      for (int i = 0; i < a.wave_count[wv]; ++i) {
+        const int w = a.wave_slot[a.wave_first[wv] + i];
+        const pgw_mc_component& C = a.comp[w];
+        double rp, rew = 0.0;
+        if (C.kind == PGW_MC_PV) {
+          const bool two = a.slot_pv2[w] != 0;
+          const double* vmin = two ? a.pv2_min_voltage : a.pv_min_voltage;
+          rp = pv_step_env(two ? a.pv2 : a.pv, e, two ? a.pv2_pmax : a.pv_pmax, C.action, vmin, C.obs);
+          if (a.slot_reward[w]) {                     // ThisPVEnv.step_reward: k_band_penalty's ops
+            const double x = vmin[e];
+            const double l = x - a.band_lo, u = a.band_hi - x;
+            const double viol = ((l < 0.0) ? l : 0.0) + ((u < 0.0) ? u : 0.0);
+            const double y = a.band_scale * viol;
+            rew = -(y * y);
+            a.slot_reward[w][e] = rew;
+          }
+        } else {
+          rp = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
+        }
+        C.real_power[e] = rp;
+        s_rp[w][lane] = rp;
+        s_rew[w][lane] = rew;
+      }
+    }
+  }
+  __syncthreads();
+  if (wv != 0 || e >= n) return;
+  double ap[PGW_MAX_AGENTS];
+#pragma unroll
+  for (int g = 0; g < PGW_MAX_AGENTS; ++g) {     // (constant indices: ap stays in registers)
+    ap[g] = 0.0;
+    if (g >= a.n_agents) continue;
+    const int c0 = a.agent_first[g];
+    if (a.agent_sum[g]) {
+      double rp_sum = 0.0, rew_sum = 0.0;
+      for (int c = c0; c < c0 + a.agent_count[g]; ++c) {
+        rp_sum = rp_sum + s_rp[c][lane];
+        rew_sum = rew_sum + s_rew[c][lane];
+      }
+      a.agent_real_power[g][e] = rp_sum;
+      a.agent_reward[g][e] = rew_sum;
+      ap[g] = rp_sum;
+    } else {
+      ap[g] = s_rp[c0][lane];
+    }
+  }
+  for (int b = 0; b < a.n_bus; ++b) {
+    double acc = 0.0;
+#pragma unroll
+    for (int g = 0; g < PGW_MAX_AGENTS; ++g)
+      acc = (g < a.n_agents && a.agent_bus[g] == b) ? acc + ap[g] : acc;
+    a.bus_p[(int64_t)b * n + e] = acc;
+  }
+}
+
 // ====================================================================== MC reduce
 __global__ void __launch_bounds__(kBlock) k_agent_reduce(pgw_reduce_args a, int64_t n,
                                                          double* __restrict__ rp,
@@ -601,6 +697,88 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   else
     hipLaunchKernelGGL(k_mc_step<false>, grid, block, 0, (hipStream_t)stream, *a, d, n);
   return check_launch("k_mc_step");
+}
+
+int32_t pgw_ma_step(const pgw_ma_step_args* a, const pgw_pf_params* pf, const pgw_pf_tables* pft,
+                    int64_t n, double* v_out, int32_t* iters, void* stream) {
+  PGW_REQUIRE(a && n >= 0 && a->n_comp >= 1 && a->n_comp <= PGW_MA_MAX_SLOTS, "pgw_ma_step: bad args");
+  PGW_REQUIRE(a->n_agents >= 1 && a->n_agents <= PGW_MAX_AGENTS, "pgw_ma_step: bad n_agents");
+  PGW_REQUIRE(a->n_bus >= 0 && a->n_bus <= PGW_PF_MAX_CTRL && (a->n_bus == 0 || a->bus_p),
+              "pgw_ma_step: bad n_bus / bus_p");
+  int once = 0, pvs = 0, next = 0;
+  for (int g = 0; g < a->n_agents; ++g) {
+    PGW_REQUIRE(a->agent_first[g] == next && a->agent_count[g] >= 1, "pgw_ma_step: agent %d slots", g);
+    next += a->agent_count[g];
+    PGW_REQUIRE(a->agent_bus[g] >= -1 && a->agent_bus[g] < a->n_bus, "pgw_ma_step: agent %d bus", g);
+    PGW_REQUIRE(!a->agent_sum[g] || (a->agent_real_power[g] && a->agent_reward[g]),
+                "pgw_ma_step: agent %d outputs", g);
+    PGW_REQUIRE(a->agent_sum[g] || a->agent_count[g] == 1, "pgw_ma_step: agent %d: one slot unless summed", g);
+    for (int c = a->agent_first[g]; c < next && c < a->n_comp; ++c)
+      PGW_REQUIRE(a->slot_agent[c] == g, "pgw_ma_step: slot %d agent", c);
+  }
+  PGW_REQUIRE(next == a->n_comp, "pgw_ma_step: agents cover %d of %d slots", next, a->n_comp);
+  PGW_REQUIRE(a->n_waves >= 1 && a->n_waves <= a->n_comp, "pgw_ma_step: bad n_waves");
+  int listed = 0, wnext = 0;
+  for (int w = 0; w < a->n_waves; ++w) {
+    PGW_REQUIRE(a->wave_first[w] == wnext && a->wave_count[w] >= 1, "pgw_ma_step: wave %d slots", w);
+    wnext += a->wave_count[w];
+  }
+  PGW_REQUIRE(wnext == a->n_comp, "pgw_ma_step: waves list %d of %d slots", wnext, a->n_comp);
+  for (int w = 0; w < a->n_waves; ++w)
+    for (int i = 0; i < a->wave_count[w]; ++i) {
+      const int k = a->comp[a->wave_slot[a->wave_first[w] + i] & (PGW_MA_MAX_SLOTS - 1)].kind;
+      PGW_REQUIRE(a->wave_count[w] == 1 || k == PGW_MC_PV || k == PGW_MC_STORAGE,
+                  "pgw_ma_step: a building or EV slot needs a wave of its own");
+    }
+  for (int i = 0; i < a->n_comp; ++i) {
+    const int c = a->wave_slot[i];
+    PGW_REQUIRE(c >= 0 && c < a->n_comp && !(listed & (1 << c)), "pgw_ma_step: wave_slot %d", i);
+    listed |= 1 << c;
+  }
+  // no building: the STD instantiation (its building branch never runs); the
+  // generic building's instantiation keeps a scratch copy of the arguments
+  bool std_bld = true;
+  for (int c = 0; c < a->n_comp; ++c) {
+    const pgw_mc_component& C = a->comp[c];
+    PGW_REQUIRE(C.kind >= 0 && C.kind <= 3, "pgw_ma_step: slot %d kind", c);
+    PGW_REQUIRE(C.action.ptr && C.obs.ptr && C.real_power, "pgw_ma_step: slot %d buffers", c);
+    if (C.kind == PGW_MC_PV) {
+      const bool two = a->slot_pv2[c] != 0;
+      PGW_REQUIRE(!(pvs & (two ? 2 : 1)), "pgw_ma_step: PV parameter set %d used twice", two ? 2 : 1);
+      pvs |= two ? 2 : 1;
+      const pgw_pv_params& p = two ? a->pv2 : a->pv;
+      const double* vmin = two ? a->pv2_min_voltage : a->pv_min_voltage;
+      PGW_REQUIRE(!p.grid_aware || vmin, "pgw_ma_step: slot %d min_voltage", c);
+      PGW_REQUIRE(!a->slot_reward[c] || vmin, "pgw_ma_step: slot %d band reward needs min_voltage", c);
+    } else {
+      PGW_REQUIRE(!(once & (1 << C.kind)), "pgw_ma_step: one building / storage / EV component at most");
+      once |= 1 << C.kind;
+      PGW_REQUIRE(!a->slot_reward[c], "pgw_ma_step: slot %d: band reward on a PV only", c);
+    }
+    if (C.kind == PGW_MC_BUILDING) {
+      PGW_REQUIRE(a->bld_x && a->bld_reward_state && a->bld.n_obs <= PGW_BLD_MAX_OBS,
+                  "pgw_ma_step: building buffers");
+      std_bld = bld_is_std(a->bld);
+    }
+    if (C.kind == PGW_MC_STORAGE) PGW_REQUIRE(a->bat_soc, "pgw_ma_step: storage buffers");
+    if (C.kind == PGW_MC_EV)
+      PGW_REQUIRE(a->ev_endp && a->ev_req && a->ev_charging && a->ev_reward &&
+                  a->ev_step.n_words <= PGW_EV_MAX_WORDS && !a->ev_step.env_start == !a->ev_step.env_endp &&
+                  (!a->ev_step.env_start || !a->ev_step.tl_rcp), "pgw_ma_step: EV buffers");
+  }
+  if (pf) PGW_REQUIRE(pft && pf->n_ctrl == a->n_bus, "pgw_ma_step: pf n_ctrl %d != n_bus %d",
+                      pf ? pf->n_ctrl : 0, a->n_bus);
+  if (n == 0) return PGW_OK;
+  const BldDerived d = make_bld_derived(a->bld);
+  const dim3 grid((unsigned)((n + 63) / 64)), block(64u * (unsigned)a->n_waves);
+  hipStream_t st = (hipStream_t)stream;
+  if (std_bld)
+    launch_timed(PGW_T_MA_STEP, k_ma_step<true>, grid, block, st, *a, d, n);
+  else
+    launch_timed(PGW_T_MA_STEP, k_ma_step<false>, grid, block, st, *a, d, n);
+  const int32_t rc = check_launch("k_ma_step");
+  if (rc || !pf) return rc;
+  return pgw_pf_solve(pf, pft, n, a->n_bus ? a->bus_p : nullptr, nullptr, v_out, iters, stream);
 }
 
 int32_t pgw_agent_reduce(const pgw_reduce_args* a, int64_t n, double* real_power, double* reward,

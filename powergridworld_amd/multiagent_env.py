@@ -105,6 +105,7 @@ class MultiAgentEnv(Env):
         self.action_space = {agent.name: agent.action_space for agent in self.agents}
 
         self._fused = None
+        self._ma = None              # fused multi-agent path (pgw_ma_step), see _setup_ma
         self._fused_steps = 0
         # every agent reports the base class's reactive power (its zero buffer)
         self._q_zero = all(type(a).reactive_power is ComponentEnv.reactive_power for a in self.agents)
@@ -116,10 +117,15 @@ class MultiAgentEnv(Env):
                     raise ValueError("dtype=%s: %s" % (self.dtype, why))
             if why is None:
                 self._setup_fused()
-            elif fused is True:
-                raise ValueError("fused=True but this configuration cannot be fused: " + why)
             else:
-                logger.info("MultiAgentEnv: generic path (%s)", why)
+                why_ma = self._ma_fusable() if self.dtype == torch.float64 else "fp32 storage"
+                if why_ma is None:
+                    self._setup_ma()
+                elif fused is True:
+                    raise ValueError("fused=True but this configuration cannot be fused: %s; "
+                                     "multi-agent step: %s" % (why, why_ma))
+                else:
+                    logger.info("MultiAgentEnv: generic path (%s; %s)", why, why_ma)
         if self._fused is None:
             buses = sorted(set(self.agent_name_bus_map.values()))
             self.pf_solver.set_controllable_loads(buses)
@@ -221,6 +227,8 @@ class MultiAgentEnv(Env):
         self.obs_dict = {}
         if self._fused is not None:
             obs, rew, done, meta = self._step_fused(action)
+        elif self._ma is not None:
+            obs, rew, done, meta = self._step_ma(action)
         else:
             obs, rew, done, meta = self._step_generic(action)
         any_done = any(done.values())
@@ -478,6 +486,10 @@ class MultiAgentEnv(Env):
         full.set_controllable_loads(ctrl)
         if reset:                                   # the reset solve: no controllable load
             full.calculate_power_flow(current_time=self.time)
+        elif self._ma is not None:                  # the step's bus loads, as the kernel summed them
+            bus_p = self._ma["bus_p"]
+            full.calculate_power_flow(p_controllable_consumed={c: bus_p[k] for k, c in enumerate(ctrl)},
+                                      current_time=self.time)
         else:
             sums, p = {}, F["params"]
             for ai in range(len(self.agents)):
@@ -614,6 +626,189 @@ class MultiAgentEnv(Env):
             F["meta"]["voltage_violation"] = F["vv"]
         F["meta"]["oob_actions"] = self.oob_count
         self._fused = F
+
+    # ================================================================ fused multi-agent path
+    def _ma_fusable(self):
+        """pgw_ma_step runs MultiAgentEnv.step for agents that are plain
+        MultiComponentEnvs of fusable components or single PV / storage / EV envs
+        (the heterogeneous scenario), with the base class's hooks and transforms,
+        at most one building / storage / EV and two PV components in all, and no
+        agent observing a bus voltage (min / max voltage are the previous solve's
+        extrema, which the power flow's epilogue writes)."""
+        from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+        if not isinstance(self.pf_solver, OpenDSSSolver):
+            return "power flow solver is not the batched OpenDSSSolver"
+        if len(self.agents) > _lib.MAX_AGENTS:
+            return "more than %d agents" % _lib.MAX_AGENTS
+        cls = type(self)
+        for hook in ("get_external_obs_vars", "step", "reset", "get_obs", "reward_transform",
+                     "meta_transform"):
+            if getattr(cls, hook) is not getattr(MultiAgentEnv, hook):
+                return "%s is overridden" % hook
+        if set(self.pf_solver.output_names) != set(self.pf_solver.feeder.node_names):
+            return "the solver does not output every node"
+        kinds, slots = [], 0
+        for a in self.agents:
+            if "bus_voltage" in a.obs_labels:
+                return "agent %s observes its bus voltage" % a.name
+            if type(a) is MultiComponentEnv:
+                if not a._mc_fusable():
+                    return "agent %s has components the fused step does not implement" % a.name
+                for e in a.envs:
+                    if getattr(type(e), "fused_band_reward", None) is not None:
+                        return "a voltage-band PV inside a MultiComponentEnv"
+                    kinds.append(type(e).mc_kind)
+                slots += len(a.envs)
+                continue
+            k = getattr(type(a), "mc_kind", None)
+            if k not in (1, 2, 3):
+                return "agent %s is neither a MultiComponentEnv nor a single PV / storage / EV" % a.name
+            owner = next(c for c in type(a).__mro__ if "mc_kind" in c.__dict__)
+            band = getattr(type(a), "fused_band_reward", None)
+            rew_owner = owner
+            if band is not None:
+                rew_owner = next(c for c in type(a).__mro__ if "fused_band_reward" in c.__dict__)
+                if not a.grid_aware:
+                    return "voltage-band PV %s does not observe min_voltage" % a.name
+            if type(a).step is not owner.step or type(a).step_reward is not rew_owner.step_reward:
+                return "agent %s overrides its step or reward" % a.name
+            kinds.append(k)
+            slots += 1
+        if slots > _lib.MA_MAX_SLOTS:
+            return "more than %d components" % _lib.MA_MAX_SLOTS
+        for k, cap in ((0, 1), (1, 2), (2, 1), (3, 1)):
+            if kinds.count(k) > cap:
+                return "more than %d component(s) of kind %d" % (cap, k)
+        return None
+
+    def _setup_ma(self):
+        n, dev = self.num_envs, self.device
+        solver = self.pf_solver
+        solver.set_controllable_loads(sorted(set(self.agent_name_bus_map.values())))
+        ctrl = list(solver._ctrl_names)
+        args = _lib.MAStepArgs()
+        ext = {"min_voltage": solver._vmin, "max_voltage": solver._vmax}
+        plan, slot, n_pv = [], 0, 0
+        for g, agent in enumerate(self.agents):
+            multi = type(agent) is MultiComponentEnv
+            envs = list(agent.envs) if multi else [agent]
+            args.agent_first[g], args.agent_count[g], args.agent_sum[g] = slot, len(envs), int(multi)
+            bus = self.agent_name_bus_map[agent.name]
+            args.agent_bus[g] = ctrl.index(bus) if bus in ctrl else -1
+            if multi:
+                args.agent_real_power[g] = agent._real_power.data_ptr()
+                args.agent_reward[g] = agent._reward.data_ptr()
+            # the external obs the agent would get (get_external_obs_vars), per component
+            kw_agent = {k: v for k, v in ext.items() if k in agent.obs_labels}
+            comps = []
+            for e in envs:
+                if getattr(type(e), "mc_kind", None) == 1:
+                    e._mc_pv_fields = ("pv", "pv_pmax", "pv_min_voltage") if n_pv == 0 else \
+                        ("pv2", "pv2_pmax", "pv2_min_voltage")
+                    args.slot_pv2[slot] = n_pv
+                    n_pv += 1
+                e._mc_static(args, slot)
+                args.slot_agent[slot] = g
+                rew = None
+                band = getattr(type(e), "fused_band_reward", None)
+                if band is not None:
+                    rew = e._band_buffer()
+                    args.slot_reward[slot] = rew.data_ptr()
+                    args.band_lo, args.band_hi, args.band_scale = [float(x) for x in band]
+                kw = {k: v for k, v in kw_agent.items() if k in e.obs_labels} if multi else kw_agent
+                comps.append((e, slot, kw, rew))
+                slot += 1
+            plan.append((agent, multi, comps))
+        args.n_comp, args.n_agents, args.n_bus = slot, len(self.agents), len(ctrl)
+        # waves of a block: the building and the EV (the long per-env chains) one
+        # each, the light PV / storage slots together in one more
+        kinds = [args.comp[c].kind for c in range(slot)]
+        waves = [[c] for c in range(slot) if kinds[c] in (0, 3)]
+        light = [c for c in range(slot) if kinds[c] not in (0, 3)]
+        if light:
+            waves.append(light)
+        args.n_waves = len(waves)
+        i = 0
+        for w, cs in enumerate(waves):
+            args.wave_first[w], args.wave_count[w] = i, len(cs)
+            for c in cs:
+                args.wave_slot[i] = c
+                i += 1
+        bus_p = torch.zeros((max(len(ctrl), 1), n), dtype=torch.float64, device=dev)
+        args.bus_p = bus_p.data_ptr()
+        self._ma = {"args": args, "plan": plan, "bus_p": bus_p, "ctrl": ctrl,
+                    "iters": torch.zeros(n, dtype=torch.int32, device=dev),
+                    "lazy_v": _FusedVoltages(self, {}, 0), "bufv": self._ma_bufv(plan)}
+
+    @staticmethod
+    def _ma_bufv(plan):
+        return tuple(e._bufv for _, _, comps in plan for e, _, _, _ in comps)
+
+    def _step_ma(self, action):
+        """MultiAgentEnv.step (multiagent_env.py:151-212) in one call: the
+        components' per-step values into the launch arguments, pgw_ma_step
+        (every agent's components + sums + bus loads, then the power flow with the
+        extrema epilogue), then the components' clocks and the return dicts."""
+        M = self._ma
+        if self._ma_bufv(M["plan"]) != M["bufv"]:        # a component re-pointed its buffers
+            self._setup_ma()
+            M = self._ma
+        args = M["args"]
+        keep = []
+        obs, rew, done, meta = {}, {}, {}, {}
+        for agent, multi, comps in M["plan"]:
+            act = action[agent.name]
+            if multi:
+                for e, slot, kw, _ in comps:
+                    keep.append(e._mc_prepare(args, slot, act[e.name], kw))
+            else:
+                e, slot, kw, _ = comps[0]
+                keep.append(e._mc_prepare(args, slot, act, kw))
+        solver = self.pf_solver
+        pfp, pft = solver.step_params(self.time), solver.step_tables(self.time)
+        H = self._hist
+        v_out = None
+        if H is not None:                            # every node into this step's history slot
+            s_ = H["t"] % H["cap"]
+            v_out = H["v"][s_].data_ptr()
+        rc = _lib.lib().pgw_ma_step(args, pfp, pft, self.num_envs, v_out, M["iters"].data_ptr(),
+                                    _lib.stream_ptr(self.device))
+        if rc:
+            _lib.check(rc)
+        agent_power_p = []
+        for agent, multi, comps in M["plan"]:
+            name = agent.name
+            if multi:
+                o, d, m = {}, False, {}
+                for e, slot, kw, _ in comps:
+                    ob, _, de, me = e._mc_finish(kw)
+                    o[e.name], m[e.name] = ob, me
+                    d = d or de
+                obs[name], rew[name], done[name], meta[name] = o, agent._reward, d, m
+            else:
+                e, slot, kw, band = comps[0]
+                ob, r, d, me = e._mc_finish(kw)
+                if band is not None:
+                    r = band
+                elif r is None:
+                    r = e._zero_reward
+                obs[name], rew[name], done[name], meta[name] = ob, r, d, me
+            agent_power_p.append(agent.real_power)
+        solver.iterations = M["iters"]
+        self._fused_steps += 1
+        if H is None:
+            # the extrema the epilogue wrote; every node solved on first access
+            lazy = M["lazy_v"]
+            lazy._step, lazy._reset, lazy._full = self._fused_steps, False, None
+            self.voltages = solver.bus_voltages = lazy
+        else:
+            solver.bind_output(H["v"][s_])
+            solver._prepare_bus_voltages()
+            self.voltages = solver.bus_voltages
+        solver._extrema = (solver._vmin, solver._vmax)
+        self._record(agent_power_p)
+        meta["oob_actions"] = self.oob_count
+        return obs, rew, done, meta
 
     def action_buffer(self):
         """Packed [n_agents, N, act_dim] action tensor the fused step reads

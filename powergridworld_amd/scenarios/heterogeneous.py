@@ -2,10 +2,12 @@
 (gridworld/scenarios/heterogeneous.py:13-112): a MultiComponentEnv building
 (building + PV + storage), a grid-aware PV farm rewarded for keeping the
 feeder's minimum voltage inside [0.95, 1.05], and 25 EVs x 40, all on load
-675c of the IEEE-13 feeder.  It runs the generic MultiAgentEnv path: the PV
-farm observes min_voltage (the minimum over all node voltages of the previous
-power flow, multiagent_env.py:107-113) and its reward is a Python hook on [N]
-tensors."""
+675c of the IEEE-13 feeder.  The PV farm observes min_voltage (the minimum over
+all node voltages of the previous power flow, multiagent_env.py:107-113) and
+is rewarded on it.  By default MultiAgentEnv runs it on the fused multi-agent
+path (pgw_ma_step: every agent in one launch plus the power flow); fused=False
+selects the generic path (per-agent kernels, the reward as a Python hook on
+[N] tensors)."""
 import pandas as pd
 import torch
 
@@ -22,14 +24,23 @@ from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
 @register_env
 class ThisPVEnv(PVEnv):
     """PV farm rewarded on the bus voltage (heterogeneous.py:47-54):
-    -(1000 (min(0, v - 0.95) + min(0, 1.05 - v)))^2 with v = min_voltage."""
+    -(1000 (min(0, v - 0.95) + min(0, 1.05 - v)))^2 with v = min_voltage.
+    The fused multi-agent step (pgw_ma_step) evaluates the same expression in its
+    kernel when this class declares it here: (lo, hi, scale)."""
+
+    fused_band_reward = (0.95, 1.05, 1000.0)
+
+    def _band_buffer(self):
+        if self.__dict__.get("_band_rew") is None:
+            self._band_rew = torch.empty(self.num_envs, dtype=torch.float64, device=self.device)
+        return self._band_rew
 
     def step_reward(self, **kwargs):
         v = as_env_tensor(kwargs["min_voltage"], self.num_envs, self.device, "min_voltage")
-        if self.__dict__.get("_band_rew") is None:
-            self._band_rew = torch.empty(self.num_envs, dtype=torch.float64, device=self.device)
+        self._band_buffer()
+        lo, hi, scale = self.fused_band_reward
         # one kernel: -(1000 (min(0, v - 0.95) + min(0, 1.05 - v)))^2
-        _lib.check(_lib.lib().pgw_voltage_band_penalty(self.num_envs, v.data_ptr(), 0.95, 1.05, 1000.0,
+        _lib.check(_lib.lib().pgw_voltage_band_penalty(self.num_envs, v.data_ptr(), lo, hi, scale,
                                                         self._band_rew.data_ptr(), self._stream()))
         return self._band_rew, {}
 

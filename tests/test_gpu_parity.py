@@ -480,17 +480,20 @@ def test_c4_batch_one_and_ragged():
 
 
 # ------------------------------------------------------------------ heterogeneous
-def test_heterogeneous_scenario_golden():
+@pytest.mark.parametrize("fused", ["auto", False])
+def test_heterogeneous_scenario_golden(fused):
     """The reference's 3-agent heterogeneous scenario (MC building, grid-aware
-    PV farm rewarded on min_voltage, EV 25x40) on the generic path, against the
-    reference run (tests/golden/het_scenario.npz, PF = the oracle behind the
-    reference's PowerFlowSolver ABC), a whole 286-step episode."""
+    PV farm rewarded on min_voltage, EV 25x40) on the fused multi-agent path
+    (pgw_ma_step, the default) and the generic path, against the reference run
+    (tests/golden/het_scenario.npz, PF = the oracle behind the reference's
+    PowerFlowSolver ABC), a whole 286-step episode."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     g = load("het_scenario")
     Tn, K, _ = g["actions"].shape
-    env = MultiAgentEnv(**make_env_config(), num_envs=K, device=DEV)
+    env = MultiAgentEnv(**make_env_config(), num_envs=K, device=DEV, fused=fused)
     assert env._fused is None
+    assert (env._ma is not None) == (fused == "auto")
     env.reset()
     bld = env.agent_dict["building"]
     bld.env_dict["storage"].reset(init_storage=T(g["init_storage"]))
@@ -513,6 +516,75 @@ def test_heterogeneous_scenario_golden():
         close(torch.stack([rew[nm] for nm in ("building", "pv", "ev-charging")], 1), g["reward"][t],
               1e-7, 1e-7)
         assert dones["__all__"] == bool(g["done"][t, 0])
+
+
+def _het_actions(rng, n, T_):
+    """Seeded uniform actions, 20 % pushed past the box (the kernels clip them)."""
+    a = rng.uniform(-1.2, 1.2, size=(T_, n, 10))
+    return torch.tensor(a, device=DEV)
+
+
+def _het_act(a):
+    return {"building": {"building": a[:, :6], "pv": a[:, 6:7], "storage": a[:, 7:8]},
+            "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
+
+
+@pytest.mark.parametrize("record_history", [False, True])
+def test_het_multiagent_step_equals_generic(record_history):
+    """pgw_ma_step (the heterogeneous scenario's fused path: every agent's
+    components in one launch, the per-bus sums, the power flow with the
+    extrema epilogue) against the generic per-agent path, bit for bit, over a
+    whole episode and across the reset into a second one, at 4 096 envs:
+    observations, rewards, dones, real powers, min/max voltage, iterations and
+    every node voltage (solved on first access on the fused path, or written
+    into the history ring)."""
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    n = 4096
+    envs = [MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=f, record_history=record_history)
+            for f in ("auto", False)]
+    assert envs[0]._ma is not None and envs[1]._ma is None
+    rng = np.random.default_rng(11)
+    acts = _het_actions(rng, n, 300)
+    soc0 = T(rng.uniform(5.0, 240.0, size=n))
+
+    def flat(o):
+        return torch.cat([o["building"]["building"], o["building"]["pv"], o["building"]["storage"],
+                          o["pv"], o["ev-charging"]], 1)
+
+    nodes = envs[0].pf_solver.feeder.node_names
+    t_act = 0
+    for ep in range(2):
+        outs = []
+        for env in envs:
+            env.reset()
+            env.agent_dict["building"].env_dict["storage"].reset(init_storage=soc0)
+            outs.append(flat(env.get_obs()))
+        assert torch.equal(outs[0], outs[1])
+        steps = 0
+        while True:
+            res = [env.step(_het_act(acts[t_act % len(acts)])) for env in envs]
+            (o0, r0, d0, m0), (o1, r1, d1, m1) = res
+            assert torch.equal(flat(o0), flat(o1))
+            for nm in ("building", "pv", "ev-charging"):
+                assert torch.equal(r0[nm], r1[nm]), nm
+                assert torch.equal(envs[0].agent_dict[nm].real_power, envs[1].agent_dict[nm].real_power), nm
+            assert d0 == d1
+            e0, e1 = envs[0].pf_solver.voltage_extrema(), envs[1].pf_solver.voltage_extrema()
+            assert torch.equal(e0[0], e1[0]) and torch.equal(e0[1], e1[1])
+            assert torch.equal(envs[0].pf_solver.iterations, envs[1].pf_solver.iterations)
+            if steps % 97 == 0 or d0["__all__"]:
+                v0, v1 = envs[0].pf_solver.get_bus_voltages(), envs[1].pf_solver.get_bus_voltages()
+                for x in nodes:
+                    assert torch.equal(v0[x], v1[x]), x
+            t_act += 1
+            steps += 1
+            if d0["__all__"] or (ep == 1 and steps == 5):
+                break
+    assert (envs[0].pf_solver.iterations > 0).all()
+    if record_history:
+        h0, h1 = envs[0].voltage_history(), envs[1].voltage_history()
+        assert torch.equal(h0[0], h1[0]) and torch.equal(h0[1], h1[1]) and h0[2] == h1[2]
 
 
 # ------------------------------------------------------------------ Home-Steward house (SURVEY 8(f) rank 1)

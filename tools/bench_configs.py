@@ -6,7 +6,8 @@ heterogeneous.py) and HS = the Home-Steward house (base_hs.py) at 65536.  Each s
 with actions resident in HBM (a pool of pre-generated batches); episodes reset
 inside the timed region.  One JSON line per config.
 
-Usage: python tools/bench_configs.py [--configs C2,C3,HET] [--steps K] [--warmup W]
+Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS] [--steps K] [--warmup W]
+(HETG: the heterogeneous scenario on the generic path, fused=False)
 """
 import argparse
 import json
@@ -89,10 +90,10 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16):
                 steps=steps, seconds=dt)
 
 
-def bench_het(dev, steps, warmup, n=65536, pool=16):
+def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto"):
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     from powergridworld_amd.multiagent_env import MultiAgentEnv
-    env = MultiAgentEnv(**make_env_config(), num_envs=n, device=dev)
+    env = MultiAgentEnv(**make_env_config(), num_envs=n, device=dev, fused=fused)
     gen = torch.Generator(dev).manual_seed(0)
     acts = []
     for _ in range(pool):
@@ -110,8 +111,10 @@ def bench_het(dev, steps, warmup, n=65536, pool=16):
         return dones["__all__"]
 
     dt = timed_loop(env, step, env.reset, steps, warmup)
-    return dict(config="HET", workload="3-agent heterogeneous (MC building, grid-aware PV farm, "
-                                       "EV 25x40) + IEEE-13 PF", batch=n, agents=3, steps=steps, seconds=dt)
+    return dict(config="HET" if fused else "HETG",
+                workload="3-agent heterogeneous (MC building, grid-aware PV farm, EV 25x40) + IEEE-13 PF, "
+                         + ("fused multi-agent step (pgw_ma_step)" if env._ma is not None else "generic path"),
+                batch=n, agents=3, steps=steps, seconds=dt)
 
 
 def bench_hs(dev, steps, warmup, n=65536, pool=16):
@@ -140,7 +143,8 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    fns = {"C2": bench_c2, "C3": bench_c3, "HET": bench_het, "HS": bench_hs}
+    fns = {"C2": bench_c2, "C3": bench_c3, "HET": bench_het, "HS": bench_hs,
+           "HETG": lambda *a: bench_het(*a, fused=False)}
     for name in args.configs.split(","):
         r = fns[name](dev, args.steps, args.warmup)
         units = r["batch"] * r["agents"] * r["steps"]

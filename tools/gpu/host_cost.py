@@ -48,8 +48,8 @@ for timing in (False, True):
     dt = time.perf_counter() - t0
     lib.pgw_coord_step = orig
     if timing:
-        tot = (_lib.C.c_double * 3)()
-        cnt = (_lib.C.c_int64 * 3)()
+        tot = (_lib.C.c_double * 8)()
+        cnt = (_lib.C.c_int64 * 8)()
         _lib.check(lib.pgw_timing_stop(tot, cnt))
     print("timing=%s: %.1f us/step total, pgw_coord_step call %.1f us" %
           (timing, dt / k * 1e6, acc[0] / max(acc[1], 1) * 1e6))

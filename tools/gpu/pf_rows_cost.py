@@ -38,7 +38,7 @@ def run(params, tables, v_out, label, reps=200):
     for _ in range(reps):
         _lib.check(lib.pgw_pf_solve(params, tables, n, cp.data_ptr(), None, v_out, None, st))
     torch.cuda.synchronize()
-    ms, cnt = (ctypes.c_double * 3)(), (ctypes.c_int64 * 3)()
+    ms, cnt = (ctypes.c_double * 8)(), (ctypes.c_int64 * 8)()
     _lib.check(lib.pgw_timing_stop(ms, cnt))
     k = 2                                        # PGW_T_PF_SOLVE
     print("%-34s %7.2f us/launch (%d timed)" % (label, ms[k] * 1e3 / max(cnt[k], 1), cnt[k]))
