@@ -44,6 +44,18 @@ inline void launch_timed(int id, K kernel, dim3 grid, dim3 block, hipStream_t st
   }
 }
 
+// A kernel's FIRST by-value struct argument read in place from the kernarg
+// segment (constant address space: scalar loads, dynamic indices included).
+// Naming the by-value parameter itself makes clang copy it into a private
+// alloca that the optimizer must then remove; in the big fused-step kernels it
+// did not always (k_ma_step<false> copied its 3.2 KB argument struct to
+// scratch per lane: a PV-only step took 38.9 us instead of 5.1).
+#ifdef __HIP_DEVICE_COMPILE__
+#define PGW_KERNARG0(T) (*(const T*)__builtin_amdgcn_kernarg_segment_ptr())
+#else
+#define PGW_KERNARG0(T) (*(const T*)nullptr)
+#endif
+
 constexpr int kBlock = 256;   // 4 waves of 64
 
 inline unsigned grid_for(int64_t n) {

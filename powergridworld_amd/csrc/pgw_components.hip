@@ -418,7 +418,8 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const pg
 // forms the sums in component order -- the same values and the same operation
 // order as one lane doing everything, without any cross-block synchronisation.
 template <bool STD>
-__global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a, BldDerived d, int64_t n) {
+__global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a_, BldDerived d, int64_t n) {
+  const pgw_mc_step_args& a = PGW_KERNARG0(pgw_mc_step_args);
   __shared__ double s_rp[4][64], s_rew[4][64];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
   const int lane = threadIdx.x & 63;
@@ -458,8 +459,9 @@ __global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a, BldDerived 
 // slot made the heterogeneous scenario's blocks 5 waves, which at the kernel's
 // register count did not all fit at once.
 template <bool STD>
-__global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_args a, BldDerived d,
+__global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_args a_, BldDerived d,
                                                                    int64_t n) {
+  const pgw_ma_step_args& a = PGW_KERNARG0(pgw_ma_step_args);
   __shared__ double s_rp[PGW_MA_MAX_SLOTS][64], s_rew[PGW_MA_MAX_SLOTS][64];
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
@@ -735,8 +737,7 @@ int32_t pgw_ma_step(const pgw_ma_step_args* a, const pgw_pf_params* pf, const pg
     PGW_REQUIRE(c >= 0 && c < a->n_comp && !(listed & (1 << c)), "pgw_ma_step: wave_slot %d", i);
     listed |= 1 << c;
   }
-  // no building: the STD instantiation (its building branch never runs); the
-  // generic building's instantiation keeps a scratch copy of the arguments
+  // no building: the STD instantiation (its building branch never runs)
   bool std_bld = true;
   for (int c = 0; c < a->n_comp; ++c) {
     const pgw_mc_component& C = a->comp[c];

@@ -792,10 +792,11 @@ __device__ __forceinline__ S ld_act(const S* p) {
 // pgw_coord_buffers (fp64) or pgw_coord_buffers_f32 (fp32 storage: loads are
 // widened, every store rounds the fp64 result once).
 template <class Bufs>
-__global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p,
+__global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p_,
                                                              pgw_coord_step_info s, int64_t n,
                                                              Bufs b, double pv_ob,
                                                              StdDerived dv) {
+  const pgw_coord_params& p = PGW_KERNARG0(pgw_coord_params);   // (no private copy)
   using S = std::remove_pointer_t<decltype(b.soc)>;
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int a = blockIdx.y;
