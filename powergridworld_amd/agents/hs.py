@@ -9,6 +9,7 @@ the house hands it views of its state.  Stepping one on its own is not
 supported -- the reference's components need the house's meta_state kwargs.
 """
 import json
+import math
 import os
 
 import numpy as np
@@ -115,7 +116,8 @@ class HSEnergyStorageEnv(_HSComponent):
         n = self.num_envs
         self.soc = torch.zeros(n, dtype=torch.float64, device=self.device)
         self.cost = torch.full((n,), float(initial_storage_cost), dtype=torch.float64, device=self.device)
-        self._rng = np.random.default_rng()
+        self._gen = torch.Generator(device=self.device)
+        self.seed(None)
 
     @property
     def current_storage(self):
@@ -126,12 +128,17 @@ class HSEnergyStorageEnv(_HSComponent):
         return self.cost
 
     def initial_soc(self, init_storage=None):
-        """reset's SoC (:80-105): clip(init_storage), or the truncated normal draw."""
+        """reset's SoC (:80-105): clip(init_storage), or the truncated normal draw
+        truncnorm(-1, 1) * std + mean, drawn on the device by inverse-CDF sampling
+        (z = sqrt(2) erfinv(2 u' - 1), u' ~ U[Phi(-1), Phi(1)]), as
+        EnergyStorageEnv does: scipy's host sampler cost ~4 ms per reset at
+        65 536 envs (14 us per step of a 286-step episode)."""
         if init_storage is None:
-            from scipy.stats import truncnorm
-            draw = truncnorm(-1, 1).rvs(size=self.num_envs, random_state=self._rng)
-            v = draw * self.initial_storage_std + self.initial_storage_mean
-            return torch.as_tensor(v, dtype=torch.float64, device=self.device)
+            lo = 0.5 * (1.0 + math.erf(-1.0 / math.sqrt(2.0)))
+            hi = 0.5 * (1.0 + math.erf(1.0 / math.sqrt(2.0)))
+            u = torch.rand(self.num_envs, dtype=torch.float64, device=self.device, generator=self._gen)
+            z = math.sqrt(2.0) * torch.special.erfinv(2.0 * (lo + u * (hi - lo)) - 1.0)
+            return z * self.initial_storage_std + self.initial_storage_mean
         t = init_storage if isinstance(init_storage, torch.Tensor) else torch.as_tensor(
             np.asarray(init_storage, dtype=np.float64))
         t = t.to(device=self.device, dtype=torch.float64).reshape(-1)
@@ -140,7 +147,8 @@ class HSEnergyStorageEnv(_HSComponent):
         return t.contiguous()
 
     def seed(self, seed=None):
-        self._rng = np.random.default_rng(seed)
+        """Seed the initial-SoC sampler (the reference draws from NumPy's global RNG)."""
+        self._gen.manual_seed(int(seed) if seed is not None else int(torch.seed() % (2 ** 63)))
 
 
 @register_env
