@@ -225,14 +225,22 @@ __device__ __forceinline__ void hs_ev(const pgw_hs_params& p, const pgw_hs_step_
 __device__ __forceinline__ void hs_devices(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
                                            bool reset, double a, const HSMeta& M, HSState& S, double& rp,
                                            double* ob, const HSRec& R) {
-  for (int c = 0; c < p.n_dev; ++c) ob[c] = rescale ? to_scaled(s.dev_obs[c], 0.0, p.dev_obs_high[c]) : s.dev_obs[c];
+#pragma unroll
+  for (int c = 0; c < PGW_HS_MAX_DEV; ++c) {
+    if (c >= p.n_dev) break;
+    ob[c] = rescale ? to_scaled(s.dev_obs[c], 0.0, p.dev_obs_high[c]) : s.dev_obs[c];
+  }
   if (reset) return;
   if (rescale) {
     oob_note(p.oob, oob_bad(a));
     a = to_raw(a, p.dev_act_low, p.dev_act_high);
   }
   double sum = 0.0;
-  for (int c = 0; c < p.n_dev; ++c) sum = sum + s.dev_power[c];
+#pragma unroll
+  for (int c = 0; c < PGW_HS_MAX_DEV; ++c) {
+    if (c >= p.n_dev) break;
+    sum = sum + s.dev_power[c];
+  }
   rp = a * sum;
   double sc = 0.0, bc = 0.0, gc = 0.0;
   if (fabs(rp) < 0.0005) {                 // round(rp, 3) == 0.0
@@ -252,9 +260,10 @@ __device__ __forceinline__ void hs_devices(const pgw_hs_params& p, const pgw_hs_
   R.put(9, M.grid - gc);
 }
 
-__global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p, pgw_hs_step_info s, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p_, pgw_hs_step_info s, int64_t n,
                                                pgw_hs_buffers b, const double* __restrict__ init_soc,
                                                int reset) {
+  const pgw_hs_params& p = PGW_KERNARG0(pgw_hs_params);   // (no private copy)
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
   HSMeta M;
@@ -266,39 +275,49 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p, pgw_hs_step_info
   S.soc_cost = b.soc_cost[e];
   S.ev_cost = b.ev_cost[e];
   S.dev_cost = b.dev_cost[e];
-  int slot_storage = -1;
-  for (int c = 0; c < p.n_comp; ++c) {
+  double rp_storage = 0.0;
+  // The chain is unrolled over its (at most 4) slots and every case stores its
+  // own observations: with a loop over n_comp the per-slot arrays (S.rp, ob)
+  // were indexed dynamically and lived in scratch (288 B per lane).
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c >= p.n_comp) break;
     const double a = reset ? 0.0 : ld(b.action, e, c);
     const HSRec R = {(!reset && b.step_meta) ? b.step_meta + (int64_t)c * PGW_HS_META_FIELDS * n : nullptr, n, e};
     double ob[8];
-    int dim = 0;
+    const int off = p.obs_off[c];
     S.rp[c] = 0.0;
     switch (p.kind[c]) {
       case PGW_HS_PV:
         hs_pv(p, s, p.rescale[c], reset, a, M, S.rp[c], ob, R);
-        dim = 1;
+        st(b.obs, e, off, ob[0]);
         break;
       case PGW_HS_STORAGE:
         if (!reset) hs_storage(p, s, p.rescale[c], a, M, S, S.rp[c], R);
-        slot_storage = c;
+        rp_storage = S.rp[c];
         ob[0] = S.soc;
         ob[1] = S.soc_cost;
         if (p.rescale[c]) {
           ob[0] = to_scaled(ob[0], p.soc_min, p.soc_max);
           ob[1] = to_scaled(ob[1], 0.0, p.max_storage_cost);
         }
-        dim = 2;
+        st(b.obs, e, off, ob[0]);
+        st(b.obs, e, off + 1, ob[1]);
         break;
       case PGW_HS_EV:
         hs_ev(p, s, p.rescale[c], reset, a, n, e, b, M, S, S.rp[c], ob, R);
-        dim = 7;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) st(b.obs, e, off + j, ob[j]);
         break;
       default:
         hs_devices(p, s, p.rescale[c], reset, a, M, S, S.rp[c], ob, R);
-        dim = p.n_dev;
+#pragma unroll
+        for (int j = 0; j < PGW_HS_MAX_DEV; ++j) {
+          if (j >= p.n_dev) break;
+          st(b.obs, e, off + j, ob[j]);
+        }
         break;
     }
-    for (int j = 0; j < dim; ++j) st(b.obs, e, p.obs_off[c] + j, ob[j]);
   }
   b.soc[e] = S.soc;
   b.soc_cost[e] = S.soc_cost;
@@ -307,11 +326,13 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p, pgw_hs_step_info
   if (reset) return;
   // base_hs.py:157-180: real power and the house reward, components in chain order
   double rp = 0.0, rew = 0.0;
-  for (int c = 0; c < p.n_comp; ++c) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c >= p.n_comp) break;
     rp = rp + S.rp[c];
     const int k = p.kind[c];
     const double r = k == PGW_HS_PV ? 0.0
-                   : k == PGW_HS_STORAGE ? hs_storage_reward(p, M, S, S.rp[slot_storage])
+                   : k == PGW_HS_STORAGE ? hs_storage_reward(p, M, S, rp_storage)
                    : k == PGW_HS_EV ? S.rew_ev : S.rew_dev;
     rew = rew + r;
   }
