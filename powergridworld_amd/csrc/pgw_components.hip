@@ -174,7 +174,7 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
 }
 
 template <bool STD>
-__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p, BldDerived d,
+__global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p_, BldDerived d,
                                                           pgw_building_exo ex,
                                                           pgw_building_exo exn, int64_t n, pgw_mat act,
                                                           double* __restrict__ x,
@@ -182,6 +182,7 @@ __global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p,
                                                           double* __restrict__ rout,
                                                           double* __restrict__ rstate, int32_t lagged,
                                                           pgw_building_ext ext, pgw_mat obs) {
+  const pgw_building_params& p = PGW_KERNARG0(pgw_building_params);   // (no private copy)
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
   (void)building_step_env<STD>(p, d, ex, exn, n, e, act, x, pcons, rout, rstate, lagged, ext, obs);

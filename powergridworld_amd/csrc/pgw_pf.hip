@@ -827,9 +827,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_agents_std(pgw_coord_params p_
 // (std_agent_compute<2>), each exactly as alone.  Needs env-minor action / obs
 // views (s_env == 1), an even n and even strides (pairs_ok).
 template <class Bufs>
-__global__ void __launch_bounds__(kBlock) k_coord_agents_std_x2(pgw_coord_params p,
+__global__ void __launch_bounds__(kBlock) k_coord_agents_std_x2(pgw_coord_params p_,
                                                                 pgw_coord_step_info s, int64_t n,
                                                                 Bufs b, double pv_ob, StdDerived dv) {
+  const pgw_coord_params& p = PGW_KERNARG0(pgw_coord_params);   // (no private copy)
   using S = std::remove_pointer_t<decltype(b.soc)>;
   typedef S S2 __attribute__((ext_vector_type(2)));
   const int64_t e = 2 * ((int64_t)blockIdx.x * kBlock + threadIdx.x);
