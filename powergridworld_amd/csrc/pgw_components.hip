@@ -275,7 +275,12 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
           C.rcs[i] = 0.0;
           C.wins[i] = (s.time >= s.env_start[(int64_t)v * n + e]) && (s.time <= floor(en));
         } else if constexpr (MODE == kEvTable) { // host table: the same IEEE quotient, and its reciprocal
-          const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[v];
+          // a VECTOR load of the (uniform) entry: it returns in order with the
+          // chunk's requirement loads (vmcnt), where scalar loads return out of
+          // order and made every chunk wait for all of them (lgkmcnt(0))
+          int vv = v;
+          asm volatile("" : "+v"(vv));
+          const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[vv];
           C.tls[i] = q.x;
           C.rcs[i] = q.y;
         } else {
