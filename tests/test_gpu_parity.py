@@ -587,6 +587,49 @@ def test_het_multiagent_step_equals_generic(record_history):
         assert torch.equal(h0[0], h1[0]) and torch.equal(h0[1], h1[1]) and h0[2] == h1[2]
 
 
+def test_heterogeneous_golden_full_batch_tiled():
+    """The heterogeneous golden's 2 reference trajectories tiled over 65 536 envs
+    on the fused multi-agent path: every env reproduces its trajectory for the
+    whole episode (obs incl. the PV farm's min_voltage, all three rewards, the
+    done flags, and the node voltages at a few steps), compared on the device."""
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    g = load("het_scenario")
+    Tn, K, _ = g["actions"].shape
+    n = 65536
+    rep = n // K
+    env = MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV)
+    assert env._ma is not None
+    env.reset()
+    env.agent_dict["building"].env_dict["storage"].reset(init_storage=T(np.tile(g["init_storage"], rep)))
+    G_obs, G_rew = T(g["obs"]), T(g["reward"])
+    names = [str(x) for x in g["node_names"]]
+
+    def flat(o):
+        return torch.cat([o["building"]["building"], o["building"]["pv"], o["building"]["storage"],
+                          o["pv"], o["ev-charging"]], 1)
+
+    def check(got, want, rtol, atol, what):
+        want = want.unsqueeze(0).expand(rep, *want.shape).reshape(got.shape)
+        bad = ~torch.isclose(got, want, rtol=rtol, atol=atol)
+        assert not bool(bad.any()), "%s: %d mismatches" % (what, int(bad.sum()))
+
+    check(flat(env.get_obs()), G_obs[0], 1e-10, 1e-10, "reset obs")
+    acts = T(np.tile(g["actions"], (1, rep, 1)))
+    for t in range(Tn):
+        a = acts[t]
+        act = {"building": {"building": a[:, :6], "pv": a[:, 6:7], "storage": a[:, 7:8]},
+               "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
+        obs, rew, dones, _ = env.step(act)
+        check(flat(obs), G_obs[t + 1], 1e-9, 1e-9, "obs step %d" % t)
+        check(torch.stack([rew[nm] for nm in ("building", "pv", "ev-charging")], 1), G_rew[t], 1e-7, 1e-7,
+              "reward step %d" % t)
+        assert dones["__all__"] == bool(g["done"][t, 0])
+        if t % 95 == 0:
+            v = torch.stack([env.pf_solver.get_bus_voltages()[nm] for nm in names], 1)
+            check(v, T(g["voltages"][t + 1]), 1e-9, 0, "voltages step %d" % t)
+
+
 # ------------------------------------------------------------------ Home-Steward house (SURVEY 8(f) rank 1)
 def _hs_run(env, g, names, n_rep=1, meta_every=1):
     """Step `env` (batch K * n_rep, golden actions tiled) through the golden's
