@@ -529,18 +529,18 @@ def _het_act(a):
             "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
 
 
-@pytest.mark.parametrize("record_history", [False, True])
-def test_het_multiagent_step_equals_generic(record_history):
+@pytest.mark.parametrize("record_history,n", [(False, 4096), (True, 4096), (False, 1000), (False, 1)])
+def test_het_multiagent_step_equals_generic(record_history, n):
     """pgw_ma_step (the heterogeneous scenario's fused path: every agent's
     components in one launch, the per-bus sums, the power flow with the
     extrema epilogue) against the generic per-agent path, bit for bit, over a
     whole episode and across the reset into a second one, at 4 096 envs:
     observations, rewards, dones, real powers, min/max voltage, iterations and
     every node voltage (solved on first access on the fused path, or written
-    into the history ring)."""
+    into the history ring); also at a ragged batch (1000: a partial last block)
+    and at batch 1."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
-    n = 4096
     envs = [MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=f, record_history=record_history)
             for f in ("auto", False)]
     assert envs[0]._ma is not None and envs[1]._ma is None
