@@ -116,13 +116,19 @@ class EnergyStorageEnv(ComponentEnv):
 
     def step(self, action, **kwargs):
         """(:131-157)"""
-        a = as_action(action, self.num_envs, 1, self.device, self.dtype)
+        if self.dtype == torch.float64:      # (pgw_mat cached per action tensor)
+            a, m = self._action_mat(action, 1)
+        else:
+            a = as_action(action, self.num_envs, 1, self.device, self.dtype)
+            m = self._act_mat(a)
         c = self.__dict__.get("_step_c")
         if c is None or c[0] is not self._real_power:      # per-layout constants, built once
             c = self._step_c = (self._real_power, getattr(_lib.lib(), self._k_step),
                                 _lib.dptr(self.soc), self._mat(self._obs), _lib.dptr(self._real_power),
                                 self._obs, {"state_of_charge": self.soc.unsqueeze(1)})
-        _lib.check(c[1](self.params, self.num_envs, self._act_mat(a), c[2], c[3], c[4], self._stream()))
+        rc = c[1](self.params, self.num_envs, m, c[2], c[3], c[4], self._stream())
+        if rc:
+            _lib.check(rc)
         self.simulation_step += 1
         return c[5], self._zero_reward, self.is_terminal(), c[6]
 
