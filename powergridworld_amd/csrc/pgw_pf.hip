@@ -446,12 +446,21 @@ __device__ __forceinline__ void pf_row_load(const double* s, int o, double (&w)[
 #pragma unroll
   for (int p = 0; p < PFRow<M>::kPairs; ++p) w[p] = r[16 * p];
 }
-template <int M, class F>
+// SQ = false: f receives |V|^2 (fma(vi, vi, vr * vr), before pf_node_pu's
+// sqrt) -- for extrema-only solves, whose min / max over the rows are the sqrt
+// of the min / max of |V|^2 (sqrt is monotone and correctly rounded).
+template <int M, bool SQ = true>
+__device__ __forceinline__ double pf_mag(double vr, double vi) {
+  const double m2 = fma(vi, vi, vr * vr);
+  return SQ ? sqrt(m2) : m2;
+}
+template <int M, bool SQ = true, class F>
 __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_lds, const double* s,
                                             int n_out, const double (&ir)[M], const double (&ii)[M],
                                             F&& f) {
-  if (!rows_lds) {
-    for (int o = 1; o < n_out; ++o) f(o, pf_node_pu<M>(t, o, ir, ii));
+  if (!rows_lds) {   // (SQ only: the extrema-only caller needs the staged rows)
+    if constexpr (SQ)
+      for (int o = 1; o < n_out; ++o) f(o, pf_node_pu<M>(t, o, ir, ii));
     return;
   }
   constexpr int P = PFRow<M>::kPairs;
@@ -470,8 +479,8 @@ __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_ld
     __builtin_amdgcn_sched_barrier(0);
     double ar, ai, br, bi, cr, ci, dr, di;
     pf_row4_dpp<M>(ar, ai, br, bi, cr, ci, dr, di, wa, wb, wc, wd, ir, ii);
-    const double ua = sqrt(fma(ai, ai, ar * ar)), ub = sqrt(fma(bi, bi, br * br));
-    const double uc = sqrt(fma(ci, ci, cr * cr)), ud = sqrt(fma(di, di, dr * dr));
+    const double ua = pf_mag<M, SQ>(ar, ai), ub = pf_mag<M, SQ>(br, bi);
+    const double uc = pf_mag<M, SQ>(cr, ci), ud = pf_mag<M, SQ>(dr, di);
     f(o, ua);
     f(o + 1, ub);
     f(o + 2, uc);
@@ -488,19 +497,19 @@ __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_ld
   if (o < n_out) {
     double ar, ai;
     pf_row1_dpp<M>(ar, ai, wa, ir, ii);
-    f(o, sqrt(fma(ai, ai, ar * ar)));
+    f(o, pf_mag<M, SQ>(ar, ai));
     ++o;
   }
   if (o < n_out) {
     double ar, ai;
     pf_row1_dpp<M>(ar, ai, wb, ir, ii);
-    f(o, sqrt(fma(ai, ai, ar * ar)));
+    f(o, pf_mag<M, SQ>(ar, ai));
     ++o;
   }
   if (o < n_out) {
     double ar, ai;
     pf_row1_dpp<M>(ar, ai, wc, ir, ii);
-    f(o, sqrt(fma(ai, ai, ar * ar)));
+    f(o, pf_mag<M, SQ>(ar, ai));
   }
 }
 
@@ -549,12 +558,26 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   // the output rows with every lane still here (their DPP broadcasts read all
   // lanes); lanes past n store nothing
   double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
-  if constexpr (kKeep)
-    pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
-      if (valid && v_out) v_out[(int64_t)o * n + e] = v;
-      vmn = (v < vmn) ? v : vmn;
-      vmx = (v > vmx) ? v : vmx;
-    });
+  if constexpr (kKeep) {
+    if (v_out || !rows_lds) {
+      pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
+        if (valid && v_out) v_out[(int64_t)o * n + e] = v;
+        vmn = (v < vmn) ? v : vmn;
+        vmx = (v > vmx) ? v : vmx;
+      });
+    } else {
+      // extrema only: min / max of |V|^2 over the rows, one sqrt each at the end
+      // -- the same values (sqrt is monotone and correctly rounded), without a
+      // sqrt per row
+      double mn2 = fma(v0i, v0i, v0r * v0r), mx2 = mn2;
+      pf_rows_out<M, false>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int, double m2) {
+        mn2 = (m2 < mn2) ? m2 : mn2;
+        mx2 = (m2 > mx2) ? m2 : mx2;
+      });
+      vmn = sqrt(mn2);
+      vmx = sqrt(mx2);
+    }
+  }
   pf_trace(trace, 5);
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
