@@ -538,7 +538,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   }
   S.powers(a, cp, cq, (t.load_scale && valid) ? t.load_scale[e] : 1.0);
   pf_trace(trace, 1);
-  S.initial(a, t, e, valid);
+  S.template initial<true>(a, t, e, valid);   // (speculative record load: see below)
   pf_trace(trace, 2);
   double v0r, v0i, ir[M], ii[M];
   const int it = S.template iterate<kKeep>(a.max_iter, valid, v0r, v0i, ir, ii);
