@@ -246,6 +246,7 @@ class FiveZoneROMEnv(ComponentEnv):
         if obs is not None:
             self._obs = obs
         self._bufv += 1
+        ComponentEnv._bufv_gen += 1
 
     def _ext(self, kw):
         n = self.num_envs

@@ -83,6 +83,7 @@ class EnergyStorageEnv(ComponentEnv):
         if obs is not None:
             self._obs = obs
         self._bufv += 1
+        ComponentEnv._bufv_gen += 1
         self._step_c = None
 
     def reset(self, init_storage=None, **kwargs):

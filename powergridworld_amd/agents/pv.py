@@ -67,6 +67,7 @@ class PVEnv(ComponentEnv):
         if obs is not None:
             self._obs = obs
         self._bufv += 1
+        ComponentEnv._bufv_gen += 1
 
     def _min_voltage(self, kwargs):
         if not self.grid_aware:

@@ -151,6 +151,7 @@ class ComponentEnv(spaces.Env, ABC):
     # _bufv counts re-pointings of the env's device buffers (_adopt): cached
     # launch arguments that hold their pointers are rebuilt when it changes.
     _bufv = 0
+    _bufv_gen = 0      # any env's re-pointing (one int for a whole agent set to check)
 
     def _act_mat(self, a):
         """pgw_mat of an action tensor, cached per (pointer, strides): a policy

@@ -736,9 +736,14 @@ class MultiAgentEnv(Env):
                 i += 1
         bus_p = torch.zeros((max(len(ctrl), 1), n), dtype=torch.float64, device=dev)
         args.bus_p = bus_p.data_ptr()
-        self._ma = {"args": args, "plan": plan, "bus_p": bus_p, "ctrl": ctrl,
+        # per-step calls, flattened: (prepare, slot, agent name, component name or
+        # None, kwargs) in slot order
+        calls = [(e._mc_prepare, slot, agent.name, e.name if multi else None, kw)
+                 for agent, multi, comps in plan for e, slot, kw, _ in comps]
+        self._ma = {"args": args, "plan": plan, "bus_p": bus_p, "ctrl": ctrl, "calls": calls,
                     "iters": torch.zeros(n, dtype=torch.int32, device=dev),
-                    "lazy_v": _FusedVoltages(self, {}, 0), "bufv": self._ma_bufv(plan)}
+                    "lazy_v": _FusedVoltages(self, {}, 0), "bufv": self._ma_bufv(plan),
+                    "gen": ComponentEnv._bufv_gen, "fn": _lib.lib().pgw_ma_step}
 
     @staticmethod
     def _ma_bufv(plan):
@@ -750,20 +755,17 @@ class MultiAgentEnv(Env):
         (every agent's components + sums + bus loads, then the power flow with the
         extrema epilogue), then the components' clocks and the return dicts."""
         M = self._ma
-        if self._ma_bufv(M["plan"]) != M["bufv"]:        # a component re-pointed its buffers
-            self._setup_ma()
+        if ComponentEnv._bufv_gen != M["gen"]:       # some env re-pointed its buffers
+            if self._ma_bufv(M["plan"]) != M["bufv"]:
+                self._setup_ma()
             M = self._ma
+            M["gen"] = ComponentEnv._bufv_gen
         args = M["args"]
         keep = []
         obs, rew, done, meta = {}, {}, {}, {}
-        for agent, multi, comps in M["plan"]:
-            act = action[agent.name]
-            if multi:
-                for e, slot, kw, _ in comps:
-                    keep.append(e._mc_prepare(args, slot, act[e.name], kw))
-            else:
-                e, slot, kw, _ = comps[0]
-                keep.append(e._mc_prepare(args, slot, act, kw))
+        for prep, slot, aname, cname, kw in M["calls"]:
+            act = action[aname]
+            keep.append(prep(args, slot, act if cname is None else act[cname], kw))
         solver = self.pf_solver
         pfp, pft = solver.step_params(self.time), solver.step_tables(self.time)
         H = self._hist
@@ -771,8 +773,7 @@ class MultiAgentEnv(Env):
         if H is not None:                            # every node into this step's history slot
             s_ = H["t"] % H["cap"]
             v_out = H["v"][s_].data_ptr()
-        rc = _lib.lib().pgw_ma_step(args, pfp, pft, self.num_envs, v_out, M["iters"].data_ptr(),
-                                    _lib.stream_ptr(self.device))
+        rc = M["fn"](args, pfp, pft, self.num_envs, v_out, M["iters"].data_ptr(), _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
         agent_power_p = []
