@@ -61,7 +61,7 @@ class OpenDSSSolver(PowerFlowSolver):
 
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = 1e-10, max_iter: int = 100,
-                 output_nodes=None, predictor: bool = True, **kwargs):
+                 output_nodes=None, predictor: bool = True, warm_start: bool = False, **kwargs):
         super().__init__(**kwargs)
         self.num_envs = int(num_envs)
         self.device = _lib.require_device(device)
@@ -83,6 +83,16 @@ class OpenDSSSolver(PowerFlowSolver):
         self._hour_memo = {}
         self._ctrl_names = []
         self.use_predictor = bool(predictor)
+        # warm_start: without a predictor table (several controllable loads),
+        # each env's solve starts from its previous solution, as OpenDSS's snap
+        # solve starts from the last one (opendss.py:134): the same fixed point
+        # to tol, in fewer iterations than from the no-load voltages -- but the
+        # last bits then depend on the env's history (off by default: results
+        # reproducible per step, and the fused multi-bus step, which always
+        # starts cold, stays bit-identical to the generic one).
+        self.warm_start = bool(warm_start)
+        self._U_prev = None
+        self._warm = None
         self.set_output_nodes(output_nodes)
 
     # ------------------------------------------------------------ configuration
@@ -172,6 +182,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self._step_cache = {}
         self._tables_cache = {}
         self._pred_index = {}
+        self._warm = None              # (cold, warm) PFTables over the previous solutions
 
     def hour_of(self, current_time):
         """Hour of year of a step time (opendss.py:98-103), memoized per time."""
@@ -316,14 +327,43 @@ class OpenDSSSolver(PowerFlowSolver):
                 zeros = torch.zeros(n, dtype=torch.float64, device=self.device)
                 cp = torch.stack([x if x is not None else zeros for x in ps])
                 cq = torch.stack([x if x is not None else zeros for x in qs])
-        tables = self.step_tables(current_time) if cp is not None else self.tables
+        tables = self.solve_tables(current_time, cp is not None)
         _lib.check(_lib.lib().pgw_pf_solve(p, tables, n, _lib.dptr(cp), _lib.dptr(cq),
                                            _lib.dptr(self.v_out), _lib.dptr(self._iters),
                                            _lib.stream_ptr(self.device)))
+        self.solved(tables)
         self.iterations = self._iters
         self._prepare_bus_voltages()
         if self._all_nodes:                        # the epilogue's min / max over every node
             self._extrema = (self._vmin, self._vmax)
+
+    def solve_tables(self, current_time, controllable=True):
+        """The PFTables a solve at `current_time` uses: the hour's predictor tables
+        (one controllable load), else the cold-start tables -- or, with
+        warm_start, the ones over each env's previous solution."""
+        tables = self.step_tables(current_time) if controllable else self.tables
+        if controllable and self.warm_start and tables is self.tables:
+            tables = self._warm_tables()
+        return tables
+
+    def solved(self, tables):
+        """Call after a solve launched with solve_tables(): the warm-start buffer
+        now holds a solution."""
+        if self._warm is not None and tables is self._warm[0]:
+            self._warm_valid = True
+
+    def _warm_tables(self):
+        """PFTables writing each env's converged element voltages into a per-env
+        buffer (U_out) and, once it holds a solution, starting from it (U_init)."""
+        if self._warm is None:
+            if self._U_prev is None or self._U_prev.shape[1] != self.M:
+                self._U_prev = torch.zeros((self.num_envs, self.M, 2), dtype=torch.float64, device=self.device)
+            cold = _lib.PFTables.from_buffer_copy(self.tables)
+            cold.U_out = self._U_prev.data_ptr()
+            warm = _lib.PFTables.from_buffer_copy(cold)
+            warm.U_init = self._U_prev.data_ptr()
+            self._warm, self._warm_valid = (cold, warm), False
+        return self._warm[1] if self._warm_valid else self._warm[0]
 
     def unconverged(self) -> int:
         """Envs whose last solve stopped at max_iter without meeting tol (the

@@ -767,7 +767,7 @@ class MultiAgentEnv(Env):
             act = action[aname]
             keep.append(prep(args, slot, act if cname is None else act[cname], kw))
         solver = self.pf_solver
-        pfp, pft = solver.step_params(self.time), solver.step_tables(self.time)
+        pfp, pft = solver.step_params(self.time), solver.solve_tables(self.time, args.n_bus > 0)
         H = self._hist
         v_out = None
         if H is not None:                            # every node into this step's history slot
@@ -776,6 +776,7 @@ class MultiAgentEnv(Env):
         rc = M["fn"](args, pfp, pft, self.num_envs, v_out, M["iters"].data_ptr(), _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
+        solver.solved(pft)
         agent_power_p = []
         for agent, multi, comps in M["plan"]:
             name = agent.name

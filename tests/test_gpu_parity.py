@@ -876,3 +876,32 @@ def test_fused_voltages_on_demand_only():
     for x in ref.voltages:
         assert torch.equal(got[x], ref.voltages[x]), x        # the on-demand rows: bit-identical
     assert "_pf_full" in env.__dict__
+
+
+def test_pf_warm_start_multi_bus():
+    """OpenDSSSolver(warm_start=True), for layouts without a predictor table (two
+    controllable buses): every env's solve starts from its previous solution, as
+    OpenDSS's snap solve does (opendss.py:134).  Same fixed point as the cold
+    start (rtol 1e-9 on every node over 40 steps), in fewer iterations."""
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    n = 4096
+    kw = dict(feeder_file="ieee_13_dss/IEEE13Nodeckt.dss",
+              loadshape_file="ieee_13_dss/annual_hourly_load_profile.csv",
+              system_load_rescale_factor=0.7, num_envs=n, device=DEV)
+    cold, warm = OpenDSSSolver(**kw), OpenDSSSolver(**kw, warm_start=True)
+    rng = np.random.default_rng(21)
+    base = rng.uniform(0, 400, size=(2, n))
+    it_c, it_w = [], []
+    for t in range(40):
+        p = base + rng.normal(0, 15, size=(2, n))            # loads drift step to step
+        loads = {"675c": T(p[0]), "671": T(p[1])}
+        time = "2020-08-12 %02d:%02d:00" % (t // 12, 5 * (t % 12))
+        for s_, its in ((cold, it_c), (warm, it_w)):
+            s_.calculate_power_flow(p_controllable_consumed=loads, current_time=time)
+            its.append(float(s_.iterations.double().mean()))
+        assert cold.unconverged() == 0 and warm.unconverged() == 0
+        vc, vw = cold.get_bus_voltages(), warm.get_bus_voltages()
+        for x in cold.feeder.node_names:
+            close(vw[x], N(vc[x]), 1e-9, 0)
+    assert it_w[0] == it_c[0]                                 # the first solve starts cold
+    assert np.mean(it_w[1:]) < np.mean(it_c[1:]) - 1.0, (np.mean(it_w[1:]), np.mean(it_c[1:]))
