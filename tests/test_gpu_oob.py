@@ -138,3 +138,29 @@ def test_oob_warning_logged_at_a_later_reset(caplog):
         torch.cuda.synchronize()
         env.reset()                    # reads it
     assert any("8 action(s)" in r.getMessage() for r in caplog.records)
+
+
+def test_oob_heterogeneous_fused_and_generic():
+    """The heterogeneous scenario on the fused multi-agent step (pgw_ma_step) and
+    on the generic path: one warning per (env, component, step) whose rescaled
+    action is out of the box -- the building's six actions count once."""
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    n, steps = 2048, 20
+    rng = np.random.default_rng(9)
+    A = actions(rng, (steps, n, 10))
+    want = 0
+    for t in range(steps):
+        want += int(bad(A[t, :, :6]).any(1).sum())                       # building
+        want += sum(int(bad(A[t, :, j]).sum()) for j in range(6, 10))   # pv, storage, pv farm, EV
+    got = []
+    for fused in ("auto", False):
+        env = MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=fused)
+        assert (env._ma is not None) == (fused == "auto")
+        env.reset()
+        for t in range(steps):
+            a = torch.tensor(A[t], device=DEV)
+            env.step({"building": {"building": a[:, :6], "pv": a[:, 6:7], "storage": a[:, 7:8]},
+                      "pv": a[:, 8:9], "ev-charging": a[:, 9:10]})
+        got.append(count(env))
+    assert got == [want, want], (got, want)
