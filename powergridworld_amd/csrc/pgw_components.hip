@@ -732,17 +732,17 @@ int32_t pgw_ma_step(const pgw_ma_step_args* a, const pgw_pf_params* pf, const pg
     wnext += a->wave_count[w];
   }
   PGW_REQUIRE(wnext == a->n_comp, "pgw_ma_step: waves list %d of %d slots", wnext, a->n_comp);
-  for (int w = 0; w < a->n_waves; ++w)
-    for (int i = 0; i < a->wave_count[w]; ++i) {
-      const int k = a->comp[a->wave_slot[a->wave_first[w] + i] & (PGW_MA_MAX_SLOTS - 1)].kind;
-      PGW_REQUIRE(a->wave_count[w] == 1 || k == PGW_MC_PV || k == PGW_MC_STORAGE,
-                  "pgw_ma_step: a building or EV slot needs a wave of its own");
-    }
   for (int i = 0; i < a->n_comp; ++i) {
     const int c = a->wave_slot[i];
     PGW_REQUIRE(c >= 0 && c < a->n_comp && !(listed & (1 << c)), "pgw_ma_step: wave_slot %d", i);
     listed |= 1 << c;
   }
+  for (int w = 0; w < a->n_waves; ++w)          // (every index below is now < n_comp)
+    for (int i = 0; i < a->wave_count[w]; ++i) {
+      const int k = a->comp[a->wave_slot[a->wave_first[w] + i]].kind;
+      PGW_REQUIRE(a->wave_count[w] == 1 || k == PGW_MC_PV || k == PGW_MC_STORAGE,
+                  "pgw_ma_step: a building or EV slot needs a wave of its own");
+    }
   // no building: the STD instantiation (its building branch never runs)
   bool std_bld = true;
   for (int c = 0; c < a->n_comp; ++c) {
