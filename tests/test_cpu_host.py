@@ -197,3 +197,68 @@ def test_env_tensor_and_action_normalisation():
     assert tuple(as_action(v, 4, 1, dev).shape) == (4, 1)
     with pytest.raises(ValueError):
         as_action(torch.zeros((3, 2)), 4, 2, dev)
+
+
+def test_ma_step_argument_checks():
+    """pgw_ma_step validates its layout before any HIP call (no GPU needed):
+    agents must cover the slots in order, every slot appear once in the waves,
+    a building / EV slot have a wave of its own, one building / storage / EV in
+    all, and the PF's controllable slots match the bus count."""
+    import ctypes as C
+    from powergridworld_amd import _lib
+    lib = _lib.lib()
+
+    def args(kinds, waves, agents):
+        a = _lib.MAStepArgs()
+        a.n_comp = len(kinds)
+        dummy = 256          # never dereferenced: the checks fail (or pass) first
+        n_pv = 0
+        for c, k in enumerate(kinds):
+            a.comp[c].kind = k
+            if k == 1:
+                a.slot_pv2[c], n_pv = n_pv, n_pv + 1
+            a.comp[c].action = _lib.Mat(dummy, 1, 1)
+            a.comp[c].obs = _lib.Mat(dummy, 1, 1)
+            a.comp[c].real_power = dummy
+        a.bld_x = a.bld_reward_state = a.bat_soc = dummy
+        a.ev_endp = a.ev_req = a.ev_charging = a.ev_reward = dummy
+        a.n_waves = len(waves)
+        i = 0
+        for w, cs in enumerate(waves):
+            a.wave_first[w], a.wave_count[w] = i, len(cs)
+            for c in cs:
+                a.wave_slot[i] = c
+                i += 1
+        a.n_agents = len(agents)
+        s = 0
+        for g, cnt in enumerate(agents):
+            a.agent_first[g], a.agent_count[g], a.agent_bus[g] = s, cnt, -1
+            a.agent_sum[g] = int(cnt > 1)
+            a.agent_real_power[g] = a.agent_reward[g] = dummy
+            for c in range(s, s + cnt):
+                a.slot_agent[c] = g
+            s += cnt
+        return a
+
+    def rc(a):
+        r = lib.pgw_ma_step(C.byref(a), None, None, 0, None, None, None)   # n = 0: checks only
+        return r, lib.pgw_last_error().decode()
+
+    B, PV, ST, EV = 0, 1, 2, 3
+    ok = args([B, PV, ST, PV, EV], [[0], [4], [1, 2, 3]], [3, 1, 1])
+    assert rc(ok)[0] == 0
+    ok.slot_pv2[3] = 0
+    r, msg = rc(ok)
+    assert r == -1 and "PV parameter set" in msg      # two PVs on one parameter set
+    r, msg = rc(args([B, PV, ST, PV, EV], [[0], [4], [1, 2]], [3, 1, 1]))
+    assert r == -1 and "waves list" in msg
+    r, msg = rc(args([B, PV, ST, PV, EV], [[0, 4], [1, 2, 3]], [3, 1, 1]))
+    assert r == -1 and "wave of its own" in msg
+    r, msg = rc(args([B, PV, ST, PV, EV], [[0], [4], [1, 2, 2]], [3, 1, 1]))
+    assert r == -1 and "wave_slot" in msg
+    bad = args([B, PV, ST, PV, EV], [[0], [4], [1, 2, 3]], [3, 2])
+    bad.agent_sum[1] = 0
+    r, msg = rc(bad)
+    assert r == -1 and "one slot unless summed" in msg
+    r, msg = rc(args([B, EV, EV], [[0], [1], [2]], [1, 1, 1]))
+    assert r == -1 and "at most" in msg
