@@ -51,10 +51,10 @@ def _bus(spec, default):
 def _accurate_inverse(Y, sweeps=3):
     """inv(Y) refined with residuals in extended precision (numpy clongdouble):
     Y is ill-conditioned (~1e7, from the 1e-7 ohm switch), so a plain fp64
-    inverse is only good to ~1e-9 relative."""
+    inverse is only good to ~1e-9 relative.  Y may be a stack (K, n, n)."""
     Z = np.linalg.inv(Y)
     Yx = Y.astype(np.clongdouble)
-    eye = np.eye(Y.shape[0], dtype=np.clongdouble)
+    eye = np.eye(Y.shape[-1], dtype=np.clongdouble)
     for _ in range(sweeps):
         R = eye - Yx @ Z.astype(np.clongdouble)
         Z = (Z.astype(np.clongdouble) + Z.astype(np.clongdouble) @ R)
@@ -305,6 +305,67 @@ class Feeder:
         V = self.V0 + I_last @ self.G.T
         return V, iters
 
+    def snap_opendss(self, load_kw, load_kvar, yprim_kw=None, yprim_kvar=None,
+                     tol=1e-4, min_iter=2, max_iter=15):
+        """OpenDSS's own snap solve, restated from its published solution method
+        (Solution.pas SolveSnap -> SolveCircuit -> DoPFLOWsolution; the
+        reference reaches it through ``Solve mode=snap``, opendss.py:134):
+
+        * ``mode=snap`` re-sets the solution mode, which clears
+          SolutionInitialized, so every call starts from SolveYDirect: the
+          system Y WITH every load's nominal admittance Yeq = conj(S)/Vbase^2
+          stamped in (Load.CalcYPrim), injected by the sources only;
+        * DoNormalSolution: each iteration injects I_src + sum over loads of
+          (Yprim V - I_load(V)) (Load.CalcYPrimContribution minus
+          DoConstantPQLoad, i.e. the compensation current) and solves Y V = I;
+        * Converged: max over ALL nodes of | |V_new| - |V_old| | / Vbase_node
+          <= tol (default 1e-4), tested after every iteration, accepted only
+          from MinIterations (default 2) on; at most MaxIterations (default 15).
+
+        ``yprim_kw/kvar`` are the powers whose Yeq sits in Y.  The Loads.kW /
+        Loads.kvar setters (DSS C-API Loads_Set_kW: kWBase, LoadSpecType,
+        RecalcElementData) do not invalidate the load's Yprim, so Y keeps the
+        Yeq of the last Y build: the DSS file's kW/kvar at the compile-time
+        ``Solve`` (pass ``spec`` base values, shape (n_loads,)).  Pass None to
+        stamp the step's own powers instead (the alternative reading, per env).
+
+        Returns (V nodes (K, n), iterations (K,))."""
+        load_kw = np.atleast_2d(np.asarray(load_kw, float))
+        load_kvar = np.atleast_2d(np.asarray(load_kvar, float))
+        K = load_kw.shape[0]
+        W_ph = load_kw[:, self.elem_load] * 1000.0 / self.elem_nph
+        var_ph = load_kvar[:, self.elem_load] * 1000.0 / self.elem_nph
+        vb2 = self.elem_vbase ** 2
+        C = self.Cinc
+        if yprim_kw is None:
+            yeq = (W_ph - 1j * var_ph) / vb2                                  # (K, m)
+            Yf = self.Y[None] + np.einsum("km,mi,mj->kij", yeq, C, C)
+            Zf = _accurate_inverse(Yf)
+        else:
+            ykw = np.asarray(yprim_kw, float)[self.elem_load] * 1000.0 / self.elem_nph
+            ykv = np.asarray(yprim_kvar, float)[self.elem_load] * 1000.0 / self.elem_nph
+            yeq = np.tile((ykw - 1j * ykv) / vb2, (K, 1))
+            Z1 = _accurate_inverse(self.Y + C.T @ np.diag(yeq[0]) @ C)
+            Zf = np.broadcast_to(Z1, (K,) + Z1.shape)
+        solve = lambda I: np.einsum("kij,kj->ki", Zf, I)
+        V = solve(np.tile(self.I_src, (K, 1)))                                # SolveYDirect
+        vbn = self.kv_ln * 1000.0
+        iters = np.zeros(K, int)
+        active = np.ones(K, bool)
+        for it in range(1, max_iter + 1):
+            U = V @ C.T
+            IL = self.load_currents(U, W_ph, var_ph)
+            J = self.I_src + (yeq * U - IL) @ C
+            Vn = solve(J)
+            err = np.max(np.abs(np.abs(Vn) - np.abs(V)) / vbn, axis=1)
+            V = np.where(active[:, None], Vn, V)
+            iters[active] = it
+            conv = (err <= tol) & (it >= min_iter)
+            active &= ~conv
+            if not active.any():
+                break
+        return V, iters
+
     def pu(self, V):
         return np.abs(V) / (self.kv_ln * 1000.0)
 
@@ -332,6 +393,18 @@ class BatchedPF:
         coef = self.shape[hour_of_year(current_time)]
         f = self.feeder
         return coef * f.base_kw * self.rescale, coef * f.base_kvar * self.rescale   # opendss.py:106-108
+
+    def loads(self, current_time, p_ctrl=None, q_ctrl=None, K=1):
+        """Per-load kW / kvar (K, n_loads) of one calculate_power_flow call
+        (opendss.py:105-131)."""
+        kw, kvar = self.base_loads(current_time)
+        kw = np.tile(kw, (K, 1)); kvar = np.tile(kvar, (K, 1))
+        names = self.feeder.load_names
+        for d, arr in ((p_ctrl, kw), (q_ctrl, kvar)):
+            for name, v in (d or {}).items():
+                if name in names:
+                    arr[:, names.index(name)] = arr[:, names.index(name)] + np.asarray(v, float)
+        return kw, kvar
 
     def calculate(self, current_time, p_ctrl=None, q_ctrl=None, K=1):
         """p_ctrl/q_ctrl: {load_name: array (K,)}.  Returns node pu voltages (K, n)."""

@@ -181,7 +181,10 @@ class ComponentEnv(spaces.Env, ABC):
             if c is not None:
                 hit = c.get(key)
                 if hit is not None:
-                    return hit
+                    # the caller's own tensor: the cache keeps only the pgw_mat
+                    # (pointer + strides), never a reference that would pin the
+                    # allocation
+                    return action, hit
         a = as_action(action, self.num_envs, dim, self.device)
         m = self._act_mat(a)
         if key is not None and a is action:
@@ -190,7 +193,7 @@ class ComponentEnv(spaces.Env, ABC):
                 c = self._am_c = {}
             if len(c) >= 64:
                 c.clear()
-            c[key] = (a, m)
+            c[key] = m
         return a, m
 
     @abstractmethod
@@ -224,6 +227,22 @@ class ComponentEnv(spaces.Env, ABC):
 
     # For the fused multi-agent kernel: which kernel component this env is.
     fused_kind = None
+
+
+# The hooks a fused kernel implements for a component: a subclass that overrides
+# any of them (e.g. a PV with a nonzero reactive_power) must take the generic
+# path, which calls them.
+FUSED_HOOKS = ("step", "step_reward", "get_obs", "is_terminal", "real_power", "reactive_power")
+
+
+def owns_fused_hooks(env, attr, hooks=FUSED_HOOKS, skip=()):
+    """True when every hook of ``type(env)`` is the one of the class that declares
+    ``attr`` (fused_kind / mc_kind), i.e. the code the kernel restates."""
+    cls = type(env)
+    owner = next((c for c in cls.__mro__ if attr in c.__dict__), None)
+    if owner is None:
+        return False
+    return all(getattr(cls, h, None) is getattr(owner, h, None) for h in hooks if h not in skip)
 
 
 def resolve_env_class(cls):
@@ -305,13 +324,11 @@ class MultiComponentEnv(ComponentEnv):
         (building with the thermal-energy reward, PV, storage, EV), each once,
         and none overrides its step."""
         if getattr(self, "_mc_fuse", None) is None:
-            def own_step(e):
-                # the class that declares mc_kind must also provide the step that runs
-                owner = next(c for c in type(e).__mro__ if "mc_kind" in c.__dict__)
-                return type(e).step is owner.step
+            # the class that declares mc_kind must also provide every hook the
+            # kernel restates (step, reward, obs, powers, terminal test)
             kinds = [getattr(type(e), "mc_kind", None) for e in self.envs]
             ok = all(k is not None for k in kinds) and len(set(kinds)) == len(kinds) and len(kinds) <= 4
-            self._mc_fuse = ok and all(own_step(e) for e in self.envs)
+            self._mc_fuse = ok and all(owns_fused_hooks(e, "mc_kind") for e in self.envs)
         return self._mc_fuse
 
     def step(self, action: dict, **kwargs):

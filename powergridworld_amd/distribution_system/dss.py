@@ -192,10 +192,11 @@ def parse_dss(path, spec=None):
                     spec["controlmode"] = v.lower()
             continue
         if verb.count(".") >= 2 and "=" in verb:      # Class.Name.Prop=value
-            path, v = toks[0].split("=", 1)
-            cls, name, prop = path.rsplit(".", 2)
-            _assign(spec, cls.lower(), name.lower(), [(prop.lower(), v.strip())] +
-                    [tuple(x.split("=", 1)) for x in toks[1:] if "=" in x])
+            target, v = toks[0].split("=", 1)
+            cls, name, prop = target.rsplit(".", 2)
+            extra = [x.split("=", 1) for x in toks[1:] if "=" in x]
+            _assign(spec, cls.lower(), name.lower(), [(prop.strip().lower(), v.strip())] +
+                    [(k.strip().lower(), val.strip()) for k, val in extra])
             continue
         if verb not in ("new", "edit"):
             continue                                  # calcv, solve, buscoords, clear, show ...
@@ -228,9 +229,17 @@ def parse_dss(path, spec=None):
     return spec
 
 
+# Classes whose Edit / property assignments cannot change the network model
+# (meters, monitors, shapes, geometry data the builder never reads).
+_EDIT_IGNORED = {"energymeter", "monitor", "loadshape", "growthshape", "tshape", "priceshape",
+                 "spectrum", "xycurve", "wiredata", "cndata", "tsdata", "linegeometry", "linespacing"}
+
+
 def _assign(spec, cls, name, props):
-    """Edit / property assignment on an element defined earlier (transformers and
-    loads; other classes are ignored like the other unsimulated commands)."""
+    """Edit / property assignment on an element defined earlier: transformers
+    and loads are updated; classes that cannot change the network are ignored;
+    any other class (capacitors, lines, sources ...) raises, since silently
+    keeping the original element would give a wrong network."""
     if cls == "transformer":
         for t in spec["transformers"]:
             if t["name"] == name:
@@ -243,6 +252,16 @@ def _assign(spec, cls, name, props):
                 _load_props(ld, props)
                 return
         raise ValueError("Edit of undefined load %r" % name)
+    if cls == "regcontrol":
+        for rc in spec["regcontrols"]:
+            if rc["name"] == name:
+                rc["props"] = list(rc["props"]) + list(props)
+                return
+        raise ValueError("Edit of undefined regcontrol %r" % name)
+    if cls in _EDIT_IGNORED:
+        return
+    raise NotImplementedError("Edit / property assignment of %s.%s (%s) is not supported"
+                              % (cls, name, ", ".join(k for k, _ in props)))
 
 
 def _array(v):

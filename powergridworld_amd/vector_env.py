@@ -4,9 +4,14 @@ RLlib MultiAgentEnv, examples/marl/rllib/heterogeneous/train.py:12-17 hands it
 to RLlib, which vectorizes by stepping `num_envs_per_worker` Python copies).
 
 Here the N copies already step together on the GPU, so the adapter only
-reshapes: RLlib's per-sub-env structures are built from views of the engine's
-[N, dim] device tensors (row i of every observation / reward is sub-env i; no
-copy, the observations stay on the device for a torch policy).
+reshapes: RLlib's per-sub-env structures are row views of [N, dim] device
+tensors (row i of every observation / reward is sub-env i; the observations
+stay on the device for a torch policy).  The engine overwrites its buffers in
+place every step, while RLlib's collectors keep each step's observations until
+they build a batch, so by default the adapter clones every batched tensor ONCE
+per step (one device copy per buffer, not per row) and hands out rows of the
+copy.  ``zero_copy=True`` hands out rows of the engine's own buffers instead:
+valid only until the next step, for callers that consume them at once.
 
 Two RLlib interfaces are provided:
 
@@ -46,6 +51,15 @@ def _row(x, i, n):
     return x
 
 
+def _snapshot(x):
+    """One clone per batched tensor (dicts recurse; bools and others are shared)."""
+    if isinstance(x, torch.Tensor):
+        return x.clone()
+    if isinstance(x, dict):
+        return {k: _snapshot(v) for k, v in x.items()}
+    return x
+
+
 def _stack(items, device):
     """Per-sub-env actions -> the batched action (dicts recurse; arrays and
     tensors are stacked along a new leading env axis on `device`)."""
@@ -60,8 +74,9 @@ def _stack(items, device):
 class MultiAgentVectorEnv(_Base):
     """RLlib VectorEnv / BaseEnv view of a batched MultiAgentEnv."""
 
-    def __init__(self, env):
+    def __init__(self, env, zero_copy=False):
         self.env = env
+        self.zero_copy = bool(zero_copy)
         self.num_envs = env.num_envs
         self.observation_space = env.observation_space
         self.action_space = env.action_space
@@ -78,13 +93,16 @@ class MultiAgentVectorEnv(_Base):
         if self._episode_over:
             raise RuntimeError("step after the episode ended: reset first")
         obs, rew, dones, meta = self.env.step(action)
+        if not self.zero_copy:
+            obs, rew, meta = _snapshot(obs), _snapshot(rew), _snapshot(meta)
         self._obs, self._rew, self._done, self._info = obs, rew, dones, meta
         self._episode_over = bool(dones["__all__"])
         self._reset_done = False
         return obs, rew, dones, meta
 
     def _reset_batch(self):
-        self._obs = self.env.reset()
+        obs = self.env.reset()
+        self._obs = obs if self.zero_copy else _snapshot(obs)
         self._episode_over = False
         self._reset_done = True
         return self._obs

@@ -131,6 +131,27 @@ def test_dss_unsupported_control_and_models_refused(tmp_path):
         Feeder(load_feeder_spec(str(p)))
 
 
+def test_dss_edits_of_unsimulated_classes_refused(tmp_path):
+    """An Edit / Class.Name.Prop= of a capacitor or line would otherwise leave the
+    original element in Y (a wrong network without an error); edits of meters
+    and shapes cannot change the network and are ignored.  Extra key=value
+    pairs of a property assignment are normalised like New's."""
+    from powergridworld_amd.distribution_system.dss import parse_dss
+    text = open(REGCAP).read()
+    for extra in ("Capacitor.C1.States=[0]", "Edit Capacitor.C1 kvar=300", "Edit Line.650632 enabled=no"):
+        p = tmp_path / "e.dss"
+        p.write_text(text + "\n" + extra + "\n")
+        with pytest.raises(NotImplementedError, match="not supported"):
+            parse_dss(str(p))
+    p = tmp_path / "ok.dss"
+    p.write_text(text + "\nEdit EnergyMeter.m1 element=Line.650632\n"
+                 "Transformer.Reg1.Taps=[1.0 1.05] XHL=0.02\n")
+    spec = parse_dss(str(p))
+    reg1 = {t["name"]: t for t in spec["transformers"]}["reg1"]
+    assert [w["tap"] for w in reg1["windings"]] == [1.0, 1.05]
+    assert reg1["xhl"] == pytest.approx(0.02)
+
+
 def test_product_synthetic_exogenous_matches_fixture(exo_frame):
     from powergridworld_amd.agents.buildings import synthetic_exogenous_data
     df = synthetic_exogenous_data()

@@ -101,3 +101,34 @@ def test_base_env_poll_send_episode_and_reset():
     again = venv.try_reset(3)                    # the same boundary: no second reset
     _eq(first[2], {a: {c: v[2] for c, v in comps.items()} for a, comps in o_ref.items()})
     _eq(again[3], {a: {c: v[3] for c, v in comps.items()} for a, comps in o_ref.items()})
+
+
+def test_poll_results_survive_the_next_step():
+    """RLlib's collectors keep each step's observations until they build a
+    batch: by default the adapter hands out rows of a per-step copy, so an
+    earlier poll() result is not overwritten by the next step.  zero_copy=True
+    hands out the engine's own buffers (valid until the next step)."""
+    from powergridworld_amd.vector_env import MultiAgentVectorEnv
+    n = 3
+    for zero_copy in (False, True):
+        ref, env = _pair(n, True)
+        venv = MultiAgentVectorEnv(env, zero_copy=zero_copy)
+        ref.reset()
+        venv.poll()
+        rng = np.random.default_rng(7)
+        act1, act2 = _batched_actions(ref, rng, n), _batched_actions(ref, rng, n)
+        venv.send_actions({i: a for i, a in enumerate(_split(act1, n))})
+        obs1, rew1, _, _, _ = venv.poll()
+        kept = {i: {a: {c: v.clone() for c, v in comps.items()} for a, comps in obs1[i].items()}
+                for i in range(n)}
+        kept_r = {i: {a: v.clone() for a, v in rew1[i].items()} for i in range(n)}
+        venv.send_actions({i: a for i, a in enumerate(_split(act2, n))})
+        obs2, _, _, _, _ = venv.poll()
+        name = env.agents[0].name
+        if zero_copy:      # the same engine buffer: now the second step's values
+            assert obs1[0][name]["storage"].data_ptr() == obs2[0][name]["storage"].data_ptr()
+        else:
+            for i in range(n):
+                _eq(obs1[i], kept[i])
+                _eq(rew1[i], kept_r[i])
+            assert not torch.equal(obs1[0][name]["building"], obs2[0][name]["building"])
