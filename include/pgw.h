@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 16
+#define PGW_ABI_VERSION 17
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -41,8 +41,9 @@ const char* pgw_last_error(void);
  * building_params, building_exo, building_ext, ev_params, ev_step_info,
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
  * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
- * mc_step_args, matf, coord_buffers_f32, ma_step_args -- lets a binding
- * verify its layouts.  Writes min(n, 23) values, returns 23. */
+ * mc_step_args, matf, coord_buffers_f32, ma_step_args, pfg_elem, pfg_params,
+ * pfg_tables -- lets a binding verify its layouts.  Writes min(n, 26) values,
+ * returns 26. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -384,6 +385,73 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
                     const double* V0_0, double* out);
 
 /* ------------------------------------------------------------------------
+ * General batched power flow: any feeder size (PGW_PFG_MAX_M load phase
+ * elements) and two stopping rules.  Replaces the same OpenDSSSolver.
+ * calculate_power_flow (opendss.py:80-165) as pgw_pf_solve, for feeders beyond
+ * PGW_PF_MAX_M and for OpenDSS's own iteration (opendss.py:134 `Solve
+ * mode=snap`):
+ *   PGW_PF_EXACT    u <- u0 + W I'(u) from u0 (or U_init) until every element's
+ *                   |du| < tol (pu of its base): the fixed point, as pgw_pf_solve;
+ *   PGW_PF_OPENDSS  OpenDSS's snap solve (Solution.pas DoNormalSolution): Y holds
+ *                   each load's nominal admittance (elem.y0), the iteration starts
+ *                   from the direct solution u0 = C Y^-1 I_src, injects the
+ *                   compensation current I_load(u) - y0 u, and stops at the first
+ *                   iteration >= min_iter whose largest change of a node-voltage
+ *                   magnitude over the n_chk check rows (every node, pu of the
+ *                   node base) is <= tol, or at max_iter.
+ * Per-unit form as pgw_pf_solve: u = U / vb, I' = I vb = (conj(S) g - y0') u with
+ * y0' = conj(S_y0) (the per-phase power whose Yeq sits in Y).  Element k draws
+ * S_k = ((coef * base_kw) * rescale + ctrl_p[ctrl]) * 1000 / nph (+ j likewise):
+ * opendss.py:105-131 then OpenDSS's per-phase WNominal.
+ * Layout: a block of 4 waves serves 64 envs (lane = env); element, check and
+ * output rows are split over the waves in chunks of 8, and every row is
+ * accumulated against the element currents through LDS with its matrix entries
+ * as wave-uniform scalar operands.  Matrices are column (element) major with
+ * rows padded to a multiple of 8: M[2 (k ld + row) + re/im].
+ * ---------------------------------------------------------------------- */
+#define PGW_PFG_MAX_M 128     /* load phase elements */
+#define PGW_PFG_MAX_CHK 256   /* OpenDSS check rows (nodes) */
+enum { PGW_PF_EXACT = 0, PGW_PF_OPENDSS = 1 };
+
+typedef struct pgw_pfg_elem {
+  double base_kw, base_kvar;   /* the element's LOAD kW / kvar before loadshape and rescale */
+  double nph;                  /* phases of that load                                  */
+  double y0r, y0i;             /* OPENDSS: conj(S) per phase (W, -var) of the Yeq in Y; 0 */
+  double vlo2, vmn2, vmx2;     /* vlow^2, vmin^2, vmax^2 (pu^2)                         */
+  int32_t ctrl, pad_;          /* controllable-load slot, -1 none                      */
+} pgw_pfg_elem;
+
+typedef struct pgw_pfg_params {
+  int32_t m;          /* element rows (padded to 8 with inert zero-power elements)   */
+  int32_t n_chk;      /* OPENDSS check rows (padded to 8; 0 for EXACT)               */
+  int32_t n_out;      /* output rows                                                 */
+  int32_t n_ctrl;
+  int32_t mode, min_iter, max_iter, pad_;
+  double tol;
+  double coef, rescale;   /* the step's loadshape coefficient, system_load_rescale_factor */
+} pgw_pfg_params;
+
+typedef struct pgw_pfg_tables {
+  const pgw_pfg_elem* elem;  /* m                                                     */
+  const double* W;           /* m x m complex (ld m): W_ik / (vb_i vb_k), W = -C Z C^T */
+  const double* U0;          /* m complex, pu (EXACT: no-load; OPENDSS: direct solution) */
+  const double* Gc;          /* OPENDSS check rows: n_chk x m complex (ld n_chk), pu     */
+  const double* V0c;         /* n_chk complex, pu                                        */
+  const double* G;           /* output rows: n_out x m complex (ld pad8(n_out)), pu      */
+  const double* V0;          /* pad8(n_out) complex, pu                                  */
+  const double* U_init;      /* optional EXACT initial guess, n x m complex env-major    */
+  double* U_out;             /* optional final element voltages, n x m complex           */
+  double* v_min_out;         /* optional min / max over the output rows (n)              */
+  double* v_max_out;
+} pgw_pfg_tables;
+
+/* ctrl_p / ctrl_q: n_ctrl x n (NULL = 0); v_out: n_out x n (nullable); iters: n
+ * (nullable; -count when stopped at max_iter unconverged). */
+int32_t pgw_pf_solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n,
+                             const double* ctrl_p, const double* ctrl_q, double* v_out,
+                             int32_t* iters, void* stream);
+
+/* ------------------------------------------------------------------------
  * Kernel timing (benchmark instrumentation): while on, every `every`-th launch
  * of each kernel below is bracketed by HIP events on its own stream.
  * pgw_timing_stop synchronizes the recorded events and returns, per kernel,
@@ -391,7 +459,7 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
  * entries each).
  * ---------------------------------------------------------------------- */
 enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COORD_FUSED = 3,
-       PGW_T_MA_STEP = 4, PGW_T_COUNT = 5 };
+       PGW_T_MA_STEP = 4, PGW_T_PF_GENERAL = 5, PGW_T_COUNT = 6 };
 /* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
 int32_t pgw_debug_pf_trace(long long* buf);

@@ -383,11 +383,15 @@ def load_loadshape():
 class BatchedPF:
     """Batched restatement of OpenDSSSolver.calculate_power_flow for K envs."""
 
-    def __init__(self, spec=None, system_load_rescale_factor=1.0, tol=1e-10):
+    def __init__(self, spec=None, system_load_rescale_factor=1.0, tol=1e-10, semantics="exact"):
+        """semantics: "exact" (the fixed point, Feeder.solve) or "opendss"
+        (OpenDSS's stopped snap iterate, Feeder.snap_opendss with the DSS
+        file's load admittances in Y)."""
         self.feeder = Feeder(spec if spec is not None else load_ieee13())
         self.rescale = system_load_rescale_factor
         self.shape = load_loadshape()
         self.tol = tol
+        self.semantics = semantics
 
     def base_loads(self, current_time):
         coef = self.shape[hour_of_year(current_time)]
@@ -415,7 +419,10 @@ class BatchedPF:
             for name, v in (d or {}).items():
                 if name in names:
                     arr[:, names.index(name)] = arr[:, names.index(name)] + np.asarray(v, float)
-        V, it = self.feeder.solve(kw, kvar, tol=self.tol)
+        if self.semantics == "opendss":
+            V, it = self.feeder.snap_opendss(kw, kvar, self.feeder.base_kw, self.feeder.base_kvar)
+        else:
+            V, it = self.feeder.solve(kw, kvar, tol=self.tol)
         self.last_iters = it
         return self.feeder.pu(V)
 

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -21,6 +21,8 @@ EV_MAX_WORDS = 16
 MAX_COMP = 8
 PF_MAX_M = 16
 PF_MAX_CTRL = 8
+PFG_MAX_M = 128
+PFG_MAX_CHK = 256
 MAX_AGENTS = 8
 
 
@@ -97,6 +99,25 @@ class PFTables(C.Structure):
     _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("U_pred", vp),
                 ("U_pred_meta", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp),
                 ("load_scale", vp), ("v_min_out", vp), ("v_max_out", vp)]
+
+
+class PFGElem(C.Structure):
+    _fields_ = [("base_kw", f64), ("base_kvar", f64), ("nph", f64), ("y0r", f64), ("y0i", f64),
+                ("vlo2", f64), ("vmn2", f64), ("vmx2", f64), ("ctrl", i32), ("pad_", i32)]
+
+
+class PFGParams(C.Structure):
+    _fields_ = [("m", i32), ("n_chk", i32), ("n_out", i32), ("n_ctrl", i32), ("mode", i32),
+                ("min_iter", i32), ("max_iter", i32), ("pad_", i32), ("tol", f64), ("coef", f64),
+                ("rescale", f64)]
+
+
+class PFGTables(C.Structure):
+    _fields_ = [("elem", vp), ("W", vp), ("U0", vp), ("Gc", vp), ("V0c", vp), ("G", vp), ("V0", vp),
+                ("U_init", vp), ("U_out", vp), ("v_min_out", vp), ("v_max_out", vp)]
+
+
+PF_EXACT, PF_OPENDSS = 0, 1
 
 
 class PredMeta(C.Structure):
@@ -225,6 +246,7 @@ _SIGS = {
     "pgw_ev_step": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
+    "pgw_pf_solve_general": (i32, [P(PFGParams), P(PFGTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_padded_m": (i32, [i32]),
     "pgw_voltage_band_penalty": (i32, [i64, vp, f64, f64, f64, vp, vp]),
     "pgw_pf_pack_size": (i64, [i32]),
@@ -252,7 +274,7 @@ EXPORTED = sorted(_SIGS)
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
            CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32,
-           MAStepArgs]
+           MAStepArgs, PFGElem, PFGParams, PFGTables]
 
 _lib = None
 

@@ -1,0 +1,423 @@
+// General batched distribution power flow (pgw_pf_solve_general): any feeder
+// size up to PGW_PFG_MAX_M load phase elements, and two stopping rules --
+// the fixed point (PGW_PF_EXACT, as pgw_pf_solve) or OpenDSS's own snap solve
+// (PGW_PF_OPENDSS).  Replaces OpenDSSSolver.calculate_power_flow
+// (gridworld/distribution_system/opendss.py:80-165); the OpenDSS semantics
+// follow its published solution method (Solution.pas SolveSnap ->
+// DoNormalSolution, Load.CalcInjCurrentArray), restated in
+// oracle/pf_oracle.py:Feeder.snap_opendss.
+//
+// Per env the solve iterates on the m load-element voltages in per unit of
+// each element's base, u_i = u0_i + sum_k W''_ik I'_k(u_k), with
+//   I'_k = (conj(S_k) g(|u_k|) - y0'_k) u_k,
+//   g = 1/clamp(|u|^2, vmin^2, vmax^2), or 1 at or below vlow (Load model 1),
+// y0' = 0 for the exact fixed point and the per-phase power of the Yeq that
+// sits in OpenDSS's Y for its iteration (the compensation current).
+//
+// Layout (gfx950): a block of 4 waves serves 64 envs, lane = env.  The rows --
+// m element rows, the OpenDSS check rows (every node) and the output rows --
+// are cut into chunks of 8 and dealt round-robin to the waves; a wave keeps its
+// element rows' voltages and its check rows' previous magnitudes in registers
+// across iterations.  Per iteration every wave writes the currents of its
+// element rows to LDS (J[k][lane], 16 B per element and env), the block
+// synchronises, and every row accumulates sum_k M[k][row] J_k with the matrix
+// entries as wave-uniform scalar operands (scalar loads through the constant
+// cache: one s_load per 8 entries, reused by the 64 envs of the wave) and J_k
+// from LDS (one ds_read_b128 per element, reused by the 8 rows of the chunk).
+// Per-env convergence is the max over the waves' partial errors (LDS), and
+// the loop runs until every env of the block has stopped; an env that stopped
+// keeps its voltages, magnitudes and currents (selects), so its result and
+// iteration count are those of solving it alone.
+#include <cmath>
+
+#include "pgw_common.h"
+
+namespace pgw {
+
+constexpr int kGW = kBlock / 64;   // waves per block (4)
+constexpr int kGR = 8;             // rows per chunk
+
+typedef const __attribute__((address_space(4))) double* cdptr;
+typedef const __attribute__((address_space(4))) pgw_pfg_elem* ceptr;
+
+// The coordinated step's prologue / epilogue (pgw_coord_step_general): bus
+// load = sum of the agents' powers in agent order (multiagent_env.py:171-181),
+// and CoordinatedMultiBuildingControlEnv.reward_transform (train.py:51-88) on
+// the common-bus voltage.  agent_power == nullptr: plain solve (ctrl_p/q).
+struct PFGCoord {
+  const double* agent_power;   // n_agents x n
+  double* reward;              // n_agents x n
+  double* vv;                  // n (nullable)
+  int32_t n_agents, vv_row, coordinated, pad_;
+  int32_t agent_ctrl[PGW_MAX_AGENTS];
+  double vv_lo, vv_hi, vv_penalty;
+};
+
+// An element record through the scalar cache (field by field: no aggregate
+// copies out of the constant address space).
+struct ElemV {
+  double base_kw, base_kvar, nph, y0r, y0i, vlo2, vmn2, vmx2;
+  int ctrl;
+};
+__device__ __forceinline__ ElemV ld_elem(ceptr el, int k) {
+  ElemV v;
+  v.base_kw = el[k].base_kw;
+  v.base_kvar = el[k].base_kvar;
+  v.nph = el[k].nph;
+  v.y0r = el[k].y0r;
+  v.y0i = el[k].y0i;
+  v.vlo2 = el[k].vlo2;
+  v.vmn2 = el[k].vmn2;
+  v.vmx2 = el[k].vmx2;
+  v.ctrl = el[k].ctrl;
+  return v;
+}
+
+__device__ __forceinline__ double g_rcp(double m) {
+  double r = __builtin_amdgcn_rcp(m);   // v_rcp_f64 + two Newton steps (~1 ulp)
+  double e = fma(-m, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-m, r, 1.0);
+  return fma(r, e, r);
+}
+
+// NaN-propagating max (an env whose error is NaN never converges).
+__device__ __forceinline__ double nmax(double a, double b) { return (b > a || b != b) ? b : a; }
+
+// One chunk of 8 rows: acc_r = base_r + sum_k M[k][row0 + r] J_k (complex).
+// Matrices and bases are padded to whole chunks (zero rows), so no guards.
+__device__ __forceinline__ void chunk_rows(cdptr M, int ld, int row0, cdptr base, int m,
+                                           const double2* __restrict__ sJ, int lane,
+                                           double (&ar)[kGR], double (&ai)[kGR]) {
+#pragma unroll
+  for (int r = 0; r < kGR; ++r) {
+    ar[r] = base[2 * (row0 + r)];
+    ai[r] = base[2 * (row0 + r) + 1];
+  }
+  for (int k = 0; k < m; ++k) {
+    const double2 j = sJ[k * 64 + lane];
+    const cdptr w = M + 2 * ((int64_t)k * ld + row0);
+#pragma unroll
+    for (int r = 0; r < kGR; ++r) {
+      const double wr = w[2 * r], wi = w[2 * r + 1];
+      ar[r] = fma(wr, j.x, ar[r]);
+      ar[r] = fma(-wi, j.y, ar[r]);
+      ai[r] = fma(wr, j.y, ai[r]);
+      ai[r] = fma(wi, j.x, ai[r]);
+    }
+  }
+}
+
+// CE: element chunks per wave (m <= 32 CE); CN: check chunks per wave (OpenDSS
+// mode, n_chk <= 32 CN; 0 = exact mode).
+template <int CE, int CN>
+__global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg_tables t, int64_t n,
+                                                       const double* __restrict__ ctrl_p,
+                                                       const double* __restrict__ ctrl_q,
+                                                       double* __restrict__ v_out,
+                                                       int32_t* __restrict__ iters, PFGCoord c) {
+  constexpr bool OD = CN > 0;
+  constexpr int kMaxRows = 32 * CE;
+  __shared__ double2 sJ[kMaxRows * 64];
+  __shared__ double s_err[kGW * 64];
+  __shared__ double s_mn[kGW * 64], s_mx[kGW * 64], s_vsel[64];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const bool valid = e < n;
+  const int64_t ec = valid ? e : 0;
+  const int m = p.m;
+  const ceptr el = (ceptr)t.elem;
+  const cdptr W = (cdptr)t.W, U0 = (cdptr)t.U0;
+
+  // ---- the env's controllable powers (kW, kvar) per slot
+  double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
+#pragma unroll
+  for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
+    cp[s] = 0.0;
+    cq[s] = 0.0;
+  }
+  if (c.agent_power) {
+    // 0 + a0 + a1 ... per bus, in agent order (the generic path's sums)
+#pragma unroll
+    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag) {
+      if (ag < c.n_agents) {
+        const double x = valid ? c.agent_power[(int64_t)ag * n + ec] : 0.0;
+        const int slot = c.agent_ctrl[ag];
+#pragma unroll
+        for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + x : cp[s];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
+      if (s < p.n_ctrl) {
+        cp[s] = (valid && ctrl_p) ? ctrl_p[(int64_t)s * n + ec] : 0.0;
+        cq[s] = (valid && ctrl_q) ? ctrl_q[(int64_t)s * n + ec] : 0.0;
+      }
+    }
+  }
+
+  // ---- owned element rows: powers conj(S) (W, var) and the initial voltages
+  double sr[CE][kGR], si[CE][kGR], ur[CE][kGR], ui[CE][kGR];
+#pragma unroll
+  for (int j = 0; j < CE; ++j) {
+    const int row0 = (wv + kGW * j) * kGR;
+#pragma unroll
+    for (int r = 0; r < kGR; ++r) {
+      const int k = row0 + r;
+      sr[j][r] = si[j][r] = ur[j][r] = ui[j][r] = 0.0;
+      if (k < m) {
+        const ElemV E = ld_elem(el, k);
+        double pk = 0.0, qk = 0.0;
+#pragma unroll
+        for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
+          pk = (E.ctrl == s) ? cp[s] : pk;
+          qk = (E.ctrl == s) ? cq[s] : qk;
+        }
+        // opendss.py:107-108 (coef * base * rescale), :128-129 (+ controllable),
+        // then OpenDSS WNominal = kW * 1000 / nphases
+        const double kw = (p.coef * E.base_kw) * p.rescale;
+        const double kvar = (p.coef * E.base_kvar) * p.rescale;
+        sr[j][r] = ((kw + pk) * 1000.0) / E.nph;
+        si[j][r] = -(((kvar + qk) * 1000.0) / E.nph);
+        if (t.U_init) {
+          ur[j][r] = t.U_init[2 * (ec * m + k)];
+          ui[j][r] = t.U_init[2 * (ec * m + k) + 1];
+        } else {
+          ur[j][r] = U0[2 * k];
+          ui[j][r] = U0[2 * k + 1];
+        }
+      }
+    }
+  }
+  // OpenDSS: the check rows' magnitudes of the previous iterate (the direct
+  // solution before the first iteration; the test only counts from min_iter)
+  double old[CN > 0 ? CN : 1][kGR];
+  if constexpr (OD) {
+    const cdptr V0c = (cdptr)t.V0c;
+#pragma unroll
+    for (int j = 0; j < CN; ++j) {
+      const int row0 = (wv + kGW * j) * kGR;
+#pragma unroll
+      for (int r = 0; r < kGR; ++r) {
+        const int o = row0 + r;
+        old[j][r] = 0.0;
+        if (o < p.n_chk) {
+          const double vr = V0c[2 * o], vi = V0c[2 * o + 1];
+          old[j][r] = sqrt(fma(vi, vi, vr * vr));
+        }
+      }
+    }
+  }
+
+  const double tol2 = p.tol * p.tol;
+  int it = 0, my_it = 0;
+  bool done = !valid, conv_ok = !valid;
+  while (true) {
+    // ---- 1. currents of the owned element rows -> LDS (a stopped env keeps its last)
+#pragma unroll
+    for (int j = 0; j < CE; ++j) {
+      const int row0 = (wv + kGW * j) * kGR;
+      if (row0 < m) {
+#pragma unroll
+        for (int r = 0; r < kGR; ++r) {
+          const int k = row0 + r;
+          const ElemV E = ld_elem(el, min(k, m - 1));
+          const double m2 = fma(ui[j][r], ui[j][r], ur[j][r] * ur[j][r]);
+          double mc = fmin(fmax(m2, E.vmn2), E.vmx2);
+          mc = (m2 <= E.vlo2) ? 1.0 : mc;
+          const double g = g_rcp(mc);
+          const double cr = OD ? fma(sr[j][r], g, -E.y0r) : sr[j][r] * g;
+          const double ci = OD ? fma(si[j][r], g, -E.y0i) : si[j][r] * g;
+          const double jr = fma(cr, ur[j][r], -(ci * ui[j][r]));
+          const double ji = fma(cr, ui[j][r], ci * ur[j][r]);
+          if (!done && k < m) sJ[k * 64 + lane] = make_double2(jr, ji);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 2. new element voltages; OpenDSS: every node's magnitude change
+    double err = 0.0;
+#pragma unroll
+    for (int j = 0; j < CE; ++j) {
+      const int row0 = (wv + kGW * j) * kGR;
+      if (row0 < m) {
+        double ar[kGR], ai[kGR];
+        chunk_rows(W, m, row0, U0, m, sJ, lane, ar, ai);
+#pragma unroll
+        for (int r = 0; r < kGR; ++r) {
+          if (!OD) {
+            const double dr = ar[r] - ur[j][r], di = ai[r] - ui[j][r];
+            err = nmax(err, fma(dr, dr, di * di));
+          }
+          ur[j][r] = done ? ur[j][r] : ar[r];
+          ui[j][r] = done ? ui[j][r] : ai[r];
+        }
+      }
+    }
+    if constexpr (OD) {
+#pragma unroll
+      for (int j = 0; j < CN; ++j) {
+        const int row0 = (wv + kGW * j) * kGR;
+        if (row0 < p.n_chk) {
+          double ar[kGR], ai[kGR];
+          chunk_rows((cdptr)t.Gc, p.n_chk, row0, (cdptr)t.V0c, m, sJ, lane, ar, ai);
+#pragma unroll
+          for (int r = 0; r < kGR; ++r) {
+            const double mag = sqrt(fma(ai[r], ai[r], ar[r] * ar[r]));
+            err = nmax(err, fabs(mag - old[j][r]));
+            old[j][r] = done ? old[j][r] : mag;
+          }
+        }
+      }
+    }
+    s_err[wv * 64 + lane] = err;
+    __syncthreads();
+    // ---- 3. per-env test (every wave forms the same value for its lane)
+    double E = s_err[lane];
+#pragma unroll
+    for (int w = 1; w < kGW; ++w) E = nmax(E, s_err[w * 64 + lane]);
+    ++it;
+    const bool conv = OD ? (E <= p.tol && it >= p.min_iter) : (E < tol2);
+    my_it = done ? my_it : it;
+    conv_ok = conv_ok || (!done && conv);
+    done = done || conv || it >= p.max_iter;
+    // (also the barrier between this iteration's s_err / J reads and the next writes)
+    if (!__syncthreads_or(!done)) break;
+  }
+
+  // ---- outputs: element voltages, then the output rows from each env's last
+  // currents (the node voltages of the accepted solve, V = V0 + G I(u_prev))
+  if (valid && t.U_out) {
+#pragma unroll
+    for (int j = 0; j < CE; ++j) {
+      const int row0 = (wv + kGW * j) * kGR;
+#pragma unroll
+      for (int r = 0; r < kGR; ++r) {
+        const int k = row0 + r;
+        if (k < m) {
+          t.U_out[2 * (e * m + k)] = ur[j][r];
+          t.U_out[2 * (e * m + k) + 1] = ui[j][r];
+        }
+      }
+    }
+  }
+  const int n_out = p.n_out;
+  const int ld_out = (n_out + kGR - 1) / kGR * kGR;
+  double vmn = INFINITY, vmx = -INFINITY, vsel = 0.0;
+  bool have = false;
+  for (int row0 = wv * kGR; row0 < n_out; row0 += kGW * kGR) {
+    double ar[kGR], ai[kGR];
+    chunk_rows((cdptr)t.G, ld_out, row0, (cdptr)t.V0, m, sJ, lane, ar, ai);
+#pragma unroll
+    for (int r = 0; r < kGR; ++r) {
+      const int o = row0 + r;
+      if (o < n_out) {
+        const double v = sqrt(fma(ai[r], ai[r], ar[r] * ar[r]));
+        if (valid && v_out) v_out[(int64_t)o * n + e] = v;
+        // Python min()/max() over the rows in order: first strict improvement
+        if (!have) {
+          vmn = vmx = v;
+          have = true;
+        } else {
+          vmn = (v < vmn) ? v : vmn;
+          vmx = (v > vmx) ? v : vmx;
+        }
+        if (o == c.vv_row) vsel = v;
+      }
+    }
+  }
+  // chunk q is wave q % 4's: rows in order across waves = chunks in order, so
+  // the waves' extrema combine in wave order of their first chunks
+  s_mn[wv * 64 + lane] = have ? vmn : NAN;
+  s_mx[wv * 64 + lane] = have ? vmx : NAN;
+  if (c.agent_power && ((c.vv_row / kGR) % kGW) == wv) s_vsel[lane] = vsel;
+  __syncthreads();
+  if (wv != 0 || !valid) return;
+  if (t.v_min_out || t.v_max_out) {
+    double mn = s_mn[lane], mx = s_mx[lane];
+    for (int w = 1; w < kGW; ++w) {
+      const double a = s_mn[w * 64 + lane], b = s_mx[w * 64 + lane];
+      if (a == a) mn = (a < mn) ? a : mn;
+      if (b == b) mx = (b > mx) ? b : mx;
+    }
+    if (t.v_min_out) t.v_min_out[e] = mn;
+    if (t.v_max_out) t.v_max_out[e] = mx;
+  }
+  const int32_t itv = conv_ok ? my_it : -my_it;
+  if (iters) iters[e] = itv;
+  if (c.agent_power && c.coordinated) {
+    const double v = s_vsel[lane];
+    const double vv = pymax(pymax(0.0, c.vv_lo - v), v - c.vv_hi);
+    if (c.vv) c.vv[e] = vv;
+    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
+    // reward -= share (no-return atomic add of -share: one IEEE add per address)
+#pragma unroll
+    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+      if (ag < c.n_agents)
+        (void)__hip_atomic_fetch_add(c.reward + (int64_t)ag * n + e, -share, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int CE, int CN>
+static int32_t launch_general(const pgw_pfg_params& p, const pgw_pfg_tables& t, int64_t n, const double* cp,
+                              const double* cq, double* v_out, int32_t* iters, const PFGCoord& c,
+                              hipStream_t st) {
+  launch_timed(PGW_T_PF_GENERAL, k_pf_general<CE, CN>, dim3((unsigned)((n + 63) / 64)), dim3(kBlock), st, p,
+               t, n, cp, cq, v_out, iters, c);
+  return check_launch("k_pf_general");
+}
+
+template <int CE>
+static int32_t dispatch_cn(const pgw_pfg_params& p, const pgw_pfg_tables& t, int64_t n, const double* cp,
+                           const double* cq, double* v_out, int32_t* iters, const PFGCoord& c, hipStream_t st) {
+  if (p.mode != PGW_PF_OPENDSS) return launch_general<CE, 0>(p, t, n, cp, cq, v_out, iters, c, st);
+  const int cn = (p.n_chk + 32 * 1 - 1) / 32;
+  if (cn <= 1) return launch_general<CE, 1>(p, t, n, cp, cq, v_out, iters, c, st);
+  if (cn <= 2) return launch_general<CE, 2>(p, t, n, cp, cq, v_out, iters, c, st);
+  if (cn <= 4) return launch_general<CE, 4>(p, t, n, cp, cq, v_out, iters, c, st);
+  return launch_general<CE, 8>(p, t, n, cp, cq, v_out, iters, c, st);
+}
+
+static int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n, const double* cp,
+                             const double* cq, double* v_out, int32_t* iters, const PFGCoord& c,
+                             void* stream) {
+  PGW_REQUIRE(p && t && n >= 0, "pgw_pf_solve_general: null argument");
+  PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PFG_MAX_M && p->m % kGR == 0,
+              "pgw_pf_solve_general: m=%d (need a multiple of 8, <= %d)", p->m, PGW_PFG_MAX_M);
+  PGW_REQUIRE(t->elem && t->W && t->U0, "pgw_pf_solve_general: missing elem / W / U0");
+  PGW_REQUIRE(p->mode == PGW_PF_EXACT || p->mode == PGW_PF_OPENDSS, "pgw_pf_solve_general: bad mode");
+  PGW_REQUIRE(p->mode != PGW_PF_OPENDSS ||
+                  (p->n_chk >= kGR && p->n_chk <= PGW_PFG_MAX_CHK && p->n_chk % kGR == 0 && t->Gc && t->V0c),
+              "pgw_pf_solve_general: OPENDSS needs n_chk check rows (multiple of 8, <= %d) and Gc / V0c",
+              PGW_PFG_MAX_CHK);
+  PGW_REQUIRE(p->mode != PGW_PF_OPENDSS || !t->U_init,
+              "pgw_pf_solve_general: OPENDSS starts from the direct solution (no U_init)");
+  PGW_REQUIRE(p->n_out >= 0 && (p->n_out == 0 || (t->G && t->V0)), "pgw_pf_solve_general: missing G / V0");
+  PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve_general: bad n_ctrl");
+  PGW_REQUIRE(p->max_iter >= 1 && p->min_iter >= 1, "pgw_pf_solve_general: bad iteration limits");
+  PGW_REQUIRE(!c.agent_power || (c.vv_row >= 0 && c.vv_row < p->n_out),
+              "pgw_pf_solve_general: bad coordinated voltage row");
+  if (n == 0) return PGW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (p->m <= 32) return dispatch_cn<1>(*p, *t, n, cp, cq, v_out, iters, c, st);
+  if (p->m <= 64) return dispatch_cn<2>(*p, *t, n, cp, cq, v_out, iters, c, st);
+  return dispatch_cn<4>(*p, *t, n, cp, cq, v_out, iters, c, st);
+}
+
+}  // namespace pgw
+
+using namespace pgw;
+
+extern "C" {
+
+int32_t pgw_pf_solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n,
+                             const double* ctrl_p, const double* ctrl_q, double* v_out, int32_t* iters,
+                             void* stream) {
+  const PFGCoord c = {};
+  return solve_general(p, t, n, ctrl_p, ctrl_q, v_out, iters, c, stream);
+}
+
+}  // extern "C"

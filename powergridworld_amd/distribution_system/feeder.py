@@ -68,8 +68,15 @@ def _seq_matrix(v1, v0, ph):
 
 
 class Feeder(object):
-    def __init__(self, spec):
+    """load_yprim=True builds OpenDSS's iteration matrix: every model-1 load's
+    nominal admittance Yeq = conj(S) / Vbase^2 (Load.CalcYPrim, at the DSS
+    file's kW / kvar: the Loads.kW / kvar setters the reference drives leave
+    the load's Yprim as built, opendss.py:146-153) is stamped into Y, so Z, V0
+    and the reductions are those of Y + loads (V0 = the direct solution)."""
+
+    def __init__(self, spec, load_yprim=False):
         self.spec = spec
+        self.load_yprim = bool(load_yprim)
         self.freq = float(spec.get("base_frequency", 60.0))
         self.bus_nodes, self.buses = {}, []
         src = spec["source"]
@@ -162,6 +169,9 @@ class Feeder(object):
         shunts = [(c, complex(0.0, c["kvar"] * 1000.0 / c["phases"])) for c in spec.get("capacitors", [])]
         shunts += [(ld, complex(ld["kw"], -ld["kvar"]) * 1000.0 / ld["phases"]) for ld in spec["loads"]
                    if ld.get("model", 1) == 2]
+        if self.load_yprim:
+            shunts += [(ld, complex(ld["kw"], -ld["kvar"]) * 1000.0 / ld["phases"]) for ld in spec["loads"]
+                       if ld.get("model", 1) == 1]
         for obj, s in shunts:
             ph = obj["phases"]
             y = s / _elem_vbase(obj, ph) ** 2
@@ -223,6 +233,25 @@ class Feeder(object):
         self.m = len(ep)
         self.base_kw = np.array([ld["kw"] for ld in self.spec["loads"]], float)
         self.base_kvar = np.array([ld["kvar"] for ld in self.spec["loads"]], float)
+
+    def reduce_rows(self, out_nodes):
+        """Unpadded reduction onto the m load elements (any m): (W [m, m],
+        U0 [m], G [n_out, m], V0 [n_out]) complex, W = -C Z C^T, U0 = C V0,
+        G = -(Z C^T)[out_nodes] (csrc/pgw_feeder.cpp pgw_pf_reduce)."""
+        m, n = self.m, self.n
+        out_nodes = np.asarray(out_nodes, np.int32)
+        no = len(out_nodes)
+        W = np.zeros(2 * m * m)
+        U0 = np.zeros(2 * m)
+        G = np.zeros(2 * max(no, 1) * m)
+        V0o = np.zeros(2 * max(no, 1))
+        Zf = np.ascontiguousarray(self.Z).view(np.float64).ravel()
+        V0f = np.ascontiguousarray(self.V0).view(np.float64).ravel()
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        _lib.check(_lib.lib().pgw_pf_reduce(n, p(Zf), p(V0f), m, p(self.elem_p), p(self.elem_q), no,
+                                            p(out_nodes), p(W), p(U0), p(G), p(V0o)))
+        return (W.view(np.complex128).reshape(m, m), U0.view(np.complex128),
+                G.view(np.complex128).reshape(max(no, 1), m)[:no], V0o.view(np.complex128)[:no])
 
     def reduce(self, out_nodes):
         """-> (M, W [M*M], U0 [M], G [n_out*M], V0_out [n_out]) complex, padded to the

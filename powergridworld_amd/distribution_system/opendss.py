@@ -59,13 +59,45 @@ class OpenDSSSolver(PowerFlowSolver):
     PREDICTOR_MAX_TABLES = 64      # hours kept on the device (~180 KB each)
     PREDICTOR_LOOKAHEAD = 24       # hours solved per table launch
 
+    # OpenDSS's snap-solve defaults (Solution.pas: ConvergenceTolerance,
+    # MinIterations, MaxIterations)
+    OPENDSS_TOL, OPENDSS_MIN_ITER, OPENDSS_MAX_ITER = 1e-4, 2, 15
+
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
-                 num_envs: int = 1, device=None, tol: float = 1e-10, max_iter: int = 100,
-                 output_nodes=None, predictor: bool = True, warm_start: bool = False, **kwargs):
+                 num_envs: int = 1, device=None, tol: float = None, max_iter: int = None,
+                 output_nodes=None, predictor: bool = True, warm_start: bool = False,
+                 convergence: str = "exact", general: bool = None, **kwargs):
+        """convergence: "exact" -- every env's solve iterates to the fixed point
+        (max |dU| < tol = 1e-10 pu), history-free and reproducible; "opendss" --
+        OpenDSS's own snap solve as the reference runs it (opendss.py:134):
+        loads' nominal admittances in Y, start from the direct solution, stop at
+        the first iteration >= 2 whose largest node-voltage magnitude change is
+        <= tol = 1e-4 pu, at most 15 (DESIGN.md section 2 measures the
+        difference).  Feeders with more than 16 load phase elements and the
+        "opendss" mode run the general kernel (pgw_pf_solve_general); general=True
+        forces it for the exact mode too (tests, measurements)."""
         super().__init__(**kwargs)
+        if convergence not in ("exact", "opendss"):
+            raise ValueError("convergence must be 'exact' or 'opendss', got %r" % (convergence,))
+        self.convergence = convergence
         self.num_envs = int(num_envs)
         self.device = _lib.require_device(device)
-        self.feeder = Feeder(load_feeder_spec(feeder_file))
+        spec = load_feeder_spec(feeder_file)
+        self.feeder = Feeder(spec)
+        self.general = bool(general) or convergence == "opendss" or self.feeder.m > _lib.PF_MAX_M
+        if self.feeder.m > _lib.PFG_MAX_M:
+            raise ValueError("feeder has %d load phase elements (max %d)" % (self.feeder.m, _lib.PFG_MAX_M))
+        if convergence == "opendss":
+            if warm_start:
+                raise ValueError("convergence='opendss' starts every solve from the direct solution "
+                                 "(no warm_start)")
+            self._fd_iter = Feeder(spec, load_yprim=True)      # OpenDSS's Y (+ loads' Yeq)
+            tol = self.OPENDSS_TOL if tol is None else tol
+            max_iter = self.OPENDSS_MAX_ITER if max_iter is None else max_iter
+        else:
+            self._fd_iter = self.feeder
+            tol = 1e-10 if tol is None else tol
+            max_iter = 100 if max_iter is None else max_iter
         self.system_load_rescale_factor = system_load_rescale_factor
         self.annual_hourly_load_profile = load_loadshape(loadshape_file)
         if len(self.annual_hourly_load_profile) != 8760:
@@ -77,6 +109,7 @@ class OpenDSSSolver(PowerFlowSolver):
                               if ld.get("model", 1) == 1]
         self.base_load = np.stack([self.feeder.base_kw, self.feeder.base_kvar], 1)
         self.tol, self.max_iter = float(tol), int(max_iter)
+        self.min_iter = self.OPENDSS_MIN_ITER if convergence == "opendss" else 1
         self.bus_voltages = {}
         self.iterations = None       # [N] int32 per env; -max_iter = stopped unconverged
         self._extrema = None
@@ -104,6 +137,8 @@ class OpenDSSSolver(PowerFlowSolver):
         self.output_names = names
         self._names_ver = getattr(self, "_names_ver", 0) + 1
         idx = [f.node_index[n] for n in names]
+        if self.general:
+            return self._set_general_tables(idx)
         M, W, U0, G, V0o = f.reduce(idx)
         self.M = M
         self._base_params()
@@ -150,6 +185,84 @@ class OpenDSSSolver(PowerFlowSolver):
                                       device=dev)
         self._pred_index = {}
 
+    # ------------------------------------------------------------ general kernel
+    def _set_general_tables(self, idx):
+        """Device tables of pgw_pf_solve_general (include/pgw.h): the iteration
+        model's reduction (W, u0; check rows = every node for "opendss") and the
+        output rows, in per unit (element / node bases), element-major, rows
+        padded to chunks of 8 with inert zero-power elements."""
+        f, fi, dev = self.feeder, self._fd_iter, self.device
+        m = f.m
+        mp = -(-m // 8) * 8
+        self.M = mp
+        no = len(idx)
+        allidx = list(range(f.n))
+        W, U0, G, V0o = fi.reduce_rows(idx)
+        vb = f.elem_vbase
+        vbn = f.kv_ln * 1000.0
+
+        def emaj(rows_cm, ld):         # [rows, m] complex -> [mp][ld] complex, zero padded
+            out = np.zeros((mp, ld), complex)
+            out[:rows_cm.shape[1], :rows_cm.shape[0]] = rows_cm.T
+            return out
+
+        def dev_c(a):
+            return torch.tensor(np.ascontiguousarray(a).view(np.float64).ravel(), dtype=torch.float64,
+                                device=dev)
+        Ws = W / (vb[:, None] * vb[None, :])
+        u0 = np.zeros(mp, complex)
+        u0[:m] = U0 / vb
+        ldo = max(-(-no // 8) * 8, 8)
+        Gs = (G / vb[None, :]) / vbn[idx][:, None]
+        V0s = np.zeros(ldo, complex)
+        V0s[:no] = V0o / vbn[idx]
+        self._g_W = dev_c(emaj(Ws.T, mp))           # column k = W''[:, k]
+        self._g_U0 = dev_c(u0)
+        self._g_G = dev_c(emaj(Gs, ldo))
+        self._g_V0 = dev_c(V0s)
+        n_chk = 0
+        self._g_Gc = self._g_V0c = None
+        if self.convergence == "opendss":
+            _, _, Gc, V0c = fi.reduce_rows(allidx)
+            n_chk = -(-f.n // 8) * 8
+            if n_chk > _lib.PFG_MAX_CHK:
+                raise ValueError("feeder has %d nodes (max %d for convergence='opendss')"
+                                 % (f.n, _lib.PFG_MAX_CHK))
+            V0cs = np.zeros(n_chk, complex)
+            V0cs[:f.n] = V0c / vbn
+            self._g_Gc = dev_c(emaj((Gc / vb[None, :]) / vbn[:, None], n_chk))
+            self._g_V0c = dev_c(V0cs)
+        self._g_n_chk = n_chk
+        self._vmin = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
+        self._vmax = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
+        self._all_nodes = len(idx) == f.n
+        self.v_out = torch.zeros((max(no, 1), self.num_envs), dtype=torch.float64, device=dev)
+        self._own_v_out = self.v_out
+        self._bv_cache = {}
+        self._iters = torch.zeros(self.num_envs, dtype=torch.int32, device=dev)
+        self._base_params()
+
+    def _general_elems(self):
+        """pgw_pfg_elem per (padded) element: the load's base kW / kvar, its
+        phases, the Yeq power in OpenDSS's Y ("opendss"), the voltage band and
+        the controllable slot."""
+        f, mp = self.feeder, self.M
+        arr = (_lib.PFGElem * mp)()
+        for k in range(mp):
+            e = arr[k]
+            if k < f.m:
+                li = f.elem_load[k]
+                e.base_kw, e.base_kvar, e.nph = f.base_kw[li], f.base_kvar[li], f.elem_nph[k]
+                if self.convergence == "opendss":
+                    e.y0r = f.base_kw[li] * 1000.0 / f.elem_nph[k]
+                    e.y0i = -(f.base_kvar[li] * 1000.0 / f.elem_nph[k])
+                e.vlo2, e.vmn2, e.vmx2 = f.elem_vlow[k] ** 2, f.elem_vmin[k] ** 2, f.elem_vmax[k] ** 2
+                ln = f.load_names[li]
+                e.ctrl = self._ctrl_names.index(ln) if ln in self._ctrl_names else -1
+            else:
+                e.nph, e.vlo2, e.vmn2, e.vmx2, e.ctrl = 1.0, 0.25, 0.9025, 1.1025, -1
+        return arr
+
     def set_controllable_loads(self, names):
         """Load names that receive per-env controllable P/Q (<= 8)."""
         names = [n for n in names if n in self.load_bus_name]
@@ -161,6 +274,8 @@ class OpenDSSSolver(PowerFlowSolver):
             self._base_params()
 
     def _base_params(self):
+        if self.general:
+            return self._base_params_general()
         f, M = self.feeder, self.M
         p = _lib.PFParams()
         for k in range(M):
@@ -184,6 +299,28 @@ class OpenDSSSolver(PowerFlowSolver):
         self._pred_index = {}
         self._warm = None              # (cold, warm) PFTables over the previous solutions
 
+    def _base_params_general(self):
+        p = _lib.PFGParams()
+        p.m, p.n_chk, p.n_out, p.n_ctrl = self.M, self._g_n_chk, len(self.output_names), len(self._ctrl_names)
+        p.mode = _lib.PF_OPENDSS if self.convergence == "opendss" else _lib.PF_EXACT
+        p.min_iter, p.max_iter, p.tol = self.min_iter, self.max_iter, self.tol
+        p.coef, p.rescale = 1.0, float(self.system_load_rescale_factor)
+        self.params = p
+        elems = self._general_elems()
+        self._g_elem = torch.tensor(np.frombuffer(bytes(elems), np.uint8), device=self.device)
+        self.tables = _lib.PFGTables(elem=self._g_elem.data_ptr(), W=self._g_W.data_ptr(),
+                                     U0=self._g_U0.data_ptr(), G=self._g_G.data_ptr(),
+                                     V0=self._g_V0.data_ptr(),
+                                     Gc=self._g_Gc.data_ptr() if self._g_Gc is not None else None,
+                                     V0c=self._g_V0c.data_ptr() if self._g_V0c is not None else None,
+                                     v_min_out=self._vmin.data_ptr(), v_max_out=self._vmax.data_ptr())
+        self._cfg_version = getattr(self, "_cfg_version", 0) + 1
+        self.tables_version = getattr(self, "tables_version", 0) + 1
+        self._step_cache = {}
+        self._tables_cache = {}
+        self._pred_index = {}
+        self._warm = None
+
     def hour_of(self, current_time):
         """Hour of year of a step time (opendss.py:98-103), memoized per time."""
         h = self._hour_memo.get(current_time)
@@ -203,6 +340,13 @@ class OpenDSSSolver(PowerFlowSolver):
         key = (hour, self._cfg_version)
         p = self._step_cache.get(key)
         if p is not None:
+            return p
+        if self.general:      # the kernel forms (coef * base) * rescale per element
+            p = _lib.PFGParams.from_buffer_copy(self.params)
+            p.coef = float(self.annual_hourly_load_profile[hour])
+            if len(self._step_cache) > 4096:
+                self._step_cache.clear()
+            self._step_cache[key] = p
             return p
         coef = self.annual_hourly_load_profile[hour]
         step_load = coef * self.base_load * self.system_load_rescale_factor
@@ -224,7 +368,7 @@ class OpenDSSSolver(PowerFlowSolver):
         PREDICTOR_LOOKAHEAD - 1 hours in ONE launch (the hours differ only by
         the loadshape coefficient, passed as a per-env load scale), so an
         episode pays for about one table solve.  Otherwise the cold-start tables."""
-        if not (self.use_predictor and len(self._ctrl_names) == 1):
+        if self.general or not (self.use_predictor and len(self._ctrl_names) == 1):
             return self.tables
         hour = self.hour_of(current_time)
         key = (hour, self._cfg_version)
@@ -328,9 +472,9 @@ class OpenDSSSolver(PowerFlowSolver):
                 cp = torch.stack([x if x is not None else zeros for x in ps])
                 cq = torch.stack([x if x is not None else zeros for x in qs])
         tables = self.solve_tables(current_time, cp is not None)
-        _lib.check(_lib.lib().pgw_pf_solve(p, tables, n, _lib.dptr(cp), _lib.dptr(cq),
-                                           _lib.dptr(self.v_out), _lib.dptr(self._iters),
-                                           _lib.stream_ptr(self.device)))
+        fn = _lib.lib().pgw_pf_solve_general if self.general else _lib.lib().pgw_pf_solve
+        _lib.check(fn(p, tables, n, _lib.dptr(cp), _lib.dptr(cq), _lib.dptr(self.v_out),
+                      _lib.dptr(self._iters), _lib.stream_ptr(self.device)))
         self.solved(tables)
         self.iterations = self._iters
         self._prepare_bus_voltages()
@@ -358,9 +502,10 @@ class OpenDSSSolver(PowerFlowSolver):
         if self._warm is None:
             if self._U_prev is None or self._U_prev.shape[1] != self.M:
                 self._U_prev = torch.zeros((self.num_envs, self.M, 2), dtype=torch.float64, device=self.device)
-            cold = _lib.PFTables.from_buffer_copy(self.tables)
+            T = type(self.tables)
+            cold = T.from_buffer_copy(self.tables)
             cold.U_out = self._U_prev.data_ptr()
-            warm = _lib.PFTables.from_buffer_copy(cold)
+            warm = T.from_buffer_copy(cold)
             warm.U_init = self._U_prev.data_ptr()
             self._warm, self._warm_valid = (cold, warm), False
         return self._warm[1] if self._warm_valid else self._warm[0]

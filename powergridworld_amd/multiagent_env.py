@@ -378,6 +378,8 @@ class MultiAgentEnv(Env):
         from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
         if not isinstance(self.pf_solver, OpenDSSSolver):
             return "power flow solver is not the batched OpenDSSSolver"
+        if self.pf_solver.general:
+            return "the power flow runs the general kernel (large feeder or convergence='opendss')"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)
@@ -641,6 +643,8 @@ class MultiAgentEnv(Env):
         from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
         if not isinstance(self.pf_solver, OpenDSSSolver):
             return "power flow solver is not the batched OpenDSSSolver"
+        if self.pf_solver.general:
+            return "the power flow runs the general kernel (large feeder or convergence='opendss')"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)

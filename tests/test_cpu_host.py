@@ -76,6 +76,7 @@ def test_pf_fixed_point_solves_nodal_equations():
     np.testing.assert_allclose(S.imag[band], var_ph[band], rtol=1e-9, atol=1e-6)
 
 
+FEEDER48 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "feeder48.dss")
 REGCAP = os.path.join(REPO, "tests", "data", "regcap_feeder.dss")
 
 
@@ -129,6 +130,32 @@ def test_dss_unsupported_control_and_models_refused(tmp_path):
     p.write_text(text.replace("Model=2 kV=2.4", "Model=5 kV=2.4"))
     with pytest.raises(NotImplementedError, match="model 5"):
         Feeder(load_feeder_spec(str(p)))
+
+
+def test_feeder48_native_build_and_opendss_model():
+    """The 48-element synthetic feeder (tests/data/feeder48.dss, beyond the fast
+    kernels' 16): native Y / Z equal the oracle's NumPy build; with the loads'
+    nominal admittances stamped (OpenDSS's iteration matrix, load_yprim) Y
+    grows by exactly C^T diag(Yeq) C, and the oracle's OpenDSS-semantics solve
+    stops within OpenDSS's tolerance of the fixed point."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    spec = load_feeder_spec(FEEDER48)
+    f, o = Feeder(spec), OracleFeeder(spec)
+    assert f.m == 48 and f.node_names == o.node_names
+    assert np.abs(f.Y - o.Y).max() / np.abs(o.Y).max() < 1e-12
+    assert np.abs(f.Z - o.Z).max() / np.abs(o.Z).max() < 1e-9
+    fy = Feeder(spec, load_yprim=True)
+    S = (f.base_kw[f.elem_load] - 1j * f.base_kvar[f.elem_load]) * 1000.0 / f.elem_nph
+    C = o.Cinc
+    np.testing.assert_allclose(fy.Y, f.Y + C.T @ np.diag(S / f.elem_vbase ** 2) @ C, rtol=0,
+                               atol=1e-12 * np.abs(f.Y).max())
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float)[None]
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float)[None]
+    V, _ = o.solve(1.2 * kw, 1.2 * kvar, tol=1e-12)
+    Vd, it = o.snap_opendss(1.2 * kw, 1.2 * kvar, o.base_kw, o.base_kvar)
+    assert 2 <= it[0] <= 15
+    assert np.abs(o.pu(Vd) - o.pu(V)).max() < 1e-4
 
 
 def test_dss_edits_of_unsimulated_classes_refused(tmp_path):
