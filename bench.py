@@ -49,19 +49,19 @@ AGENT_BYTES = 112 + 200
 AGENT_BYTES_F32 = AGENT_BYTES // 2       # the same items in fp32 (pgw_coord_step_f32)
 # k_coord_pf -- per env: reads 5 agent powers + 5 rewards, writes 5 rewards + v + vv + iters
 PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
-# k_coord_fused -- the whole C4 step per env: 5 agents (312 B each, reward and
-# power written once) + V675.3, vv (8 B each) and PF iterations (4 B)
-FUSED_BYTES = AGENT_BYTES * N_AGENTS + 8 + 8 + 4
 # k_coord_pf -- algorithmic fp64 FLOPs (m = 14 load phase elements): per fixed-point
 # iteration 8 m^2 (complex matvec) + 12 m (PQ current law) + 6 m (update, |du|^2 test);
 # per env once more the final currents (12 m), one node voltage (8 m + 4) and the reward.
 M_ELEM = 14
 PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
 PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
-PF_KERNEL = ("k_coord_pf_split" if os.environ.get("PGW_PF_SPLIT", "0").startswith("1")
-             else "k_coord_pf<14,true,false,false>")
-PF_HALF = os.environ.get("PGW_PF_HALF", "0").startswith("1")   # 32 envs per PF wave (option, slower)
-KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_fused", "k_ma_step")   # PGW_T_* order
+# k_pf_general in OpenDSS mode (m = 16 padded element rows, 40 padded check rows =
+# every node): per iteration 8 x 16 x (16 + 40) complex-MAC flops + the current
+# law, per env the output row
+PFG_FLOPS_ITER = 8 * 16 * (16 + 40) + 14 * 16
+PF_KERNEL = "k_coord_pf<14,true,false,false>"
+# PGW_T_* order (include/pgw.h); slot 3 is unused since round 3
+KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "(unused)", "k_ma_step", "k_pf_general")
 
 
 def parse():
@@ -111,14 +111,12 @@ def f32_variant(n, steps, warmup, pool_size, seed, dev):
                 env.reset()
     run(warmup)
     torch.cuda.synchronize()
-    _lib.check(_lib.lib().pgw_timing_start(16))
     t0 = time.perf_counter()
     run(steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    tot = (_lib.C.c_double * len(KERNELS))()
-    cnt = (_lib.C.c_int64 * len(KERNELS))()
-    _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
+    # kernel durations in a separate pass (every launch event-timed), as the headline's
+    tot, cnt = timed_pass(run, 64)
     a_us = tot[0] / cnt[0] * 1e3 if cnt[0] else None
     p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
     out = {"dtype": "f32 storage, f64 arithmetic", "value": N_AGENTS * n * steps / dt,
@@ -129,9 +127,66 @@ def f32_variant(n, steps, warmup, pool_size, seed, dev):
                                   "achieved": (AGENT_BYTES_F32 * N_AGENTS * n / (a_us * 1e-6) / 1e9
                                                if a_us else None),
                                   "peak": HBM_PEAK_GBS, "unit": "GB/s"},
-           "k_coord_pf_avg_us": p_us}
+           "k_coord_pf_avg_us": p_us,
+           "kernel_timing": "every launch of a separate 64-step pass after the timed region"}
     if a_us:
         out["k_coord_agents_std"]["frac"] = out["k_coord_agents_std"]["achieved"] / HBM_PEAK_GBS
+    return out
+
+
+def timed_pass(run, steps):
+    """Kernel durations: `steps` more steps with every launch bracketed by HIP
+    events on its own stream (pgw_timing_*); returns (total ms, launches) per
+    PGW_T_* slot.  Never inside a timed region: an event-bracketed launch costs
+    ~10 us of step time."""
+    from powergridworld_amd import _lib
+    _lib.check(_lib.lib().pgw_timing_start(1))
+    run(steps)
+    torch.cuda.synchronize()
+    tot = (_lib.C.c_double * len(KERNELS))()
+    cnt = (_lib.C.c_int64 * len(KERNELS))()
+    _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
+    return tot, cnt
+
+
+def opendss_variant(n, steps, warmup, pool, dev):
+    """The same C4 workload with OpenDSSSolver(convergence="opendss") -- OpenDSS's
+    own snap-solve stopping rule (loads' Yeq in Y, direct-solution start, node
+    magnitude test at 1e-4, 2..15 iterations), on the fused general-PF step
+    (pgw_coord_step_general).  Reported beside the headline: the default
+    solver converges every env to the fixed point."""
+    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
+                                                          make_c4_config)
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence="opendss"), num_envs=n,
+                                             device=dev, fused=True)
+    P = pool.shape[0]
+    env.reset()
+    k = [0]
+
+    def run(m):
+        for _ in range(m):
+            _, _, dones, _ = env.step(pool[k[0] % P])
+            k[0] += 1
+            if dones["__all__"]:
+                env.reset()
+    run(warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tot, cnt = timed_pass(run, 64)
+    it = env.pf_solver.iterations.abs().double()
+    g_us = tot[5] / cnt[5] * 1e3 if cnt[5] else None
+    out = {"pf_convergence": "opendss", "value": N_AGENTS * n * steps / dt, "unit": "agent-env-steps/s",
+           "ms_per_step": dt / steps * 1e3, "steps": steps, "pf_iterations_mean": float(it.mean()),
+           "k_coord_agents_std_avg_us": tot[0] / cnt[0] * 1e3 if cnt[0] else None,
+           "k_pf_general": {"avg_us": g_us, "bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFS,
+                            "note": "fp64 VALU; 38 node rows checked every iteration"}}
+    if g_us:
+        tfs = (PFG_FLOPS_ITER * float(it.mean())) * n / (g_us * 1e-6) / 1e12
+        out["k_pf_general"].update(achieved=tfs, frac=tfs / FP64_PEAK_TFS)
+    del env
     return out
 
 
@@ -321,12 +376,28 @@ def main():
     # an event-bracketed launch costs ~10 us of extra step time (measured: the
     # driver-shaped 20-step run went 36 -> 44 us/step with every 2nd launch timed).
     time_steps = max(8, min(args.steps, args.time_steps))
-    _lib.check(_lib.lib().pgw_timing_start(1))
-    run(time_steps)
+    tot, cnt = timed_pass(run, time_steps)
+    # one whole episode: from the first step after a reset through
+    # its last step AND the reset that follows (per-episode reset kernels, the
+    # predictor-table solves of the next hours), no events; reported beside the
+    # driver's region, which is shorter than an episode
+    while True:
+        _, _, dones, _ = env.step(packed[step_count % P])
+        step_count += 1
+        if dones["__all__"]:
+            env.reset()
+            break
     torch.cuda.synchronize()
-    tot = (_lib.C.c_double * len(KERNELS))()
-    cnt = (_lib.C.c_int64 * len(KERNELS))()
-    _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
+    ep0, ep_steps = time.perf_counter(), 0
+    while True:
+        _, _, dones, _ = env.step(packed[step_count % P])
+        step_count += 1
+        ep_steps += 1
+        if dones["__all__"]:
+            env.reset()
+            break
+    torch.cuda.synchronize()
+    ep_elapsed = pgd.max_over_ranks(time.perf_counter() - ep0, dev)
     total_envs = n * world
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
@@ -336,7 +407,7 @@ def main():
         mean_it, max_it = float(it.mean()), int(it.max())
         # the PF kernel runs one wave (64 envs) per SIMD: its time follows the
         # slowest wave, so report how many waves need 1, 2, ... iterations
-        wenv = 32 if (PF_KERNEL == "k_coord_pf_split" or PF_HALF) else 64      # envs per PF wave
+        wenv = 64                                                             # envs per PF wave
         wmax = env.pf_solver.iterations.abs()[: (n // wenv) * wenv].view(-1, wenv).max(1).values
         wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
         traffic = load_traffic()
@@ -353,23 +424,11 @@ def main():
             tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (p_us * 1e-6) / 1e12
             kernels[KERNELS[1]] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
                                    "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); "
-                                           "latency-bound; %s" % ("32 envs per wave (each on two "
-                                           "lanes), two waves per SIMD at 65,536 envs" if PF_HALF else
-                                           "one wave per SIMD at 65,536 envs"),
+                                           "latency-bound; one wave per SIMD at 65,536 envs",
                                    "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                                    "frac": tfs / FP64_PEAK_TFS,
                                    "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
                                    "traffic": traffic.get(KERNELS[1])}
-        f_us = avg_us[KERNELS[3]]
-        if f_us:
-            gbs = FUSED_BYTES * n / (f_us * 1e-6) / 1e9
-            tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (f_us * 1e-6) / 1e12
-            kernels[KERNELS[3]] = {"avg_us": f_us, "timed_launches": cnt[3], "bound": "hbm",
-                                   "note": "agents + power flow in one launch (C4 fast path); "
-                                           "PF fp64 TFLOP/s over the same launch in pf_tflops",
-                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": FUSED_BYTES * n,
-                                   "traffic": traffic.get(KERNELS[3]), "pf_tflops": tfs}
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "
@@ -399,6 +458,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step_episode": ep_elapsed / ep_steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -421,10 +481,17 @@ def main():
                                       "`steps` steps right after the timed region (not inside it)"},
             "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist,
                               "unconverged_envs": unconverged},
+            "episode": {"steps": ep_steps, "ms_per_step": ep_elapsed / ep_steps * 1e3,
+                        "value": N_AGENTS * total_envs * ep_steps / ep_elapsed,
+                        "note": "one whole episode after the timed region: its %d steps and the "
+                                "env.reset() that ends it (reset kernels, predictor tables of the "
+                                "next hours), no events" % ep_steps},
         }
         if world == 1 and not args.no_variants:
             out["variants"] = {"f32": f32_variant(n, min(args.steps, 286), args.warmup, P,
-                                                  pgd.rank_seed(0, rank), dev)}
+                                                  pgd.rank_seed(0, rank), dev),
+                               "opendss_pf": opendss_variant(n, min(args.steps, 286), args.warmup, packed,
+                                                             dev)}
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out))

@@ -458,7 +458,7 @@ int32_t pgw_pf_solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, i
  * the summed duration (ms) and the number of timed launches (PGW_T_COUNT
  * entries each).
  * ---------------------------------------------------------------------- */
-enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COORD_FUSED = 3,
+enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_RESERVED3 = 3,
        PGW_T_MA_STEP = 4, PGW_T_PF_GENERAL = 5, PGW_T_COUNT = 6 };
 /* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
@@ -573,6 +573,14 @@ typedef struct pgw_coord_buffers_f32 {
   float* vv;
   int32_t* iters;
 } pgw_coord_buffers_f32;
+
+/* The same coordinated step with the general power flow (pgw_pf_solve_general:
+ * large feeders, OpenDSS's stopping rule): the agents' kernel, then the general
+ * solve with the bus loads summed from agent_power (agent order) and the
+ * coordinated voltage-violation epilogue on output row p->vv_row. */
+int32_t pgw_coord_step_general(const pgw_coord_params* p, const pgw_pfg_params* pf,
+                               const pgw_pfg_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                               pgw_coord_buffers b, void* stream);
 
 int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
                            const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,

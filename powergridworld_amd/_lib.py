@@ -263,6 +263,8 @@ _SIGS = {
                              CoordBuffers, vp]),
     "pgw_coord_step_f32": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
                                  CoordBuffersF32, vp]),
+    "pgw_coord_step_general": (i32, [P(CoordParams), P(PFGParams), P(PFGTables), P(CoordStepInfo), i64,
+                                     CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
     "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
     "pgw_hs_step": (i32, [P(HSParams), P(HSStepInfo), i64, HSBuffers, vp]),

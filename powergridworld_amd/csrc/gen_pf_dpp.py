@@ -246,102 +246,6 @@ def gen_rows(M):
     return "\n".join(res)
 
 
-# ---------------------------------------------------------------- split solve
-# k_coord_pf_split: an env's M load elements split over S lanes (one per
-# 64/S-lane part of the wave; part h owns elements h*P .. h*P+P-1, P = M/S).
-# Each part's resident entries sit in its own 16-lane rows, so one
-# row_newbcast feeds every part its own operand.  Per-part layout:
-#   W''(c, i, k)  at k*3P + c*P + i     (own row i < P, column k < M, c = Re/Im/Re+Im)
-#   u0 re / im / re+im of own element i at 3PM + {0, P, 2P} + i
-#   output row 0: G re (M), G im (M), V0 re, V0 im   (the same in every part)
-# and the s tables (s0 re, s0 im, d/d kW, d/d kvar of own element j) at
-# {0, P, 2P, 3P} + j of their own pairs.
-def split_layout(M, S):
-    P = M // S
-    u0re = 3 * P * M
-    g0re = u0re + 3 * P
-    return dict(P=P, u0re=u0re, u0im=u0re + P, u0sum=u0re + 2 * P, g0re=g0re, g0im=g0re + M,
-                v0re=g0re + 2 * M, v0im=g0re + 2 * M + 1, size=g0re + 2 * M + 2)
-
-
-def gen_split(M, S):
-    L = split_layout(M, S)
-    P = L["P"]
-    nr = (L["size"] + 15) // 16
-    ns = (4 * P + 15) // 16
-    tag = "%d, %d" % (M, S)
-    res = []
-
-    def bcast(name, groups):
-        ents = [g + i for g in groups for i in range(P)]
-        ps, pidx = pairs_of(ents)
-        n_out = len(groups) * P
-        lines = ["v_mov_b64_dpp %%%d, %%%d row_newbcast:%d %s"
-                 % (j * P + i, n_out + pidx[(g + i) // 16], (g + i) % 16, DPP)
-                 for j, g in enumerate(groups) for i in range(P)]
-        outs = ['"=&v"(o%d[%d])' % (j, i) for j in range(len(groups)) for i in range(P)]
-        ins = ['"v"(w[%d])' % p for p in ps]
-        args = ", ".join("double (&o%d)[%d]" % (j, P) for j in range(len(groups)))
-        return ("template <> __device__ __forceinline__ void %s<%s>(%s, const double (&w)[%d]) {\n%s}\n"
-                % (name, tag, args, nr, asm_stmt(lines, outs, ins)))
-
-    res.append(bcast("pfs_acc_init", [L["u0re"], L["u0sum"]]))
-    res.append(bcast("pfs_u0", [L["u0re"], L["u0im"]]))
-    ps, pidx = pairs_of([L["v0re"], L["v0im"]])
-    lines = ["v_mov_b64_dpp %%0, %%%d row_newbcast:%d %s" % (2 + pidx[L["v0re"] // 16], L["v0re"] % 16, DPP),
-             "v_mov_b64_dpp %%1, %%%d row_newbcast:%d %s" % (2 + pidx[L["v0im"] // 16], L["v0im"] % 16, DPP)]
-    res.append("template <> __device__ __forceinline__ void pfs_v0<%s>(double& vr, double& vi, "
-               "const double (&w)[%d]) {\n%s}\n"
-               % (tag, nr, asm_stmt(lines, ['"=&v"(vr)', '"=&v"(vi)'], ['"v"(w[%d])' % p for p in ps])))
-    for j in range(P):
-        e_sr, e_si, e_fr, e_fi = j, P + j, 2 * P + j, 3 * P + j
-        ps, pidx = pairs_of([e_sr, e_si, e_fr, e_fi])
-        op = lambda e: "%%%d" % (2 + pidx[e // 16])
-        pc, qc = "%%%d" % (2 + len(ps)), "%%%d" % (3 + len(ps))
-        lines = ["v_mov_b64_dpp %%0, %s row_newbcast:%d %s" % (op(e_sr), e_sr % 16, DPP),
-                 "v_fmac_f64_dpp %%0, %s, %s row_newbcast:%d %s" % (op(e_fr), pc, e_fr % 16, DPP),
-                 "v_mov_b64_dpp %%1, %s row_newbcast:%d %s" % (op(e_si), e_si % 16, DPP),
-                 "v_fmac_f64_dpp %%1, %s, %s row_newbcast:%d %s" % (op(e_fi), qc, e_fi % 16, DPP)]
-        res.append("template <> __device__ __forceinline__ void pfs_power<%s, %d>(\n"
-                   "    double& s_r, double& s_i, const double (&s)[%d], double pc, double qc) {\n%s}\n"
-                   % (tag, j, ns, asm_stmt(lines, ['"=&v"(s_r)', '"=&v"(s_i)'],
-                                           ['"v"(s[%d])' % p for p in ps] + ['"v"(pc)', '"v"(qc)'])))
-    for k in range(M):
-        # the column's own-row accumulations, then output row 0 (pf_column_v's
-        # operations for the rows this part owns, in the same order per chain)
-        gr, gi = L["g0re"] + k, L["g0im"] + k
-        ents = [k * 3 * P + c * P + i for c in range(3) for i in range(P)] + [gr, gi]
-        ps, pidx = pairs_of(ents)
-        n_out = 3 * P + 2
-        xs = n_out + len(ps)
-        w = lambda e: "%%%d" % (n_out + pidx[e // 16])
-        lines = []
-        for c in range(3):
-            for i in range(P):
-                e = k * 3 * P + c * P + i
-                lines.append("v_fmac_f64_dpp %%%d, %s, %%%d row_newbcast:%d %s"
-                             % (c * P + i, w(e), xs + c, e % 16, DPP))
-        vr, vi, ir, ii = "%%%d" % (3 * P), "%%%d" % (3 * P + 1), "%%%d" % xs, "%%%d" % (xs + 1)
-        node = ["v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vr, w(gr), ir, gr % 16, DPP),
-                "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gr), ii, gr % 16, DPP),
-                "v_fmac_f64_dpp %s, -%s, %s row_newbcast:%d %s" % (vr, w(gi), ii, gi % 16, DPP),
-                "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gi), ir, gi % 16, DPP)]
-        step = len(lines) // 4
-        for j in reversed(range(4)):
-            lines.insert(step * j + step // 2, node[j])
-        outs = ['"+v"(A[%d])' % i for i in range(P)] + ['"+v"(B[%d])' % i for i in range(P)] + \
-               ['"+v"(C[%d])' % i for i in range(P)] + ['"+v"(vr)', '"+v"(vi)']
-        ins = ['"v"(w[%d])' % p for p in ps] + ['"v"(ir)', '"v"(ii)', '"v"(is)']
-        res.append("template <> __device__ __forceinline__ void pfs_column_v<%s, %d>(\n"
-                   "    double (&A)[%d], double (&B)[%d], double (&C)[%d], double& vr, double& vi,\n"
-                   "    const double (&w)[%d], double ir, double ii, double is) {\n%s}\n"
-                   % (tag, k, P, P, P, nr, asm_stmt(lines, outs, ins)))
-    return res
-
-
-SPLITS = ((14, 2),)
-
-
 def main():
     ns = (4 * 16 + 15) // 16          # resident s tables: 4 x PGW_PF_MAX_M entries
     out = ["// GENERATED by gen_pf_dpp.py -- do not edit.  DPP-broadcast asm groups of",
@@ -388,23 +292,6 @@ def main():
             out.append(gen_column_v(M, k))
             out.append(gen_power(M, k, ns))
             out.append(gen_band(M, k, nr))
-    out += ["// ---- split solve (k_coord_pf_split): element parts over S lanes",
-            "template <int M, int S> __device__ __forceinline__ void pfs_acc_init(",
-            "    double (&o0)[M / S], double (&o1)[M / S], const double (&w)[PFSplit<M, S>::kPairs]);",
-            "template <int M, int S> __device__ __forceinline__ void pfs_u0(",
-            "    double (&o0)[M / S], double (&o1)[M / S], const double (&w)[PFSplit<M, S>::kPairs]);",
-            "template <int M, int S> __device__ __forceinline__ void pfs_v0(",
-            "    double& vr, double& vi, const double (&w)[PFSplit<M, S>::kPairs]);",
-            "template <int M, int S, int J> __device__ __forceinline__ void pfs_power(",
-            "    double& s_r, double& s_i, const double (&s)[PFSplit<M, S>::kSPairs], double pc, double qc);",
-            "template <int M, int S, int K> __device__ __forceinline__ void pfs_column_v(",
-            "    double (&A)[M / S], double (&B)[M / S], double (&C)[M / S], double& vr, double& vi,",
-            "    const double (&w)[PFSplit<M, S>::kPairs], double ir, double ii, double is);",
-            ""]
-    for M, S in SPLITS:
-        L = split_layout(M, S)
-        out.append("// ---- M = %d split over S = %d lanes (%d resident pairs)" % (M, S, (L["size"] + 15) // 16))
-        out += gen_split(M, S)
     sys.stdout.write("\n".join(out))
 
 

@@ -58,6 +58,22 @@ inline void launch_timed(int id, K kernel, dim3 grid, dim3 block, hipStream_t st
 
 constexpr int kBlock = 256;   // 4 waves of 64
 
+// The general power flow (pgw_pf_general.hip) with an optional coordinated
+// prologue / epilogue (pgw_coord_step_general): bus load = sum of the agents'
+// powers in agent order (multiagent_env.py:171-181), and
+// CoordinatedMultiBuildingControlEnv.reward_transform (train.py:51-88) on the
+// common-bus voltage row.  agent_power == nullptr: a plain solve (ctrl_p/q).
+struct PFGCoord {
+  const double* agent_power;   // n_agents x n
+  double* reward;              // n_agents x n
+  double* vv;                  // n (nullable)
+  int32_t n_agents, vv_row, coordinated, pad_;
+  int32_t agent_ctrl[PGW_MAX_AGENTS];
+  double vv_lo, vv_hi, vv_penalty;
+};
+int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n, const double* cp,
+                      const double* cq, double* v_out, int32_t* iters, const PFGCoord& c, void* stream);
+
 inline unsigned grid_for(int64_t n) {
   return static_cast<unsigned>((n + kBlock - 1) / kBlock);
 }

@@ -85,19 +85,6 @@ constexpr int kSPairs = (4 * PGW_PF_MAX_M + 15) / 16;   // resident s0 / f entri
 template <int M> struct PFRow {
   static constexpr int kPairs = (2 * M + 2 + 15) / 16;
 };
-// Split solve (k_coord_pf_split): the M elements of an env over S lanes, part h
-// owning elements h P .. h P + P - 1 (P = M / S); the per-part resident layout
-// is gen_pf_dpp.py's split_layout.
-template <int M, int S> struct PFSplit {
-  static_assert(M % S == 0, "elements must split evenly");
-  static constexpr int P = M / S;
-  static constexpr int kW = 3 * P * M;                 // W''(c, i, k) at k 3P + c P + i
-  static constexpr int kU0re = kW, kU0im = kW + P, kU0sum = kW + 2 * P;
-  static constexpr int kG0re = kW + 3 * P, kG0im = kG0re + M, kV0re = kG0re + 2 * M;
-  static constexpr int kSize = kV0re + 2;
-  static constexpr int kPairs = (kSize + 15) / 16;
-  static constexpr int kSPairs = (4 * P + 15) / 16;    // s0 re, s0 im, d/d kW, d/d kvar of own j
-};
 #include "pgw_pf_dpp.inc"
 
 __device__ __forceinline__ double fast_rcp(double m) {
@@ -927,19 +914,15 @@ struct CoordPFArgs {
   double vv_lo, vv_hi, vv_penalty;
 };
 
-// EPW = envs per wave: 64 (one lane per env) or 32 (lanes l and l + 32 solve
-// the same env, and only the low half stores).  With 32 a launch has twice the
-// waves -- at 65,536 envs two per SIMD instead of one -- for the same
-// instructions per wave (the idea: a lone fp64 wave per SIMD issues its DPP
-// FMAs at about half the rate two waves reach, profiles/r01/fp64_issue.txt).
-// Slower in practice: see pf_half_waves.
-template <int M, bool UB, bool GC, bool KEEP, class Bufs, int EPW = 64>
+// One lane per env (measured alternatives, removed in round 3: 32 envs per
+// wave, two lanes per env, and agents + PF in one launch were all slower --
+// profiles/r02/pf_half_waves.txt, pf_rows_split_dropped.txt,
+// fused_kernel_dropped.txt).
+template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
                                                      int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;   // double, or float (_f32)
-  const int64_t e = EPW == 64 ? (int64_t)blockIdx.x * kBlock + threadIdx.x
-                              : ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * EPW + (threadIdx.x & (EPW - 1));
-  const bool owner = EPW == 64 || (threadIdx.x & 63) < EPW;   // the lane that stores env e
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   // read once: a reload per phase would put an L2 round trip on the chain
   long long* const trace = g_pf_trace;
@@ -990,10 +973,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   double vsel = v0;
   if constexpr (kKeep)
     pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
-      if (valid && owner && b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
+      if (valid && b.v_out) b.v_out[(int64_t)o * n + e] = (Sto)v;
       vsel = (o == c.vv_row) ? v : vsel;
     });
-  if (!valid || !owner) return;
+  if (!valid) return;
   if (b.v_out) b.v_out[e] = (Sto)v0;
   if (b.iters) b.iters[e] = it;
   pf_trace(trace, 5);
@@ -1011,433 +994,6 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
         (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// K2 split (the C4 fast path: m = 14, uniform band, one controllable slot, one
-// output row): the same step with each env's 14 load elements over TWO lanes,
-// lanes l and l + 32 of a wave (32 envs a wave), part h = l / 32 owning elements
-// 7h .. 7h + 6.  At 65 536 envs that is 2 048 waves, two per SIMD, where the
-// one-lane kernel had one wave per SIMD whose latency chain (agent-power loads
-// -> predictor gathers -> iteration) nothing else could hide.  Per part:
-//   - the resident operands of its own rows (PFSplit), in its own 16-lane
-//     rows, so one row_newbcast feeds each part its own W'' entry;
-//   - its own elements' predictor record slices and currents;
-//   - the other part's currents arrive by v_permlane32_swap, after which
-//     every row accumulates columns 0 .. 13 in order, i.e. the one-lane
-//     kernel's operations per accumulator: the result is bit-identical to
-//     k_coord_pf<14, true, false, false> (and so to the generic path).
-// An env is converged when both its parts are (ballot), so both parts leave
-// the loop together; part 0 writes the outputs.
-__device__ __forceinline__ void swap_halves(double x, double& p0, double& p1) {
-  // v_permlane32_swap of a value with itself: [p0 | p0] and [p1 | p1]
-  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
-  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
-  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  p0 = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
-  p1 = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
-}
-
-template <class Bufs>
-__global__ void __launch_bounds__(kBlock, 2) k_coord_pf_split(CoordPFArgs c, PFArgs a,
-                                                              pgw_pf_tables t, int64_t n, Bufs b) {
-  constexpr int M = 14, S = 2;
-  using L = PFSplit<M, S>;
-  using B = PFBlock<M>;
-  constexpr int P = L::P;
-  using Sto = std::remove_pointer_t<decltype(b.reward)>;
-  const int lane = threadIdx.x & 63;
-  const int h = lane >> 5;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-  const int64_t e = wave * 32 + (lane & 31);
-  const bool valid = e < n;
-  long long* const trace = g_pf_trace;
-  pf_trace(trace, 0);
-  // agent powers first (both parts load the same addresses: one request)
-  double rp[PGW_MAX_AGENTS];
-  const int64_t ec = valid ? e : 0;
-#pragma unroll
-  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-    rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
-             ((valid && ag < c.n_agents) ? 1.0 : 0.0);
-  // this part's resident operands, gathered from the packed block
-  const int l16 = lane & 15;
-  double w[L::kPairs], sres[L::kSPairs];
-#pragma unroll
-  for (int j = 0; j < L::kPairs; ++j) {
-    const int el = 16 * j + l16;
-    int src = -1;
-    if (el < L::kW) {
-      const int k = el / (3 * P), r = el - k * 3 * P, cc = r / P, i = h * P + (r - cc * P);
-      const int lo = min(i, k), hi = max(i, k);
-      src = cc * B::kTri + lo * M - lo * (lo - 1) / 2 + (hi - lo);
-    } else if (el < L::kG0re) {
-      const int r = el - L::kW, q = r / P;
-      src = B::kU0re + q * M + h * P + (r - q * P);
-    } else if (el < L::kSize) {
-      src = B::kG0re + (el - L::kG0re);
-    }
-    w[j] = src >= 0 ? t.block[src] : 0.0;
-  }
-#pragma unroll
-  for (int j = 0; j < L::kSPairs; ++j) {
-    const int el = 16 * j + l16, q = el / P;
-    const int k = q < 4 ? h * P + (el - q * P) : 0;
-    sres[j] = q == 0 ? a.sr0[k] : q == 1 ? a.si0[k] : q == 2 ? a.fr[k] : q == 3 ? a.fi[k] : 0.0;
-  }
-  double cp[PGW_PF_MAX_CTRL];
-#pragma unroll
-  for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = 0.0;
-#pragma unroll
-  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag) {
-    const int slot = ag < c.n_agents ? c.agent_ctrl[ag] : -1;
-#pragma unroll
-    for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
-  }
-  const double pc = cp[0], qc = 0.0;
-  pf_trace(trace, 1);
-  // first guess: the own elements' slice of the predictor record
-  double ur[P], ui[P];
-  if (a.use_pred) {
-    const double g = (pc - a.pred_x0) * a.pred_inv_h;
-    const int c0 = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
-    auto load = [&](int cc, double2 (&u)[P], float2 (&d1)[P], float2 (&d2)[P]) {
-      const char* r = reinterpret_cast<const char*>(t.U_pred) + (int64_t)cc * (32 * M);
-      const double2* pu = reinterpret_cast<const double2*>(r) + h * P;
-      const float2* p1 = reinterpret_cast<const float2*>(r + 16 * M) + h * P;
-      const float2* p2 = reinterpret_cast<const float2*>(r + 24 * M) + h * P;
-#pragma unroll
-      for (int k = 0; k < P; ++k) {
-        u[k] = pu[k];
-        d1[k] = p1[k];
-        d2[k] = p2[k];
-      }
-    };
-    double2 u[P];
-    float2 d1[P], d2[P];
-    int cc = c0;
-    if (t.U_pred_meta) {
-      const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
-      const pgw_pred_meta m = t.U_pred_meta[j];
-      load(c0, u, d1, d2);               // speculatively, with the metadata
-      cc = (g - (double)j < m.tstar) ? m.left : m.right;
-      if (cc != c0) load(cc, u, d1, d2);
-    } else {
-      load(c0, u, d1, d2);
-    }
-    const double tt = g - (double)cc;
-    const double h1 = 0.5 * tt, h2 = 0.5 * tt * tt;
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      ur[k] = fma(h2, (double)d2[k].x, fma(h1, (double)d1[k].x, u[k].x));
-      ui[k] = fma(h2, (double)d2[k].y, fma(h1, (double)d1[k].y, u[k].y));
-    }
-  } else {
-    pfs_u0<M, S>(ur, ui, w);
-  }
-  pf_trace(trace, 2);
-  const double lo2 = a.lo2, mn2 = a.mn2, mx2 = a.mx2, tol2 = a.tol2;
-  int it = 0, my_it = 0;
-  bool done = !valid, conv_ok = !valid;
-  double v0r = 0.0, v0i = 0.0;
-  while (true) {
-    double A[P], Bs[P], C[P], vr, vi, IR[M], II[M];
-    pfs_acc_init<M, S>(A, C, w);
-    pfs_v0<M, S>(vr, vi, w);
-#pragma unroll
-    for (int i = 0; i < P; ++i) Bs[i] = 0.0;
-    // own currents (PFSolver::current's operations), then the exchange
-    static_for<0, P>([&](auto j) {
-      double s_r, s_i;
-      pfs_power<M, S, decltype(j)::value>(s_r, s_i, sres, pc, qc);
-      const double m2 = fma(ui[j], ui[j], ur[j] * ur[j]);
-      double mc = fmin(fmax(m2, mn2), mx2);
-      mc = (m2 <= lo2) ? 1.0 : mc;
-      const double gg = fast_rcp(mc);
-      const double gr = gg * ur[j], gi = gg * ui[j];
-      const double ir = fma(s_r, gr, -(s_i * gi));
-      const double ii = fma(s_r, gi, s_i * gr);
-      swap_halves(ir, IR[j], IR[P + j]);
-      swap_halves(ii, II[j], II[P + j]);
-    });
-    static_for<0, M>([&](auto k) {
-      const double is = IR[k] + II[k];
-      pfs_column_v<M, S, decltype(k)::value>(A, Bs, C, vr, vi, w, IR[k], II[k], is);
-    });
-    bool conv = true;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const double nr = A[i] - Bs[i];
-      const double ni = (C[i] - A[i]) - Bs[i];
-      const double dr = nr - ur[i], di = ni - ui[i];
-      conv &= fma(dr, dr, di * di) < tol2;
-      ur[i] = done ? ur[i] : nr;
-      ui[i] = done ? ui[i] : ni;
-    }
-    // the env has converged when both of its parts have
-    const uint64_t nc = __ballot(!conv);
-    const bool conv_env = ((nc >> lane) & 1ull) == 0 && ((nc >> (lane ^ 32)) & 1ull) == 0;
-    v0r = done ? v0r : vr;
-    v0i = done ? v0i : vi;
-    ++it;
-    my_it = done ? my_it : it;
-    conv_ok = conv_ok || (!done && conv_env);
-    done = done || conv_env || it >= a.max_iter;
-    if (__ballot(!done) == 0ull) break;
-  }
-  pf_trace(trace, 3);
-  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
-  pf_trace(trace, 4);
-  if (!valid || h != 0) return;
-  if (b.v_out) b.v_out[e] = (Sto)v0;
-  if (b.iters) b.iters[e] = conv_ok ? my_it : -my_it;
-  pf_trace(trace, 5);
-  if (c.coordinated) {
-    const double vv = pymax(pymax(0.0, c.vv_lo - v0), v0 - c.vv_hi);
-    if (b.vv) b.vv[e] = (Sto)vv;
-    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
-#pragma unroll
-    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-      if (ag < c.n_agents)
-        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// PGW_PF_SPLIT=1 selects the split kernel (read per call: the tests compare the
-// two in one process).  Off by default: measured slower at 65 536 envs
-// (13.1 vs 9.6 us).
-// ---- K1 + K2 fused (the C4 fast path, fp64): ONE launch per step -----------
-// A block is NW waves over the same 64 envs: wave a first runs agent a's step
-// for them (k_coord_agents_std's arithmetic), leaving the agent's power in LDS
-// and its reward in a register; after a barrier the block solves the 64 envs'
-// power flow together, the 14 load elements' rows spread over the waves (wave
-// w owns rows R w .. R w + R - 1, the last wave also the output row).  Per
-// iteration each wave evaluates the currents of its own elements into LDS;
-// after a barrier every wave accumulates its rows over columns 0 .. 13 in
-// order, reading the currents from LDS and W'' from the operand block through
-// the scalar cache -- per accumulator the one-lane kernel's operations in its
-// order, so the result is bit-identical to k_coord_agents_std +
-// k_coord_pf<14, true, false, false> (and so to the generic path).  The
-// per-env convergence test ANDs the waves' flags through LDS.  Finally the
-// reward is r + (-share), the same single IEEE add the two-launch path's
-// atomic performs, stored once.
-// The aim: in the two-launch step the PF kernel runs one latency-bound wave per
-// SIMD after the agents kernel, with HBM idle (PF ~10 us of a ~30 us step);
-// here the PF's arithmetic and L2 gathers were to overlap other blocks' HBM
-// streaming.  They do not (see coord_fused_enabled): kept as an option.
-constexpr int kFusedM = 14;
-
-template <int NW, int W>
-__device__ __forceinline__ void fused_pf_rows(const PFArgs& a, const pgw_pf_tables& t, const double* blk,
-                                              const CoordPFArgs& c, int64_t n, int64_t e, bool valid,
-                                              int l, double pc, double (*s_ir)[64], double (*s_ii)[64],
-                                              int (*s_flag)[64], double* s_v, double& vsel, int& it_out) {
-  constexpr int M = kFusedM, R = (M + NW - 1) / NW, K0 = R * W;
-  constexpr int NR = (K0 + R <= M) ? R : (K0 < M ? M - K0 : 0);   // rows this wave owns
-  constexpr bool OUT = (W == NW - 1);                             // and the output row
-  using Lo = PFBlock<M>;
-  constexpr int T = Lo::kTri;
-  auto tri = [](int i, int k) { return i <= k ? i * M - i * (i - 1) / 2 + (k - i) : k * M - k * (k - 1) / 2 + (i - k); };
-  const double qc = 0.0;
-  // ---- first guess of the own elements (PFSolver::initial, SPEC form)
-  double ur[R > 0 ? R : 1], ui[R > 0 ? R : 1];
-  if (a.use_pred) {
-    const double g = (pc - a.pred_x0) * a.pred_inv_h;
-    int cc = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
-    if (t.U_pred_meta) {
-      const int j = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
-      const pgw_pred_meta m = t.U_pred_meta[j];
-      cc = (g - (double)j < m.tstar) ? m.left : m.right;
-    }
-    const char* r = reinterpret_cast<const char*>(t.U_pred) + (int64_t)cc * (32 * M);
-    const double2* v = reinterpret_cast<const double2*>(r);
-    const float2* d1 = reinterpret_cast<const float2*>(r + 16 * M);
-    const float2* d2 = reinterpret_cast<const float2*>(r + 24 * M);
-    const double tt = g - (double)cc;
-    const double h1 = 0.5 * tt, h2 = 0.5 * tt * tt;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const double2 u = v[K0 + q];
-      const float2 e1 = d1[K0 + q], e2 = d2[K0 + q];
-      ur[q] = fma(h2, (double)e2.x, fma(h1, (double)e1.x, u.x));
-      ui[q] = fma(h2, (double)e2.y, fma(h1, (double)e1.y, u.y));
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      ur[q] = blk[Lo::kU0re + K0 + q];
-      ui[q] = blk[Lo::kU0im + K0 + q];
-    }
-  }
-  // ---- fixed point (PFSolver::iterate<false>)
-  int it = 0, my_it = 0;
-  bool done = !valid, conv_ok = !valid;
-  double v0r = 0.0, v0i = 0.0;
-  while (true) {
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {       // currents of the own elements (PFSolver::current)
-      const int k = K0 + q;
-      const double s_r = fma(a.fr[k], pc, a.sr0[k]);
-      const double s_i = fma(a.fi[k], qc, a.si0[k]);
-      const double m2 = fma(ui[q], ui[q], ur[q] * ur[q]);
-      double mc = fmin(fmax(m2, a.mn2), a.mx2);
-      mc = (m2 <= a.lo2) ? 1.0 : mc;
-      const double gg = fast_rcp(mc);
-      const double gr = gg * ur[q], gi = gg * ui[q];
-      s_ir[k][l] = fma(s_r, gr, -(s_i * gi));
-      s_ii[k][l] = fma(s_r, gi, s_i * gr);
-    }
-    __syncthreads();
-    double A[R > 0 ? R : 1], Bs[R > 0 ? R : 1], C[R > 0 ? R : 1];
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      A[q] = blk[Lo::kU0re + K0 + q];
-      C[q] = blk[Lo::kU0sum + K0 + q];
-      Bs[q] = 0.0;
-    }
-    double vr = 0.0, vi = 0.0;
-    if constexpr (OUT) {
-      vr = blk[Lo::kV0re];
-      vi = blk[Lo::kV0im];
-    }
-#pragma unroll 1
-    for (int k = 0; k < M; ++k) {
-      const double ir = s_ir[k][l], ii = s_ii[k][l];
-      const double is = ir + ii;
-#pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        const int e3 = tri(K0 + q, k);
-        A[q] = fma(blk[e3], ir, A[q]);
-        Bs[q] = fma(blk[T + e3], ii, Bs[q]);
-        C[q] = fma(blk[2 * T + e3], is, C[q]);
-      }
-      if constexpr (OUT) {
-        const double gr = blk[Lo::kG0re + k], gi = blk[Lo::kG0im + k];
-        vr = fma(gr, ir, vr);
-        vi = fma(gr, ii, vi);
-        vr = fma(-gi, ii, vr);
-        vi = fma(gi, ir, vi);
-      }
-    }
-    bool conv = true;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const double nr = A[q] - Bs[q];
-      const double ni = (C[q] - A[q]) - Bs[q];
-      const double dr = nr - ur[q], di = ni - ui[q];
-      conv &= fma(dr, dr, di * di) < a.tol2;
-      ur[q] = done ? ur[q] : nr;
-      ui[q] = done ? ui[q] : ni;
-    }
-    if constexpr (OUT) {
-      v0r = done ? v0r : vr;
-      v0i = done ? v0i : vi;
-    }
-    s_flag[W][l] = conv ? 1 : 0;
-    __syncthreads();
-    bool all = true;
-#pragma unroll
-    for (int ww = 0; ww < NW; ++ww) all = all && (s_flag[ww][l] != 0);
-    ++it;
-    my_it = done ? my_it : it;
-    conv_ok = conv_ok || (!done && all);
-    done = done || all || it >= a.max_iter;
-    // every wave saw the same flags, so every wave leaves on the same iteration
-    if (__syncthreads_or(!done) == 0) break;
-  }
-  it_out = conv_ok ? my_it : -my_it;
-  if constexpr (OUT) s_v[l] = sqrt(fma(v0i, v0i, v0r * v0r));
-  __syncthreads();
-  vsel = s_v[l];
-  (void)c; (void)n; (void)e;
-}
-
-template <int NW>
-__global__ void __launch_bounds__(64 * NW, 5) k_coord_fused(pgw_coord_params p, pgw_coord_step_info s,
-                                                            int64_t n, pgw_coord_buffers b, double pv_ob,
-                                                            StdDerived dv, CoordPFArgs c, PFArgs a,
-                                                            pgw_pf_tables t, int dbg) {
-  __shared__ double s_pow[NW][64];
-  __shared__ double s_ir[kFusedM][64], s_ii[kFusedM][64];
-  __shared__ int s_flag[NW][64];
-  __shared__ double s_v[64];
-  __shared__ double s_blk[PFBlock<kFusedM>::kSize];   // the operand block, read by broadcast
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int64_t e = (int64_t)blockIdx.x * 64 + l;
-  const bool valid = e < n;
-  for (int i = threadIdx.x; i < PFBlock<kFusedM>::kSize; i += 64 * NW) s_blk[i] = t.block[i];
-  // ---- agent w of this env (k_coord_agents_std)
-  double my_rew = 0.0, my_pow = 0.0;
-  if (dbg & 1) {
-    if (valid) my_pow = b.agent_power[(int64_t)w * n + e];
-  } else if (valid) {
-    StdAgentIn in[1];
-    const double* ap = b.action.ptr + w * b.act_stride_agent + e * b.action.s_env;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) in[0].av[j] = ld_act(ap + j * b.action.s_dim);
-    double* xp = b.x + (int64_t)w * 5 * n + e;
-#pragma unroll
-    for (int z = 0; z < 5; ++z) in[0].xs[z] = xp[z * n];
-    double* socp = b.soc + (int64_t)w * n + e;
-    in[0].soc = *socp;
-    double* op = b.obs.ptr + w * b.obs_stride_agent + e * b.obs.s_env;
-    std_agent_compute<1>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
-      if (slot < kSlotSoc) xp[slot * n] = v[0];
-      else if (slot == kSlotSoc) *socp = v[0];
-      else if (slot < kSlotPower) st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
-      else if (slot == kSlotPower) {
-        b.agent_power[(int64_t)w * n + e] = v[0];
-        my_pow = v[0];
-      } else my_rew = v[0];
-    });
-  }
-  s_pow[w][l] = my_pow;
-  __syncthreads();
-  // bus load of the controllable slot (multiagent_env.py:171-181), agents in order
-  double pc = 0.0;
-#pragma unroll
-  for (int ag = 0; ag < NW; ++ag) pc = (c.agent_ctrl[ag] == 0) ? pc + s_pow[ag][l] : pc;
-  double vsel = 0.0;
-  int it = 0;
-  const double* blk = s_blk;
-  if (!(dbg & 2)) static_for<0, NW>([&](auto W) {
-    if (w == decltype(W)::value)
-      fused_pf_rows<NW, decltype(W)::value>(a, t, blk, c, n, e, valid, l, pc, s_ir, s_ii, s_flag, s_v, vsel, it);
-  });
-  if (!valid) return;
-  if (w == 0) {
-    if (b.v_out) b.v_out[e] = vsel;
-    if (b.iters) b.iters[e] = it;
-  }
-  double r = my_rew;
-  if (c.coordinated) {
-    const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
-    if (w == 0 && b.vv) b.vv[e] = vv;
-    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
-    r = r + (-share);
-  }
-  b.reward[(int64_t)w * n + e] = r;
-}
-
-static int coord_fused_dbg() {   // measurement only: 1 = skip the agents' arithmetic, 2 = skip the PF
-  const char* v = getenv("PGW_COORD_FUSED_DBG");
-  return v ? atoi(v) : 0;
-}
-
-// Measured and not the default: with 65,536 envs every
-// block is resident at once, so all blocks run their agent phase together and
-// then their PF phase together -- nothing overlaps, and the block-shaped agent
-// phase itself ran slower (28.7 us alone vs 18 us for k_coord_agents_std).
-// PGW_COORD_FUSED=1 selects it (tests/test_gpu_parity.py checks it bit for bit).
-static bool coord_fused_enabled() {
-  const char* v = getenv("PGW_COORD_FUSED");
-  return v && v[0] == '1';
-}
-
-static bool pf_split_enabled() {
-  const char* v = getenv("PGW_PF_SPLIT");
-  return v && v[0] == '1';
 }
 
 // Stencil metadata of the predictor grid (one thread per segment): in a
@@ -1592,25 +1148,9 @@ static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t 
   return check_launch("k_pf_solve");
 }
 
-// Measured and not the default: 32 envs per wave ran 12.6 us against 9.2 us
-// (profiles/r02/pf_half_waves.txt) -- the iteration phase did not speed up
-// (3.6 vs 3.8 us per wave) and the waves' first loads and L2 gathers got
-// slower.  PGW_PF_HALF=1 selects it.
-static bool pf_half_waves() {
-  const char* v = getenv("PGW_PF_HALF");
-  return v && v[0] == '1';
-}
-
 template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 static int32_t launch_coord_pf(const CoordPFArgs& c, const PFArgs& a, const pgw_pf_tables& t,
                                int64_t n, const Bufs& b, hipStream_t st) {
-  if constexpr (M == 14 && UB && !GC && !KEEP) {
-    if (pf_half_waves()) {   // 32 envs per wave (the C4 fast path)
-      launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP, Bufs, 32>,
-                   dim3((unsigned)((n + 127) / 128)), dim3(kBlock), st, c, a, t, n, b);
-      return check_launch("k_coord_pf");
-    }
-  }
   launch_timed(PGW_T_COORD_PF, k_coord_pf<M, UB, GC, KEEP, Bufs>, dim3(grid_for(n)), dim3(kBlock), st, c, a,
                t, n, b);
   return check_launch("k_coord_pf");
@@ -1654,6 +1194,19 @@ __global__ void __launch_bounds__(kBlock) k_band_penalty(int64_t n, const double
 using namespace pgw;
 
 // pgw_coord_step / pgw_coord_step_f32
+// The agents' half of the coordinated step (k_coord_agents_std or the generic
+// k_coord_agents), fp64 buffers.
+static int32_t launch_coord_agents(const pgw_coord_params& p, const pgw_coord_step_info& s, int64_t n,
+                                   const pgw_coord_buffers& b, double pv_ob, bool std_layout, hipStream_t st) {
+  if (std_layout)
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std<pgw_coord_buffers>, dim3(grid_for(n), p.n_agents),
+                 dim3(kBlock), st, p, s, n, b, pv_ob, make_std_derived(p));
+  else
+    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents, dim3(grid_for(n), p.n_agents), dim3(kBlock), st, p, s, n,
+                 b);
+  return check_launch("k_coord_agents");
+}
+
 template <class Bufs>
 static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
                           const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream) {
@@ -1698,20 +1251,17 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   c.vv_hi = p->vv_hi;
   c.vv_penalty = p->vv_penalty;
   const PFArgs a = make_pf_args(*pf, *pft);
-  if constexpr (!kF32) {
-    bool one_slot = true;
-    for (int ag = 0; ag < p->n_agents; ++ag) one_slot = one_slot && p->agent_ctrl[ag] <= 0;
-    if (std_layout && p->n_agents == 5 && pf->m == 14 && uniform_band(*pf) && pf->n_ctrl <= 1 &&
-        pf->n_out <= 1 && p->vv_row == 0 && one_slot && coord_fused_enabled()) {
-      launch_timed(PGW_T_COORD_FUSED, k_coord_fused<5>, dim3((unsigned)((n + 63) / 64)), dim3(5 * 64), st,
-                   *p, *s, n, b, pv_ob, make_std_derived(*p), c, a, *pft, coord_fused_dbg());
-      return check_launch("k_coord_fused");
+  // fp32: env pairs per lane (float2 accesses).  The pair layout measured for
+  // fp64 too (19.5 -> 20.2 us), so it is instantiated for fp32 only.
+  bool done = false;
+  if constexpr (kF32) {
+    if (std_layout && pairs_ok(b, n)) {
+      launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std_x2<Bufs>, dim3(grid_for(n / 2), p->n_agents),
+                   dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
+      done = true;
     }
   }
-  // (the pair layout measured for fp64 too: 19.5 -> 20.2 us, so fp32 only)
-  if (std_layout && kF32 && pairs_ok(b, n)) {
-    launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std_x2<Bufs>, dim3(grid_for(n / 2), p->n_agents),
-                 dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
+  if (done) {
   } else if (std_layout) {
     launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std<Bufs>, dim3(grid_for(n), p->n_agents),
                  dim3(kBlock), st, *p, *s, n, b, pv_ob, make_std_derived(*p));
@@ -1721,17 +1271,55 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
-  if (pf->m == 14 && uniform_band(*pf) && pf->n_ctrl <= 1 && !pft->load_scale && pf->n_out <= 1 &&
-      pf_split_enabled()) {
-    // two lanes per env, 32 envs per wave (k_coord_pf_split)
-    launch_timed(PGW_T_COORD_PF, k_coord_pf_split<Bufs>, dim3((unsigned)((n + 127) / 128)),
-                 dim3(kBlock), st, c, a, *pft, n, b);
-    return check_launch("k_coord_pf_split");
-  }
   PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
 }
 
+// pgw_coord_step_general: the agents' kernel, then the general power flow with
+// the coordinated prologue (bus load = agent powers summed in agent order) and
+// epilogue (voltage violation, reward -= share) of k_coord_pf.
+static int32_t coord_step_general(const pgw_coord_params* p, const pgw_pfg_params* pf,
+                                  const pgw_pfg_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                                  const pgw_coord_buffers& b, void* stream) {
+  PGW_REQUIRE(p && pf && pft && s && n >= 0, "pgw_coord_step_general: null argument");
+  PGW_REQUIRE(p->n_agents >= 1 && p->n_agents <= PGW_MAX_AGENTS, "pgw_coord_step_general: bad n_agents");
+  PGW_REQUIRE(p->n_comp >= 1 && p->n_comp <= 3, "pgw_coord_step_general: bad n_comp");
+  PGW_REQUIRE(b.action.ptr && b.obs.ptr && b.reward && b.agent_power, "pgw_coord_step_general: null buffer");
+  PGW_REQUIRE(pf->n_out >= 1 && p->vv_row >= 0 && p->vv_row < pf->n_out, "pgw_coord_step_general: bad vv_row");
+  for (int a = 0; a < p->n_agents; ++a)
+    PGW_REQUIRE(p->agent_ctrl[a] < pf->n_ctrl, "pgw_coord_step_general: agent_ctrl out of range");
+  for (int c = 0; c < p->n_comp; ++c) {
+    int k = p->comp_order[c];
+    PGW_REQUIRE(k >= 0 && k <= 2, "pgw_coord_step_general: bad comp_order");
+    if (k == 0) PGW_REQUIRE(b.x && p->act_bld >= 0 && p->bld.n_obs <= PGW_BLD_MAX_OBS, "pgw_coord_step_general: building");
+    if (k == 2) PGW_REQUIRE(b.soc && p->act_bat >= 0, "pgw_coord_step_general: storage");
+  }
+  if (n == 0) return PGW_OK;
+  const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
+                                        - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
+                                     : -s->pv_pmax;
+  int32_t rc = launch_coord_agents(*p, *s, n, b, pv_ob, coord_is_std(*p), (hipStream_t)stream);
+  if (rc) return rc;
+  PFGCoord c = {};
+  c.agent_power = b.agent_power;
+  c.reward = b.reward;
+  c.vv = b.vv;
+  c.n_agents = p->n_agents;
+  c.vv_row = p->vv_row;
+  c.coordinated = p->coordinated;
+  for (int a = 0; a < p->n_agents; ++a) c.agent_ctrl[a] = p->agent_ctrl[a];
+  c.vv_lo = p->vv_lo;
+  c.vv_hi = p->vv_hi;
+  c.vv_penalty = p->vv_penalty;
+  return solve_general(pf, pft, n, nullptr, nullptr, b.v_out, b.iters, c, stream);
+}
+
 extern "C" {
+
+int32_t pgw_coord_step_general(const pgw_coord_params* p, const pgw_pfg_params* pf,
+                               const pgw_pfg_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                               pgw_coord_buffers b, void* stream) {
+  return coord_step_general(p, pf, pft, s, n, b, stream);
+}
 
 int32_t pgw_pf_padded_m(int32_t m) { return padded_m(m); }
 

@@ -40,19 +40,6 @@ constexpr int kGR = 8;             // rows per chunk
 typedef const __attribute__((address_space(4))) double* cdptr;
 typedef const __attribute__((address_space(4))) pgw_pfg_elem* ceptr;
 
-// The coordinated step's prologue / epilogue (pgw_coord_step_general): bus
-// load = sum of the agents' powers in agent order (multiagent_env.py:171-181),
-// and CoordinatedMultiBuildingControlEnv.reward_transform (train.py:51-88) on
-// the common-bus voltage.  agent_power == nullptr: plain solve (ctrl_p/q).
-struct PFGCoord {
-  const double* agent_power;   // n_agents x n
-  double* reward;              // n_agents x n
-  double* vv;                  // n (nullable)
-  int32_t n_agents, vv_row, coordinated, pad_;
-  int32_t agent_ctrl[PGW_MAX_AGENTS];
-  double vv_lo, vv_hi, vv_penalty;
-};
-
 // An element record through the scalar cache (field by field: no aggregate
 // copies out of the constant address space).
 struct ElemV {
@@ -381,9 +368,8 @@ static int32_t dispatch_cn(const pgw_pfg_params& p, const pgw_pfg_tables& t, int
   return launch_general<CE, 8>(p, t, n, cp, cq, v_out, iters, c, st);
 }
 
-static int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n, const double* cp,
-                             const double* cq, double* v_out, int32_t* iters, const PFGCoord& c,
-                             void* stream) {
+int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n, const double* cp,
+                      const double* cq, double* v_out, int32_t* iters, const PFGCoord& c, void* stream) {
   PGW_REQUIRE(p && t && n >= 0, "pgw_pf_solve_general: null argument");
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PFG_MAX_M && p->m % kGR == 0,
               "pgw_pf_solve_general: m=%d (need a multiple of 8, <= %d)", p->m, PGW_PFG_MAX_M);

@@ -40,11 +40,16 @@ class CoordinatedMultiBuildingControlEnv(MultiAgentEnv):
                              v - self.VOLTAGE_LIMITS[1])
 
 
-def make_c4_config(num_buildings=5, sys_load=1.2):
-    """The BASELINE C4 scenario: make_env (train.py:165-188) with 5 buildings."""
-    return make_env_config(
+def make_c4_config(num_buildings=5, sys_load=1.2, pf_convergence="exact"):
+    """The BASELINE C4 scenario: make_env (train.py:165-188) with 5 buildings.
+    pf_convergence: the power flow's stopping rule (OpenDSSSolver convergence:
+    "exact" fixed point, or "opendss" -- OpenDSS's own snap iterate)."""
+    cfg = make_env_config(
         building_config={},
         pv_config={"profile_csv": "pv_profile.csv", "scaling_factor": 40.},
         storage_config={"max_power": 15., "storage_range": (3., 50.)},
         system_load_rescale_factor=sys_load,
         num_buildings=num_buildings)
+    if pf_convergence != "exact":
+        cfg["pf_config"]["config"]["convergence"] = pf_convergence
+    return cfg

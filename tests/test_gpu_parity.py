@@ -408,53 +408,6 @@ def test_c4_fused_equals_generic_full_batch():
         assert d_f == d_g
 
 
-@pytest.mark.parametrize("n", [65536, 1000, 33])
-@pytest.mark.parametrize("variant", ["fused", "split"])
-def test_c4_split_pf_equals_one_lane_pf(n, variant, monkeypatch):
-    """The C4 step's alternative kernels against the two-launch path
-    (k_coord_agents_std + one-lane k_coord_pf), bit for bit: obs, rewards,
-    agent powers, voltage violation, V675.3 and PF iterations over an episode
-    boundary, with bus loads spread over the whole predictor grid (so lanes
-    reload a second record) and batches that leave a wave part-filled.
-    fused: k_coord_fused (agents + PF in one launch, the default);
-    split: k_coord_pf_split (two lanes per env, currents exchanged by
-    permlane32 swap)."""
-    from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
-                                                          make_c4_config)
-    out = []
-    modes = [("1", "0"), ("0", "0")] if variant == "fused" else [("0", "1"), ("0", "0")]
-    for fused_k, split in modes:
-        monkeypatch.setenv("PGW_COORD_FUSED", fused_k)
-        monkeypatch.setenv("PGW_PF_SPLIT", split)
-        env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
-        gen = torch.Generator(DEV).manual_seed(7)
-        rec = []
-        for ep in range(2):
-            env.reset()
-            init = torch.rand((5, n), dtype=torch.float64, device=DEV, generator=gen) * 47 + 3
-            for a, agent in enumerate(env.agents):
-                agent.env_dict["storage"].reset(init_storage=init[a])
-            steps = 3 if ep == 0 else 2
-            for t in range(steps):
-                act = torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2
-                _, rew, _, meta = env.step(act)
-                rec.append((env.packed_obs().clone(), torch.stack([rew[a.name] for a in env.agents]),
-                            torch.stack([a.real_power for a in env.agents]).clone(),
-                            meta["voltage_violation"].clone(),
-                            env.pf_solver.get_bus_voltage_by_name("675c").clone(),
-                            env.pf_solver.iterations.clone()))
-            if ep == 0:        # run the rest of the episode through the boundary
-                done = False
-                while not done:
-                    _, _, d, _ = env.step(act)
-                    done = d["__all__"]
-        out.append(rec)
-        del env
-    for a, b in zip(*out):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
-    its = out[0][-1][5]
-    assert int(its.abs().max()) >= 1 and int((its < 0).sum()) == 0
 
 
 def test_c4_batch_one_and_ragged():
