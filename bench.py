@@ -60,8 +60,12 @@ PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 # law, per env the output row
 PFG_FLOPS_ITER = 8 * 16 * (16 + 40) + 14 * 16
 PF_KERNEL = "k_coord_pf<14,true,false,false>"
-# PGW_T_* order (include/pgw.h); slot 3 is unused since round 3
-KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "(unused)", "k_ma_step", "k_pf_general")
+# PGW_T_* order (include/pgw.h)
+KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_coop", "k_ma_step", "k_pf_general")
+# k_coord_coop (the one-launch C4 step): the agents' bytes plus the PF's own
+# outputs per env (V675.3 8 + vv 8 + iterations 4; the agent powers and rewards
+# stay in LDS / are written once, counted in AGENT_BYTES)
+COOP_BYTES_ENV = AGENT_BYTES * N_AGENTS + 8 + 8 + 4
 
 
 def parse():
@@ -377,6 +381,10 @@ def main():
     # driver-shaped 20-step run went 36 -> 44 us/step with every 2nd launch timed).
     time_steps = max(8, min(args.steps, args.time_steps))
     tot, cnt = timed_pass(run, time_steps)
+    # the PF iteration counts of the last timed-pass step (before the episode
+    # pass below, which ends with a reset whose cold solve would overwrite them)
+    iters_last = env.pf_solver.iterations.clone()
+    unconverged = env.pf_solver.unconverged()
     # one whole episode: from the first step after a reset through
     # its last step AND the reset that follows (per-episode reset kernels, the
     # predictor-table solves of the next hours), no events; reported beside the
@@ -402,13 +410,12 @@ def main():
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
         avg_us = {KERNELS[k]: (tot[k] / cnt[k] * 1e3 if cnt[k] else None) for k in range(len(KERNELS))}
-        unconverged = env.pf_solver.unconverged()
-        it = env.pf_solver.iterations.abs().double()
+        it = iters_last.abs().double()
         mean_it, max_it = float(it.mean()), int(it.max())
-        # the PF kernel runs one wave (64 envs) per SIMD: its time follows the
-        # slowest wave, so report how many waves need 1, 2, ... iterations
+        # the PF runs one wave (64 envs) per SIMD: its time follows the slowest
+        # wave, so report how many waves need 1, 2, ... iterations
         wenv = 64                                                             # envs per PF wave
-        wmax = env.pf_solver.iterations.abs()[: (n // wenv) * wenv].view(-1, wenv).max(1).values
+        wmax = iters_last.abs()[: (n // wenv) * wenv].view(-1, wenv).max(1).values
         wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
         traffic = load_traffic()
         kernels = {}
@@ -429,6 +436,15 @@ def main():
                                    "frac": tfs / FP64_PEAK_TFS,
                                    "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
                                    "traffic": traffic.get(KERNELS[1])}
+        c_us = avg_us[KERNELS[3]]
+        if c_us:
+            gbs = COOP_BYTES_ENV * n / (c_us * 1e-6) / 1e9
+            kernels[KERNELS[3]] = {"avg_us": c_us, "timed_launches": cnt[3], "bound": "hbm",
+                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": COOP_BYTES_ENV * n,
+                                   "traffic": traffic.get(KERNELS[3]),
+                                   "note": "the whole C4 step in one launch: 5 agent waves per 64 envs, "
+                                           "then their power flow shared by the same waves"}
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "

@@ -478,15 +478,19 @@ class MultiAgentEnv(Env):
         same snap solve as the kernel's -- the bus loads summed in agent order
         from the step's agent powers, the same predictor first guess -- on a
         second solver that outputs all nodes, so the values are the ones the
-        generic path reports (tests/test_gpu_parity.py checks fused == generic)."""
+        generic path reports (tests/test_gpu_parity.py checks fused == generic).
+        With OpenDSSSolver(warm_start=True) the kernel started each env from its
+        previous solution, which its own solve has since overwritten: the second
+        solver then starts cold (it keeps no history of its own), so these nodes
+        equal the kernel's solve to the solver tolerance, not bit for bit."""
         if step_no != self._fused_steps:
             raise RuntimeError("voltages of an earlier step: the fused path solves the other nodes "
                                "on demand from the step's agent powers, which a later step overwrote")
         F, solver = self._fused, self.pf_solver
         full = self.__dict__.get("_pf_full")
         if full is None:
-            full = self._pf_full = type(solver)(**self.pf_config["config"], num_envs=self.num_envs,
-                                               device=self.device)
+            cfg = dict(self.pf_config["config"], warm_start=False)
+            full = self._pf_full = type(solver)(**cfg, num_envs=self.num_envs, device=self.device)
         ctrl = solver._ctrl_names
         full.set_controllable_loads(ctrl)
         if reset:                                   # the reset solve: no controllable load
