@@ -60,12 +60,9 @@ PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 # law, per env the output row
 PFG_FLOPS_ITER = 8 * 16 * (16 + 40) + 14 * 16
 PF_KERNEL = "k_coord_pf<14,true,false,false>"
-# PGW_T_* order (include/pgw.h)
-KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "k_coord_coop", "k_ma_step", "k_pf_general")
-# k_coord_coop (the one-launch C4 step): the agents' bytes plus the PF's own
-# outputs per env (V675.3 8 + vv 8 + iterations 4; the agent powers and rewards
-# stay in LDS / are written once, counted in AGENT_BYTES)
-COOP_BYTES_ENV = AGENT_BYTES * N_AGENTS + 8 + 8 + 4
+# PGW_T_* order (include/pgw.h); slot 3 is unused (the one-launch C4 step of
+# round 3 measured slower: profiles/r03/coop_dropped.txt)
+KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "(unused)", "k_ma_step", "k_pf_general")
 
 
 def parse():
@@ -436,15 +433,6 @@ def main():
                                    "frac": tfs / FP64_PEAK_TFS,
                                    "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
                                    "traffic": traffic.get(KERNELS[1])}
-        c_us = avg_us[KERNELS[3]]
-        if c_us:
-            gbs = COOP_BYTES_ENV * n / (c_us * 1e-6) / 1e9
-            kernels[KERNELS[3]] = {"avg_us": c_us, "timed_launches": cnt[3], "bound": "hbm",
-                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": COOP_BYTES_ENV * n,
-                                   "traffic": traffic.get(KERNELS[3]),
-                                   "note": "the whole C4 step in one launch: 5 agent waves per 64 envs, "
-                                           "then their power flow shared by the same waves"}
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "

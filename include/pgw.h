@@ -458,7 +458,7 @@ int32_t pgw_pf_solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, i
  * the summed duration (ms) and the number of timed launches (PGW_T_COUNT
  * entries each).
  * ---------------------------------------------------------------------- */
-enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_COORD_COOP = 3,
+enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_RESERVED3 = 3,
        PGW_T_MA_STEP = 4, PGW_T_PF_GENERAL = 5, PGW_T_COUNT = 6 };
 /* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */

@@ -246,109 +246,6 @@ def gen_rows(M):
     return "\n".join(res)
 
 
-# ---- cooperative groups (k_coord_coop): the coordinated step's power flow
-# shared by the block's five agent waves.  Wave a owns the element rows
-# COOP_ROWS[a] (and the last wave the output row) and keeps a resident table of
-# its own: for its rows q and every column k the three parts of W''[row q][k]
-# (entry c * nr * M + q * M + k), then u0re, u0im, u0sum of its rows, then (the
-# output wave) G0re[k], G0im[k], V0re, V0im.  Per chain the operations and their
-# order are pf_column / pf_column_v's, so every row is bit-identical to the
-# one-lane kernel's.
-COOP_M = 14
-COOP_ROWS = ((0, 1, 2), (3, 4, 5), (6, 7, 8), (9, 10, 11), (12, 13))
-COOP_OUT = 4
-COOP_PAIRS = 9
-
-
-def coop_layout(a):
-    M, nr = COOP_M, len(COOP_ROWS[a])
-    L = dict(nr=nr, u0re=3 * nr * M, u0im=3 * nr * M + nr, u0sum=3 * nr * M + 2 * nr)
-    g = 3 * nr * M + 3 * nr
-    L.update(g0re=g, g0im=g + M, v0re=g + 2 * M, v0im=g + 2 * M + 1)
-    L["size"] = g + (2 * M + 2 if a == COOP_OUT else 0)
-    assert L["size"] <= 16 * COOP_PAIRS
-    return L
-
-
-def gen_coop(a):
-    M, L = COOP_M, coop_layout(a)
-    nr = L["nr"]
-    NP = COOP_PAIRS
-    res = []
-    # accumulator start (u0re, u0sum) and the cold start (u0re, u0im)
-    for name, (g0, g1) in (("coop_acc_init", ("u0re", "u0sum")), ("coop_u0", ("u0re", "u0im"))):
-        lines = []
-        for j, g in enumerate((g0, g1)):
-            for q in range(nr):
-                e = L[g] + q
-                lines.append("v_mov_b64_dpp %%%d, %%%d row_newbcast:%d %s" % (j * nr + q, 2 * nr + e // 16, e % 16, DPP))
-        outs = ['"=&v"(o0[%d])' % q for q in range(nr)] + ['"=&v"(o1[%d])' % q for q in range(nr)]
-        ins = ['"v"(w[%d])' % p for p in range(NP)]
-        res.append("template <> __device__ __forceinline__ void %s<%d>(double (&o0)[%d], double (&o1)[%d], "
-                   "const double (&w)[%d]) {\n%s}\n" % (name, a, nr, nr, NP, asm_stmt(lines, outs, ins)))
-    for k in range(M):
-        lines = []
-        for c in range(3):
-            for q in range(nr):
-                e = c * nr * M + q * M + k
-                lines.append("v_fmac_f64_dpp %%%d, %%%d, %%%d row_newbcast:%d %s"
-                             % (c * nr + q, 3 * nr + 2 * (a == COOP_OUT) + e // 16,
-                                3 * nr + 2 * (a == COOP_OUT) + NP + c, e % 16, DPP))
-        outs = ['"+v"(A[%d])' % q for q in range(nr)] + ['"+v"(B[%d])' % q for q in range(nr)] + \
-               ['"+v"(C[%d])' % q for q in range(nr)]
-        if a == COOP_OUT:
-            w = lambda e: "%%%d" % (3 * nr + 2 + e // 16)
-            xs = 3 * nr + 2 + NP
-            vr, vi, ir, ii = "%%%d" % (3 * nr), "%%%d" % (3 * nr + 1), "%%%d" % xs, "%%%d" % (xs + 1)
-            gr, gi = L["g0re"] + k, L["g0im"] + k
-            node = ["v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vr, w(gr), ir, gr % 16, DPP),
-                    "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gr), ii, gr % 16, DPP),
-                    "v_fmac_f64_dpp %s, -%s, %s row_newbcast:%d %s" % (vr, w(gi), ii, gi % 16, DPP),
-                    "v_fmac_f64_dpp %s, %s, %s row_newbcast:%d %s" % (vi, w(gi), ir, gi % 16, DPP)]
-            step = max(1, len(lines) // 4)
-            for j in reversed(range(4)):
-                lines.insert(min(len(lines), step * j + step // 2), node[j])
-            outs += ['"+v"(vr)', '"+v"(vi)']
-        ins = ['"v"(w[%d])' % p for p in range(NP)] + ['"v"(ir)', '"v"(ii)', '"v"(is)']
-        res.append("template <> __device__ __forceinline__ void coop_column<%d, %d>(\n"
-                   "    double (&A)[%d], double (&B)[%d], double (&C)[%d], double& vr, double& vi,\n"
-                   "    const double (&w)[%d], double ir, double ii, double is) {\n%s%s}\n"
-                   % (a, k, nr, nr, nr, NP, "" if a == COOP_OUT else "  (void)vr;\n  (void)vi;\n",
-                      asm_stmt(lines, outs, ins)))
-    if a == COOP_OUT:
-        lines = ["v_mov_b64_dpp %%0, %%%d row_newbcast:%d %s" % (2 + L["v0re"] // 16, L["v0re"] % 16, DPP),
-                 "v_mov_b64_dpp %%1, %%%d row_newbcast:%d %s" % (2 + L["v0im"] // 16, L["v0im"] % 16, DPP)]
-        ins = ['"v"(w[%d])' % p for p in range(NP)]
-        res.append("__device__ __forceinline__ void coop_v0(double& vr, double& vi, const double (&w)[%d]) {\n%s}\n"
-                   % (NP, asm_stmt(lines, ['"=&v"(vr)', '"=&v"(vi)'], ins)))
-    return "\n".join(res)
-
-
-def coop_main():
-    out = ["// ---- cooperative groups (k_coord_coop): M = %d, rows per wave %s, output row on wave %d"
-           % (COOP_M, COOP_ROWS, COOP_OUT),
-           "constexpr int kCoopM = %d, kCoopWaves = %d, kCoopOut = %d, kCoopPairs = %d;"
-           % (COOP_M, len(COOP_ROWS), COOP_OUT, COOP_PAIRS),
-           "template <int A> struct CoopRows;"]
-    for a, rows in enumerate(COOP_ROWS):
-        L = coop_layout(a)
-        out.append("template <> struct CoopRows<%d> { static constexpr int kN = %d, kFirst = %d, kU0re = %d, "
-                   "kU0im = %d, kU0sum = %d, kG0re = %d, kG0im = %d, kV0re = %d, kV0im = %d, kSize = %d; };"
-                   % (a, len(rows), rows[0], L["u0re"], L["u0im"], L["u0sum"], L["g0re"], L["g0im"],
-                      L["v0re"], L["v0im"], L["size"]))
-    out += ["template <int A> __device__ __forceinline__ void coop_acc_init(",
-            "    double (&o0)[CoopRows<A>::kN], double (&o1)[CoopRows<A>::kN], const double (&w)[kCoopPairs]);",
-            "template <int A> __device__ __forceinline__ void coop_u0(",
-            "    double (&o0)[CoopRows<A>::kN], double (&o1)[CoopRows<A>::kN], const double (&w)[kCoopPairs]);",
-            "template <int A, int K> __device__ __forceinline__ void coop_column(",
-            "    double (&A_)[CoopRows<A>::kN], double (&B)[CoopRows<A>::kN], double (&C)[CoopRows<A>::kN],",
-            "    double& vr, double& vi, const double (&w)[kCoopPairs], double ir, double ii, double is);",
-            ""]
-    for a in range(len(COOP_ROWS)):
-        out.append(gen_coop(a))
-    return "\n".join(out)
-
-
 def main():
     ns = (4 * 16 + 15) // 16          # resident s tables: 4 x PGW_PF_MAX_M entries
     out = ["// GENERATED by gen_pf_dpp.py -- do not edit.  DPP-broadcast asm groups of",
@@ -395,7 +292,6 @@ def main():
             out.append(gen_column_v(M, k))
             out.append(gen_power(M, k, ns))
             out.append(gen_band(M, k, nr))
-    out.append(coop_main())
     sys.stdout.write("\n".join(out))
 
 

@@ -682,131 +682,8 @@ struct StdAgentIn {
   double soc;
 };
 
-// Output slots handed to the store callback.
+// Output slots handed to the store callback as soon as they are final.
 enum StdSlot { kSlotX = 0, kSlotSoc = 5, kSlotObs = 6, kSlotPower = 23, kSlotReward = 24 };
-
-// One standard agent step for E envs at once (E = 1 or 2, computed stage by
-// stage so both envs' chains interleave), in two phases:
-//   std_agent_state: the building state, the storage SoC (in place in `in`),
-//     the building's p_consumed, the agent power and its fresh reward;
-//   std_agent_obs:   the observations from that state, and every store.
-// k_coord_agents_std runs them back to back; k_coord_coop issues its power-flow
-// loads between them (the obs are recomputed from the held state, not held).
-// std_agent_power: the agent's real power from its actions and SoC alone
-// (to_raw of every action, p_consumed, PV, storage step -- the building state
-// is not needed); std_agent_building: the building state update and the fresh
-// reward.  Together they are std_agent_compute's state phase, op for op.
-template <int E>
-__device__ __forceinline__ void std_agent_power(const pgw_coord_params& p, const StdDerived& dv,
-                                                const pgw_coord_step_info& s, StdAgentIn (&in)[E],
-                                                double (&pc)[E], double (&agent_power)[E]) {
-  const pgw_building_params& B = p.bld;
-#pragma unroll
-  for (int q = 0; q < E; ++q) {
-    bool bad = false;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {   // to_raw (utils.py:27-43) with host (hi - lo), (hi + lo)
-      bad = bad || oob_bad(in[q].av[j]);
-      in[q].av[j] = B.rescale ? (clip_fast(in[q].av[j], -1.0, 1.0) * dv.act_rng[j] + dv.act_sum[j]) * 0.5
-                              : in[q].av[j];
-    }
-    if (B.rescale) oob_note(B.oob, bad);
-    pc[q] = building_p_consumed(in[q].av, s.ex_t.T_oa);
-    const double rp_pv = pv_real_power(p.pv, in[q].av[6], s.pv_pmax);
-    const double power = battery_step_rcp(p.bat, in[q].av[7], in[q].soc, dv.rcp_eta_d, dv.rcp_dt_h);
-    // MultiComponentEnv sum (base.py:131-137)
-    double agent_rp = 0.0;
-    agent_rp = agent_rp + pc[q];
-    agent_rp = agent_rp + rp_pv;
-    agent_rp = agent_rp + (-power);
-    agent_power[q] = agent_rp;
-  }
-}
-
-template <int E>
-__device__ __forceinline__ void std_agent_building(const pgw_coord_params& p, const pgw_coord_step_info& s,
-                                                   StdAgentIn (&in)[E], const double (&pc)[E],
-                                                   double (&agent_reward)[E]) {
-  const pgw_building_params& B = p.bld;
-  double T[E][5];
-#pragma unroll
-  for (int q = 0; q < E; ++q)
-#pragma unroll
-    for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
-#pragma unroll
-  for (int z = 0; z < 5; ++z) {
-    const int nz = z < 2 ? 4 : (z == 2 ? 3 : 2);
-#pragma unroll
-    for (int q = 0; q < E; ++q) {
-      const double u0 = s.ex_t.T_oa - T[q][z];
-      const double u1 = in[q].av[z] * (in[q].av[5] - T[q][z]);
-      const double u2 = T[q][nz] - T[q][z];
-      const double u3 = s.ex_t.q_solar[z];
-      double bu = B.B[z][0] * u0;
-      bu = bu + B.B[z][1] * u1;
-      bu = bu + B.B[z][2] * u2;
-      bu = bu + B.B[z][3] * u3;
-      in[q].xs[z] = B.A[z] * in[q].xs[z] + bu;   // T[q][*] still holds the pre-step temps
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < E; ++q) {
-#pragma unroll
-    for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
-    const double r_bld = building_reward(B, T[q], s.ex_next.comfort_lb, s.ex_next.comfort_ub, pc[q],
-                                         exact_div(-pc[q], 12.0, 1.0 / 12.0));
-    double agent_rew = 0.0;
-    agent_rew = agent_rew + r_bld;
-    agent_rew = agent_rew + 0.0;
-    agent_rew = agent_rew + 0.0;
-    agent_reward[q] = agent_rew;
-  }
-}
-
-template <int E, class Store>
-__device__ __forceinline__ void std_agent_obs(const pgw_coord_params& p, const StdDerived& dv,
-                                              const pgw_coord_step_info& s, double pv_ob,
-                                              const StdAgentIn (&in)[E], const double (&pc)[E],
-                                              Store&& store) {
-  const pgw_building_params& B = p.bld;
-  double T[E][5], v[E];
-#pragma unroll
-  for (int z = 0; z < 5; ++z) {
-#pragma unroll
-    for (int q = 0; q < E; ++q) v[q] = in[q].xs[z];
-    store(kSlotX + z, v);
-  }
-#pragma unroll
-  for (int q = 0; q < E; ++q)
-#pragma unroll
-    for (int z = 0; z < 5; ++z) T[q][z] = B.C[z] * in[q].xs[z] + B.mean[z];
-  const double lb = s.ex_next.comfort_lb, ub = s.ex_next.comfort_ub;
-#pragma unroll
-  for (int j = 0; j < 15; ++j) {
-#pragma unroll
-    for (int q = 0; q < E; ++q) {
-      const double o = j < 5 ? T[q][j] - ub : j < 10 ? lb - T[q][j - 5] : j == 10 ? lb
-                     : j == 11 ? ub : j == 12 ? s.ex_next.T_oa : j == 13 ? pc[q] : s.ex_next.time_of_day;
-      double c = clip_fast(o, B.obs_low[j], B.obs_high[j]);
-      if (B.rescale) c = exact_div(2.0 * c - dv.obs_sum[j], dv.obs_rng[j], dv.obs_rcp[j]);
-      v[q] = c;
-    }
-    store(kSlotObs + j, v);
-  }
-  // pv (obs is env-independent: computed once on the host)
-#pragma unroll
-  for (int q = 0; q < E; ++q) v[q] = pv_ob;
-  store(kSlotObs + 15, v);
-#pragma unroll
-  for (int q = 0; q < E; ++q) v[q] = in[q].soc;
-  store(kSlotSoc, v);
-#pragma unroll
-  for (int q = 0; q < E; ++q) {
-    const double c = clip_fast(in[q].soc, p.bat.soc_min, p.bat.soc_max);
-    v[q] = p.bat.rescale ? exact_div(2.0 * c - dv.bat_sum, dv.bat_rng, dv.bat_rcp) : in[q].soc;
-  }
-  store(kSlotObs + 16, v);
-}
 
 // One standard agent step for E envs at once (E = 1 or 2, computed stage by
 // stage so both envs' chains interleave); every output goes to
@@ -1119,293 +996,6 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   }
 }
 
-// ============================================================ cooperative step
-// k_coord_coop: the whole C4 step in ONE launch, a block per 64 envs with one
-// wave per agent (wave a = agent a).  Each wave runs k_coord_agents_std's agent
-// step for its agent, leaves the agent power in LDS and keeps its other outputs
-// in registers; after the block barrier the five waves share the power flow of
-// their 64 envs: wave a owns the element rows COOP_ROWS[a] (gen_pf_dpp.py), their
-// predictor first guess, currents and matvec rows, the last wave also the output
-// row V675.3.  The agent's observations are computed from its held state after
-// the power-flow loads are out (std_agent_obs), so only 9 values stay live.  Currents cross waves through LDS, the convergence test is ANDed
-// through LDS flags.  Why one launch: k_coord_pf is latency-bound (one wave per
-// SIMD, 1 537 instructions on one dependent chain) and ran serially after the
-// HBM-bound agents kernel; here each block's power flow starts as soon as its own
-// agents are done, beside the other blocks' streaming.
-//
-// Ordering: the agent stores are issued AFTER the predictor loads.  Vector
-// memory operations retire in issue order (vmcnt), so a load issued behind the
-// agents' 25 stores would wait for them to reach L2, which under the step's
-// write stream takes the stores' HBM time.  The barriers wait on LDS only
-// (lgkmcnt); a __syncthreads() would wait for the outstanding stores too.
-//
-// Every operation and its order are k_coord_agents_std's and k_coord_pf's (one
-// lane per env): the same rows, the same chains, the same selects -- the outputs
-// are bit-identical to the two-launch step (tests/test_gpu_parity.py).
-struct CoopLds {
-  double pow[kCoopWaves][64];
-  double2 cur[kCoopM][64];
-  int flag[kCoopWaves][64];
-  double share[64];
-};
-
-// s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding: vmcnt in [3:0] and
-// [15:14], expcnt [6:4], lgkmcnt [11:8])
-constexpr int kWaitVmcnt0 = 0x0F70;
-
-__device__ __forceinline__ void coop_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// Entry e of wave A's resident table -> index into the packed PF block, or -1.
-template <int A>
-__device__ __forceinline__ int coop_src(int e) {
-  using R = CoopRows<A>;
-  using Lo = PFBlock<kCoopM>;
-  constexpr int M = kCoopM, nr = R::kN, T = Lo::kTri;
-  if (e < 3 * nr * M) {
-    const int c = e / (nr * M), r = e - c * nr * M, q = r / M, k = r - q * M;
-    const int i0 = R::kFirst + q, i = min(i0, k), kk = max(i0, k);
-    return c * T + i * M - i * (i - 1) / 2 + (kk - i);
-  }
-  e -= 3 * nr * M;
-  if (e < nr) return Lo::kU0re + R::kFirst + e;
-  e -= nr;
-  if (e < nr) return Lo::kU0im + R::kFirst + e;
-  e -= nr;
-  if (e < nr) return Lo::kU0sum + R::kFirst + e;
-  e -= nr;
-  if constexpr (A == kCoopOut) {
-    if (e < M) return Lo::kG0re + e;
-    e -= M;
-    if (e < M) return Lo::kG0im + e;
-    e -= M;
-    if (e == 0) return Lo::kV0re;
-    if (e == 1) return Lo::kV0im;
-  }
-  return -1;
-}
-
-// PFSolver::current's operations (model-1 load law, uniform band), element of
-// power (s_r, s_i).
-__device__ __forceinline__ void coop_current(double ur, double ui, double s_r, double s_i, const PFArgs& a,
-                                             double& ir, double& ii) {
-  const double m2 = fma(ui, ui, ur * ur);
-  double mc = fmin(fmax(m2, a.mn2), a.mx2);
-  mc = (m2 <= a.lo2) ? 1.0 : mc;
-  const double g = fast_rcp(mc);
-  const double gr = g * ur, gi = g * ui;
-  ir = fma(s_r, gr, -(s_i * gi));
-  ii = fma(s_r, gi, s_i * gr);
-}
-
-template <int A, int DBG>
-__device__ __forceinline__ void coop_wave(const pgw_coord_params& p, const pgw_coord_step_info& s,
-                                          int64_t n, const pgw_coord_buffers& b, double pv_ob,
-                                          const StdDerived& dv, const CoordPFArgs& c, const PFArgs& a,
-                                          const pgw_pf_tables& t, CoopLds& L) {
-  using R = CoopRows<A>;
-  constexpr int nr = R::kN;
-  const int l = threadIdx.x & 63;
-  const int64_t e = (int64_t)blockIdx.x * 64 + l;
-  const bool valid = e < n;
-  const int64_t ec = valid ? e : 0;
-  // ---- agent A of env e (k_coord_agents_std); lanes past n step env 0 with
-  // in-range actions (no warning counted) and store nothing
-  StdAgentIn in[1];
-  const double* ap = b.action.ptr + A * b.act_stride_agent + ec * b.action.s_env;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const double v = ld_act(ap + j * b.action.s_dim);
-    in[0].av[j] = valid ? v : 0.0;
-  }
-  double* xp = b.x + (int64_t)A * 5 * n + ec;
-#pragma unroll
-  for (int z = 0; z < 5; ++z) in[0].xs[z] = xp[z * n];
-  double* socp = b.soc + (int64_t)A * n + ec;
-  in[0].soc = *socp;
-  double pcons[1], power[1], rew[1];
-  std_agent_power<1>(p, dv, s, in, pcons, power);
-  L.pow[A][l] = power[0];
-  if constexpr (DBG == 1) {   // measurement: the block-shaped agent phase alone
-    std_agent_building<1>(p, s, in, pcons, rew);
-    if (valid) {
-      double* op = b.obs.ptr + A * b.obs_stride_agent + e * b.obs.s_env;
-      std_agent_obs<1>(p, dv, s, pv_ob, in, pcons, [&](int slot, const double (&v)[1]) {
-        if (slot < kSlotSoc) xp[slot * n] = v[0];
-        else if (slot == kSlotSoc) *socp = v[0];
-        else st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
-      });
-      b.agent_power[(int64_t)A * n + e] = power[0];
-      b.reward[(int64_t)A * n + e] = rew[0];
-    }
-    return;
-  }
-  coop_barrier();
-  // ---- bus load of the controllable slot, agents in order (k_coord_pf)
-  double pc = 0.0;
-#pragma unroll
-  for (int ag = 0; ag < kCoopWaves; ++ag) pc = (c.agent_ctrl[ag] == 0) ? pc + L.pow[ag][l] : pc;
-  const double qc = 0.0;
-  // ---- first guess of this wave's elements (PFSolver::initial<SPEC = true>):
-  // the gathers go out first, the building step runs while they are in flight
-  double ur[nr], ui[nr];
-  const bool pred = a.use_pred && DBG != 4;
-  const double g = (pc - a.pred_x0) * a.pred_inv_h;
-  const int c0 = (int)fmin(fmax(rint(g), 1.0), (double)(a.pred_n - 2));
-  const int jseg = (int)fmin(fmax(floor(g), 0.0), (double)(a.pred_n - 2));
-  double2 ru[nr];
-  float2 r1[nr], r2[nr];
-  auto rec_load = [&](int cc) {
-    const char* r = reinterpret_cast<const char*>(t.U_pred) + (int64_t)cc * (32 * kCoopM);
-#pragma unroll
-    for (int q = 0; q < nr; ++q) {
-      ru[q] = reinterpret_cast<const double2*>(r)[R::kFirst + q];
-      r1[q] = reinterpret_cast<const float2*>(r + 16 * kCoopM)[R::kFirst + q];
-      r2[q] = reinterpret_cast<const float2*>(r + 24 * kCoopM)[R::kFirst + q];
-    }
-  };
-  pgw_pred_meta m = {0.5, c0, c0};
-  if (pred) {
-    if (t.U_pred_meta) m = t.U_pred_meta[jseg];
-    rec_load(c0);
-  }
-  std_agent_building<1>(p, s, in, pcons, rew);
-  // resident table of this wave's rows (a hot 3.4 KB block in L2), ahead of
-  // the agent stores
-  double w[kCoopPairs];
-#pragma unroll
-  for (int j = 0; j < kCoopPairs; ++j) {
-    const int src = coop_src<A>(16 * j + (l & 15));
-    w[j] = src >= 0 ? t.block[src] : 0.0;
-  }
-  if (pred) {
-    int cc = c0;
-    if (t.U_pred_meta) {
-      cc = (g - (double)jseg < m.tstar) ? m.left : m.right;
-      if (cc != c0) rec_load(cc);
-    }
-    const double tt = g - (double)cc;
-    const double h1 = 0.5 * tt, h2 = 0.5 * tt * tt;
-#pragma unroll
-    for (int q = 0; q < nr; ++q) {
-      ur[q] = fma(h2, (double)r2[q].x, fma(h1, (double)r1[q].x, ru[q].x));
-      ui[q] = fma(h2, (double)r2[q].y, fma(h1, (double)r1[q].y, ru[q].y));
-    }
-  } else {
-    coop_u0<A>(ur, ui, w);
-  }
-  // ---- the agent's stores, behind the predictor loads.  Wait for those loads
-  // (and the resident table) first, with a wait the compiler's scoreboard sees:
-  // a use of w inside the loop would otherwise get a conservative vmcnt(0), i.e.
-  // wait for the stores below (measured: +18 us per step).
-  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-  if (valid) {
-    double* op = b.obs.ptr + A * b.obs_stride_agent + e * b.obs.s_env;
-    std_agent_obs<1>(p, dv, s, pv_ob, in, pcons, [&](int slot, const double (&v)[1]) {
-      if (slot < kSlotSoc) xp[slot * n] = v[0];
-      else if (slot == kSlotSoc) *socp = v[0];
-      else st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
-    });
-    b.agent_power[(int64_t)A * n + e] = power[0];
-  }
-  // ---- fixed-point iteration (PFSolver::iterate<false>), rows shared by the waves
-  int it = 0, my_it = 0;
-  bool done = !valid, conv_ok = !valid;
-  double v0r = 0.0, v0i = 0.0;
-  if constexpr (DBG == 3) {   // measurement: the loads of the power flow, no iteration
-    double acc = 0.0;
-#pragma unroll
-    for (int q = 0; q < nr; ++q) acc += ur[q] + ui[q];
-#pragma unroll
-    for (int j = 0; j < kCoopPairs; ++j) acc += w[j];
-    if (valid && b.vv) b.vv[e] = acc;
-  }
-  while (DBG != 2 && DBG != 3) {
-#pragma unroll
-    for (int q = 0; q < nr; ++q) {
-      // the element's power (pf_power: s = s0 + f * pc), formed per iteration
-      // rather than held (12 fewer VGPRs in the loop)
-      const double sr = fma(a.fr[R::kFirst + q], pc, a.sr0[R::kFirst + q]);
-      const double si = fma(a.fi[R::kFirst + q], qc, a.si0[R::kFirst + q]);
-      double ir, ii;
-      coop_current(ur[q], ui[q], sr, si, a, ir, ii);
-      L.cur[R::kFirst + q][l] = make_double2(ir, ii);
-    }
-    coop_barrier();
-    double Ac[nr], Bc[nr], Cc[nr], vr = 0.0, vi = 0.0;
-    coop_acc_init<A>(Ac, Cc, w);
-#pragma unroll
-    for (int q = 0; q < nr; ++q) Bc[q] = 0.0;
-    if constexpr (A == kCoopOut) coop_v0(vr, vi, w);
-    static_for<0, kCoopM>([&](auto k) {
-      const double2 x = L.cur[decltype(k)::value][l];
-      coop_column<A, decltype(k)::value>(Ac, Bc, Cc, vr, vi, w, x.x, x.y, x.x + x.y);
-    });
-    bool conv = true;
-#pragma unroll
-    for (int q = 0; q < nr; ++q) {
-      const double nre = Ac[q] - Bc[q];
-      const double nim = (Cc[q] - Ac[q]) - Bc[q];
-      const double dr = nre - ur[q], di = nim - ui[q];
-      conv &= fma(dr, dr, di * di) < a.tol2;
-      ur[q] = done ? ur[q] : nre;
-      ui[q] = done ? ui[q] : nim;
-    }
-    if constexpr (A == kCoopOut) {
-      v0r = done ? v0r : vr;
-      v0i = done ? v0i : vi;
-    }
-    L.flag[A][l] = conv ? 1 : 0;
-    coop_barrier();
-    bool all = true;
-#pragma unroll
-    for (int ww = 0; ww < kCoopWaves; ++ww) all = all && (L.flag[ww][l] != 0);
-    ++it;
-    my_it = done ? my_it : it;
-    conv_ok = conv_ok || (!done && all);
-    done = done || all || it >= a.max_iter;
-    // every wave saw the same flags: all five leave on the same iteration
-    if (__ballot(!done) == 0ull) break;
-  }
-  // ---- V675.3, voltage violation, coordinated reward (k_coord_pf's epilogue)
-  if constexpr (A == kCoopOut) {
-    const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
-    double share = 0.0;
-    if (valid) {
-      if (b.v_out) b.v_out[e] = v0;
-      if (b.iters) b.iters[e] = conv_ok ? my_it : -my_it;
-    }
-    if (c.coordinated) {
-      const double vv = pymax(pymax(0.0, c.vv_lo - v0), v0 - c.vv_hi);
-      if (valid && b.vv) b.vv[e] = vv;
-      share = (vv * c.vv_penalty) / (double)c.n_agents;
-    }
-    L.share[l] = share;
-  }
-  coop_barrier();
-  if (valid) {
-    const double r = c.coordinated ? rew[0] + (-L.share[l]) : rew[0];
-    b.reward[(int64_t)A * n + e] = r;
-  }
-}
-
-template <int MINW, int DBG>
-__global__ void __launch_bounds__(64 * kCoopWaves, MINW) k_coord_coop(pgw_coord_params p_, pgw_coord_step_info s,
-                                                               int64_t n, pgw_coord_buffers b, double pv_ob,
-                                                               StdDerived dv, CoordPFArgs c, PFArgs a,
-                                                               pgw_pf_tables t) {
-  const pgw_coord_params& p = PGW_KERNARG0(pgw_coord_params);   // (no private copy)
-  __shared__ CoopLds L;
-  switch (threadIdx.x >> 6) {
-    case 0: coop_wave<0, DBG>(p, s, n, b, pv_ob, dv, c, a, t, L); break;
-    case 1: coop_wave<1, DBG>(p, s, n, b, pv_ob, dv, c, a, t, L); break;
-    case 2: coop_wave<2, DBG>(p, s, n, b, pv_ob, dv, c, a, t, L); break;
-    case 3: coop_wave<3, DBG>(p, s, n, b, pv_ob, dv, c, a, t, L); break;
-    default: coop_wave<4, DBG>(p, s, n, b, pv_ob, dv, c, a, t, L); break;
-  }
-}
-
 // Stencil metadata of the predictor grid (one thread per segment): in a
 // segment whose two ends share the band signature the switch sits at t* = 1/2
 // (the nearest-point rule) and both sides use a 3-point stencil of that
@@ -1617,16 +1207,6 @@ static int32_t launch_coord_agents(const pgw_coord_params& p, const pgw_coord_st
   return check_launch("k_coord_agents");
 }
 
-// k_coord_coop serves the standard C4 step: five agents of the standard layout,
-// IEEE-13 (m = 14, uniform band), one controllable slot, one output row.
-// PGW_COORD_COOP=0 selects the two-launch step instead (measurements, tests).
-static bool coop_eligible(const pgw_coord_params& p, const pgw_pf_params& pf, const pgw_pf_tables& t) {
-  const char* v = getenv("PGW_COORD_COOP");
-  if (v && v[0] == '0') return false;
-  return p.n_agents == kCoopWaves && coord_is_std(p) && pf.m == kCoopM && uniform_band(pf) &&
-         pf.n_ctrl <= 1 && !t.load_scale && !t.U_init && pf.n_out <= 1 && p.vv_row == 0;
-}
-
 template <class Bufs>
 static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
                           const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream) {
@@ -1674,25 +1254,6 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   // fp32: env pairs per lane (float2 accesses).  The pair layout measured for
   // fp64 too (19.5 -> 20.2 us), so it is instantiated for fp32 only.
   bool done = false;
-  if constexpr (!kF32) {
-    if (coop_eligible(*p, *pf, *pft)) {
-      const char* v = getenv("PGW_COORD_COOP");
-      const char* dbg = getenv("PGW_COOP_DBG");
-      const int d = dbg ? atoi(dbg) : 0;
-      const dim3 g((unsigned)((n + 63) / 64)), blk(64 * kCoopWaves);
-      const StdDerived dvv = make_std_derived(*p);
-#define PGW_COOP_LAUNCH(W, D) launch_timed(PGW_T_COORD_COOP, k_coord_coop<W, D>, g, blk, st, *p, *s, n, b, pv_ob, dvv, c, a, *pft)
-      if (v && v[0] == '4') PGW_COOP_LAUNCH(4, 0);
-      else if (d == 1) PGW_COOP_LAUNCH(5, 1);
-      else if (d == 2) PGW_COOP_LAUNCH(5, 2);
-      else if (d == 3) PGW_COOP_LAUNCH(5, 3);
-      else if (d == 4) PGW_COOP_LAUNCH(4, 4);
-      else if (d == 5) PGW_COOP_LAUNCH(4, 3);
-      else PGW_COOP_LAUNCH(5, 0);
-#undef PGW_COOP_LAUNCH
-      return check_launch("k_coord_coop");
-    }
-  }
   if constexpr (kF32) {
     if (std_layout && pairs_ok(b, n)) {
       launch_timed(PGW_T_COORD_AGENTS, k_coord_agents_std_x2<Bufs>, dim3(grid_for(n / 2), p->n_agents),
