@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 17
+#define PGW_ABI_VERSION 18
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -418,7 +418,17 @@ typedef struct pgw_pfg_elem {
   double nph;                  /* phases of that load                                  */
   double y0r, y0i;             /* OPENDSS: conj(S) per phase (W, -var) of the Yeq in Y; 0 */
   double vlo2, vmn2, vmx2;     /* vlow^2, vmin^2, vmax^2 (pu^2)                         */
-  int32_t ctrl, pad_;          /* controllable-load slot, -1 none                      */
+  int32_t ctrl;                /* controllable-load slot, -1 none                      */
+  /* OpenDSS load model of the element: 1 constant PQ (loadshape-scaled, may be
+   * controllable), 3 constant P + constant-Z Q, 4 exponential (exp_p = CVRwatts,
+   * exp_q = CVRvars), 5 constant current magnitude, 6 constant P + fixed Q,
+   * 7 constant P + fixed-impedance Q, 8 ZIP (zip = Zp Ip Pp Zq Iq Pq, load off
+   * below vcut2 = cutoff^2).  Models 3-8 keep base_kw / base_kvar unscaled (the
+   * reference re-sets model-1 loads only, opendss.py:71,149). */
+  int32_t model;
+  double exp_p, exp_q;
+  double zip[6];
+  double vcut2;
 } pgw_pfg_elem;
 
 typedef struct pgw_pfg_params {

@@ -14,9 +14,15 @@ models the reference's call sites rely on:
 * OpenDSS element models: Vsource (Thevenin from MVAsc3/MVAsc1, X1/R1=4,
   X0/R0=3), 2-winding transformers (leakage %r1+%r2 + jXHL, wye/delta,
   winding taps), lines (R/X/C matrices x length, C split half/half),
-  capacitors and constant-Z (model 2) loads as fixed shunt admittances, PQ
+  capacitors and constant-Z (model 2) loads as fixed shunt admittances,
+  series capacitors (bus2) as the same admittance between the two buses, PQ
   loads (model 1: constant PQ inside [Vminpu, Vmaxpu], constant Z outside,
-  Vlowpu floor).
+  Vlowpu floor) and the other OpenDSS load models as per-element current laws
+  (``Feeder.LAWS``: 3 constant P + constant-Z Q, 4 exponential CVRwatts /
+  CVRvars, 5 constant current magnitude, 6 constant P + fixed Q, 7 constant P +
+  fixed-impedance Q, 8 ZIP with ZIPV cutoff).  Only model-1 loads follow the
+  loadshape and take controllable power (opendss.py:71, 149: the reference
+  re-sets model 1 only); the others stay at the DSS file's kW / kvar.
 
 Solve: nodal admittance Y (no loads) -> Z = Y^-1, no-load voltages V0 =
 Z I_src; the load-element voltages U obey U = U0 + W f(U) with W = -C Z C^T
@@ -88,8 +94,10 @@ class Feeder:
             b, nds = _bus(ld["bus1"], [1, 2, 3][:ld["phases"]])
             touch(b, nds)
         for cap in spec.get("capacitors", []):
-            b, nds = _bus(cap["bus1"], [1, 2, 3][:cap["phases"]])
-            touch(b, nds)
+            for key in ("bus1", "bus2"):
+                if cap.get(key):
+                    b, nds = _bus(cap[key], [1, 2, 3][:cap["phases"]])
+                    touch(b, nds)
         for ln in spec["lines"]:
             for key in ("bus1", "bus2"):
                 b, nds = _bus(ln[key], [1, 2, 3][:ln["phases"]])
@@ -202,11 +210,16 @@ class Feeder:
             ph = obj["phases"]
             b, nds = _bus(obj["bus1"], [1, 2, 3][:ph])
             delta = obj.get("conn", "wye") == "delta"
-            v = obj["kv"] * 1000 / (math.sqrt(3) if (not delta and ph >= 2) else 1.0)
+            series = obj.get("bus2") is not None
+            v = obj["kv"] * 1000 / (math.sqrt(3) if ((series or not delta) and ph >= 2) else 1.0)
             y = s / (v * v)
             for p in range(ph):
                 hi = self.node(b, nds[p])
-                lo = (self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])) if delta else -1
+                if series:     # capacitor bank between bus1 and bus2, phase by phase
+                    b2, n2 = _bus(obj["bus2"], [1, 2, 3][:ph])
+                    lo = self.node(b2, n2[p])
+                else:
+                    lo = (self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])) if delta else -1
                 self._stamp([hi, lo], np.array([[y, -y], [-y, y]]))
         self.Z = _accurate_inverse(self.Y)
         self.V0 = (self.Z.astype(np.clongdouble) @ self.I_src.astype(np.clongdouble)).astype(complex)
@@ -221,15 +234,33 @@ class Feeder:
             base = bases[np.argmin(np.abs(bases - vll))]
             self.kv_ln[ids] = base / math.sqrt(3)
 
+    # OpenDSS load models as current laws (Load.pas documentation): per element
+    # I = conj(S(v)) / conj(U), S(v) = P0 f_P(v) + j Q0 f_Q(v) (v = |U| / Vbase),
+    # written as the coefficient A(v) = S(v) / v^2 of the element's nominal
+    # admittance conj(S0) / Vbase^2 per part:
+    #   band  model 1's: 1 / clamp(v^2, vmin^2, vmax^2)  (constant S inside)
+    #   z     constant impedance: 1
+    #   i     constant current magnitude: 1 / v
+    #   fixed constant power, no band: 1 / v^2
+    #   exp   exponential: v^(k - 2)
+    #   zip   Z + I / v + P / v^2
+    # and every law but ZIP takes the nominal admittance at or below Vlowpu; ZIP
+    # loads are off below their ZIPV cutoff.
+    LAWS = {1: ("band", "band"), 3: ("band", "z"), 4: ("exp", "exp"), 5: ("i", "i"),
+            6: ("band", "fixed"), 7: ("band", "z"), 8: ("zip", "zip")}
+
     def _build_loads(self):
-        """PQ load phase elements: (p node, q node, Vbase, load index)."""
+        """Load phase elements: (p node, q node, Vbase, load index) of every load
+        but the constant-Z ones (model 2: a shunt in Y)."""
         self.load_names = [ld["name"] for ld in self.spec["loads"]]
         self.elem_p, self.elem_q, self.elem_vbase, self.elem_load, self.elem_nph = [], [], [], [], []
         self.load_vmin, self.load_vmax, self.load_vlow = [], [], []
         for li, ld in enumerate(self.spec["loads"]):
-            if ld.get("model", 1) != 1:    # model 2: a shunt in Y (the reference re-sets model 1 only)
+            if ld.get("model", 1) == 2:
                 self.load_vmin.append(0.95); self.load_vmax.append(1.05); self.load_vlow.append(0.5)
                 continue
+            if ld.get("model", 1) not in self.LAWS:
+                raise NotImplementedError("load model %d" % ld["model"])
             ph = ld["phases"]
             b, nds = _bus(ld["bus1"], [1, 2, 3][:ph])
             for p in range(ph):
@@ -262,18 +293,47 @@ class Feeder:
 
     # ------------------------------------------------------------------ solve
     def load_currents(self, U, W_ph, var_ph):
-        """OpenDSS Load.DoConstantPQLoad, per element (K, m) complex."""
+        """The loads' current laws (Load.DoConstantPQLoad and the other
+        models, LAWS above), per element (K, m) complex."""
         vb = self.elem_vbase
         vmin = np.array(self.load_vmin)[self.elem_load]
         vmax = np.array(self.load_vmax)[self.elem_load]
         vlow = np.array(self.load_vlow)[self.elem_load]
-        S = W_ph + 1j * var_ph
-        yeq = np.conj(S) / (vb * vb)
-        mag = np.abs(U)
-        i_pq = np.conj(S) / np.conj(np.where(mag > 0, U, 1.0))
-        I = np.where(mag <= vlow * vb, yeq * U,
-            np.where(mag <= vmin * vb, (yeq / (vmin * vmin)) * U,
-            np.where(mag > vmax * vb, (yeq / (vmax * vmax)) * U, i_pq)))
+        models = [self.spec["loads"][li].get("model", 1) for li in self.elem_load]
+        if all(md == 1 for md in models):
+            S = W_ph + 1j * var_ph
+            yeq = np.conj(S) / (vb * vb)
+            mag = np.abs(U)
+            i_pq = np.conj(S) / np.conj(np.where(mag > 0, U, 1.0))
+            I = np.where(mag <= vlow * vb, yeq * U,
+                np.where(mag <= vmin * vb, (yeq / (vmin * vmin)) * U,
+                np.where(mag > vmax * vb, (yeq / (vmax * vmax)) * U, i_pq)))
+            return I
+        v = np.abs(U) / vb                                            # (K, m) pu
+        I = np.zeros_like(U)
+        for k, md in enumerate(models):
+            ld = self.spec["loads"][self.elem_load[k]]
+            vk = v[:, k]
+            below = vk <= vlow[k]
+            zip_ = ld.get("zipv") or [1.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0]
+
+            def coef(law, part):
+                if law == "band":
+                    return np.where(below, 1.0, 1.0 / np.clip(vk * vk, vmin[k] ** 2, vmax[k] ** 2))
+                if law == "z":
+                    return np.ones_like(vk)
+                if law == "i":
+                    return np.where(below, 1.0, 1.0 / vk)
+                if law == "fixed":
+                    return np.where(below, 1.0, 1.0 / (vk * vk))
+                if law == "exp":
+                    ex = ld.get("cvrwatts", 1.0) if part == 0 else ld.get("cvrvars", 2.0)
+                    return np.where(below, 1.0, vk ** (ex - 2.0))
+                z, i_, p_ = zip_[3 * part: 3 * part + 3]
+                return np.where(vk < zip_[6], 0.0, z + i_ / vk + p_ / (vk * vk))
+            lp, lq = self.LAWS[md]
+            A = W_ph[:, k] * coef(lp, 0) - 1j * var_ph[:, k] * coef(lq, 1)
+            I[:, k] = A / (vb[k] * vb[k]) * U[:, k]
         return I
 
     def solve(self, load_kw, load_kvar, tol=1e-10, max_iter=100):
@@ -394,9 +454,13 @@ class BatchedPF:
         self.semantics = semantics
 
     def base_loads(self, current_time):
+        """opendss.py:106-108 for the model-1 loads; the others keep the DSS file's
+        kW / kvar (the reference re-sets model 1 only, :149)."""
         coef = self.shape[hour_of_year(current_time)]
         f = self.feeder
-        return coef * f.base_kw * self.rescale, coef * f.base_kvar * self.rescale   # opendss.py:106-108
+        pq = np.array([ld.get("model", 1) == 1 for ld in f.spec["loads"]])
+        return (np.where(pq, coef * f.base_kw * self.rescale, f.base_kw),
+                np.where(pq, coef * f.base_kvar * self.rescale, f.base_kvar))
 
     def loads(self, current_time, p_ctrl=None, q_ctrl=None, K=1):
         """Per-load kW / kvar (K, n_loads) of one calculate_power_flow call
@@ -406,7 +470,7 @@ class BatchedPF:
         names = self.feeder.load_names
         for d, arr in ((p_ctrl, kw), (q_ctrl, kvar)):
             for name, v in (d or {}).items():
-                if name in names:
+                if name in names and self.feeder.spec["loads"][names.index(name)].get("model", 1) == 1:
                     arr[:, names.index(name)] = arr[:, names.index(name)] + np.asarray(v, float)
         return kw, kvar
 
@@ -417,7 +481,7 @@ class BatchedPF:
         names = self.feeder.load_names
         for d, arr in ((p_ctrl, kw), (q_ctrl, kvar)):
             for name, v in (d or {}).items():
-                if name in names:
+                if name in names and self.feeder.spec["loads"][names.index(name)].get("model", 1) == 1:
                     arr[:, names.index(name)] = arr[:, names.index(name)] + np.asarray(v, float)
         if self.semantics == "opendss":
             V, it = self.feeder.snap_opendss(kw, kvar, self.feeder.base_kw, self.feeder.base_kvar)

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -103,7 +103,8 @@ class PFTables(C.Structure):
 
 class PFGElem(C.Structure):
     _fields_ = [("base_kw", f64), ("base_kvar", f64), ("nph", f64), ("y0r", f64), ("y0i", f64),
-                ("vlo2", f64), ("vmn2", f64), ("vmx2", f64), ("ctrl", i32), ("pad_", i32)]
+                ("vlo2", f64), ("vmn2", f64), ("vmx2", f64), ("ctrl", i32), ("model", i32),
+                ("exp_p", f64), ("exp_q", f64), ("zip", f64 * 6), ("vcut2", f64)]
 
 
 class PFGParams(C.Structure):

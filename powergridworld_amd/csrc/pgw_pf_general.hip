@@ -44,7 +44,7 @@ typedef const __attribute__((address_space(4))) pgw_pfg_elem* ceptr;
 // copies out of the constant address space).
 struct ElemV {
   double base_kw, base_kvar, nph, y0r, y0i, vlo2, vmn2, vmx2;
-  int ctrl;
+  int ctrl, model;
 };
 __device__ __forceinline__ ElemV ld_elem(ceptr el, int k) {
   ElemV v;
@@ -57,6 +57,7 @@ __device__ __forceinline__ ElemV ld_elem(ceptr el, int k) {
   v.vmn2 = el[k].vmn2;
   v.vmx2 = el[k].vmx2;
   v.ctrl = el[k].ctrl;
+  v.model = el[k].model;
   return v;
 }
 
@@ -66,6 +67,40 @@ __device__ __forceinline__ double g_rcp(double m) {
   r = fma(r, e, r);
   e = fma(-m, r, 1.0);
   return fma(r, e, r);
+}
+
+// The current-law coefficients (f_P, f_Q) of a load element of model != 1 at
+// |u|^2 = m2: S(v) = P0 v^2 f_P + j Q0 v^2 f_Q, i.e. the factors of the nominal
+// admittance per part (oracle/pf_oracle.py Feeder.LAWS):
+//   band  1 / clamp(v^2, vmin^2, vmax^2)   z  1   i  1 / v   fixed  1 / v^2
+//   exp   v^(k - 2)                        zip  Z + I / v + P / v^2
+// every law but ZIP at the nominal admittance (1) at or below vlow; ZIP loads
+// off (0) below their cutoff.  Model 1 stays on its own inline path.
+__device__ __forceinline__ void elem_law(ceptr el, int k, const ElemV& E, double m2, double& fp,
+                                         double& fq) {
+  const int md = E.model;
+  const double v = sqrt(m2);
+  const double band = g_rcp(fmin(fmax(m2, E.vmn2), E.vmx2));
+  if (md == 8) {
+    const double zp = el[k].zip[0], ip = el[k].zip[1], pp = el[k].zip[2];
+    const double zq = el[k].zip[3], iq = el[k].zip[4], pq = el[k].zip[5];
+    const bool off = m2 < el[k].vcut2;
+    fp = off ? 0.0 : (zp + ip / v) + pp / m2;
+    fq = off ? 0.0 : (zq + iq / v) + pq / m2;
+    return;
+  }
+  if (md == 4) {
+    fp = pow(v, el[k].exp_p - 2.0);
+    fq = pow(v, el[k].exp_q - 2.0);
+  } else if (md == 5) {
+    fp = fq = 1.0 / v;
+  } else {                         // 3, 7: band P, constant-Z Q; 6: band P, fixed Q
+    fp = band;
+    fq = md == 6 ? 1.0 / m2 : 1.0;
+  }
+  const bool low = m2 <= E.vlo2;
+  fp = low ? 1.0 : fp;
+  fq = low ? 1.0 : fq;
 }
 
 // NaN-propagating max (an env whose error is NaN never converges).
@@ -163,9 +198,11 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
           qk = (E.ctrl == s) ? cq[s] : qk;
         }
         // opendss.py:107-108 (coef * base * rescale), :128-129 (+ controllable),
-        // then OpenDSS WNominal = kW * 1000 / nphases
-        const double kw = (p.coef * E.base_kw) * p.rescale;
-        const double kvar = (p.coef * E.base_kvar) * p.rescale;
+        // then OpenDSS WNominal = kW * 1000 / nphases; loads of other models
+        // keep the DSS file's kW / kvar (the reference re-sets model 1 only)
+        const bool pq = E.model == 1;
+        const double kw = pq ? (p.coef * E.base_kw) * p.rescale : E.base_kw;
+        const double kvar = pq ? (p.coef * E.base_kvar) * p.rescale : E.base_kvar;
         sr[j][r] = ((kw + pk) * 1000.0) / E.nph;
         si[j][r] = -(((kvar + qk) * 1000.0) / E.nph);
         if (t.U_init) {
@@ -212,11 +249,16 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
           const int k = row0 + r;
           const ElemV E = ld_elem(el, min(k, m - 1));
           const double m2 = fma(ui[j][r], ui[j][r], ur[j][r] * ur[j][r]);
-          double mc = fmin(fmax(m2, E.vmn2), E.vmx2);
-          mc = (m2 <= E.vlo2) ? 1.0 : mc;
-          const double g = g_rcp(mc);
-          const double cr = OD ? fma(sr[j][r], g, -E.y0r) : sr[j][r] * g;
-          const double ci = OD ? fma(si[j][r], g, -E.y0i) : si[j][r] * g;
+          double fp, fq;
+          if (E.model == 1) {          // constant PQ (Load.DoConstantPQLoad)
+            double mc = fmin(fmax(m2, E.vmn2), E.vmx2);
+            mc = (m2 <= E.vlo2) ? 1.0 : mc;
+            fp = fq = g_rcp(mc);
+          } else {
+            elem_law(el, min(k, m - 1), E, m2, fp, fq);
+          }
+          const double cr = OD ? fma(sr[j][r], fp, -E.y0r) : sr[j][r] * fp;
+          const double ci = OD ? fma(si[j][r], fq, -E.y0i) : si[j][r] * fq;
           const double jr = fma(cr, ur[j][r], -(ci * ui[j][r]));
           const double ji = fma(cr, ui[j][r], ci * ur[j][r]);
           if (!done && k < m) sJ[k * 64 + lane] = make_double2(jr, ji);

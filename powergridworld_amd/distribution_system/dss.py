@@ -11,8 +11,9 @@ Supported: comments (``!``, ``//``, ``/* */``), ``~``/``more`` continuation,
 ``transformer`` (2 windings; ``wdg=k`` positional blocks or the array forms
 ``buses= conns= kvs= kvas= taps= %rs=``, ``tap=``, ``%loadloss=``; 1-phase
 units, e.g. the IEEE-13 voltage regulators at fixed taps), ``linecode``,
-``line`` (linecode or r1/x1/r0/x0/c1/c0, ``Switch=y``), ``load`` and
-``capacitor``; ``RegControl`` is recorded (automatic tap control is not
+``line`` (linecode or r1/x1/r0/x0/c1/c0, ``Switch=y``), ``load`` (models 1-8 with
+``CVRwatts``/``CVRvars``/``ZIPV``) and ``capacitor`` (shunt, or series with
+``bus2``); ``RegControl`` is recorded (automatic tap control is not
 simulated: the feeder model refuses it unless ``Set Controlmode=OFF``);
 property assignments ``Class.Name.Prop=value`` (e.g.
 ``Transformer.Reg1.Taps=[1.0 1.0625]``); ``Redirect`` of further files;
@@ -271,12 +272,12 @@ def _array(v):
 def _new_capacitor(spec, name, props):
     """OpenDSS Capacitor defaults: 3 phases, wye, 12.47 kV, 1200 kvar; a kvar
     array (several steps) counts as its sum (all steps in)."""
-    c = dict(name=name.lower(), bus1=None, phases=3, conn="wye", kv=12.47, kvar=1200.0)
+    c = dict(name=name.lower(), bus1=None, bus2=None, phases=3, conn="wye", kv=12.47, kvar=1200.0)
     for k, v in props:
         if k == "bus1":
             c["bus1"] = v
-        elif k == "bus2":
-            raise NotImplementedError("capacitor %s: series (bus2) capacitors are not supported" % name)
+        elif k == "bus2":          # a series capacitor (bus1 -> bus2, phase by phase)
+            c["bus2"] = v
         elif k == "phases":
             c["phases"] = int(parse_number(v))
         elif k == "conn":
@@ -398,7 +399,8 @@ def _new_line(spec, name, props):
 
 def _new_load(spec, name, props):
     ld = dict(name=name.lower(), bus1=None, phases=3, conn="wye", model=1, kv=12.47,
-              kw=10.0, kvar=5.0, vminpu=0.95, vmaxpu=1.05, vlowpu=0.50)
+              kw=10.0, kvar=5.0, vminpu=0.95, vmaxpu=1.05, vlowpu=0.50, cvrwatts=1.0, cvrvars=2.0,
+              zipv=None)
     _load_props(ld, props)
     spec["loads"].append(ld)
 
@@ -413,5 +415,7 @@ def _load_props(ld, props):
             ld["conn"] = "delta" if v.lower().startswith("d") or v.lower().startswith("l") else "wye"
         elif k == "model":
             ld["model"] = int(parse_number(v))
-        elif k in ("kv", "kw", "kvar", "vminpu", "vmaxpu", "vlowpu"):
+        elif k in ("kv", "kw", "kvar", "vminpu", "vmaxpu", "vlowpu", "cvrwatts", "cvrvars"):
             ld[k] = parse_number(v)
+        elif k == "zipv":          # [Zp Ip Pp Zq Iq Pq Vcutoff]
+            ld["zipv"] = [parse_number(x) for x in _array(v)]

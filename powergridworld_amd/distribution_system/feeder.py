@@ -87,7 +87,9 @@ class Feeder(object):
         for ld in spec["loads"]:
             self._touch(*_bus(ld["bus1"], [1, 2, 3][:ld["phases"]]))
         for cap in spec.get("capacitors", []):
-            self._touch(*_bus(cap["bus1"], [1, 2, 3][:cap["phases"]]))
+            for key in ("bus1", "bus2"):
+                if cap.get(key):
+                    self._touch(*_bus(cap[key], [1, 2, 3][:cap["phases"]]))
         for ln in spec["lines"]:
             for key in ("bus1", "bus2"):
                 self._touch(*_bus(ln[key], [1, 2, 3][:ln["phases"]]))
@@ -98,8 +100,8 @@ class Feeder(object):
             raise NotImplementedError("RegControl (automatic regulator tap control) is not simulated: "
                                       "fix the taps (Transformer.X.Taps=[...]) and Set Controlmode=OFF")
         for ld in spec["loads"]:
-            if ld.get("model", 1) not in (1, 2):
-                raise NotImplementedError("load %s: model %d (only 1 = constant PQ and 2 = constant Z)"
+            if ld.get("model", 1) not in range(1, 9):
+                raise NotImplementedError("load %s: model %d (OpenDSS load models are 1-8)"
                                           % (ld["name"], ld["model"]))
         self._build()
         self._bases()
@@ -169,16 +171,25 @@ class Feeder(object):
         shunts = [(c, complex(0.0, c["kvar"] * 1000.0 / c["phases"])) for c in spec.get("capacitors", [])]
         shunts += [(ld, complex(ld["kw"], -ld["kvar"]) * 1000.0 / ld["phases"]) for ld in spec["loads"]
                    if ld.get("model", 1) == 2]
-        if self.load_yprim:
+        if self.load_yprim:     # OpenDSS's Y holds every load's nominal admittance
             shunts += [(ld, complex(ld["kw"], -ld["kvar"]) * 1000.0 / ld["phases"]) for ld in spec["loads"]
-                       if ld.get("model", 1) == 1]
+                       if ld.get("model", 1) != 2]
         for obj, s in shunts:
             ph = obj["phases"]
-            y = s / _elem_vbase(obj, ph) ** 2
+            series = obj.get("bus2") is not None
+            # a series capacitor: the same per-phase admittance between bus1 and
+            # bus2 (its kV is line-to-line for 3 phases, as a wye shunt's)
+            y = s / (_elem_vbase(dict(obj, conn="wye"), ph) if series else _elem_vbase(obj, ph)) ** 2
             e = _lib.FeederElem(kind=_lib.PGW_ELEM_SHUNT, nphases=ph, freq=self.freq)
-            for p, (b, hi, lo) in enumerate(_branches(obj["bus1"], ph, obj.get("conn", "wye"))):
-                e.node1[p], e.node2[p] = self.node(b, hi), self.node(b, lo)
-                e.r[p], e.x[p] = y.real, y.imag
+            if series:
+                (b1, n1), (b2, n2) = _bus(obj["bus1"], [1, 2, 3][:ph]), _bus(obj["bus2"], [1, 2, 3][:ph])
+                for p in range(ph):
+                    e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
+                    e.r[p], e.x[p] = y.real, y.imag
+            else:
+                for p, (b, hi, lo) in enumerate(_branches(obj["bus1"], ph, obj.get("conn", "wye"))):
+                    e.node1[p], e.node2[p] = self.node(b, hi), self.node(b, lo)
+                    e.r[p], e.x[p] = y.real, y.imag
             els.append(e)
         return els
 
@@ -209,9 +220,10 @@ class Feeder(object):
     def _loads(self):
         self.load_names = [ld["name"] for ld in self.spec["loads"]]
         ep, eq, vb, el, nph, vmin, vmax, vlow = [], [], [], [], [], [], [], []
+        mdl = []
         for li, ld in enumerate(self.spec["loads"]):
-            if ld.get("model", 1) != 1:
-                continue          # the reference only drives model-1 (PQ) loads (opendss.py:71,149)
+            if ld.get("model", 1) == 2:
+                continue          # constant Z: a shunt in Y
             ph = ld["phases"]
             b, nds = _bus(ld["bus1"], [1, 2, 3][:ph])
             for p in range(ph):
@@ -223,6 +235,7 @@ class Feeder(object):
                 vb.append(_elem_vbase(ld, ph))
                 el.append(li)
                 nph.append(float(ph))
+                mdl.append(ld.get("model", 1))
                 vmin.append(ld.get("vminpu", 0.95))
                 vmax.append(ld.get("vmaxpu", 1.05))
                 vlow.append(ld.get("vlowpu", 0.50))
@@ -230,6 +243,10 @@ class Feeder(object):
         self.elem_vbase, self.elem_load = np.array(vb), np.array(el)
         self.elem_nph = np.array(nph)
         self.elem_vmin, self.elem_vmax, self.elem_vlow = np.array(vmin), np.array(vmax), np.array(vlow)
+        # the element's OpenDSS load model: 1 = constant PQ (the loads the reference
+        # drives, opendss.py:71,149: loadshape + controllable power); 3-8 keep the
+        # DSS file's kW / kvar under their own current law (pgw_pfg_elem.model)
+        self.elem_model = np.array(mdl, np.int32)
         self.m = len(ep)
         self.base_kw = np.array([ld["kw"] for ld in self.spec["loads"]], float)
         self.base_kvar = np.array([ld["kvar"] for ld in self.spec["loads"]], float)

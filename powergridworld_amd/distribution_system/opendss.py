@@ -84,7 +84,10 @@ class OpenDSSSolver(PowerFlowSolver):
         self.device = _lib.require_device(device)
         spec = load_feeder_spec(feeder_file)
         self.feeder = Feeder(spec)
-        self.general = bool(general) or convergence == "opendss" or self.feeder.m > _lib.PF_MAX_M
+        # the fast kernels hold up to PF_MAX_M constant-PQ elements; larger feeders,
+        # other load models and OpenDSS's stopping rule run the general kernel
+        self.general = (bool(general) or convergence == "opendss" or self.feeder.m > _lib.PF_MAX_M
+                        or bool((self.feeder.elem_model != 1).any()))
         if self.feeder.m > _lib.PFG_MAX_M:
             raise ValueError("feeder has %d load phase elements (max %d)" % (self.feeder.m, _lib.PFG_MAX_M))
         if convergence == "opendss":
@@ -252,15 +255,25 @@ class OpenDSSSolver(PowerFlowSolver):
             e = arr[k]
             if k < f.m:
                 li = f.elem_load[k]
+                ld = f.spec["loads"][li]
                 e.base_kw, e.base_kvar, e.nph = f.base_kw[li], f.base_kvar[li], f.elem_nph[k]
                 if self.convergence == "opendss":
                     e.y0r = f.base_kw[li] * 1000.0 / f.elem_nph[k]
                     e.y0i = -(f.base_kvar[li] * 1000.0 / f.elem_nph[k])
                 e.vlo2, e.vmn2, e.vmx2 = f.elem_vlow[k] ** 2, f.elem_vmin[k] ** 2, f.elem_vmax[k] ** 2
+                e.model = int(f.elem_model[k])
+                e.exp_p, e.exp_q = float(ld.get("cvrwatts", 1.0)), float(ld.get("cvrvars", 2.0))
+                if e.model == 8:
+                    z = ld.get("zipv") or [1.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0]
+                    if len(z) != 7:
+                        raise ValueError("load %s: ZIPV needs 7 values, got %d" % (ld["name"], len(z)))
+                    for i in range(6):
+                        e.zip[i] = float(z[i])
+                    e.vcut2 = float(z[6]) ** 2
                 ln = f.load_names[li]
                 e.ctrl = self._ctrl_names.index(ln) if ln in self._ctrl_names else -1
             else:
-                e.nph, e.vlo2, e.vmn2, e.vmx2, e.ctrl = 1.0, 0.25, 0.9025, 1.1025, -1
+                e.nph, e.vlo2, e.vmn2, e.vmx2, e.ctrl, e.model = 1.0, 0.25, 0.9025, 1.1025, -1, 1
         return arr
 
     def set_controllable_loads(self, names):

@@ -126,9 +126,9 @@ def test_dss_unsupported_control_and_models_refused(tmp_path):
     p.write_text(text.replace("Set Controlmode=OFF", ""))
     with pytest.raises(NotImplementedError, match="RegControl"):
         Feeder(load_feeder_spec(str(p)))
-    p = tmp_path / "m5.dss"
-    p.write_text(text.replace("Model=2 kV=2.4", "Model=5 kV=2.4"))
-    with pytest.raises(NotImplementedError, match="model 5"):
+    p = tmp_path / "m9.dss"
+    p.write_text(text.replace("Model=2 kV=2.4", "Model=9 kV=2.4"))
+    with pytest.raises(NotImplementedError, match="model 9"):
         Feeder(load_feeder_spec(str(p)))
 
 
@@ -310,3 +310,55 @@ def test_ma_step_argument_checks():
     assert r == -1 and "one slot unless summed" in msg
     r, msg = rc(args([B, EV, EV], [[0], [1], [2]], [1, 1, 1]))
     assert r == -1 and "at most" in msg
+
+
+MODELS = os.path.join(REPO, "tests", "data", "models_feeder.dss")
+
+
+def test_dss_load_models_and_series_capacitor():
+    """OpenDSS load models 1-8 and a series capacitor (tests/data/models_feeder.dss).
+    Parity unpinned (no OpenDSS): the native build equals the oracle's
+    independent NumPy build; a converged oracle solve satisfies the nodal
+    equations; every element draws the power its model's law gives at its
+    voltage (Feeder.LAWS); the series capacitor raises the voltage across it."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    spec = load_feeder_spec(MODELS)
+    cap = [c for c in spec["capacitors"] if c["bus2"]]
+    assert len(cap) == 1 and cap[0]["bus2"] == "B.1.2.3"
+    m8 = [ld for ld in spec["loads"] if ld["model"] == 8][0]
+    assert m8["zipv"] == [0.3, 0.3, 0.4, 0.5, 0.2, 0.3, 0.6]
+    f, o = Feeder(spec), OracleFeeder(spec)
+    assert f.node_names == o.node_names
+    assert sorted(set(f.elem_model.tolist())) == [1, 3, 4, 5, 6, 7, 8]     # model 2: a shunt
+    assert f.m == 3 + 1 + 1 + 3 + 1 + 1 + 3 + 3
+    assert np.abs(f.Y - o.Y).max() / np.abs(o.Y).max() < 1e-12
+    assert np.abs(f.Z - o.Z).max() / np.abs(o.Z).max() < 1e-10
+    W, U0, G, V0 = f.reduce_rows([f.node_index["c.1"]])
+    assert np.abs(W - o.W).max() / np.abs(o.W).max() < 1e-10
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float)
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float)
+    V, it = o.solve(kw[None] * 1.3, kvar[None] * 1.3, tol=1e-13)
+    W_ph = 1.3 * kw[o.elem_load] * 1000.0 / o.elem_nph
+    var_ph = 1.3 * kvar[o.elem_load] * 1000.0 / o.elem_nph
+    U = o.Cinc @ V[0]
+    I = o.load_currents(U[None], W_ph[None], var_ph[None])[0]
+    resid = np.abs(o.Y @ V[0] - (o.I_src - o.Cinc.T @ I)).max() / np.abs(o.I_src).max()
+    assert resid < 1e-8
+    S = U * np.conj(I)
+    v = np.abs(U) / o.elem_vbase
+    for k, li in enumerate(o.elem_load):
+        ld = spec["loads"][li]
+        md, vk = ld["model"], v[k]
+        assert 0.9 < vk <= 1.05, (ld["name"], vk)
+        P, Q = W_ph[k], var_ph[k]
+        exp = {1: (P, Q), 3: (P, Q * vk ** 2), 4: (P * vk ** ld["cvrwatts"], Q * vk ** ld["cvrvars"]),
+               5: (P * vk, Q * vk), 6: (P, Q), 7: (P, Q * vk ** 2)}
+        if md == 8:
+            z = ld["zipv"]
+            exp[8] = (P * (z[0] * vk ** 2 + z[1] * vk + z[2]), Q * (z[3] * vk ** 2 + z[4] * vk + z[5]))
+        if md in (1, 3, 6, 7) and vk <= 0.95:      # below Vminpu the constant-P part is constant Z
+            continue
+        np.testing.assert_allclose([S[k].real, S[k].imag], exp[md], rtol=1e-9, err_msg=ld["name"])
+    i = f.node_index
+    assert all(abs(V[0][o.idx["b.%d" % p]]) > abs(V[0][o.idx["a.%d" % p]]) for p in (1, 2, 3))

@@ -166,65 +166,63 @@ def test_c4_two_episodes_tiled_full_batch():
 def test_c5_shards_bit_identical_to_unsharded_batch():
     """C5 = 8 x 65,536 envs.  Each rank's shard (shard_bounds, per-rank seeds as
     in bench.py) stepped as its own env equals the same envs of one unsharded
-    524,288-env batch bit for bit, across an episode boundary; 16 sampled envs
-    per shard match the oracle."""
+    524,288-env batch bit for bit at every step of a whole episode and across
+    the episode boundary (286 steps, the reset, 4 more); 16 sampled envs per
+    shard match the oracle throughout."""
     from oracle.ma_oracle import CoordinatedOracle
     from powergridworld_amd.distributed import rank_seed, shard_bounds
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     world, per = 8, 65536
     total = world * per
-    steps = 3
+    steps = 290
     shards = [shard_bounds(total, r, world) for r in range(world)]
-    inits, acts = [], []
-    for r, sh in enumerate(shards):
-        gen = torch.Generator(DEV).manual_seed(rank_seed(0, r))
-        inits.append(torch.rand((5, sh.count), dtype=torch.float64, device=DEV, generator=gen) * 47 + 3)
-        acts.append(torch.rand((steps, 5, sh.count, 8), dtype=torch.float64, device=DEV,
-                               generator=gen) * 2.2 - 1.1)
-    init_all, act_all = torch.cat(inits, 1), torch.cat(acts, 2)
-
-    def run(env, init, act, hook):
-        env.reset()
-        for a, agent in enumerate(env.agents):
-            agent.env_dict["storage"].reset(init_storage=init[a])
-        for t in range(steps):
-            _, rew, _, meta = env.step(act[t])
-            hook(t, env.packed_obs(), torch.stack([rew[a.name] for a in env.agents]),
-                 meta["voltage_violation"], env.pf_solver.get_bus_voltage_by_name("675c"))
-
-    ref = {}
+    gens = [torch.Generator(DEV).manual_seed(rank_seed(0, r)) for r in range(world)]
     big = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=total, device=DEV, fused=True)
-    run(big, init_all, act_all,
-        lambda t, o, r, v, u: ref.__setitem__(t, (o.clone(), r.clone(), v.clone(), u.clone())))
-    assert big.pf_solver.unconverged() == 0
-    del big
-    torch.cuda.empty_cache()
+    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=sh.count, device=DEV, fused=True)
+            for sh in shards]
     rng = np.random.default_rng(5)
-    for r, sh in enumerate(shards):
-        env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=sh.count, device=DEV,
-                                                 fused=True)
-        got = {}
-        run(env, inits[r], acts[r],
-            lambda t, o, rw, v, u: got.__setitem__(t, (o.clone(), rw.clone(), v.clone(), u.clone())))
-        for t in range(steps):
-            o, rw, v, u = got[t]
-            ro, rr, rv, ru = ref[t]
-            assert torch.equal(o, ro[:, sh.start:sh.stop]), (r, t)
-            assert torch.equal(rw, rr[:, sh.start:sh.stop]), (r, t)
-            assert torch.equal(v, rv[sh.start:sh.stop]), (r, t)
-            assert torch.equal(u, ru[sh.start:sh.stop]), (r, t)
-        pick = np.sort(rng.choice(sh.count, 16, replace=False))
-        orc = CoordinatedOracle(16)
-        orc.reset(N(inits[r])[:, pick])
-        for t in range(steps):
-            oo, orw, ovv = orc.step(N(acts[r][t])[:, pick])
-            o, rw, v, _ = got[t]
-            close(o[:, pick], oo, 1e-10, 1e-10)
-            close(rw[:, pick], orw, 1e-7, 1e-7)
-            close(v[pick], ovv, 1e-8, 1e-11)
-        del env, got
-        torch.cuda.empty_cache()
+    picks = [np.sort(rng.choice(sh.count, 16, replace=False)) for sh in shards]
+    orcs = [CoordinatedOracle(16) for _ in shards]
+
+    def reset_all():
+        inits = [torch.rand((5, sh.count), dtype=torch.float64, device=DEV, generator=gens[r]) * 47 + 3
+                 for r, sh in enumerate(shards)]
+        init_all = torch.cat(inits, 1)
+        for env, init in list(zip(envs, inits)) + [(big, init_all)]:
+            env.reset()
+            for a, agent in enumerate(env.agents):
+                agent.env_dict["storage"].reset(init_storage=init[a])
+        for r in range(world):
+            orcs[r].reset(N(inits[r])[:, picks[r]])
+        for r, sh in enumerate(shards):
+            assert torch.equal(envs[r].packed_obs(), big.packed_obs()[:, sh.start:sh.stop]), ("reset", r)
+
+    reset_all()
+    boundary = False
+    for t in range(steps):
+        acts = [torch.rand((5, sh.count, 8), dtype=torch.float64, device=DEV, generator=gens[r]) * 2.2 - 1.1
+                for r, sh in enumerate(shards)]
+        _, rew_b, done_b, meta_b = big.step(torch.cat(acts, 1))
+        r_big = torch.stack([rew_b[a.name] for a in big.agents])
+        o_big, vv_big = big.packed_obs(), meta_b["voltage_violation"]
+        u_big = big.pf_solver.get_bus_voltage_by_name("675c")
+        for r, sh in enumerate(shards):
+            _, rew, done, meta = envs[r].step(acts[r])
+            assert done == done_b
+            assert torch.equal(envs[r].packed_obs(), o_big[:, sh.start:sh.stop]), (r, t)
+            assert torch.equal(torch.stack([rew[a.name] for a in envs[r].agents]), r_big[:, sh.start:sh.stop]), (r, t)
+            assert torch.equal(meta["voltage_violation"], vv_big[sh.start:sh.stop]), (r, t)
+            assert torch.equal(envs[r].pf_solver.get_bus_voltage_by_name("675c"), u_big[sh.start:sh.stop]), (r, t)
+            oo, orw, ovv = orcs[r].step(N(acts[r])[:, picks[r]])
+            close(envs[r].packed_obs()[:, picks[r]], oo, 1e-10, 1e-10)
+            close(torch.stack([rew[a.name] for a in envs[r].agents])[:, picks[r]], orw, 1e-7, 1e-7)
+            close(meta["voltage_violation"][picks[r]], ovv, 1e-8, 1e-11)
+        assert big.pf_solver.unconverged() == 0
+        if done_b["__all__"]:
+            boundary = True
+            reset_all()
+    assert boundary
 
 
 # ------------------------------------------------------------------ fused-path eligibility
