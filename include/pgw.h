@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 18
+#define PGW_ABI_VERSION 19
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -488,8 +488,18 @@ int32_t pgw_stream_copy(const void* src, void* dst, int64_t bytes, int32_t reps,
  * ---------------------------------------------------------------------- */
 /* PGW_ELEM_SHUNT: a constant admittance per phase, y_p = r[p] + j x[p] (siemens),
  * between node1[p] and node2[p] (-1 = ground): capacitors and constant-Z
- * (model 2) loads. */
-enum { PGW_ELEM_LINE = 1, PGW_ELEM_XFMR = 2, PGW_ELEM_VSOURCE = 3, PGW_ELEM_SHUNT = 4 };
+ * (model 2) loads.
+ * PGW_ELEM_XFMR_N: a 2- or 3-winding transformer with explicit terminals:
+ * winding w of phase p spans wnode[(w * 3 + p) * 2] (hi) -> wnode[... + 1]
+ * (lo, -1 = ground), so centre-tapped secondaries (bus.1.0 / bus.0.2) and
+ * phase-to-phase single-phase windings are expressed directly.  The leakage
+ * model is OpenDSS's N-winding one (Transformer.pas CalcY): short-circuit
+ * impedances Z_ij = R_i + R_j + j X_ij on winding 1's kVA (R_k = %R_k / 100
+ * referred from winding k's kVA), ZB = the (nw-1)^2 matrix of winding k+1
+ * against winding 1, Y_pu = A ZB^-1 A^T (A: winding 1 row -1, the others the
+ * identity), Y_ij = Y_pu,ij S_ph / (V_i V_j) with V_k = the winding's phase
+ * voltage times its tap. */
+enum { PGW_ELEM_LINE = 1, PGW_ELEM_XFMR = 2, PGW_ELEM_VSOURCE = 3, PGW_ELEM_SHUNT = 4, PGW_ELEM_XFMR_N = 5 };
 
 typedef struct pgw_feeder_elem {
   int32_t kind;          /* PGW_ELEM_*                                     */
@@ -503,6 +513,12 @@ typedef struct pgw_feeder_elem {
   double kv1, kv2, kva, pct_r1, pct_r2, xhl;       /* transformer          */
   double tap1, tap2;     /* transformer winding taps (pu of kv, 0 = 1.0)  */
   double basekv, pu, angle, mvasc3, mvasc1, x1r1, x0r0;  /* vsource        */
+  /* PGW_ELEM_XFMR_N (winding 1 and 2 use kv1 / kv2, pct_r1 / pct_r2, tap1 /
+   * tap2, conn1 / conn2 and kva above; kva is winding 1's, the X base)    */
+  int32_t nwindings;     /* 2 or 3                                         */
+  int32_t conn3;
+  int32_t wnode[18];     /* [winding][phase][hi, lo] terminal nodes        */
+  double kv3, kva2, kva3, pct_r3, tap3, xht, xlt;  /* xht = X13, xlt = X23 (%) */
 } pgw_feeder_elem;
 
 /* Assemble the nodal admittance Y (n_nodes^2, complex interleaved, loads

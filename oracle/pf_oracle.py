@@ -13,7 +13,8 @@ models the reference's call sites rely on:
 * ``get_bus_voltage_by_name`` (``opendss.py:173-186``): 'xxxc' -> 'xxx.3';
 * OpenDSS element models: Vsource (Thevenin from MVAsc3/MVAsc1, X1/R1=4,
   X0/R0=3), 2-winding transformers (leakage %r1+%r2 + jXHL, wye/delta,
-  winding taps), lines (R/X/C matrices x length, C split half/half),
+  winding taps), 3-winding / centre-tapped transformers (the N-winding
+  short-circuit model, ``Feeder._stamp_nwinding``), lines (R/X/C matrices x length, C split half/half),
   capacitors and constant-Z (model 2) loads as fixed shunt admittances,
   series capacitors (bus2) as the same admittance between the two buses, PQ
   loads (model 1: constant PQ inside [Vminpu, Vmaxpu], constant Z outside,
@@ -121,6 +122,54 @@ class Feeder:
                     continue
                 self.Y[na, nb] += yprim[a, b]
 
+    def _explicit_terminals(self, t):
+        ph = t["phases"]
+        for w in t["windings"]:
+            b, nds = _bus(w["bus"], [1, 2, 3][:ph])
+            if len(nds) > ph or 0 in nds[:ph] or (w["conn"] == "delta" and ph == 1):
+                return True
+        return False
+
+    def _stamp_nwinding(self, t):
+        """OpenDSS's N-winding transformer (Transformer.pas CalcY, restated): per
+        phase, winding k's voltage e_k = (V_hi - V_lo) / (Vbase_k tap_k) in pu;
+        the leakage network between the windings has the short-circuit
+        impedances Z_1k = R_1 + R_k + j X_1k (on winding 1's kVA; R_k = %R_k/100
+        referred from winding k's kVA) and, for 3 windings, the star point fixed
+        by Z_23; its branch currents solve ZB i = (e_k - e_1)_k, which gives the
+        terminal admittance A ZB^-1 A^T in pu, scaled to siemens by S_ph /
+        (V_i V_j).  Wye windings: phase node -> neutral node (ground when not
+        given); delta windings: phase p -> p+1."""
+        ph, W = t["phases"], t["windings"]
+        nw = len(W)
+        s3 = math.sqrt(3.0)
+        kva1 = W[0]["kva"]
+        v = [w["kv"] * 1000 / (s3 if (w["conn"] == "wye" and ph == 3) else 1.0) * w.get("tap", 1.0) for w in W]
+        R = [w["pct_r"] / 100.0 * kva1 / w["kva"] for w in W]
+        X = {(0, 1): t["xhl"], (0, 2): t.get("xht", 35.0), (1, 2): t.get("xlt", 30.0)}
+        zsc = lambda i, j: complex(R[i] + R[j], X[(min(i, j), max(i, j))] / 100.0)
+        ZB = np.zeros((nw - 1, nw - 1), complex)
+        for a in range(nw - 1):
+            for b in range(nw - 1):
+                ZB[a, b] = zsc(0, a + 1) if a == b else 0.5 * (zsc(0, a + 1) + zsc(0, b + 1) - zsc(a + 1, b + 1))
+        A = np.vstack([-np.ones((1, nw - 1)), np.eye(nw - 1)])
+        Ypu = A @ np.linalg.inv(ZB) @ A.T
+        Ysi = Ypu * (kva1 * 1000.0 / ph) / np.outer(v, v)
+        for p in range(ph):
+            inc = np.zeros((nw, self.n), complex)
+            for k, w in enumerate(W):
+                b, nds = _bus(w["bus"], [1, 2, 3][:ph])
+                hi = nds[p]
+                if w["conn"] == "delta":
+                    lo = nds[(p + 1) % ph] if ph > 1 else (nds[1] if len(nds) > 1 else 0)
+                else:
+                    lo = nds[ph] if len(nds) > ph else 0
+                if hi != 0:
+                    inc[k, self.node(b, hi)] += 1
+                if lo != 0:
+                    inc[k, self.node(b, lo)] -= 1
+            self.Y += inc.T @ Ysi @ inc
+
     def _build_y(self):
         spec = self.spec
         f = spec.get("base_frequency", 60.0)
@@ -152,6 +201,9 @@ class Feeder:
         # --- transformers
         for t in spec["transformers"]:
             ph = t["phases"]
+            if len(t["windings"]) == 3 or self._explicit_terminals(t):
+                self._stamp_nwinding(t)
+                continue
             w1, w2 = t["windings"]
             b1, n1 = _bus(w1["bus"], [1, 2, 3][:ph])
             b2, n2 = _bus(w2["bus"], [1, 2, 3][:ph])
@@ -219,7 +271,8 @@ class Feeder:
                     b2, n2 = _bus(obj["bus2"], [1, 2, 3][:ph])
                     lo = self.node(b2, n2[p])
                 else:
-                    lo = (self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])) if delta else -1
+                    lo = ((self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])) if delta
+                          else (self.node(b, nds[ph]) if len(nds) > ph else -1))
                 self._stamp([hi, lo], np.array([[y, -y], [-y, y]]))
         self.Z = _accurate_inverse(self.Y)
         self.V0 = (self.Z.astype(np.clongdouble) @ self.I_src.astype(np.clongdouble)).astype(complex)
@@ -268,8 +321,8 @@ class Feeder:
                 if ld["conn"] == "delta":
                     lo = self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1])
                     vb = ld["kv"] * 1000
-                else:
-                    lo = -1
+                else:   # wye: phase node -> the neutral node if the bus names one
+                    lo = self.node(b, nds[ph]) if len(nds) > ph else -1
                     vb = ld["kv"] * 1000 / (math.sqrt(3) if ph >= 2 else 1.0)
                 self.elem_p.append(hi); self.elem_q.append(lo); self.elem_vbase.append(vb)
                 self.elem_load.append(li); self.elem_nph.append(ph)

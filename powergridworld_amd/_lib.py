@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -131,7 +131,9 @@ class FeederElem(C.Structure):
                 ("length", f64), ("freq", f64), ("kv1", f64), ("kv2", f64), ("kva", f64),
                 ("pct_r1", f64), ("pct_r2", f64), ("xhl", f64), ("tap1", f64), ("tap2", f64),
                 ("basekv", f64), ("pu", f64),
-                ("angle", f64), ("mvasc3", f64), ("mvasc1", f64), ("x1r1", f64), ("x0r0", f64)]
+                ("angle", f64), ("mvasc3", f64), ("mvasc1", f64), ("x1r1", f64), ("x0r0", f64),
+                ("nwindings", i32), ("conn3", i32), ("wnode", i32 * 18), ("kv3", f64), ("kva2", f64),
+                ("kva3", f64), ("pct_r3", f64), ("tap3", f64), ("xht", f64), ("xlt", f64)]
 
 
 class CoordParams(C.Structure):
@@ -226,7 +228,7 @@ class HSBuffers(C.Structure):
                 ("reward", vp), ("real_power", vp), ("meta_out", vp), ("step_meta", vp)]
 
 
-PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE, PGW_ELEM_SHUNT = 1, 2, 3, 4
+PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE, PGW_ELEM_SHUNT, PGW_ELEM_XFMR_N = 1, 2, 3, 4, 5
 
 _SIGS = {
     "pgw_abi_version": (i32, []),

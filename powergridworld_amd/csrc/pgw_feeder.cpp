@@ -15,6 +15,8 @@
 //            delta windings span phase p -> p+1.
 //            Taps scale the winding voltages: t = (Vw1 tap1)/(Vw2 tap2), and the
 //            leakage impedance is referred to winding 1 at Vw1 tap1.
+//   Transformer, N windings (PGW_ELEM_XFMR_N, 2 or 3): OpenDSS's ZB form, see
+//            pgw.h; explicit hi / lo terminal per winding and phase.
 //   Line     Z = (R + jX) len,  Yc = j 2 pi f C 1e-9 len, split half/half.
 //   Shunt    a constant admittance per phase (capacitor, constant-Z load).
 #include <cmath>
@@ -160,6 +162,65 @@ bool add_transformer(Builder& B, const pgw_feeder_elem& e) {
   return true;
 }
 
+// PGW_ELEM_XFMR_N (pgw.h): OpenDSS's N-winding leakage model, explicit terminals.
+bool add_transformer_n(Builder& B, const pgw_feeder_elem& e) {
+  const int ph = e.nphases, nw = e.nwindings;
+  if (nw < 2 || nw > 3) return false;
+  const double s3 = std::sqrt(3.0);
+  const double kv[3] = {e.kv1, e.kv2, e.kv3}, tap[3] = {e.tap1, e.tap2, e.tap3};
+  const double kva[3] = {e.kva, e.kva2 > 0.0 ? e.kva2 : e.kva, e.kva3 > 0.0 ? e.kva3 : e.kva};
+  const double pct_r[3] = {e.pct_r1, e.pct_r2, e.pct_r3};
+  const int conn[3] = {e.conn1, e.conn2, e.conn3};
+  double v[3], r[3];
+  for (int k = 0; k < nw; ++k) {
+    v[k] = kv[k] * 1000.0 / ((conn[k] == 0 && ph == 3) ? s3 : 1.0) * (tap[k] != 0.0 ? tap[k] : 1.0);
+    r[k] = pct_r[k] / 100.0 * (kva[0] / kva[k]);     // on winding 1's kVA
+  }
+  // ZB: winding k+1 against winding 1 (pu on winding 1's kVA)
+  const cplx z12(r[0] + r[1], e.xhl / 100.0);
+  Mat ZB;
+  if (nw == 2) {
+    ZB = {z12};
+  } else {
+    const cplx z13(r[0] + r[2], e.xht / 100.0), z23(r[1] + r[2], e.xlt / 100.0);
+    const cplx zm = 0.5 * (z12 + z13 - z23);
+    ZB = {z12, zm, zm, z13};
+  }
+  if (!invert(ZB, nw - 1)) return false;
+  // Y_pu = A ZB^-1 A^T: row / column 0 = -(sums), the rest ZB^-1
+  Mat Yw(static_cast<size_t>(nw) * nw);
+  const int q = nw - 1;
+  cplx tot(0.0, 0.0);
+  for (int i = 0; i < q; ++i) {
+    cplx row(0.0, 0.0);
+    for (int j = 0; j < q; ++j) {
+      Yw[(i + 1) * nw + (j + 1)] = ZB[i * q + j];
+      row += ZB[i * q + j];
+    }
+    Yw[(i + 1) * nw] = -row;
+    Yw[i + 1] = -row;                                 // (ZB^-1 symmetric)
+    tot += row;
+  }
+  Yw[0] = tot;
+  const double s_ph = kva[0] * 1000.0 / ph;
+  for (int i = 0; i < nw; ++i)
+    for (int j = 0; j < nw; ++j) Yw[i * nw + j] *= s_ph / (v[i] * v[j]);
+  for (int p = 0; p < ph; ++p) {
+    std::vector<int> nodes;
+    for (int k = 0; k < nw; ++k) {
+      nodes.push_back(e.wnode[(k * 3 + p) * 2]);
+      nodes.push_back(e.wnode[(k * 3 + p) * 2 + 1]);
+    }
+    const int nt = 2 * nw;
+    Mat yp(static_cast<size_t>(nt) * nt);
+    for (int a = 0; a < nt; ++a)
+      for (int b = 0; b < nt; ++b)
+        yp[a * nt + b] = ((a & 1) ? -1.0 : 1.0) * ((b & 1) ? -1.0 : 1.0) * Yw[(a >> 1) * nw + (b >> 1)];
+    if (!B.stamp(nodes, yp)) return false;
+  }
+  return true;
+}
+
 bool add_line(Builder& B, const pgw_feeder_elem& e) {
   const int ph = e.nphases;
   Mat Z(static_cast<size_t>(ph) * ph);
@@ -244,6 +305,7 @@ int32_t pgw_feeder_build(const pgw_feeder_elem* elems, int32_t n_elems, int32_t 
       switch (e.kind) {
         case PGW_ELEM_VSOURCE: ok = add_vsource(B, e); break;
         case PGW_ELEM_XFMR: ok = add_transformer(B, e); break;
+        case PGW_ELEM_XFMR_N: ok = add_transformer_n(B, e); break;
         case PGW_ELEM_LINE: ok = add_line(B, e); break;
         case PGW_ELEM_SHUNT: ok = add_shunt(B, e); break;
         default: ok = false;

@@ -8,9 +8,11 @@ admittance matrix natively (``csrc/pgw_feeder.cpp``).
 
 Supported: comments (``!``, ``//``, ``/* */``), ``~``/``more`` continuation,
 ``Clear``, ``Set``, ``New``/``Edit`` for ``circuit``/``vsource``,
-``transformer`` (2 windings; ``wdg=k`` positional blocks or the array forms
-``buses= conns= kvs= kvas= taps= %rs=``, ``tap=``, ``%loadloss=``; 1-phase
-units, e.g. the IEEE-13 voltage regulators at fixed taps), ``linecode``,
+``transformer`` (2 or 3 windings; ``wdg=k`` positional blocks or the array
+forms ``buses= conns= kvs= kvas= taps= %rs=``, ``tap=``, ``XHL/XHT/XLT``,
+``%loadloss=``, ``numtaps/mintap/maxtap``; 1-phase units, e.g. the IEEE-13
+voltage regulators, and centre-tapped secondaries ``bus.1.0`` / ``bus.0.2``),
+``linecode``,
 ``line`` (linecode or r1/x1/r0/x0/c1/c0, ``Switch=y``), ``load`` (models 1-8 with
 ``CVRwatts``/``CVRvars``/``ZIPV``) and ``capacitor`` (shunt, or series with
 ``bus2``); ``RegControl`` is recorded (automatic tap control is not
@@ -303,13 +305,16 @@ def _new_source(spec, name, props):
 
 
 def _new_transformer(spec, name, props):
-    t = dict(name=name.lower(), phases=3, windings=[{}, {}], xhl=7.0, _w=0)
+    """OpenDSS Transformer defaults: 3 phases, 2 windings, XHL 7 %, XHT 35 %,
+    XLT 30 %, each winding wye, 1000 kVA, %R 0.2, tap 1."""
+    t = dict(name=name.lower(), phases=3, windings=[{}, {}], xhl=7.0, xht=35.0, xlt=30.0, _w=0)
     _transformer_props(t, props)
     for wd in t["windings"]:
         wd.setdefault("conn", "wye")
-        wd.setdefault("kva", 1000.0)
+        wd.setdefault("kva", t["windings"][0].get("kva", 1000.0))
         wd.setdefault("pct_r", 0.2)
         wd.setdefault("tap", 1.0)
+    t["windings"][0].setdefault("kva", 1000.0)
     spec["transformers"].append(t)
 
 
@@ -319,37 +324,53 @@ def _conn(v):
 
 def _transformer_props(t, props):
     w = t.get("_w", 0)
+    W = t["windings"]
     for k, v in props:
         if k == "phases":
             t["phases"] = int(parse_number(v))
         elif k == "windings":
             n = int(parse_number(v))
-            assert n == 2, "only 2-winding transformers are supported"
+            if n not in (2, 3):
+                raise NotImplementedError("transformer %s: %d windings (2 or 3 supported)" % (t["name"], n))
+            while len(W) < n:
+                W.append({})
+            del W[n:]
         elif k == "wdg":
             w = int(parse_number(v)) - 1
+            if w >= len(W):
+                raise ValueError("transformer %s: wdg=%d beyond windings=%d" % (t["name"], w + 1, len(W)))
         elif k == "bus":
-            t["windings"][w]["bus"] = v
+            W[w]["bus"] = v
         elif k == "conn":
-            t["windings"][w]["conn"] = _conn(v)
+            W[w]["conn"] = _conn(v)
         elif k == "kv":
-            t["windings"][w]["kv"] = parse_number(v)
+            W[w]["kv"] = parse_number(v)
         elif k == "kva":
-            t["windings"][w]["kva"] = parse_number(v)
+            W[w]["kva"] = parse_number(v)
         elif k in ("%r", "%r1"):
-            t["windings"][w]["pct_r"] = parse_number(v)
+            W[w]["pct_r"] = parse_number(v)
         elif k == "tap":
-            t["windings"][w]["tap"] = parse_number(v)
+            W[w]["tap"] = parse_number(v)
         elif k in ("xhl", "x12"):
             t["xhl"] = parse_number(v)
+        elif k in ("xht", "x13"):
+            t["xht"] = parse_number(v)
+        elif k in ("xlt", "x23"):
+            t["xlt"] = parse_number(v)
         elif k in ("buses", "conns", "kvs", "kvas", "taps", "%rs"):
             key = {"buses": "bus", "conns": "conn", "kvs": "kv", "kvas": "kva", "taps": "tap",
                    "%rs": "pct_r"}[k]
-            for i, x in enumerate(_array(v)[:2]):
-                t["windings"][i][key] = x if key == "bus" else _conn(x) if key == "conn" else parse_number(x)
+            vals = _array(v)
+            if len(vals) > len(W):
+                raise ValueError("transformer %s: %s has %d entries for %d windings"
+                                 % (t["name"], k, len(vals), len(W)))
+            for i, x in enumerate(vals):
+                W[i][key] = x if key == "bus" else _conn(x) if key == "conn" else parse_number(x)
         elif k == "%loadloss":
-            for wd in t["windings"]:
+            for wd in W:
                 wd["pct_r"] = parse_number(v) / 2.0
-        # XHT/XLT only matter for 3-winding units
+        elif k in ("numtaps", "maxtap", "mintap"):       # the regulator's tap range (RegControl)
+            t[k] = parse_number(v)
     t["_w"] = w
 
 

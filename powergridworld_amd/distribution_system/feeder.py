@@ -57,9 +57,27 @@ def _branches(bus_spec, ph, conn):
         if conn == "delta":
             lo = nds[(p + 1) % ph] if ph > 1 else (nds[1] if len(nds) > 1 else 0)
         else:
-            lo = 0
+            lo = nds[ph] if len(nds) > ph else 0
         out.append((b, nds[p], lo))
     return out
+
+
+def _winding_terminals(bus_spec, ph, conn):
+    """A transformer winding's (hi, lo) node pair per phase (0 = ground) and
+    whether the bus spec names terminals beyond the phase nodes.  OpenDSS: a
+    wye winding's conductors are the phase nodes then the neutral (bus.1.0,
+    bus.0.2, bus.1.2.3.4), a delta winding spans phase p -> p+1 (a 1-phase
+    delta winding bus.1.2)."""
+    b, nds = _bus(bus_spec, [1, 2, 3][:ph])
+    out = []
+    for p in range(ph):
+        if conn == "delta":
+            lo = nds[(p + 1) % ph] if ph > 1 else (nds[1] if len(nds) > 1 else 0)
+        else:
+            lo = nds[ph] if len(nds) > ph else 0
+        out.append((nds[p], lo))
+    explicit = len(nds) > ph or (conn == "delta" and ph == 1) or any(hi == 0 for hi, _ in out)
+    return b, out, explicit
 
 
 def _seq_matrix(v1, v0, ph):
@@ -129,16 +147,33 @@ class Feeder(object):
             e.node1[p], e.node2[p] = self.node(s["bus"], p + 1), -1
         els.append(e)
         for t in spec["transformers"]:
-            ph = t["phases"]
-            w1, w2 = t["windings"]
-            (b1, n1), (b2, n2) = _bus(w1["bus"], [1, 2, 3][:ph]), _bus(w2["bus"], [1, 2, 3][:ph])
-            e = _lib.FeederElem(kind=_lib.PGW_ELEM_XFMR, nphases=ph,
-                                conn1=int(w1["conn"] == "delta"), conn2=int(w2["conn"] == "delta"),
-                                kv1=w1["kv"], kv2=w2["kv"], kva=w1["kva"], pct_r1=w1["pct_r"],
-                                pct_r2=w2["pct_r"], xhl=t["xhl"], tap1=w1.get("tap", 1.0),
-                                tap2=w2.get("tap", 1.0), freq=self.freq)
-            for p in range(ph):
-                e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
+            ph, W = t["phases"], t["windings"]
+            terms = [_winding_terminals(w["bus"], ph, w["conn"]) for w in W]
+            if len(W) == 2 and not any(explicit for _, _, explicit in terms):
+                w1, w2 = W
+                (b1, n1), (b2, n2) = _bus(w1["bus"], [1, 2, 3][:ph]), _bus(w2["bus"], [1, 2, 3][:ph])
+                e = _lib.FeederElem(kind=_lib.PGW_ELEM_XFMR, nphases=ph,
+                                    conn1=int(w1["conn"] == "delta"), conn2=int(w2["conn"] == "delta"),
+                                    kv1=w1["kv"], kv2=w2["kv"], kva=w1["kva"], pct_r1=w1["pct_r"],
+                                    pct_r2=w2["pct_r"], xhl=t["xhl"], tap1=w1.get("tap", 1.0),
+                                    tap2=w2.get("tap", 1.0), freq=self.freq)
+                for p in range(ph):
+                    e.node1[p], e.node2[p] = self.node(b1, n1[p]), self.node(b2, n2[p])
+            else:
+                # 3 windings, or explicit winding terminals (centre taps, phase-to-phase
+                # single-phase windings): the N-winding element with its terminal list
+                w3 = W[2] if len(W) == 3 else dict(kv=0.0, kva=0.0, pct_r=0.0, tap=1.0, conn="wye")
+                e = _lib.FeederElem(kind=_lib.PGW_ELEM_XFMR_N, nphases=ph, nwindings=len(W),
+                                    conn1=int(W[0]["conn"] == "delta"), conn2=int(W[1]["conn"] == "delta"),
+                                    conn3=int(w3["conn"] == "delta"), kv1=W[0]["kv"], kv2=W[1]["kv"],
+                                    kv3=w3["kv"], kva=W[0]["kva"], kva2=W[1]["kva"], kva3=w3["kva"],
+                                    pct_r1=W[0]["pct_r"], pct_r2=W[1]["pct_r"], pct_r3=w3["pct_r"],
+                                    tap1=W[0].get("tap", 1.0), tap2=W[1].get("tap", 1.0),
+                                    tap3=w3.get("tap", 1.0), xhl=t["xhl"], xht=t.get("xht", 35.0),
+                                    xlt=t.get("xlt", 30.0), freq=self.freq)
+                for k, (b, pairs, _) in enumerate(terms):
+                    for p, (hi, lo) in enumerate(pairs):
+                        e.wnode[(k * 3 + p) * 2], e.wnode[(k * 3 + p) * 2 + 1] = self.node(b, hi), self.node(b, lo)
             els.append(e)
         for ln in spec["lines"]:
             ph = ln["phases"]
@@ -230,8 +265,8 @@ class Feeder(object):
                 ep.append(self.node(b, nds[p]))
                 if ld["conn"] == "delta":
                     eq.append(self.node(b, nds[(p + 1) % ph]) if ph > 1 else self.node(b, nds[1]))
-                else:
-                    eq.append(-1)
+                else:   # wye: to the neutral node when the bus names one (bus.1.2 for 1 phase)
+                    eq.append(self.node(b, nds[ph]) if len(nds) > ph else -1)
                 vb.append(_elem_vbase(ld, ph))
                 el.append(li)
                 nph.append(float(ph))

@@ -362,3 +362,57 @@ def test_dss_load_models_and_series_capacitor():
         np.testing.assert_allclose([S[k].real, S[k].imag], exp[md], rtol=1e-9, err_msg=ld["name"])
     i = f.node_index
     assert all(abs(V[0][o.idx["b.%d" % p]]) > abs(V[0][o.idx["a.%d" % p]]) for p in (1, 2, 3))
+
+
+XFMR3 = os.path.join(REPO, "tests", "data", "xfmr3_feeder.dss")
+
+
+def test_dss_three_winding_and_centre_tap_transformers():
+    """3-winding and centre-tapped transformers (tests/data/xfmr3_feeder.dss).
+    Parity unpinned (no OpenDSS): the native N-winding element equals the
+    oracle's independent NumPy stamp; a converged solve satisfies the nodal
+    equations; the unit's winding voltages sit at its turns ratios at no load
+    (X at the 1.025 tap); the centre tap splits 240 V into two 120 V legs of
+    opposite phase; the windings' complex powers balance up to the leakage
+    losses (sum of S over all terminals = the losses, with P >= 0)."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    spec = load_feeder_spec(XFMR3)
+    t3 = [t for t in spec["transformers"] if t["name"] == "t3"][0]
+    assert len(t3["windings"]) == 3 and (t3["xhl"], t3["xht"], t3["xlt"]) == (4.5, 8.0, 3.5)
+    assert [w["kva"] for w in t3["windings"]] == [1500.0, 1000.0, 500.0]
+    f, o = Feeder(spec), OracleFeeder(spec)
+    assert f.node_names == o.node_names
+    assert np.abs(f.Y - o.Y).max() / np.abs(o.Y).max() < 1e-12
+    assert np.abs(f.V0 - o.V0).max() / np.abs(o.V0).max() < 1e-12
+    i = o.idx
+    # no load: X at 0.48 kV x 1.025 over B's 4.16, T at B's; S legs 120 V, opposite phase
+    pu0 = o.pu(o.V0)
+    np.testing.assert_allclose(pu0[[i["x.1"], i["x.2"], i["x.3"]]] / pu0[i["b.1"]], 1.025, rtol=1e-6)
+    np.testing.assert_allclose(abs(o.V0[i["s.1"]]) / abs(o.V0[i["a.1"]]), 0.12 / 2.4, rtol=1e-6)
+    assert abs(o.V0[i["s.1"]] + o.V0[i["s.2"]]) < 1e-6 * abs(o.V0[i["s.1"]])
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float)
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float)
+    V, it = o.solve(kw[None], kvar[None], tol=1e-13)
+    W_ph = kw[o.elem_load] * 1000.0 / o.elem_nph
+    var_ph = kvar[o.elem_load] * 1000.0 / o.elem_nph
+    U = o.Cinc @ V[0]
+    I = o.load_currents(U[None], W_ph[None], var_ph[None])[0]
+    resid = np.abs(o.Y @ V[0] - (o.I_src - o.Cinc.T @ I)).max() / np.abs(o.I_src).max()
+    assert resid < 1e-8
+    # the loads draw their power inside their band (below Vminpu: constant Z)
+    S = U * np.conj(I)
+    inb = np.abs(U) / o.elem_vbase > 0.95
+    assert inb.sum() >= 10
+    np.testing.assert_allclose(S.real[inb], W_ph[inb], rtol=1e-9)
+    np.testing.assert_allclose(S.imag[inb], var_ph[inb], rtol=1e-9)
+    # T3's terminal power: its own stamp (an oracle feeder of the source and T3
+    # alone; the source stamp sits on sourcebus only) at the solved voltages
+    o2 = OracleFeeder(dict(spec, transformers=[t3], lines=[], loads=[], capacitors=[]))
+    names = [nm for nm in o2.node_names if not nm.startswith("sourcebus")]
+    a = [o2.idx[nm] for nm in names]
+    Vt = V[0][[o.idx[nm] for nm in names]]
+    S_in = Vt * np.conj(o2.Y[np.ix_(a, a)] @ Vt)          # into the unit per terminal
+    loss = S_in.sum()
+    p_through = S_in[:3].sum().real                        # from B (winding 1)
+    assert p_through > 0 and 0 < loss.real < 0.02 * p_through

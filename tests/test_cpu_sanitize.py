@@ -18,7 +18,8 @@ from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_sp
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "powergridworld_amd", "csrc")
 FEEDERS = ["IEEE13Nodeckt.dss", os.path.join(REPO, "tests", "data", "regcap_feeder.dss"),
-           os.path.join(REPO, "tests", "data", "feeder48.dss")]
+           os.path.join(REPO, "tests", "data", "feeder48.dss"),
+           os.path.join(REPO, "tests", "data", "xfmr3_feeder.dss")]
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +35,7 @@ def driver(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize("feeder_file", FEEDERS, ids=["ieee13", "regcap", "feeder48"])
+@pytest.mark.parametrize("feeder_file", FEEDERS, ids=["ieee13", "regcap", "feeder48", "xfmr3"])
 def test_feeder_builder_under_asan_ubsan(driver, feeder_file):
     f = Feeder(load_feeder_spec(feeder_file))
     els = f.elements()

@@ -22,6 +22,7 @@ DEV = "cuda:0"
 HERE = os.path.dirname(os.path.abspath(__file__))
 FEEDER48 = os.path.join(HERE, "data", "feeder48.dss")
 MODELS = os.path.join(HERE, "data", "models_feeder.dss")
+XFMR3 = os.path.join(HERE, "data", "xfmr3_feeder.dss")
 IEEE13 = "ieee_13_dss/IEEE13Nodeckt.dss"
 SHAPE = "ieee_13_dss/annual_hourly_load_profile.csv"
 
@@ -34,7 +35,7 @@ def _solver(feeder, **kw):
 def _oracle(feeder_file, rescale):
     from oracle.pf_oracle import BatchedPF
     from powergridworld_amd.distribution_system.feeder import load_feeder_spec
-    spec = load_feeder_spec(feeder_file) if feeder_file.endswith(("feeder48.dss", "models_feeder.dss")) else None
+    spec = load_feeder_spec(feeder_file) if os.path.exists(feeder_file) else None
     return BatchedPF(spec=spec, system_load_rescale_factor=rescale)
 
 
@@ -146,6 +147,25 @@ def test_load_models_and_series_capacitor_vs_oracle():
     np.testing.assert_allclose(g, ov, rtol=1e-9, atol=0)
     d = _solver(MODELS, system_load_rescale_factor=1.1, num_envs=K, convergence="opendss")
     g2, o2, git2, oit2 = _run(d, o, TIMES, "pq1", -100.0, 400.0, K, np.random.default_rng(8), "opendss")
+    np.testing.assert_array_equal(git2, oit2)
+    np.testing.assert_allclose(g2, o2, rtol=1e-9, atol=0)
+
+
+def test_three_winding_and_centre_tap_transformers_vs_oracle():
+    """3-winding and centre-tapped transformers (tests/data/xfmr3_feeder.dss,
+    the native N-winding element): the fast kernel, the general kernel and
+    OpenDSS semantics against the oracle's independent stamp, every node within
+    1e-9 rel.  Parity unpinned (no OpenDSS)."""
+    K = 2048
+    o = _oracle(XFMR3, 1.0)
+    for general in (False, True):
+        s = _solver(XFMR3, num_envs=K, general=general)
+        assert s.general == general and s.feeder.m == 16
+        g, ov, git, _ = _run(s, o, TIMES, "x1", -300.0, 500.0, K, np.random.default_rng(9), "exact")
+        assert (git > 0).all()
+        np.testing.assert_allclose(g, ov, rtol=1e-9, atol=0)
+    d = _solver(XFMR3, num_envs=K, convergence="opendss")
+    g2, o2, git2, oit2 = _run(d, o, TIMES, "x1", -300.0, 500.0, K, np.random.default_rng(10), "opendss")
     np.testing.assert_array_equal(git2, oit2)
     np.testing.assert_allclose(g2, o2, rtol=1e-9, atol=0)
 
