@@ -42,8 +42,8 @@ const char* pgw_last_error(void);
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
  * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
  * mc_step_args, matf, coord_buffers_f32, ma_step_args, pfg_elem, pfg_params,
- * pfg_tables -- lets a binding verify its layouts.  Writes min(n, 26) values,
- * returns 26. */
+ * pfg_tables, reg_params -- lets a binding verify its layouts.  Writes
+ * min(n, 27) values, returns 27. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -439,7 +439,16 @@ typedef struct pgw_pfg_params {
   int32_t mode, min_iter, max_iter, pad_;
   double tol;
   double coef, rescale;   /* the step's loadshape coefficient, system_load_rescale_factor */
+  /* Regulators under RegControl (per-env taps): n_reg regulator terminal nodes
+   * R (padded to 8, <= PGW_PFG_MAX_REG; 0 = none), r_reg of them real.  The
+   * solve with taps t is the DSS-tap solve (the tables) corrected exactly
+   * (Woodbury): with x = the DSS-tap node voltages at R for the iterate's
+   * currents, c = K(t) x (per env, pgw_reg_factor) and every row gains -(Z0 U c)
+   * -- as n_reg extra current columns c after the m element columns of W, Gc
+   * and G (so those tables have m + n_reg columns). */
+  int32_t n_reg, r_reg;
 } pgw_pfg_params;
+#define PGW_PFG_MAX_REG 24     /* regulator terminal nodes (12 regulated phases) */
 
 typedef struct pgw_pfg_tables {
   const pgw_pfg_elem* elem;  /* m                                                     */
@@ -453,6 +462,14 @@ typedef struct pgw_pfg_tables {
   double* U_out;             /* optional final element voltages, n x m complex           */
   double* v_min_out;         /* optional min / max over the output rows (n)              */
   double* v_max_out;
+  /* n_reg > 0 (RegControl): W / Gc / G carry n_reg extra columns (k = m ..
+   * m + n_reg - 1: the rows' response to the correction currents c, pu per A) */
+  const double* Greg;        /* x rows: n_reg x m complex (ld n_reg): G_R,k / (vb_k rho_j)  */
+  const double* V0reg;       /* n_reg complex: V0_R / rho                                  */
+  const double* Kreg;        /* per env K(t) rho: r_reg^2 complex, [(j r_reg + l) n + e]   */
+  double* reg_x;             /* out: x per env, r_reg complex, [j n + e] (pu of rho)       */
+  double* reg_c;             /* out: c per env, r_reg complex, [j n + e] (A)               */
+  const int32_t* env_active; /* optional: envs with 0 are left untouched (control loop)   */
 } pgw_pfg_tables;
 
 /* ctrl_p / ctrl_q: n_ctrl x n (NULL = 0); v_out: n_out x n (nullable); iters: n
@@ -460,6 +477,59 @@ typedef struct pgw_pfg_tables {
 int32_t pgw_pf_solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t n,
                              const double* ctrl_p, const double* ctrl_q, double* v_out,
                              int32_t* iters, void* stream);
+
+/* ------------------------------------------------------------------------
+ * RegControl (automatic regulator taps, OpenDSS RegControl in STATIC control
+ * mode) on the general power flow.  A regulated phase is one phase of a
+ * 2-winding transformer whose windings are wye to ground: its primitive
+ * admittance over (a = winding-1 node, b = winding-2 node) is
+ *   [[A / t1^2, B / (t1 t2)], [B / (t1 t2), C / t2^2]]
+ * (A, B, C at unit taps; t1, t2 the winding taps, one of them the RegControl's
+ * tap).  D(t) = Y(t) - Y(DSS taps) over R; K(t) = (I + D S)^-1 D with S =
+ * U^T Z0 U, so that V(t) = V(DSS) - Z0 U K(t) U^T V(DSS) (Woodbury).
+ * ---------------------------------------------------------------------- */
+#define PGW_REG_MAX_PHASES 12
+#define PGW_REG_MAX_CTRL 12
+typedef struct pgw_reg_phase {
+  int32_t a, b;              /* R indices of the winding-1 / winding-2 terminal     */
+  int32_t ctrl;              /* the RegControl whose tap this phase follows          */
+  int32_t tap_winding;       /* 1 or 2                                               */
+  double A[2], B[2], C[2];   /* complex, siemens at unit taps                        */
+  double tap1, tap2;         /* the DSS taps (those of Z0)                           */
+} pgw_reg_phase;
+typedef struct pgw_reg_ctrl {
+  int32_t pt_node;           /* R index of the monitored winding's PT-phase terminal */
+  int32_t pt_phase;          /* the pgw_reg_phase of that terminal (LDC current)     */
+  int32_t winding;           /* the monitored winding (1 or 2)                       */
+  int32_t max_tap_change;    /* taps per control action                              */
+  double vreg, band, ptratio, ctprim, r_ldc, x_ldc;  /* RegControl properties        */
+  double vbase;              /* the winding's rated phase voltage / ptratio (V)      */
+  double incr, min_tap, max_tap, delay;
+} pgw_reg_ctrl;
+typedef struct pgw_reg_params {
+  int32_t n_reg, r_reg;      /* as pgw_pfg_params                                    */
+  int32_t n_phase, n_ctrl;
+  pgw_reg_phase phase[PGW_REG_MAX_PHASES];
+  pgw_reg_ctrl ctrl[PGW_REG_MAX_CTRL];
+  const double* S;           /* r_reg x r_reg complex (ohm), row-major, device       */
+  const double* rho;         /* r_reg: the volts per unit of x (node bases), device  */
+} pgw_reg_params;
+
+/* K(t) rho for the envs with active[e] != 0 (NULL: all), from the taps
+ * (n_ctrl x n, the RegControls' present taps).  An env whose I + D S is
+ * singular gets NaN in K, so its next solve reports unconverged. */
+int32_t pgw_reg_factor(const pgw_reg_params* p, int64_t n, const double* taps, const int32_t* active,
+                       double* Kreg, void* stream);
+/* One control pass (RegControl.Sample + DoPendingAction, STATIC mode) after a
+ * solve that wrote reg_x / reg_c: per env and RegControl, the monitored
+ * voltage V / ptratio, less the line-drop compensation (R + jX) I / ctprim,
+ * against vreg +- band / 2; an out-of-band control moves its tap by the
+ * needed change truncated to whole steps (at least one, at most
+ * max_tap_change, inside [min_tap, max_tap]); of the controls that act, only
+ * those with the smallest delay do so this pass.  active[e] = 1 where any
+ * tap moved (else 0); *n_changed (device int32) += that count. */
+int32_t pgw_reg_control(const pgw_reg_params* p, int64_t n, const double* reg_x, const double* reg_c,
+                        double* taps, int32_t* active, int32_t* n_changed, void* stream);
 
 /* ------------------------------------------------------------------------
  * Kernel timing (benchmark instrumentation): while on, every `every`-th launch

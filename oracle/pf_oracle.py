@@ -482,6 +482,133 @@ class Feeder:
     def pu(self, V):
         return np.abs(V) / (self.kv_ln * 1000.0)
 
+    # ------------------------------------------------------------ RegControl
+    # OpenDSS RegControl (RegControl.pas, STATIC control mode), restated from its
+    # published documentation: Sample() reads the monitored winding's PT-phase
+    # voltage on the 120-V base (V / PTratio) less the line-drop compensation
+    # (R + jX) * I / CTprim (I = the current the regulator delivers into the
+    # bus); outside Vreg +- band/2 it queues the needed tap change, which
+    # DoPendingAction (STATIC) applies truncated to whole steps (at least one,
+    # at most MaxTapChange, inside [MinTap, MaxTap]; step = (MaxTap - MinTap) /
+    # NumTaps); SolveSnap solves, samples, executes the queue's nearest-delay
+    # actions (DoNearestActions) and repeats until no control acts, at most
+    # MaxControlIterations (15).  Every re-solve here rebuilds Y with the new
+    # taps and inverts it (independent of the product's Woodbury correction).
+    REG_DEFAULTS = dict(winding="1", vreg="120", band="3", ptratio="60", ctprim="300", r="0", x="0",
+                        ptphase="1", maxtapchange="16", delay="15")
+
+    def reg_controls(self):
+        """[(transformer dict, settings dict)] of the feeder's RegControls."""
+        out = []
+        xf = {t["name"]: t for t in self.spec["transformers"]}
+        for rc in self.spec.get("regcontrols") or []:
+            pr = dict(self.REG_DEFAULTS)
+            pr.update({k: v for k, v in rc["props"]})
+            t = xf[pr["transformer"].lower()]
+            f = lambda k: float(pr[k])
+            step = (float(t.get("maxtap", 1.1)) - float(t.get("mintap", 0.9))) / float(t.get("numtaps", 32))
+            out.append((t, dict(winding=int(f("winding")), vreg=f("vreg"), band=f("band"), ptratio=f("ptratio"),
+                                ctprim=f("ctprim"), R=f("r"), X=f("x"), ptphase=int(f("ptphase")),
+                                maxtapchange=int(f("maxtapchange")), delay=f("delay"), step=step,
+                                mintap=float(t.get("mintap", 0.9)), maxtap=float(t.get("maxtap", 1.1)),
+                                tap0=t["windings"][int(f("winding")) - 1].get("tap", 1.0))))
+        return out
+
+    def _reg_yw(self, t, taps):
+        """2-winding transformer per-phase Yprim (the _build_y formula) at winding taps."""
+        ph = t["phases"]
+        w1, w2 = t["windings"]
+        vw1 = w1["kv"] * 1000 / (math.sqrt(3) if ph == 3 else 1.0) * taps[0]
+        vw2 = w2["kv"] * 1000 / (math.sqrt(3) if ph == 3 else 1.0) * taps[1]
+        zpu = complex((w1["pct_r"] + w2["pct_r"]) / 100.0, t["xhl"] / 100.0)
+        y = 1.0 / (zpu * vw1 * vw1 / (w1["kva"] * 1000 / ph))
+        nr = vw1 / vw2
+        return y * np.array([[1, -nr], [-nr, nr * nr]])
+
+    def _reg_nodes(self, t, p):
+        (b1, n1), (b2, n2) = [_bus(w["bus"], [1, 2, 3][:t["phases"]]) for w in t["windings"]]
+        return self.node(b1, n1[p]), self.node(b2, n2[p])
+
+    def with_taps(self, taps):
+        """A copy of this feeder whose RegControl transformers sit at `taps`
+        (one per RegControl, on its monitored winding): Y re-stamped and
+        re-inverted, V0 / W / U0 / G recomputed."""
+        import copy
+        o = copy.copy(self)
+        Y = self.Y.copy()
+        for (t, c), tap in zip(self.reg_controls(), taps):
+            base = [w.get("tap", 1.0) for w in t["windings"]]
+            new = list(base)
+            new[c["winding"] - 1] = tap
+            dY = self._reg_yw(t, new) - self._reg_yw(t, base)
+            for p in range(t["phases"]):
+                a, b = self._reg_nodes(t, p)
+                Y[np.ix_([a, b], [a, b])] += dY
+        o.Y = Y
+        o.Z = _accurate_inverse(Y)
+        o.V0 = (o.Z.astype(np.clongdouble) @ self.I_src.astype(np.clongdouble)).astype(complex)
+        C = self.Cinc
+        o.W, o.U0, o.G = -C @ o.Z @ C.T, C @ o.V0, -o.Z @ C.T
+        return o
+
+    def reg_control_pass(self, V, taps):
+        """One Sample + DoPendingAction pass over the RegControls at node
+        voltages V (one env): the new taps (only the nearest-delay actions)."""
+        want, delays = list(taps), []
+        ctrls = self.reg_controls()
+        for g, (t, c) in enumerate(ctrls):
+            p = c["ptphase"] - 1
+            a, b = self._reg_nodes(t, p)
+            vc = V[a if c["winding"] == 1 else b] / c["ptratio"]
+            if c["R"] != 0.0 or c["X"] != 0.0:
+                tp = [w.get("tap", 1.0) for w in t["windings"]]
+                tp[c["winding"] - 1] = taps[g]
+                i_in = self._reg_yw(t, tp)[c["winding"] - 1] @ np.array([V[a], V[b]])
+                vc = vc - complex(c["R"], c["X"]) * (-i_in / c["ctprim"])
+            dv = c["vreg"] - abs(vc)
+            if abs(dv) > c["band"] / 2:
+                w = t["windings"][c["winding"] - 1]
+                vbase = w["kv"] * 1000 / (math.sqrt(3) if t["phases"] == 3 else 1.0) / c["ptratio"]
+                need = dv / vbase
+                steps = min(max(math.trunc(abs(need) / c["step"]), 1), c["maxtapchange"])
+                nt = taps[g] + (steps if need > 0 else -steps) * c["step"]
+                nt = min(max(nt, c["mintap"]), c["maxtap"])
+                if nt != taps[g]:
+                    want[g] = nt
+                    delays.append(c["delay"])
+        if not delays:
+            return list(taps), False
+        dmin = min(delays)
+        out = [want[g] if (want[g] != taps[g] and ctrls[g][1]["delay"] == dmin) else taps[g]
+               for g in range(len(ctrls))]
+        return out, True
+
+    def solve_regulated(self, load_kw, load_kvar, taps, semantics="exact", yprim_kw=None, yprim_kvar=None,
+                        max_control_iter=15, tol=1e-12):
+        """SolveSnap with RegControls, env by env.  taps: (K, n_ctrl) present
+        taps.  Returns (V (K, n), iterations of the last solve (K,), new taps
+        (K, n_ctrl), control passes (K,))."""
+        load_kw, load_kvar = np.atleast_2d(load_kw), np.atleast_2d(load_kvar)
+        K = load_kw.shape[0]
+        Vs, its, tps, cps = [], [], [], []
+        memo = {}
+        for k in range(K):
+            tp = list(np.atleast_2d(taps)[k])
+            for ci in range(1, max_control_iter + 1):
+                key = tuple(tp)
+                if key not in memo:
+                    memo[key] = self.with_taps(tp)
+                f = memo[key]
+                if semantics == "opendss":
+                    V, it = f.snap_opendss(load_kw[k:k + 1], load_kvar[k:k + 1], yprim_kw, yprim_kvar)
+                else:
+                    V, it = f.solve(load_kw[k:k + 1], load_kvar[k:k + 1], tol=tol)
+                tp, moved = self.reg_control_pass(V[0], tp)
+                if not moved:
+                    break
+            Vs.append(V[0]); its.append(it[0]); tps.append(tp); cps.append(ci)
+        return np.array(Vs), np.array(its), np.array(tps), np.array(cps)
+
 
 def hour_of_year(ts):
     """opendss.py:98-103"""

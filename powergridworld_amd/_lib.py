@@ -110,12 +110,35 @@ class PFGElem(C.Structure):
 class PFGParams(C.Structure):
     _fields_ = [("m", i32), ("n_chk", i32), ("n_out", i32), ("n_ctrl", i32), ("mode", i32),
                 ("min_iter", i32), ("max_iter", i32), ("pad_", i32), ("tol", f64), ("coef", f64),
-                ("rescale", f64)]
+                ("rescale", f64), ("n_reg", i32), ("r_reg", i32)]
 
 
 class PFGTables(C.Structure):
     _fields_ = [("elem", vp), ("W", vp), ("U0", vp), ("Gc", vp), ("V0c", vp), ("G", vp), ("V0", vp),
-                ("U_init", vp), ("U_out", vp), ("v_min_out", vp), ("v_max_out", vp)]
+                ("U_init", vp), ("U_out", vp), ("v_min_out", vp), ("v_max_out", vp),
+                ("Greg", vp), ("V0reg", vp), ("Kreg", vp), ("reg_x", vp), ("reg_c", vp),
+                ("env_active", vp)]
+
+
+PFG_MAX_REG, REG_MAX_PHASES, REG_MAX_CTRL = 24, 12, 12
+
+
+class RegPhase(C.Structure):
+    _fields_ = [("a", i32), ("b", i32), ("ctrl", i32), ("tap_winding", i32), ("A", f64 * 2),
+                ("B", f64 * 2), ("C", f64 * 2), ("tap1", f64), ("tap2", f64)]
+
+
+class RegCtrl(C.Structure):
+    _fields_ = [("pt_node", i32), ("pt_phase", i32), ("winding", i32), ("max_tap_change", i32),
+                ("vreg", f64), ("band", f64), ("ptratio", f64), ("ctprim", f64), ("r_ldc", f64),
+                ("x_ldc", f64), ("vbase", f64), ("incr", f64), ("min_tap", f64), ("max_tap", f64),
+                ("delay", f64)]
+
+
+class RegParams(C.Structure):
+    _fields_ = [("n_reg", i32), ("r_reg", i32), ("n_phase", i32), ("n_ctrl", i32),
+                ("phase", RegPhase * REG_MAX_PHASES), ("ctrl", RegCtrl * REG_MAX_CTRL), ("S", vp),
+                ("rho", vp)]
 
 
 PF_EXACT, PF_OPENDSS = 0, 1
@@ -250,6 +273,8 @@ _SIGS = {
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_solve_general": (i32, [P(PFGParams), P(PFGTables), i64, vp, vp, vp, vp, vp]),
+    "pgw_reg_factor": (i32, [P(RegParams), i64, vp, vp, vp, vp]),
+    "pgw_reg_control": (i32, [P(RegParams), i64, vp, vp, vp, vp, vp, vp]),
     "pgw_pf_padded_m": (i32, [i32]),
     "pgw_voltage_band_penalty": (i32, [i64, vp, f64, f64, f64, vp, vp]),
     "pgw_pf_pack_size": (i64, [i32]),
@@ -279,7 +304,7 @@ EXPORTED = sorted(_SIGS)
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
            CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32,
-           MAStepArgs, PFGElem, PFGParams, PFGTables]
+           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams]
 
 _lib = None
 

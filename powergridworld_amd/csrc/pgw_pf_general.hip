@@ -130,9 +130,18 @@ __device__ __forceinline__ void chunk_rows(cdptr M, int ld, int row0, cdptr base
   }
 }
 
-// CE: element chunks per wave (m <= 32 CE); CN: check chunks per wave (OpenDSS
-// mode, n_chk <= 32 CN; 0 = exact mode).
-template <int CE, int CN>
+// CE: element chunks per wave (m + n_reg <= 32 CE); CN: check chunks per wave
+// (OpenDSS mode, n_chk <= 32 CN; 0 = exact mode); REG: regulators with
+// per-env taps (pgw_pfg_params.n_reg > 0).
+//
+// REG: the sJ columns m .. m + n_reg - 1 hold the env's correction currents c
+// (pgw.h).  Each pass: the currents J of the element rows -> LDS; the x rows
+// (the DSS-tap voltages at the regulator nodes, x = V0reg + Greg J) -> LDS;
+// c = K x per env (K from HBM, rows dealt to the waves) -> sJ; then every row
+// as before over m + n_reg columns.  A first pass with J = 0 starts the solve
+// from the direct solution at the env's taps (the element voltages and, for
+// OpenDSS, the check rows' magnitudes), unless U_init is given.
+template <int CE, int CN, bool REG>
 __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg_tables t, int64_t n,
                                                        const double* __restrict__ ctrl_p,
                                                        const double* __restrict__ ctrl_q,
@@ -141,14 +150,16 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
   constexpr bool OD = CN > 0;
   constexpr int kMaxRows = 32 * CE;
   __shared__ double2 sJ[kMaxRows * 64];
+  __shared__ double2 s_x[REG ? PGW_PFG_MAX_REG * 64 : 1];
   __shared__ double s_err[kGW * 64];
   __shared__ double s_mn[kGW * 64], s_mx[kGW * 64], s_vsel[64];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
-  const bool valid = e < n;
-  const int64_t ec = valid ? e : 0;
+  const bool valid = e < n && (!t.env_active || t.env_active[e < n ? e : 0] != 0);
+  const int64_t ec = e < n ? e : 0;
   const int m = p.m;
+  const int mtot = REG ? m + p.n_reg : m;     // columns of W / Gc / G
   const ceptr el = (ceptr)t.elem;
   const cdptr W = (cdptr)t.W, U0 = (cdptr)t.U0;
 
@@ -238,6 +249,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
   const double tol2 = p.tol * p.tol;
   int it = 0, my_it = 0;
   bool done = !valid, conv_ok = !valid;
+  bool first = REG && !t.U_init;     // REG: the direct-solution pass (J = 0) first
   while (true) {
     // ---- 1. currents of the owned element rows -> LDS (a stopped env keeps its last)
 #pragma unroll
@@ -259,13 +271,41 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
           }
           const double cr = OD ? fma(sr[j][r], fp, -E.y0r) : sr[j][r] * fp;
           const double ci = OD ? fma(si[j][r], fq, -E.y0i) : si[j][r] * fq;
-          const double jr = fma(cr, ur[j][r], -(ci * ui[j][r]));
-          const double ji = fma(cr, ui[j][r], ci * ur[j][r]);
+          double jr = fma(cr, ur[j][r], -(ci * ui[j][r]));
+          double ji = fma(cr, ui[j][r], ci * ur[j][r]);
+          if (REG && first) jr = ji = 0.0;
           if (!done && k < m) sJ[k * 64 + lane] = make_double2(jr, ji);
         }
       }
     }
     __syncthreads();
+    if constexpr (REG) {
+      // ---- 1b. x rows (DSS-tap voltages at the regulator nodes) -> LDS
+      for (int row0 = wv * kGR; row0 < p.n_reg; row0 += kGW * kGR) {
+        double ar[kGR], ai[kGR];
+        chunk_rows((cdptr)t.Greg, p.n_reg, row0, (cdptr)t.V0reg, m, sJ, lane, ar, ai);
+#pragma unroll
+        for (int r = 0; r < kGR; ++r) s_x[(row0 + r) * 64 + lane] = make_double2(ar[r], ai[r]);
+      }
+      __syncthreads();
+      // ---- 1c. c = K x per env -> the correction columns of sJ
+      const int rr = p.r_reg;
+      for (int jr0 = wv; jr0 < rr; jr0 += kGW) {
+        double cr_ = 0.0, ci_ = 0.0;
+        const double* kr = t.Kreg + 2 * ((int64_t)jr0 * rr * n + ec);
+        for (int l = 0; l < rr; ++l) {
+          const double2 x = s_x[l * 64 + lane];
+          const double kx = kr[2 * (int64_t)l * n], ky = kr[2 * (int64_t)l * n + 1];
+          cr_ = fma(kx, x.x, cr_);
+          cr_ = fma(-ky, x.y, cr_);
+          ci_ = fma(kx, x.y, ci_);
+          ci_ = fma(ky, x.x, ci_);
+        }
+        if (!done) sJ[(m + jr0) * 64 + lane] = make_double2(cr_, ci_);
+      }
+      for (int jr0 = rr + wv; jr0 < p.n_reg; jr0 += kGW) sJ[(m + jr0) * 64 + lane] = make_double2(0.0, 0.0);
+      __syncthreads();
+    }
     // ---- 2. new element voltages; OpenDSS: every node's magnitude change
     double err = 0.0;
 #pragma unroll
@@ -273,7 +313,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
       const int row0 = (wv + kGW * j) * kGR;
       if (row0 < m) {
         double ar[kGR], ai[kGR];
-        chunk_rows(W, m, row0, U0, m, sJ, lane, ar, ai);
+        chunk_rows(W, m, row0, U0, mtot, sJ, lane, ar, ai);
 #pragma unroll
         for (int r = 0; r < kGR; ++r) {
           if (!OD) {
@@ -291,7 +331,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
         const int row0 = (wv + kGW * j) * kGR;
         if (row0 < p.n_chk) {
           double ar[kGR], ai[kGR];
-          chunk_rows((cdptr)t.Gc, p.n_chk, row0, (cdptr)t.V0c, m, sJ, lane, ar, ai);
+          chunk_rows((cdptr)t.Gc, p.n_chk, row0, (cdptr)t.V0c, mtot, sJ, lane, ar, ai);
 #pragma unroll
           for (int r = 0; r < kGR; ++r) {
             const double mag = sqrt(fma(ai[r], ai[r], ar[r] * ar[r]));
@@ -300,6 +340,11 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
           }
         }
       }
+    }
+    if (REG && first) {                // the start is set; the iterations begin
+      first = false;
+      __syncthreads();
+      continue;
     }
     s_err[wv * 64 + lane] = err;
     __syncthreads();
@@ -338,7 +383,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
   bool have = false;
   for (int row0 = wv * kGR; row0 < n_out; row0 += kGW * kGR) {
     double ar[kGR], ai[kGR];
-    chunk_rows((cdptr)t.G, ld_out, row0, (cdptr)t.V0, m, sJ, lane, ar, ai);
+    chunk_rows((cdptr)t.G, ld_out, row0, (cdptr)t.V0, mtot, sJ, lane, ar, ai);
 #pragma unroll
     for (int r = 0; r < kGR; ++r) {
       const int o = row0 + r;
@@ -355,6 +400,15 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
         }
         if (o == c.vv_row) vsel = v;
       }
+    }
+  }
+  if (REG && valid) {                // the control pass's inputs: x and c of the accepted solve
+    for (int j = wv; j < p.r_reg; j += kGW) {
+      const double2 x = s_x[j * 64 + lane], cc = sJ[(m + j) * 64 + lane];
+      t.reg_x[2 * ((int64_t)j * n + e)] = x.x;
+      t.reg_x[2 * ((int64_t)j * n + e) + 1] = x.y;
+      t.reg_c[2 * ((int64_t)j * n + e)] = cc.x;
+      t.reg_c[2 * ((int64_t)j * n + e) + 1] = cc.y;
     }
   }
   // chunk q is wave q % 4's: rows in order across waves = chunks in order, so
@@ -394,8 +448,12 @@ template <int CE, int CN>
 static int32_t launch_general(const pgw_pfg_params& p, const pgw_pfg_tables& t, int64_t n, const double* cp,
                               const double* cq, double* v_out, int32_t* iters, const PFGCoord& c,
                               hipStream_t st) {
-  launch_timed(PGW_T_PF_GENERAL, k_pf_general<CE, CN>, dim3((unsigned)((n + 63) / 64)), dim3(kBlock), st, p,
-               t, n, cp, cq, v_out, iters, c);
+  if (p.n_reg > 0)
+    launch_timed(PGW_T_PF_GENERAL, k_pf_general<CE, CN, true>, dim3((unsigned)((n + 63) / 64)), dim3(kBlock),
+                 st, p, t, n, cp, cq, v_out, iters, c);
+  else
+    launch_timed(PGW_T_PF_GENERAL, k_pf_general<CE, CN, false>, dim3((unsigned)((n + 63) / 64)), dim3(kBlock),
+                 st, p, t, n, cp, cq, v_out, iters, c);
   return check_launch("k_pf_general");
 }
 
@@ -428,10 +486,18 @@ int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t 
   PGW_REQUIRE(p->max_iter >= 1 && p->min_iter >= 1, "pgw_pf_solve_general: bad iteration limits");
   PGW_REQUIRE(!c.agent_power || (c.vv_row >= 0 && c.vv_row < p->n_out),
               "pgw_pf_solve_general: bad coordinated voltage row");
+  PGW_REQUIRE(p->n_reg >= 0 && p->n_reg <= PGW_PFG_MAX_REG && p->n_reg % kGR == 0 && p->r_reg >= 0 &&
+                  p->r_reg <= p->n_reg && (p->n_reg == 0) == (p->r_reg == 0) &&
+                  p->m + p->n_reg <= PGW_PFG_MAX_M,
+              "pgw_pf_solve_general: bad n_reg %d / r_reg %d (m %d)", p->n_reg, p->r_reg, p->m);
+  PGW_REQUIRE(p->n_reg == 0 || (t->Greg && t->V0reg && t->Kreg && t->reg_x && t->reg_c),
+              "pgw_pf_solve_general: regulators need Greg / V0reg / Kreg / reg_x / reg_c");
+  PGW_REQUIRE(p->n_reg == 0 || !c.agent_power, "pgw_pf_solve_general: regulators on the fused step");
   if (n == 0) return PGW_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (p->m <= 32) return dispatch_cn<1>(*p, *t, n, cp, cq, v_out, iters, c, st);
-  if (p->m <= 64) return dispatch_cn<2>(*p, *t, n, cp, cq, v_out, iters, c, st);
+  const int cols = p->m + p->n_reg;
+  if (cols <= 32) return dispatch_cn<1>(*p, *t, n, cp, cq, v_out, iters, c, st);
+  if (cols <= 64) return dispatch_cn<2>(*p, *t, n, cp, cq, v_out, iters, c, st);
   return dispatch_cn<4>(*p, *t, n, cp, cq, v_out, iters, c, st);
 }
 

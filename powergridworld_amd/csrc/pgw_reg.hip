@@ -1,0 +1,255 @@
+// RegControl on the general power flow (include/pgw.h, "RegControl"): the
+// per-env Woodbury factor K(t) of the regulators' tap deviation and the
+// control pass of OpenDSS's RegControl in STATIC mode.  Replaces what the
+// OpenDSS engine does inside the reference's `Solve mode=snap`
+// (gridworld/distribution_system/opendss.py:134) for a feeder file with
+// RegControl objects (opendss.py:36-39 redirects any DSS file); the rules are
+// restated from OpenDSS's published RegControl / SolveSnap documentation in
+// oracle/pf_oracle.py (Feeder.solve_regulated), which the tests compare.
+//
+// Layout (gfx950): the factor is one wave per env -- lane j owns column j of
+// the augmented [I + D S | D] (r <= 24 rows, 2r <= 48 columns) in LDS,
+// Gauss-Jordan with partial pivoting, the pivot column read into registers
+// before the wave updates its columns; the control pass is one lane per env
+// (a handful of complex multiply-adds per RegControl).  Both are tiny next to
+// the power flow itself: K is rebuilt only for the envs whose taps moved.
+#include <cmath>
+
+#include "pgw_common.h"
+
+namespace pgw {
+
+constexpr int kRegMax = PGW_PFG_MAX_REG;
+
+struct c2 {
+  double x, y;
+};
+__device__ __forceinline__ c2 cmul(c2 a, c2 b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ c2 cadd(c2 a, c2 b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ c2 csub(c2 a, c2 b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ c2 cscale(c2 a, double s) { return {a.x * s, a.y * s}; }
+
+// The regulated phase's primitive admittance at taps (t1, t2) over (a, b).
+__device__ __forceinline__ void reg_yprim(const pgw_reg_phase& ph, double t1, double t2, c2& yaa, c2& yab,
+                                          c2& ybb) {
+  yaa = cscale({ph.A[0], ph.A[1]}, 1.0 / (t1 * t1));
+  yab = cscale({ph.B[0], ph.B[1]}, 1.0 / (t1 * t2));
+  ybb = cscale({ph.C[0], ph.C[1]}, 1.0 / (t2 * t2));
+}
+__device__ __forceinline__ void reg_taps(const pgw_reg_phase& ph, double tap, double& t1, double& t2) {
+  t1 = ph.tap_winding == 1 ? tap : ph.tap1;
+  t2 = ph.tap_winding == 2 ? tap : ph.tap2;
+}
+
+__global__ void __launch_bounds__(64) k_reg_factor(pgw_reg_params p_, int64_t n, const double* __restrict__ taps,
+                                                   const int32_t* __restrict__ active, double* __restrict__ K) {
+  const pgw_reg_params& p = PGW_KERNARG0(pgw_reg_params);
+  const int64_t e = blockIdx.x;
+  if (active && active[e] == 0) return;
+  const int r = p.r_reg, lane = threadIdx.x;
+  __shared__ c2 A[kRegMax * 64];        // row i, column `lane`
+  __shared__ c2 D[kRegMax * kRegMax];
+  for (int i = lane; i < r * r; i += 64) D[i] = {0.0, 0.0};
+  __syncthreads();
+  if (lane == 0) {                      // D = Y(t) - Y(DSS taps) over R, phase by phase
+    for (int q = 0; q < p.n_phase; ++q) {
+      const pgw_reg_phase& ph = p.phase[q];
+      double t1, t2;
+      reg_taps(ph, taps[(int64_t)ph.ctrl * n + e], t1, t2);
+      c2 aa, ab, bb, aa0, ab0, bb0;
+      reg_yprim(ph, t1, t2, aa, ab, bb);
+      reg_yprim(ph, ph.tap1, ph.tap2, aa0, ab0, bb0);
+      const int a = ph.a, b = ph.b;
+      D[a * r + a] = cadd(D[a * r + a], csub(aa, aa0));
+      D[a * r + b] = cadd(D[a * r + b], csub(ab, ab0));
+      D[b * r + a] = cadd(D[b * r + a], csub(ab, ab0));
+      D[b * r + b] = cadd(D[b * r + b], csub(bb, bb0));
+    }
+  }
+  __syncthreads();
+  const c2* S = reinterpret_cast<const c2*>(p.S);
+  for (int i = 0; i < r; ++i) {
+    c2 v = {0.0, 0.0};
+    if (lane < r) {                     // (I + D S)[i][lane]
+      v = {i == lane ? 1.0 : 0.0, 0.0};
+      for (int l = 0; l < r; ++l) v = cadd(v, cmul(D[i * r + l], S[l * r + lane]));
+    } else if (lane < 2 * r) {
+      v = D[i * r + (lane - r)];
+    }
+    A[i * 64 + lane] = v;
+  }
+  __syncthreads();
+  bool singular = false;
+  for (int c = 0; c < r; ++c) {
+    // pivot: the largest |A[i][c]|, i >= c (every lane finds the same row)
+    int pr = c;
+    double best = -1.0;
+    for (int i = c; i < r; ++i) {
+      const c2 v = A[i * 64 + c];
+      const double a2 = v.x * v.x + v.y * v.y;
+      if (a2 > best) {
+        best = a2;
+        pr = i;
+      }
+    }
+    singular = singular || !(best > 0.0) || !isfinite(best);
+    c2 pc[kRegMax];                     // the pivot column, rows swapped
+#pragma unroll
+    for (int i = 0; i < kRegMax; ++i) {
+      const int src = (i == c) ? pr : (i == pr ? c : i);
+      pc[i] = i < r ? A[src * 64 + c] : c2{0.0, 0.0};
+    }
+    c2 rowc = A[pr * 64 + lane], rowp = A[c * 64 + lane];
+    __syncthreads();                    // (all reads of column c done)
+    // normalise the pivot row, eliminate the others (this lane's column)
+    const c2 pv = pc[c];
+    const double inv = 1.0 / (pv.x * pv.x + pv.y * pv.y);
+    const c2 f = cmul(rowc, {pv.x * inv, -pv.y * inv});
+#pragma unroll
+    for (int i = 0; i < kRegMax; ++i) {
+      if (i < r) {
+        c2 v;
+        if (i == c) v = f;
+        else {
+          const c2 old = (i == pr) ? rowp : A[i * 64 + lane];
+          v = csub(old, cmul(pc[i], f));
+        }
+        A[i * 64 + lane] = v;
+      }
+    }
+    __syncthreads();
+  }
+  // K rho: columns r .. 2r - 1 hold (I + D S)^-1 D
+  if (lane >= r && lane < 2 * r) {
+    const int j = lane - r;
+    const double rho = p.rho[j];
+    for (int i = 0; i < r; ++i) {
+      const c2 v = A[i * 64 + lane];
+      const int64_t o = 2 * (((int64_t)i * r + j) * n + e);
+      K[o] = singular ? NAN : v.x * rho;
+      K[o + 1] = singular ? NAN : v.y * rho;
+    }
+  }
+}
+
+// V at regulator node j: x_j rho_j - sum_l S_jl c_l.
+__device__ __forceinline__ c2 reg_node_v(const pgw_reg_params& p, int j, const double* __restrict__ rx,
+                                         const double* __restrict__ rc, int64_t n, int64_t e) {
+  const int r = p.r_reg;
+  const c2* S = reinterpret_cast<const c2*>(p.S);
+  c2 v = cscale({rx[2 * ((int64_t)j * n + e)], rx[2 * ((int64_t)j * n + e) + 1]}, p.rho[j]);
+  for (int l = 0; l < r; ++l) {
+    const c2 cl = {rc[2 * ((int64_t)l * n + e)], rc[2 * ((int64_t)l * n + e) + 1]};
+    v = csub(v, cmul(S[j * r + l], cl));
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64_t n, const double* __restrict__ rx,
+                                                        const double* __restrict__ rc, double* __restrict__ taps,
+                                                        int32_t* __restrict__ active, int32_t* __restrict__ n_changed) {
+  const pgw_reg_params& p = PGW_KERNARG0(pgw_reg_params);
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  double want[PGW_REG_MAX_CTRL];
+  double dmin = INFINITY;
+  for (int g = 0; g < p.n_ctrl; ++g) {
+    const pgw_reg_ctrl& C = p.ctrl[g];
+    const double tap = taps[(int64_t)g * n + e];
+    want[g] = tap;
+    // RegControl.Sample: the PT voltage on the 120-V base, less the line-drop
+    // compensation (R + jX) I / CTprim with I the current the regulator delivers
+    // from the monitored winding into its bus
+    const c2 vpt = reg_node_v(p, C.pt_node, rx, rc, n, e);
+    c2 vc = cscale(vpt, 1.0 / C.ptratio);
+    if (C.r_ldc != 0.0 || C.x_ldc != 0.0) {
+      const pgw_reg_phase& ph = p.phase[C.pt_phase];
+      double t1, t2;
+      reg_taps(ph, tap, t1, t2);
+      c2 yaa, yab, ybb;
+      reg_yprim(ph, t1, t2, yaa, yab, ybb);
+      const c2 va = reg_node_v(p, ph.a, rx, rc, n, e), vb = reg_node_v(p, ph.b, rx, rc, n, e);
+      const c2 i_in = C.winding == 2 ? cadd(cmul(yab, va), cmul(ybb, vb)) : cadd(cmul(yaa, va), cmul(yab, vb));
+      const c2 i_out = cscale(i_in, -1.0 / C.ctprim);
+      vc = csub(vc, cmul({C.r_ldc, C.x_ldc}, i_out));
+    }
+    const double vact = sqrt(vc.x * vc.x + vc.y * vc.y);
+    const double dv = C.vreg - vact;
+    if (fabs(dv) > C.band * 0.5) {
+      // DoPendingAction (STATIC): the needed change, truncated to whole taps,
+      // at least one, at most max_tap_change, inside [min_tap, max_tap]
+      const double need = dv / C.vbase;
+      double steps = trunc(fabs(need) / C.incr);
+      steps = fmin(fmax(steps, 1.0), (double)C.max_tap_change);
+      double nt = tap + (need > 0.0 ? steps : -steps) * C.incr;
+      nt = fmin(fmax(nt, C.min_tap), C.max_tap);
+      if (nt != tap) {
+        want[g] = nt;
+        dmin = fmin(dmin, C.delay);
+      }
+    }
+  }
+  // ControlQueue.DoNearestActions: only the actions with the smallest delay
+  bool moved = false;
+  for (int g = 0; g < p.n_ctrl; ++g) {
+    const double tap = taps[(int64_t)g * n + e];
+    if (want[g] != tap && p.ctrl[g].delay == dmin) {
+      taps[(int64_t)g * n + e] = want[g];
+      moved = true;
+    }
+  }
+  active[e] = moved ? 1 : 0;
+  if (moved && n_changed) atomicAdd(n_changed, 1);
+}
+
+}  // namespace pgw
+
+using namespace pgw;
+
+extern "C" {
+
+static int32_t reg_check(const pgw_reg_params* p, const char* who) {
+  PGW_REQUIRE(p && p->r_reg >= 1 && p->r_reg <= p->n_reg && p->n_reg <= PGW_PFG_MAX_REG && p->S && p->rho,
+              "%s: bad regulator parameters", who);
+  PGW_REQUIRE(p->n_phase >= 1 && p->n_phase <= PGW_REG_MAX_PHASES && p->n_ctrl >= 1 &&
+                  p->n_ctrl <= PGW_REG_MAX_CTRL, "%s: %d phases / %d controls", who, p->n_phase, p->n_ctrl);
+  for (int q = 0; q < p->n_phase; ++q) {
+    const pgw_reg_phase& ph = p->phase[q];
+    PGW_REQUIRE(ph.a >= 0 && ph.a < p->r_reg && ph.b >= 0 && ph.b < p->r_reg && ph.a != ph.b &&
+                    ph.ctrl >= 0 && ph.ctrl < p->n_ctrl && (ph.tap_winding == 1 || ph.tap_winding == 2),
+                "%s: regulated phase %d", who, q);
+  }
+  for (int g = 0; g < p->n_ctrl; ++g) {
+    const pgw_reg_ctrl& C = p->ctrl[g];
+    PGW_REQUIRE(C.pt_node >= 0 && C.pt_node < p->r_reg && C.pt_phase >= 0 && C.pt_phase < p->n_phase &&
+                    (C.winding == 1 || C.winding == 2) && C.ptratio > 0.0 && C.ctprim > 0.0 && C.incr > 0.0 &&
+                    C.vbase > 0.0 && C.min_tap <= C.max_tap && C.max_tap_change >= 1,
+                "%s: RegControl %d", who, g);
+  }
+  return PGW_OK;
+}
+
+int32_t pgw_reg_factor(const pgw_reg_params* p, int64_t n, const double* taps, const int32_t* active,
+                       double* Kreg, void* stream) {
+  const int32_t rc = reg_check(p, "pgw_reg_factor");
+  if (rc) return rc;
+  PGW_REQUIRE(taps && Kreg && n >= 0, "pgw_reg_factor: null argument");
+  PGW_REQUIRE(2 * p->r_reg <= 64, "pgw_reg_factor: r_reg %d > 32", p->r_reg);
+  if (n == 0) return PGW_OK;
+  hipLaunchKernelGGL(k_reg_factor, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, *p, n, taps, active,
+                     Kreg);
+  return check_launch("k_reg_factor");
+}
+
+int32_t pgw_reg_control(const pgw_reg_params* p, int64_t n, const double* reg_x, const double* reg_c,
+                        double* taps, int32_t* active, int32_t* n_changed, void* stream) {
+  const int32_t rc = reg_check(p, "pgw_reg_control");
+  if (rc) return rc;
+  PGW_REQUIRE(reg_x && reg_c && taps && active && n >= 0, "pgw_reg_control: null argument");
+  if (n == 0) return PGW_OK;
+  hipLaunchKernelGGL(k_reg_control, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, *p, n, reg_x, reg_c, taps, active, n_changed);
+  return check_launch("k_reg_control");
+}
+
+}  // extern "C"

@@ -15,8 +15,9 @@ voltage regulators, and centre-tapped secondaries ``bus.1.0`` / ``bus.0.2``),
 ``linecode``,
 ``line`` (linecode or r1/x1/r0/x0/c1/c0, ``Switch=y``), ``load`` (models 1-8 with
 ``CVRwatts``/``CVRvars``/``ZIPV``) and ``capacitor`` (shunt, or series with
-``bus2``); ``RegControl`` is recorded (automatic tap control is not
-simulated: the feeder model refuses it unless ``Set Controlmode=OFF``);
+``bus2``); ``RegControl`` (automatic tap control in the snap solve's STATIC
+control mode, feeder.Feeder.regulators; ``Set Controlmode=OFF`` keeps the DSS
+taps fixed);
 property assignments ``Class.Name.Prop=value`` (e.g.
 ``Transformer.Reg1.Taps=[1.0 1.0625]``); ``Redirect`` of further files;
 in-line RPN ``(8 1000 /)``; lower-triangular matrices ``(a | b c | ...)``.

@@ -114,9 +114,9 @@ class Feeder(object):
         self.node_names = ["%s.%d" % (b, nd) for b in self.buses for nd in self.bus_nodes[b]]
         self.node_index = {nm: i for i, nm in enumerate(self.node_names)}
         self.n = len(self.node_names)
-        if spec.get("regcontrols") and spec.get("controlmode", "static") != "off":
-            raise NotImplementedError("RegControl (automatic regulator tap control) is not simulated: "
-                                      "fix the taps (Transformer.X.Taps=[...]) and Set Controlmode=OFF")
+        if spec.get("controlmode", "static") not in ("static", "off"):
+            raise NotImplementedError("Set Controlmode=%s: only STATIC (the snap solve's default) and OFF"
+                                      % spec["controlmode"])
         for ld in spec["loads"]:
             if ld.get("model", 1) not in range(1, 9):
                 raise NotImplementedError("load %s: model %d (OpenDSS load models are 1-8)"
@@ -330,3 +330,99 @@ class Feeder(object):
         Gc = np.zeros((max(no, 1), M), complex)
         Gc[:, :m] = G.view(np.complex128).reshape(max(no, 1), m)
         return M, Wc, U0c, Gc[:no], V0o.view(np.complex128)[:no]
+
+    # ------------------------------------------------------------ RegControl
+    REG_DEFAULTS = dict(winding=1, vreg=120.0, band=3.0, ptratio=60.0, ctprim=300.0, r=0.0, x=0.0,
+                        ptphase=1, maxtapchange=16, delay=15.0, tapdelay=2.0, enabled=True)
+
+    def regulators(self, Z=None):
+        """The RegControl model (None without RegControls or with Controlmode=OFF):
+        the regulator terminal nodes R, each regulated phase's unit-tap
+        admittance (pgw_reg_phase), each control's settings (pgw_reg_ctrl), its
+        initial tap (the DSS file's) and S = Z[R][:, R] of the iteration model's
+        Z (pass it; default this feeder's).  OpenDSS RegControl properties
+        (RegControl.pas): transformer, winding, vreg (120), band (3), ptratio
+        (60), CTprim (300), R / X (line-drop compensation, V at CT rating),
+        PTphase (1), maxtapchange (16), delay (15 s: the STATIC mode's order),
+        tapwinding (= winding); the transformer's NumTaps (32) / MaxTap (1.1) /
+        MinTap (0.9) give the tap step.  Refused: reversible, vlimit, remote bus
+        sensing, inverse time, PTphase=max/min, a tap winding other than the
+        monitored one, delta or centre-tapped regulator windings."""
+        spec = self.spec
+        rcs = spec.get("regcontrols") or []
+        if not rcs or spec.get("controlmode", "static") == "off":
+            return None
+        xf = {t["name"]: t for t in spec["transformers"]}
+        rnodes, phases, ctrls, taps0, seen = [], [], [], [], set()
+
+        def rix(node):
+            if node not in rnodes:
+                rnodes.append(node)
+            return rnodes.index(node)
+        for g, rc in enumerate(rcs):
+            pr = dict(self.REG_DEFAULTS)
+            for k, v in rc["props"]:
+                pr[k] = v
+            name = str(pr.get("transformer", "")).lower()
+            if name not in xf:
+                raise ValueError("RegControl %s: transformer %r not defined" % (rc["name"], name))
+            if name in seen:
+                raise NotImplementedError("RegControl %s: a second control on transformer %s" % (rc["name"], name))
+            seen.add(name)
+            for bad in ("reversible", "revvreg", "revband", "vlimit", "bus", "inversetime", "revneutral",
+                        "ldc_z", "rev_z", "cogen"):
+                v = str(pr.get(bad, "")).lower()
+                if bad in pr and v not in ("", "no", "n", "false", "0", "0.0"):
+                    raise NotImplementedError("RegControl %s: %s=%s is not simulated" % (rc["name"], bad, v))
+            from powergridworld_amd.distribution_system.dss import parse_number
+            num = lambda k: parse_number(str(pr[k]))
+            w = int(num("winding"))
+            tw = int(num("tapwinding")) if "tapwinding" in pr else w
+            if tw != w or w not in (1, 2):
+                raise NotImplementedError("RegControl %s: tap winding %d, monitored winding %d" % (rc["name"], tw, w))
+            t = xf[name]
+            ph = t["phases"]
+            if len(t["windings"]) != 2:
+                raise NotImplementedError("RegControl %s: regulator %s has %d windings" % (rc["name"], name,
+                                                                                        len(t["windings"])))
+            terms = [_winding_terminals(wd["bus"], ph, wd["conn"]) for wd in t["windings"]]
+            if any(wd["conn"] != "wye" for wd in t["windings"]) or any(lo != 0 for _, prs, _ in terms
+                                                                        for _, lo in prs):
+                raise NotImplementedError("RegControl %s: regulator %s needs wye windings to ground" % (rc["name"], name))
+            ptp = str(pr["ptphase"]).lower()
+            if not ptp.isdigit() or not 1 <= int(ptp) <= ph:
+                raise NotImplementedError("RegControl %s: PTphase=%s" % (rc["name"], ptp))
+            w1, w2 = t["windings"]
+            s3 = math.sqrt(3.0)
+            vw1 = w1["kv"] * 1000.0 / (s3 if ph == 3 else 1.0)
+            vw2 = w2["kv"] * 1000.0 / (s3 if ph == 3 else 1.0)
+            kva_ph = w1["kva"] * 1000.0 / ph
+            zpu = complex((w1["pct_r"] + w2["pct_r"]) / 100.0, t["xhl"] / 100.0)
+            y1 = 1.0 / (zpu * (vw1 * vw1 / kva_ph))          # at unit taps (pgw_feeder.cpp's model)
+            A, B, C = y1, -y1 * vw1 / vw2, y1 * vw1 * vw1 / (vw2 * vw2)
+            first = len(phases)
+            for p in range(ph):
+                a = rix(self.node(terms[0][0], terms[0][1][p][0]))
+                b = rix(self.node(terms[1][0], terms[1][1][p][0]))
+                phases.append(dict(a=a, b=b, ctrl=g, tap_winding=tw, A=A, B=B, C=C,
+                                   tap1=w1.get("tap", 1.0), tap2=w2.get("tap", 1.0)))
+            ptph = first + int(ptp) - 1
+            numtaps = float(t.get("numtaps", 32.0))
+            maxtap, mintap = float(t.get("maxtap", 1.10)), float(t.get("mintap", 0.90))
+            ptratio = num("ptratio")
+            vw = vw1 if w == 1 else vw2
+            ctrls.append(dict(pt_node=phases[ptph]["a" if w == 1 else "b"], pt_phase=ptph, winding=w,
+                              max_tap_change=int(num("maxtapchange")), vreg=num("vreg"), band=num("band"),
+                              ptratio=ptratio, ctprim=num("ctprim"), r_ldc=num("r"), x_ldc=num("x"),
+                              vbase=vw / ptratio, incr=(maxtap - mintap) / numtaps, min_tap=mintap,
+                              max_tap=maxtap, delay=num("delay"), name=rc["name"]))
+            taps0.append(t["windings"][w - 1].get("tap", 1.0))
+        if len(phases) > _lib.REG_MAX_PHASES or len(ctrls) > _lib.REG_MAX_CTRL:
+            raise NotImplementedError("%d regulated phases / %d RegControls (max %d / %d)"
+                                      % (len(phases), len(ctrls), _lib.REG_MAX_PHASES, _lib.REG_MAX_CTRL))
+        if len(rnodes) > _lib.PFG_MAX_REG:
+            raise NotImplementedError("%d regulator nodes (max %d)" % (len(rnodes), _lib.PFG_MAX_REG))
+        Z = self.Z if Z is None else Z
+        R = np.array(rnodes, int)
+        return dict(nodes=R, phases=phases, ctrls=ctrls, taps0=np.array(taps0, float),
+                    S=np.ascontiguousarray(Z[np.ix_(R, R)]), rho=self.kv_ln[R] * 1000.0)

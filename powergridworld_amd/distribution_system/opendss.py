@@ -86,8 +86,10 @@ class OpenDSSSolver(PowerFlowSolver):
         self.feeder = Feeder(spec)
         # the fast kernels hold up to PF_MAX_M constant-PQ elements; larger feeders,
         # other load models and OpenDSS's stopping rule run the general kernel
+        self.regulators = None
         self.general = (bool(general) or convergence == "opendss" or self.feeder.m > _lib.PF_MAX_M
-                        or bool((self.feeder.elem_model != 1).any()))
+                        or bool((self.feeder.elem_model != 1).any())
+                        or bool(spec.get("regcontrols") and spec.get("controlmode", "static") != "off"))
         if self.feeder.m > _lib.PFG_MAX_M:
             raise ValueError("feeder has %d load phase elements (max %d)" % (self.feeder.m, _lib.PFG_MAX_M))
         if convergence == "opendss":
@@ -101,6 +103,11 @@ class OpenDSSSolver(PowerFlowSolver):
             self._fd_iter = self.feeder
             tol = 1e-10 if tol is None else tol
             max_iter = 100 if max_iter is None else max_iter
+        # RegControl (automatic regulator taps, STATIC control mode): per-env taps,
+        # the control loop in calculate_power_flow (pgw_reg_control / pgw_reg_factor)
+        self.regulators = self.feeder.regulators(Z=self._fd_iter.Z)
+        if self.regulators is not None:
+            self._init_regulators()
         self.system_load_rescale_factor = system_load_rescale_factor
         self.annual_hourly_load_profile = load_loadshape(loadshape_file)
         if len(self.annual_hourly_load_profile) != 8760:
@@ -219,9 +226,38 @@ class OpenDSSSolver(PowerFlowSolver):
         Gs = (G / vb[None, :]) / vbn[idx][:, None]
         V0s = np.zeros(ldo, complex)
         V0s[:no] = V0o / vbn[idx]
-        self._g_W = dev_c(emaj(Ws.T, mp))           # column k = W''[:, k]
+        # RegControl: n_reg extra columns -- each row's response to the correction
+        # currents c (amps) at the regulator nodes R: -(Z U)[row, R] in the row's pu
+        reg = self.regulators
+        nreg = 0
+        if reg is not None:
+            R, r = reg["nodes"], len(reg["nodes"])
+            nreg = -(-r // 8) * 8
+            ZR = fi.Z[:, R]                                        # [n, r]
+            CZ = np.zeros((m, r), complex)
+            for k in range(m):
+                CZ[k] = ZR[f.elem_p[k]] - (ZR[f.elem_q[k]] if f.elem_q[k] >= 0 else 0.0)
+            pad = lambda a: np.pad(a, ((0, 0), (0, nreg - r)))
+            Ws_aug = np.hstack([np.pad(Ws, ((0, 0), (0, mp - m))), pad(-CZ / vb[:, None])])   # [m, mp + nreg]
+            Gs_aug = np.hstack([np.pad(Gs, ((0, 0), (0, mp - m))), pad(-ZR[idx] / vbn[idx][:, None])])
+            _, _, GR, V0R = fi.reduce_rows(list(R))
+            rho = reg["rho"]
+            V0rs = np.zeros(nreg, complex)
+            V0rs[:r] = V0R / rho
+            self._g_Greg = dev_c(emaj((GR / vb[None, :]) / rho[:, None], nreg))
+            self._g_V0reg = dev_c(V0rs)
+
+            def emaj_aug(rows_cm, ld):     # [rows, mp + nreg] -> [mp + nreg][ld]
+                out = np.zeros((mp + nreg, ld), complex)
+                out[:, :rows_cm.shape[0]] = rows_cm.T
+                return out
+            self._g_W = dev_c(emaj_aug(np.pad(Ws_aug, ((0, mp - m), (0, 0))), mp))
+            self._g_G = dev_c(emaj_aug(Gs_aug, ldo))
+        else:
+            self._g_W = dev_c(emaj(Ws.T, mp))           # column k = W''[:, k]
+            self._g_G = dev_c(emaj(Gs, ldo))
+        self._g_nreg = nreg
         self._g_U0 = dev_c(u0)
-        self._g_G = dev_c(emaj(Gs, ldo))
         self._g_V0 = dev_c(V0s)
         n_chk = 0
         self._g_Gc = self._g_V0c = None
@@ -233,7 +269,12 @@ class OpenDSSSolver(PowerFlowSolver):
                                  % (f.n, _lib.PFG_MAX_CHK))
             V0cs = np.zeros(n_chk, complex)
             V0cs[:f.n] = V0c / vbn
-            self._g_Gc = dev_c(emaj((Gc / vb[None, :]) / vbn[:, None], n_chk))
+            Gcs = (Gc / vb[None, :]) / vbn[:, None]
+            if reg is not None:
+                Gcs = np.hstack([np.pad(Gcs, ((0, 0), (0, mp - m))), pad(-ZR / vbn[:, None])])
+                self._g_Gc = dev_c(emaj_aug(Gcs, n_chk))
+            else:
+                self._g_Gc = dev_c(emaj(Gcs, n_chk))
             self._g_V0c = dev_c(V0cs)
         self._g_n_chk = n_chk
         self._vmin = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
@@ -318,6 +359,9 @@ class OpenDSSSolver(PowerFlowSolver):
         p.mode = _lib.PF_OPENDSS if self.convergence == "opendss" else _lib.PF_EXACT
         p.min_iter, p.max_iter, p.tol = self.min_iter, self.max_iter, self.tol
         p.coef, p.rescale = 1.0, float(self.system_load_rescale_factor)
+        reg = self.regulators
+        if reg is not None:
+            p.n_reg, p.r_reg = self._g_nreg, len(reg["nodes"])
         self.params = p
         elems = self._general_elems()
         self._g_elem = torch.tensor(np.frombuffer(bytes(elems), np.uint8), device=self.device)
@@ -327,6 +371,10 @@ class OpenDSSSolver(PowerFlowSolver):
                                      Gc=self._g_Gc.data_ptr() if self._g_Gc is not None else None,
                                      V0c=self._g_V0c.data_ptr() if self._g_V0c is not None else None,
                                      v_min_out=self._vmin.data_ptr(), v_max_out=self._vmax.data_ptr())
+        if reg is not None:
+            t = self.tables
+            t.Greg, t.V0reg = self._g_Greg.data_ptr(), self._g_V0reg.data_ptr()
+            t.Kreg, t.reg_x, t.reg_c = self._Kreg.data_ptr(), self._reg_x.data_ptr(), self._reg_c.data_ptr()
         self._cfg_version = getattr(self, "_cfg_version", 0) + 1
         self.tables_version = getattr(self, "tables_version", 0) + 1
         self._step_cache = {}
@@ -486,13 +534,81 @@ class OpenDSSSolver(PowerFlowSolver):
                 cq = torch.stack([x if x is not None else zeros for x in qs])
         tables = self.solve_tables(current_time, cp is not None)
         fn = _lib.lib().pgw_pf_solve_general if self.general else _lib.lib().pgw_pf_solve
-        _lib.check(fn(p, tables, n, _lib.dptr(cp), _lib.dptr(cq), _lib.dptr(self.v_out),
-                      _lib.dptr(self._iters), _lib.stream_ptr(self.device)))
+        if self.regulators is not None:
+            self._solve_regulated(fn, p, tables, cp, cq)
+        else:
+            _lib.check(fn(p, tables, n, _lib.dptr(cp), _lib.dptr(cq), _lib.dptr(self.v_out),
+                          _lib.dptr(self._iters), _lib.stream_ptr(self.device)))
         self.solved(tables)
         self.iterations = self._iters
         self._prepare_bus_voltages()
         if self._all_nodes:                        # the epilogue's min / max over every node
             self._extrema = (self._vmin, self._vmax)
+
+    # ------------------------------------------------------------ RegControl
+    # OpenDSS's snap solve with controls (SolveSnap): solve, sample every
+    # control, execute the pending actions (STATIC: the nearest delay first),
+    # repeat until no control acts or MaxControlIterations.  Taps persist
+    # across solves and episodes, as the regulator objects do in the
+    # reference's one OpenDSS circuit (opendss.py:36-39 compiles it once).
+    OPENDSS_MAX_CONTROL_ITER = 15
+
+    def _init_regulators(self):
+        reg, n, dev = self.regulators, self.num_envs, self.device
+        r, nc = len(reg["nodes"]), len(reg["ctrls"])
+        self.reg_taps = torch.tensor(np.repeat(reg["taps0"][:, None], n, 1), dtype=torch.float64, device=dev)
+        self._Kreg = torch.zeros((r * r, n, 2), dtype=torch.float64, device=dev)     # DSS taps: K = 0
+        self._reg_x = torch.zeros((r, n, 2), dtype=torch.float64, device=dev)
+        self._reg_c = torch.zeros((r, n, 2), dtype=torch.float64, device=dev)
+        self._reg_active = torch.ones(n, dtype=torch.int32, device=dev)
+        self._reg_nchg = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._reg_S = torch.tensor(np.ascontiguousarray(reg["S"]).view(np.float64).ravel(), device=dev)
+        self._reg_rho = torch.tensor(reg["rho"], dtype=torch.float64, device=dev)
+        rp = _lib.RegParams()
+        rp.n_reg, rp.r_reg = -(-r // 8) * 8, r
+        rp.n_phase, rp.n_ctrl = len(reg["phases"]), nc
+        for q, ph in enumerate(reg["phases"]):
+            d = rp.phase[q]
+            d.a, d.b, d.ctrl, d.tap_winding = ph["a"], ph["b"], ph["ctrl"], ph["tap_winding"]
+            for key in ("A", "B", "C"):
+                getattr(d, key)[0], getattr(d, key)[1] = ph[key].real, ph[key].imag
+            d.tap1, d.tap2 = ph["tap1"], ph["tap2"]
+        for g, c in enumerate(reg["ctrls"]):
+            d = rp.ctrl[g]
+            for key in ("pt_node", "pt_phase", "winding", "max_tap_change", "vreg", "band", "ptratio",
+                        "ctprim", "r_ldc", "x_ldc", "vbase", "incr", "min_tap", "max_tap", "delay"):
+                setattr(d, key, c[key])
+        rp.S, rp.rho = self._reg_S.data_ptr(), self._reg_rho.data_ptr()
+        self._reg_params = rp
+        self.control_iterations = 0
+
+    def set_regulator_taps(self, taps):
+        """Set every env's RegControl taps ([n_ctrl] or [n_ctrl, N], pu) and
+        refactor the Woodbury correction for them."""
+        t = torch.as_tensor(taps, dtype=torch.float64, device=self.device)
+        self.reg_taps.copy_(t.reshape(len(self.regulators["ctrls"]), -1).expand_as(self.reg_taps))
+        _lib.check(_lib.lib().pgw_reg_factor(self._reg_params, self.num_envs, self.reg_taps.data_ptr(), None,
+                                             self._Kreg.data_ptr(), _lib.stream_ptr(self.device)))
+
+    def _solve_regulated(self, fn, p, tables, cp, cq):
+        n, st, lib = self.num_envs, _lib.stream_ptr(self.device), _lib.lib()
+        t = type(tables).from_buffer_copy(tables)
+        t.Kreg, t.reg_x, t.reg_c = self._Kreg.data_ptr(), self._reg_x.data_ptr(), self._reg_c.data_ptr()
+        active = None
+        for it in range(1, self.OPENDSS_MAX_CONTROL_ITER + 1):
+            t.env_active = active
+            _lib.check(fn(p, t, n, _lib.dptr(cp), _lib.dptr(cq), _lib.dptr(self.v_out),
+                          _lib.dptr(self._iters), st))
+            self._reg_nchg.zero_()
+            _lib.check(lib.pgw_reg_control(self._reg_params, n, self._reg_x.data_ptr(), self._reg_c.data_ptr(),
+                                           self.reg_taps.data_ptr(), self._reg_active.data_ptr(),
+                                           self._reg_nchg.data_ptr(), st))
+            _lib.check(lib.pgw_reg_factor(self._reg_params, n, self.reg_taps.data_ptr(),
+                                          self._reg_active.data_ptr(), self._Kreg.data_ptr(), st))
+            self.control_iterations = it
+            if int(self._reg_nchg.item()) == 0:          # (one host sync per control pass)
+                break
+            active = self._reg_active.data_ptr()
 
     def solve_tables(self, current_time, controllable=True):
         """The PFTables a solve at `current_time` uses: the hour's predictor tables

@@ -380,6 +380,8 @@ class MultiAgentEnv(Env):
             return "power flow solver is not the batched OpenDSSSolver"
         if self.pf_solver.general and self.dtype != torch.float64:
             return "the general power flow (large feeder or convergence='opendss') has no fp32 fused step"
+        if getattr(self.pf_solver, "regulators", None) is not None:
+            return "RegControl (the control loop runs in OpenDSSSolver.calculate_power_flow)"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)

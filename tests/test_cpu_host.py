@@ -124,7 +124,13 @@ def test_dss_unsupported_control_and_models_refused(tmp_path):
     text = open(REGCAP).read()
     p = tmp_path / "ctl.dss"
     p.write_text(text.replace("Set Controlmode=OFF", ""))
-    with pytest.raises(NotImplementedError, match="RegControl"):
+    assert len(Feeder(load_feeder_spec(str(p))).regulators()["ctrls"]) == 1     # STATIC: simulated
+    assert Feeder(load_feeder_spec(REGCAP)).regulators() is None                  # OFF: fixed taps
+    p.write_text(text.replace("Set Controlmode=OFF", "").replace("R=3 X=9", "R=3 X=9 reversible=yes"))
+    with pytest.raises(NotImplementedError, match="reversible"):
+        Feeder(load_feeder_spec(str(p))).regulators()
+    p.write_text(text.replace("Set Controlmode=OFF", "Set Controlmode=TIME"))
+    with pytest.raises(NotImplementedError, match="Controlmode"):
         Feeder(load_feeder_spec(str(p)))
     p = tmp_path / "m9.dss"
     p.write_text(text.replace("Model=2 kV=2.4", "Model=9 kV=2.4"))
@@ -416,3 +422,47 @@ def test_dss_three_winding_and_centre_tap_transformers():
     loss = S_in.sum()
     p_through = S_in[:3].sum().real                        # from B (winding 1)
     assert p_through > 0 and 0 < loss.real < 0.02 * p_through
+
+
+REGCTL = os.path.join(REPO, "tests", "data", "regctl_feeder.dss")
+
+
+def test_regcontrol_model_woodbury_matches_rebuilt_network():
+    """RegControl model (Feeder.regulators, tests/data/regctl_feeder.dss): the
+    regulated phases' unit-tap admittances and the regulator nodes R give, through
+    the Woodbury form the kernels use (Z(t) = Z0 - Z0 U K U^T Z0, K = (I + D S)^-1 D),
+    the no-load voltages of the oracle's network rebuilt and re-inverted at the
+    same taps; the oracle's control loop moves out-of-band regulators into band
+    in whole steps (MaxTapChange respected).  Parity unpinned (no OpenDSS)."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    spec = load_feeder_spec(REGCTL)
+    f, o = Feeder(spec), OracleFeeder(spec)
+    reg = f.regulators()
+    assert reg is not None and len(reg["ctrls"]) == 4 and len(reg["phases"]) == 6
+    assert len(reg["nodes"]) == 12
+    np.testing.assert_allclose(reg["taps0"], [1.0, 1.0125, 0.99375, 1.0])
+    R, r = reg["nodes"], len(reg["nodes"])
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        taps = reg["taps0"] + 0.00625 * rng.integers(-8, 9, size=4)
+        D = np.zeros((r, r), complex)
+        for ph in reg["phases"]:
+            t = taps[ph["ctrl"]]
+            t1 = t if ph["tap_winding"] == 1 else ph["tap1"]
+            t2 = t if ph["tap_winding"] == 2 else ph["tap2"]
+            Y = lambda a, b: np.array([[ph["A"] / a ** 2, ph["B"] / (a * b)], [ph["B"] / (a * b), ph["C"] / b ** 2]])
+            D[np.ix_([ph["a"], ph["b"]], [ph["a"], ph["b"]])] += Y(t1, t2) - Y(ph["tap1"], ph["tap2"])
+        K = np.linalg.solve(np.eye(r) + D @ reg["S"], D)
+        V = f.V0 - f.Z[:, R] @ (K @ f.V0[R])
+        ot = o.with_taps(list(taps))
+        np.testing.assert_allclose(V, ot.V0, rtol=1e-9, atol=1e-9 * np.abs(ot.V0).max())
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float)
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float)
+    V, it, tp, cp = o.solve_regulated(kw[None], kvar[None], reg["taps0"][None])
+    assert cp[0] >= 2 and (tp[0] != reg["taps0"]).any()
+    steps = (tp[0] - reg["taps0"]) / 0.00625
+    np.testing.assert_allclose(steps, np.round(steps), atol=1e-9)
+    # in band after the loop (the last pass moved nothing)
+    _, moved = o.reg_control_pass(V[0], list(tp[0]))
+    assert not moved
