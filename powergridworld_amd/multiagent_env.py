@@ -967,6 +967,17 @@ class MultiAgentEnv(Env):
             if key not in F["step_cache"]:
                 self._step_entry(key)
 
+    def state_dict(self):
+        """The env's whole state (device tensors, generator states, clocks):
+        powergridworld_amd.checkpoint.state_dict."""
+        from powergridworld_amd.checkpoint import state_dict
+        return state_dict(self)
+
+    def load_state_dict(self, sd, strict=False):
+        """Restore a state_dict() of an env of the same configuration (in place)."""
+        from powergridworld_amd.checkpoint import load_state_dict
+        return load_state_dict(self, sd, strict)
+
     def packed_obs(self):
         """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""
         return self._fused["obs"].transpose(1, 2)

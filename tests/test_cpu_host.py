@@ -466,3 +466,37 @@ def test_regcontrol_model_woodbury_matches_rebuilt_network():
     # in band after the loop (the last pass moved nothing)
     _, moved = o.reg_control_pass(V[0], list(tp[0]))
     assert not moved
+
+
+def test_checkpoint_walk_restores_in_place():
+    """checkpoint.state_dict / load_state_dict on a stand-in object tree (CPU
+    tensors): tensors restored in place (identity kept), a view restored
+    through its base, generator states and clocks reset, caches and version
+    counters left alone."""
+    import torch
+    from powergridworld_amd import checkpoint
+
+    class Part:                      # (module powergridworld_amd: walked)
+        pass
+    Part.__module__ = "powergridworld_amd.test_stub"
+    env = Part()
+    env.time_index, env.tables_version, env.step_cache = 3, 7, {"k": 1}
+    env.soc = torch.arange(4.0)
+    env.obs_view = env.soc.view(2, 2).t()
+    env.gen = torch.Generator().manual_seed(1)
+    env.sub = Part()
+    env.sub.x = torch.ones(3)
+    env.sub.flags = {"a": torch.zeros(2), "n": 5}
+    sd = checkpoint.state_dict(env)
+    soc_id = id(env.soc)
+    env.soc += 10
+    env.sub.x.mul_(3)
+    env.sub.flags["a"].fill_(9)
+    env.time_index, env.tables_version = 9, 8
+    r1 = torch.rand(2, generator=env.gen)
+    checkpoint.load_state_dict(env, sd)
+    assert id(env.soc) == soc_id and torch.equal(env.soc, torch.arange(4.0))
+    assert torch.equal(env.sub.x, torch.ones(3)) and torch.equal(env.sub.flags["a"], torch.zeros(2))
+    assert env.time_index == 3 and env.tables_version == 8          # (version counters untouched)
+    assert torch.equal(torch.rand(2, generator=env.gen), r1)
+    assert "step_cache" not in " ".join(sd)

@@ -1,0 +1,165 @@
+"""state_dict() / load_state_dict() (powergridworld_amd/checkpoint.py, SURVEY 5
+"Checkpoint / resume"): restoring a saved state and replaying the same actions
+reproduces the same trajectory bit for bit -- in the same env (rewound) and in
+a freshly built env of the same configuration -- across an episode boundary,
+for the fused C4 step, the fused heterogeneous step, the HS house, the
+randomized EV and the RegControl power flow.  Needs an MI355X."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _flat(x):
+    """Every tensor of a (nested) step output, cloned, in a stable order."""
+    out = []
+    if isinstance(x, torch.Tensor):
+        out.append(x.detach().clone())
+    elif isinstance(x, dict):
+        for k in sorted(x, key=str):
+            out += _flat(x[k])
+    elif isinstance(x, (list, tuple)):
+        for v in x:
+            out += _flat(v)
+    elif isinstance(x, (bool, int, float)):
+        out.append(torch.tensor(float(x)))
+    return out
+
+
+def _replay(env, acts, step):
+    outs = []
+    for a in acts:
+        outs.append(_flat(step(env, a)))
+    torch.cuda.synchronize()
+    return outs
+
+
+def _check(make, acts_before, acts_after, step, reset=lambda e: e.reset()):
+    env = make()
+    reset(env)
+    for a in acts_before:
+        step(env, a)
+    sd = env.state_dict()
+    ref = _replay(env, acts_after, step)
+    env.load_state_dict(sd)                     # rewind the same env
+    again = _replay(env, acts_after, step)
+    fresh = make()                              # a new env of the same configuration
+    reset(fresh)
+    fresh.load_state_dict(sd)
+    other = _replay(fresh, acts_after, step)
+    for t, (x, y, z) in enumerate(zip(ref, again, other)):
+        assert len(x) == len(y) == len(z), t
+        for i, (u, v, w) in enumerate(zip(x, y, z)):
+            assert torch.equal(u, v), "rewound env, step %d output %d" % (t, i)
+            assert torch.equal(u, w), "fresh env, step %d output %d" % (t, i)
+
+
+def _step_ma(env, a):
+    o, r, d, m = env.step(a)
+    return o, r, d["__all__"], m.get("voltage_violation") if isinstance(m, dict) else None
+
+
+def test_checkpoint_c4_fused_across_reset():
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    n = 2048
+    g = torch.Generator(DEV).manual_seed(5)
+    acts = [torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=g) * 2.2 - 1.1 for _ in range(300)]
+
+    def step(env, a):
+        o, r, d, m = env.step(a)
+        if d["__all__"]:
+            env.reset()
+        return env.packed_obs(), r, d["__all__"], m["voltage_violation"], env.pf_solver.get_bus_voltage_by_name("675c")
+    make = lambda: CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV)
+    _check(make, acts[:280], acts[280:], step)
+
+
+def test_checkpoint_heterogeneous_fused():
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    n = 1024
+    rng = np.random.default_rng(3)
+    acts = [torch.tensor(rng.uniform(-1.2, 1.2, (n, 10)), device=DEV) for _ in range(40)]
+
+    def step(env, a):
+        act = {"building": {"building": a[:, :6], "pv": a[:, 6:7], "storage": a[:, 7:8]},
+               "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
+        o, r, d, m = env.step(act)
+        return o, r, d["__all__"], env.pf_solver.voltage_extrema()
+    make = lambda: MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV)
+    _check(make, acts[:25], acts[25:], step)
+
+
+def test_checkpoint_hs_house_across_reset():
+    from powergridworld_amd.base_hs import HSMultiComponentEnv
+    from powergridworld_amd.scenarios.heterogeneous_hs import make_env_config
+    n = 512
+    make = lambda: HSMultiComponentEnv(**make_env_config(), num_envs=n, device=DEV)
+    names = [e.name for e in make().envs]
+    rng = np.random.default_rng(4)
+    acts = [torch.tensor(rng.uniform(-1.1, 1.1, (n, len(names))), device=DEV) for _ in range(300)]
+
+    def step(env, a):
+        o, r, d, m = env.step({nm: a[:, i:i + 1] for i, nm in enumerate(names)})
+        if d:
+            env.reset()
+        return o, r, d, env.real_power, m["pv_power"], m["es_power"], m["grid_power"]
+    _check(make, acts[:283], acts[283:], step)
+
+
+def test_checkpoint_ev_randomized():
+    from powergridworld_amd.agents.vehicles import EVChargingEnv
+    n = 1024
+    g = torch.Generator(DEV).manual_seed(6)
+    acts = [torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=g) * 2 - 1 for _ in range(300)]
+
+    def make():
+        e = EVChargingEnv(num_vehicles=25, minutes_per_step=5, max_charge_rate_kw=7.0, peak_threshold=200.0,
+                          vehicle_multiplier=40.0, rescale_spaces=True, randomize=True, num_envs=n, device=DEV)
+        e.seed(7)
+        return e
+
+    def step(env, a):
+        o, r, d, m = env.step(a)
+        if d:
+            env.reset()
+        return o, r, d, env.real_power
+    _check(make, acts[:280], acts[280:], step)
+
+
+def test_checkpoint_regcontrol_solver():
+    from powergridworld_amd.checkpoint import load_state_dict, state_dict
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    import pandas as pd
+    n = 256
+    make = lambda: OpenDSSSolver(os.path.join(HERE, "data", "regctl_feeder.dss"),
+                                 "ieee_13_dss/annual_hourly_load_profile.csv", num_envs=n, device=DEV)
+    rng = np.random.default_rng(8)
+    loads = [torch.tensor(rng.uniform(-300, 900, n), device=DEV) for _ in range(8)]
+    times = [pd.Timestamp("08-12-2021 %02d:00:00" % h) for h in range(8)]
+    s = make()
+    for p, t in zip(loads[:4], times[:4]):
+        s.calculate_power_flow({"f1": p}, None, current_time=t)
+    sd = state_dict(s)
+
+    def run(solver):
+        out = []
+        for p, t in zip(loads[4:], times[4:]):
+            solver.calculate_power_flow({"f1": p}, None, current_time=t)
+            out.append(torch.stack(list(solver.get_bus_voltages().values())).clone())
+            out.append(solver.reg_taps.clone())
+        return out
+    ref = run(s)
+    load_state_dict(s, sd)
+    again = run(s)
+    f = make()
+    f.calculate_power_flow({"f1": loads[0]}, None, current_time=times[0])     # (same controllable set)
+    load_state_dict(f, sd)
+    other = run(f)
+    for x, y, z in zip(ref, again, other):
+        assert torch.equal(x, y) and torch.equal(x, z)
