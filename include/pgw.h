@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 19
+#define PGW_ABI_VERSION 20
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -830,6 +830,8 @@ typedef struct pgw_hs_params {
   double dev_obs_high[PGW_HS_MAX_DEV];
   double max_grid_power;
   uint64_t* oob;                  /* nullable device counter, see PGW_OOB     */
+  int32_t pv_grid_aware;          /* HSPVEnv(grid_aware): obs + min_voltage (0.9, 1.1) */
+  int32_t pad_;
 } pgw_hs_params;
 
 /* Per-step values shared by all envs (the house steps in lockstep). */
@@ -881,6 +883,12 @@ typedef struct pgw_hs_buffers {
   double* real_power;
   double* meta_out;
   double* step_meta;
+  /* meta_state pv_power carried from step to step (base_hs.py keeps one
+   * meta_state dict: a component ahead of the PV in the chain sees the last
+   * step's final pv_power; NaN stands for the reference's initial None).
+   * NULL: 0 at every step start (a PV-first chain never reads it). */
+  double* pv_power_last;
+  const double* min_voltage;  /* n, the grid-aware PV's observation (NULL otherwise) */
 } pgw_hs_buffers;
 
 /* reset (base_hs.py:66-91): PV and devices at row 0, storage SoC := clip(

@@ -612,8 +612,59 @@ HS_META_FIELDS = 13
 HS_CUSTOM_KEYS = {}
 
 
+# The same house with the chain in another order -- [PV (grid-aware), EV,
+# devices, storage] -- and a per-step min_voltage keyword: the devices draw on
+# the resources before the storage does, the storage's reward sees what the EV
+# and the devices left.  (A component ahead of the PV is not a configuration the
+# reference runs: its meta_state pv_power is None until the PV's first step,
+# and the EV's reset step and every component's step_meta subtract from it.)
+def gen_hs_order():
+    from gridworld import HSMultiComponentEnv
+    from gridworld.scenarios.heterogeneous_hs import make_env_config as make_hs_config
+    rng = np.random.default_rng(909)
+    K, EPISODES = 3, 2
+    cfg = make_hs_config()
+    by = {c["name"]: c for c in cfg["components"]}
+    cfg["components"] = [by["pv"], by["ev-charging"], by["other-devices"], by["storage"]]
+    by["pv"]["config"]["grid_aware"] = True
+    names = [c["name"] for c in cfg["components"]]
+    runs = []
+    for k in range(K):
+        env = HSMultiComponentEnv(**copy.deepcopy(cfg))
+        rec = dict(obs=[], act=[], rew=[], rp=[], done=[], meta=[], soc=[], mv=[])
+        for ep in range(EPISODES):
+            mv = float(rng.uniform(0.88, 1.12))
+            rec["mv"].append(mv)
+            with quiet():
+                o = env.reset(min_voltage=mv)
+            rec["obs"].append(np.concatenate([np.ravel(o[n]) for n in names]))
+            rec["meta"].append([np.nan] * 3)
+            rec["soc"].append(env.env_dict["storage"].current_storage)
+            while True:
+                a = rng.uniform(-1.1, 1.1, len(names))
+                a[rng.random(len(names)) < 0.05] = 0.0
+                mv = float(rng.uniform(0.88, 1.12))
+                with quiet():
+                    o, r, d, m = env.step({n: a[i:i + 1].copy() for i, n in enumerate(names)}, min_voltage=mv)
+                rec["act"].append(a)
+                rec["mv"].append(mv)
+                rec["obs"].append(np.concatenate([np.ravel(o[n]) for n in names]))
+                rec["rew"].append(float(r))
+                rec["rp"].append(float(env.real_power))
+                rec["done"].append(bool(d))
+                rec["meta"].append([m["pv_power"], m["es_power"], m["grid_power"]])
+                rec["soc"].append(env.env_dict["storage"].current_storage)
+                if d:
+                    break
+        runs.append(rec)
+    stack = lambda key: np.stack([np.asarray(r[key], dtype=np.float64) for r in runs], 1)
+    _save("hs_order", names=np.array(names), actions=stack("act"), obs=stack("obs"), reward=stack("rew"),
+          real_power=stack("rp"), done=stack("done").astype(bool), meta=stack("meta"), soc=stack("soc"),
+          min_voltage=stack("mv"), episodes=np.array(EPISODES))
+
+
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "evrand": gen_ev_random, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes, "het": gen_het, "hs": gen_hs}
+              "ev": gen_ev, "evrand": gen_ev_random, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes, "het": gen_het, "hs": gen_hs, "hs_order": gen_hs_order}
 
 
 def main():

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -236,7 +236,8 @@ class HSParams(C.Structure):
                 ("ev_unserved_penalty", f64), ("ev_obs_low", f64 * 7), ("ev_obs_high", f64 * 7),
                 ("ev_end_park", f64 * HS_MAX_VEHICLES), ("ev_req0", f64 * HS_MAX_VEHICLES),
                 ("dev_act_low", f64), ("dev_act_high", f64), ("dev_hours_per_step", f64),
-                ("dev_obs_high", f64 * HS_MAX_DEV), ("max_grid_power", f64), ("oob", vp)]
+                ("dev_obs_high", f64 * HS_MAX_DEV), ("max_grid_power", f64), ("oob", vp),
+                ("pv_grid_aware", i32), ("pad_", i32)]
 
 
 class HSStepInfo(C.Structure):
@@ -248,7 +249,8 @@ class HSStepInfo(C.Structure):
 class HSBuffers(C.Structure):
     _fields_ = [("action", Mat), ("obs", Mat), ("soc", vp), ("soc_cost", vp), ("ev_req", vp),
                 ("ev_charging", vp), ("ev_cost", vp), ("dev_cost", vp), ("es_power_last", vp),
-                ("reward", vp), ("real_power", vp), ("meta_out", vp), ("step_meta", vp)]
+                ("reward", vp), ("real_power", vp), ("meta_out", vp), ("step_meta", vp),
+                ("pv_power_last", vp), ("min_voltage", vp)]
 
 
 PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE, PGW_ELEM_SHUNT, PGW_ELEM_XFMR_N = 1, 2, 3, 4, 5

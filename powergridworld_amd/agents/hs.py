@@ -50,7 +50,8 @@ class _HSComponent(ComponentEnv):
 
 @register_env
 class HSPVEnv(_HSComponent):
-    """pv_profile_env_hs.py:15-98: action box (0.98, 1), obs -data[index]."""
+    """pv_profile_env_hs.py:15-98: action box (0.98, 1), obs -data[index]
+    (+ min_voltage when grid_aware)."""
 
     hs_kind = 0
 
@@ -59,8 +60,7 @@ class HSPVEnv(_HSComponent):
                  grid_aware: bool = False, max_episode_steps: int = None, minutes_per_step: int = 5,
                  num_envs: int = 1, device=None, **kwargs):
         super().__init__(name=name, num_envs=num_envs, device=device)
-        if grid_aware:
-            raise NotImplementedError("grid-aware HSPVEnv: the house supplies no min_voltage")
+        self.grid_aware = bool(grid_aware)
         self.scaling_factor = scaling_factor
         self.rescale_spaces = rescale_spaces
         self.minutes_per_step = minutes_per_step
@@ -72,9 +72,14 @@ class HSPVEnv(_HSComponent):
         self.episode_length = len(self.data)
         if max_episode_steps is not None:
             self.episode_length = min(max_episode_steps, self.episode_length)
-        self._obs_labels = ["real_power"]
-        self._observation_space = spaces.Box(shape=(1,), low=np.array([-np.max(self.data)]),
-                                             high=np.array([0.]), dtype=np.float64)
+        # grid_aware (:47-48, 81-85): min_voltage joins the obs, box (0.9, 1.1); the
+        # house takes it as a step / reset keyword (MultiAgentEnv passes it)
+        self._obs_labels = ["real_power"] + (["min_voltage"] if self.grid_aware else [])
+        lo, hi = [-np.max(self.data)], [0.]
+        if self.grid_aware:
+            lo, hi = lo + [0.9], hi + [1.1]
+        self._observation_space = spaces.Box(shape=(len(lo),), low=np.array(lo), high=np.array(hi),
+                                             dtype=np.float64)
         self.observation_space = maybe_rescale_box_space(self._observation_space, rescale_spaces)
         self._action_space = spaces.Box(shape=(1,), low=0.98, high=1., dtype=np.float64)
         self.action_space = maybe_rescale_box_space(self._action_space, rescale_spaces)

@@ -23,7 +23,7 @@ import pandas as pd
 import torch
 
 from powergridworld_amd import _lib
-from powergridworld_amd.base import MultiComponentEnv, as_action, oob_poll, register_env
+from powergridworld_amd.base import MultiComponentEnv, as_action, as_env_tensor, oob_poll, register_env
 
 
 # device_custom_info keys of each HS kind's step_meta record, in the reference's
@@ -70,6 +70,10 @@ class HSMultiComponentEnv(MultiComponentEnv):
         if len(set(kinds)) != len(kinds):
             raise ValueError("each HS component kind may appear once")
         if kinds[0] != 0:
+            # meta_state pv_power is None until the PV's first step (base_hs.py:58):
+            # in the reference a component ahead of the PV raises TypeError in its
+            # first reset / step (the EV's reset step and every step_meta subtract
+            # from it); the order after the PV is free
             raise NotImplementedError("the HS chain must start with the PV (it sets pv_power)")
         self._kinds = kinds
         self._by_kind = {k: e for k, e in zip(kinds, self.envs)}
@@ -126,6 +130,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
             for j in range(p.n_dev):
                 p.dev_obs_high[j] = dv.obs_high[j]
         p.max_grid_power = float(self.max_grid_power)
+        p.pv_grid_aware = int(bool(pv is not None and pv.grid_aware))
         self.params = p
         self._bind_oob(self.oob_count)
 
@@ -141,6 +146,10 @@ class HSMultiComponentEnv(MultiComponentEnv):
         self._ev_cost = torch.zeros(n, **f64)
         self._dev_cost = torch.zeros(n, **f64)
         self._es_last = torch.zeros(n, **f64)       # meta_state es_power = 0.0 (base_hs.py:59)
+        # meta_state pv_power (base_hs.py:58: None until the PV's first step; NaN here):
+        # carried from step to step, so components ahead of the PV see the last one
+        self._pv_last = torch.full((n,), float("nan"), **f64)
+        self._mv_state = None          # meta_state min_voltage (set by the first step)
         self._reward = torch.zeros(n, **f64)
         self._meta = torch.zeros((3, n), **f64)
         self._init_soc = torch.zeros(n, **f64)
@@ -151,6 +160,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
         b.ev_req, b.ev_charging = self._ev_req.data_ptr(), self._ev_chg.data_ptr()
         b.ev_cost, b.dev_cost = self._ev_cost.data_ptr(), self._dev_cost.data_ptr()
         b.es_power_last = self._es_last.data_ptr()
+        b.pv_power_last = self._pv_last.data_ptr()
         b.reward, b.real_power = self._reward.data_ptr(), self._real_power.data_ptr()
         b.meta_out = self._meta.data_ptr()
         self._step_meta = None
@@ -228,12 +238,34 @@ class HSMultiComponentEnv(MultiComponentEnv):
             ev.time_index = 0
             ev.time = t0 = ev.simulation_times[0]
         s = self._info(t0, t0)
+        self._bind_min_voltage(kwargs)
         _lib.check(_lib.lib().pgw_hs_reset(self.params, s, self.num_envs, _lib.dptr(self._init_soc),
                                            self._bufs, self._stream()))
         if ev is not None:
             ev.time = ev.simulation_times[ev.time_index]
             ev.time_index += 1
         return self.get_obs(**kwargs)[0]
+
+    def _bind_min_voltage(self, kwargs, stepping=False):
+        """The grid-aware PV's min_voltage (pv_profile_env_hs.py:110-111 reads
+        kwargs["min_voltage"]), as the reference's house delivers it: the PV
+        gets the step's keywords UPDATED WITH meta_state (base_hs.py:130-132),
+        and its returned meta -- the keywords it saw, min_voltage included --
+        is merged into meta_state (:147-153).  So the first step's min_voltage
+        stays in meta_state and every later reset and step observes that value,
+        whatever is passed then; before the first step the keyword is used.
+        (Pinned by the reference's own run, tests/golden/hs_order.npz.)"""
+        if not self.params.pv_grid_aware:
+            return
+        mv = self._mv_state
+        if mv is None:
+            if "min_voltage" not in kwargs:
+                raise KeyError("min_voltage (the grid-aware HSPVEnv observes it)")
+            mv = as_env_tensor(kwargs["min_voltage"], self.num_envs, self.device, "min_voltage").clone()
+            if stepping:
+                self._mv_state = mv
+        self._mv_hold = mv
+        self._bufs.min_voltage = mv.data_ptr()
 
     def get_obs(self, **kwargs):
         return {e.name: e._obs for e in self.envs}, {}
@@ -273,6 +305,7 @@ class HSMultiComponentEnv(MultiComponentEnv):
         if ev is not None:
             ev_time, ev_next = ev.time, ev.simulation_times[ev.time_index]
         s = self._info(ev_time, ev_next)
+        self._bind_min_voltage(kwargs, stepping=True)
         _lib.check(_lib.lib().pgw_hs_step(self.params, s, self.num_envs, self._bufs, self._stream()))
         dones = []
         for k, e in zip(self._kinds, self.envs):

@@ -39,10 +39,12 @@ struct HSRec {
 
 // HSPVEnv (pv_profile_env_hs.py:96-160): obs before the advance; the curtailed
 // power a * data[index] becomes meta_state pv_power (rew_meta, :146).
+// Grid-aware (:81-85, 110-111): min_voltage appended to the obs, box (0.9, 1.1).
 __device__ __forceinline__ void hs_pv(const pgw_hs_params& p, const pgw_hs_step_info& s, int rescale,
-                                      bool reset, double a, HSMeta& M, double& rp, double* ob,
+                                      bool reset, double a, double vmin, HSMeta& M, double& rp, double* ob,
                                       const HSRec& R) {
   ob[0] = rescale ? to_scaled(-s.pv_avail, p.pv_obs_low, 0.0) : -s.pv_avail;
+  ob[1] = rescale ? to_scaled(vmin, 0.9, 1.1) : vmin;
   if (reset) {
     M.pv = s.pv_avail;   // get_obs meta pv_power (:118-121)
     return;
@@ -267,7 +269,7 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p_, pgw_hs_step_inf
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
   HSMeta M;
-  M.pv = 0.0;
+  M.pv = b.pv_power_last ? b.pv_power_last[e] : 0.0;   // meta_state carried over (None = NaN)
   M.es = b.es_power_last[e];
   M.grid = p.max_grid_power;
   HSState S = {};
@@ -289,8 +291,9 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p_, pgw_hs_step_inf
     S.rp[c] = 0.0;
     switch (p.kind[c]) {
       case PGW_HS_PV:
-        hs_pv(p, s, p.rescale[c], reset, a, M, S.rp[c], ob, R);
+        hs_pv(p, s, p.rescale[c], reset, a, p.pv_grid_aware ? b.min_voltage[e] : 0.0, M, S.rp[c], ob, R);
         st(b.obs, e, off, ob[0]);
+        if (p.pv_grid_aware) st(b.obs, e, off + 1, ob[1]);
         break;
       case PGW_HS_STORAGE:
         if (!reset) hs_storage(p, s, p.rescale[c], a, M, S, S.rp[c], R);
@@ -339,6 +342,7 @@ __global__ void __launch_bounds__(kBlock) k_hs(pgw_hs_params p_, pgw_hs_step_inf
   b.real_power[e] = rp;
   b.reward[e] = rew;
   b.es_power_last[e] = M.es;
+  if (b.pv_power_last) b.pv_power_last[e] = M.pv;
   if (b.meta_out) {
     b.meta_out[e] = M.pv;
     b.meta_out[n + e] = M.es;
@@ -360,6 +364,8 @@ static int32_t hs_check(const pgw_hs_params* p, const pgw_hs_step_info* s, int64
   PGW_REQUIRE(b.obs.ptr && b.soc && b.soc_cost && b.ev_cost && b.dev_cost && b.es_power_last,
               "pgw_hs: null buffer");
   PGW_REQUIRE(!(seen & (1 << PGW_HS_EV)) || (b.ev_req && b.ev_charging), "pgw_hs: null EV buffer");
+  PGW_REQUIRE(!p->pv_grid_aware || ((seen & (1 << PGW_HS_PV)) && b.min_voltage),
+              "pgw_hs: the grid-aware PV needs min_voltage");
   return PGW_OK;
 }
 
