@@ -123,6 +123,12 @@ int32_t pgw_pv_obs(const pgw_pv_params* p, int64_t n, double pmax, const double*
 /* obs (pre-advance, :143) and real_power = to_raw(a,0,1) * (-pmax) (:144). */
 int32_t pgw_pv_step(const pgw_pv_params* p, int64_t n, double pmax, pgw_mat action,
                     const double* min_voltage, pgw_mat obs, double* real_power, void* stream);
+/* fp32 storage (obs, action, real power), fp64 arithmetic; min_voltage stays
+ * the fp64 power-flow output. */
+int32_t pgw_pv_obs_f32(const pgw_pv_params* p, int64_t n, double pmax, const double* min_voltage,
+                       pgw_matf obs, void* stream);
+int32_t pgw_pv_step_f32(const pgw_pv_params* p, int64_t n, double pmax, pgw_matf action,
+                        const double* min_voltage, pgw_matf obs, float* real_power, void* stream);
 
 /* ------------------------------------------------------------------------
  * Five-zone reduced-order building.  Replaces FiveZoneROMEnv.reset/step_/get_obs
@@ -199,6 +205,15 @@ int32_t pgw_building_step(const pgw_building_params* p, const pgw_building_exo* 
                           const pgw_building_exo* ex_next, int64_t n, pgw_mat action, double* x,
                           double* p_consumed, double* reward_out, double* reward_state,
                           int32_t lagged, pgw_building_ext ext, pgw_mat obs, void* stream);
+/* fp32 storage of the state (x, p_consumed, rewards), obs and actions; fp64
+ * arithmetic, each value rounded once at its store. */
+int32_t pgw_building_reset_f32(const pgw_building_params* p, const pgw_building_exo* ex0, int64_t n,
+                               float* x, float* p_consumed, float* reward_state,
+                               pgw_building_ext ext, pgw_matf obs, void* stream);
+int32_t pgw_building_step_f32(const pgw_building_params* p, const pgw_building_exo* ex_t,
+                              const pgw_building_exo* ex_next, int64_t n, pgw_matf action, float* x,
+                              float* p_consumed, float* reward_out, float* reward_state,
+                              int32_t lagged, pgw_building_ext ext, pgw_matf obs, void* stream);
 
 /* ------------------------------------------------------------------------
  * EV charging station.  Replaces EVChargingEnv.reset/step/step_reward
@@ -253,6 +268,15 @@ int32_t pgw_ev_reset_tables(const pgw_ev_params* p, int64_t n, const double* req
 int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
                     const double* endp, double* req, uint64_t* charging, pgw_mat obs,
                     double* real_power, double* reward, void* stream);
+/* fp32 storage of the requirements, obs, actions, real power and reward;
+ * fp64 arithmetic (the parked masks, the vehicle tables and req0 as above). */
+int32_t pgw_ev_reset_f32(const pgw_ev_params* p, int64_t n, const double* req0, float* req,
+                         uint64_t* charging, void* stream);
+int32_t pgw_ev_reset_tables_f32(const pgw_ev_params* p, int64_t n, const double* req0_env, float* req,
+                                uint64_t* charging, void* stream);
+int32_t pgw_ev_step_f32(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_matf action,
+                        const double* endp, float* req, uint64_t* charging, pgw_matf obs,
+                        float* real_power, float* reward, void* stream);
 
 /* ------------------------------------------------------------------------
  * MultiComponentEnv reduction (gridworld/base.py:125-156): real_power and

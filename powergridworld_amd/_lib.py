@@ -271,6 +271,14 @@ _SIGS = {
                                 vp, vp, i32, BuildingExt, Mat, vp]),
     "pgw_ev_reset": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
     "pgw_ev_reset_tables": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
+    "pgw_pv_obs_f32": (i32, [P(PVParams), i64, f64, vp, Matf, vp]),
+    "pgw_pv_step_f32": (i32, [P(PVParams), i64, f64, Matf, vp, Matf, vp, vp]),
+    "pgw_building_reset_f32": (i32, [P(BuildingParams), P(BuildingExo), i64, vp, vp, vp, BuildingExt, Matf, vp]),
+    "pgw_building_step_f32": (i32, [P(BuildingParams), P(BuildingExo), P(BuildingExo), i64, Matf, vp, vp, vp, vp,
+                                    i32, BuildingExt, Matf, vp]),
+    "pgw_ev_reset_f32": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
+    "pgw_ev_reset_tables_f32": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
+    "pgw_ev_step_f32": (i32, [P(EVParams), P(EVStepInfo), i64, Matf, vp, vp, vp, Matf, vp, vp, vp]),
     "pgw_ev_step": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),

@@ -141,13 +141,14 @@ class FiveZoneROMEnv(ComponentEnv):
 
     fused_kind = None           # only the ThermalEnergy reward is fused
     reward_kind = "viol"
+    supported_dtypes = (torch.float64, torch.float32)    # fp32: pgw_building_*_f32
 
     def __init__(self, name: str = None, obs_config: dict = None,
                  start_time: Union[str, pd.Timestamp] = None, end_time: Union[str, pd.Timestamp] = None,
                  comfort_bounds=None, zone_temp_init: np.ndarray = None, max_episode_steps: int = None,
                  rescale_spaces: bool = True, exogenous_data=None, num_envs: int = 1, device=None,
-                 **kwargs):
-        super().__init__(name=name, num_envs=num_envs, device=device)
+                 dtype=None, **kwargs):
+        super().__init__(name=name, num_envs=num_envs, device=device, dtype=dtype)
         self.rescale_spaces = rescale_spaces
         self.num_zones = 5
         self.obs_config = obs_config if obs_config is not None else default_obs_config
@@ -169,10 +170,10 @@ class FiveZoneROMEnv(ComponentEnv):
         self._bind_oob(self.oob_count)
         n = self.num_envs
         x0 = np.array([float(np.ravel(m["x_k"])[0]) for m in self.models])
-        self.x = torch.tensor(np.tile(x0[:, None], (1, n)), dtype=torch.float64, device=self.device)
-        self.p_consumed = torch.zeros(n, dtype=torch.float64, device=self.device)
-        self._reward_state = torch.zeros(n, dtype=torch.float64, device=self.device)
-        self._reward_out = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self.x = torch.tensor(np.tile(x0[:, None], (1, n)), dtype=self.dtype, device=self.device)
+        self.p_consumed = torch.zeros(n, dtype=self.dtype, device=self.device)
+        self._reward_state = torch.zeros(n, dtype=self.dtype, device=self.device)
+        self._reward_out = torch.zeros(n, dtype=self.dtype, device=self.device)
         self._obs = self._new_obs(len(self._obs_labels))
         self.time_index = None
 
@@ -269,16 +270,16 @@ class FiveZoneROMEnv(ComponentEnv):
         self.time_index = 0
         oob_poll(self.oob_count)
         ext, keep = self._ext(obs_kwargs)
-        _lib.check(_lib.lib().pgw_building_reset(
+        _lib.check(self._kernel("pgw_building_reset")(
             self.params, self._exo[0], self.num_envs, _lib.dptr(self.x), _lib.dptr(self.p_consumed),
-            _lib.dptr(self._reward_state), ext, _lib.mat(self._obs), self._stream()))
+            _lib.dptr(self._reward_state), ext, self._mat(self._obs), self._stream()))
         self._prev_viol_reward = None
         return self._obs
 
     def step(self, action, **obs_kwargs):
         """(:183-225).  Standalone: returns the reward of the PREVIOUS state (:215);
         inside a MultiComponentEnv the reward is the fresh one (base.py:137)."""
-        a = as_action(action, self.num_envs, 6, self.device)
+        a = as_action(action, self.num_envs, 6, self.device, self.dtype)
         t = self.time_index
         if t + 1 >= len(self._exo):
             raise IndexError("building stepped past the end of its exogenous data")
@@ -286,10 +287,10 @@ class FiveZoneROMEnv(ComponentEnv):
         lagged = 0 if self._in_multicomponent else 1
         if self.reward_kind == "viol":
             prev = self._viol_reward()
-        _lib.check(_lib.lib().pgw_building_step(
-            self.params, self._exo[t], self._exo[t + 1], self.num_envs, _lib.mat(a),
+        _lib.check(self._kernel("pgw_building_step")(
+            self.params, self._exo[t], self._exo[t + 1], self.num_envs, self._mat(a),
             _lib.dptr(self.x), _lib.dptr(self.p_consumed), _lib.dptr(self._reward_out),
-            _lib.dptr(self._reward_state), lagged, ext, _lib.mat(self._obs), self._stream()))
+            _lib.dptr(self._reward_state), lagged, ext, self._mat(self._obs), self._stream()))
         self.time_index += 1
         rew = self._reward_out
         if self.reward_kind == "viol":

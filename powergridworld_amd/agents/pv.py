@@ -33,11 +33,12 @@ class PVEnv(ComponentEnv):
 
     fused_kind = "pv"
     index: int = None
+    supported_dtypes = (torch.float64, torch.float32)    # fp32: pgw_pv_*_f32
 
     def __init__(self, name: str = None, profile_csv: str = None, profile_path: str = None,
                  scaling_factor: float = 1., rescale_spaces: bool = True, grid_aware: bool = False,
-                 max_episode_steps: int = None, num_envs: int = 1, device=None, **kwargs):
-        super().__init__(name=name, num_envs=num_envs, device=device)
+                 max_episode_steps: int = None, num_envs: int = 1, device=None, dtype=None, **kwargs):
+        super().__init__(name=name, num_envs=num_envs, device=device, dtype=dtype)
         self.scaling_factor = scaling_factor
         self.rescale_spaces = rescale_spaces
         self.grid_aware = grid_aware
@@ -77,8 +78,8 @@ class PVEnv(ComponentEnv):
     def get_obs(self, **kwargs):
         """Max real power available at the current profile row (:102-114)."""
         vmin = self._min_voltage(kwargs)
-        _lib.check(_lib.lib().pgw_pv_obs(self.params, self.num_envs, float(self.data[self.index]),
-                                         _lib.dptr(vmin), _lib.mat(self._obs), self._stream()))
+        _lib.check(self._kernel("pgw_pv_obs")(self.params, self.num_envs, float(self.data[self.index]),
+                                              _lib.dptr(vmin), self._mat(self._obs), self._stream()))
         return self._obs, {"real_power": float(-self.data[self.index])}
 
     mc_kind = 1
@@ -125,11 +126,11 @@ class PVEnv(ComponentEnv):
 
     def step(self, action, **kwargs):
         """Obs of the current row, then curtailment, then advance (:133-148)."""
-        a = as_action(action, self.num_envs, 1, self.device)
+        a = as_action(action, self.num_envs, 1, self.device, self.dtype)
         vmin = self._min_voltage(kwargs)
         c = self.__dict__.get("_step_c")
         if c is None or c[0] != self._bufv:           # per-layout constants, built once
-            c = self._step_c = (self._bufv, _lib.lib().pgw_pv_step, _lib.mat(self._obs),
+            c = self._step_c = (self._bufv, self._kernel("pgw_pv_step"), self._mat(self._obs),
                                 _lib.dptr(self._real_power), [float(x) for x in self.data])
         pmax = c[4][self.index]
         _lib.check(c[1](self.params, self.num_envs, pmax, self._act_mat(a), _lib.dptr(vmin), c[2], c[3],

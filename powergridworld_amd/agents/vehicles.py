@@ -45,13 +45,15 @@ class EVChargingEnv(ComponentEnv):
 
     fused_kind = None
 
+    supported_dtypes = (torch.float64, torch.float32)    # fp32: pgw_ev_*_f32
+
     def __init__(self, num_vehicles: int = 100, minutes_per_step: int = 5,
                  max_charge_rate_kw: float = 7.0, max_episode_steps: int = None,
                  unserved_penalty: float = 1., peak_penalty: float = 1., peak_threshold: float = 10.,
                  reward_scale: float = 1e5, name: str = None, randomize: bool = False,
                  vehicle_csv: str = None, vehicle_multiplier: int = 1, rescale_spaces: bool = True,
-                 num_envs: int = 1, device=None, **kwargs):
-        super().__init__(name=name, num_envs=num_envs, device=device)
+                 num_envs: int = 1, device=None, dtype=None, **kwargs):
+        super().__init__(name=name, num_envs=num_envs, device=device, dtype=dtype)
         self.num_vehicles = num_vehicles
         self.max_charge_rate_kw = max_charge_rate_kw
         self.minutes_per_step = minutes_per_step
@@ -108,7 +110,7 @@ class EVChargingEnv(ComponentEnv):
         self._bind_oob(self.oob_count)
         n, V = self.num_envs, self.num_vehicles
         self._words = (V + 63) // 64
-        self.req = torch.zeros((max(V, 1), n), dtype=torch.float64, device=self.device)
+        self.req = torch.zeros((max(V, 1), n), dtype=self.dtype, device=self.device)
         self.charging = torch.zeros((max(self._words, 1), n), dtype=torch.int64, device=self.device)
         self._req0_dev = torch.tensor(self._req0, dtype=torch.float64, device=self.device)
         self._endp_dev = torch.tensor(endp.astype(np.float64), dtype=torch.float64, device=self.device)
@@ -136,7 +138,7 @@ class EVChargingEnv(ComponentEnv):
             self.vehicle_ids = torch.zeros((n, V), dtype=torch.int64, device=self.device)
             self._gen = torch.Generator(device=self.device)
             self.seed(None)
-        self._reward = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self._reward = torch.zeros(n, dtype=self.dtype, device=self.device)
         self._obs = self._new_obs(6)
         self.time_index = None
         self.time = None
@@ -179,11 +181,11 @@ class EVChargingEnv(ComponentEnv):
 
     def _advance(self, action):
         s = self._step_info(action is not None)
-        a = _lib.mat(as_action(action, self.num_envs, 1, self.device)) if action is not None \
-            else _lib.Mat(None, 0, 0)
-        _lib.check(_lib.lib().pgw_ev_step(
+        a = self._mat(as_action(action, self.num_envs, 1, self.device, self.dtype)) if action is not None \
+            else self._mat(None)
+        _lib.check(self._kernel("pgw_ev_step")(
             self.params, s, self.num_envs, a, _lib.dptr(self._endp_dev), _lib.dptr(self.req),
-            _lib.dptr(self.charging), _lib.mat(self._obs), _lib.dptr(self._real_power),
+            _lib.dptr(self.charging), self._mat(self._obs), _lib.dptr(self._real_power),
             _lib.dptr(self._reward), self._stream()))
         self.time_index += 1
         self.time = self.simulation_times[self.time_index]
@@ -250,15 +252,15 @@ class EVChargingEnv(ComponentEnv):
         oob_poll(self.oob_count)
         if self.randomize:
             self._sample_vehicles(vehicle_ids)
-            _lib.check(_lib.lib().pgw_ev_reset_tables(self.params, self.num_envs, _lib.dptr(self._req0_env),
-                                                      _lib.dptr(self.req), _lib.dptr(self.charging),
-                                                      self._stream()))
+            _lib.check(self._kernel("pgw_ev_reset_tables")(self.params, self.num_envs, _lib.dptr(self._req0_env),
+                                                           _lib.dptr(self.req), _lib.dptr(self.charging),
+                                                           self._stream()))
         else:
             if vehicle_ids is not None:
                 raise ValueError("vehicle_ids needs randomize=True")
-            _lib.check(_lib.lib().pgw_ev_reset(self.params, self.num_envs, _lib.dptr(self._req0_dev),
-                                               _lib.dptr(self.req), _lib.dptr(self.charging),
-                                               self._stream()))
+            _lib.check(self._kernel("pgw_ev_reset")(self.params, self.num_envs, _lib.dptr(self._req0_dev),
+                                                    _lib.dptr(self.req), _lib.dptr(self.charging),
+                                                    self._stream()))
         self._advance(None)
         return self._obs, {}
 

@@ -147,6 +147,15 @@ class ComponentEnv(spaces.Env, ABC):
     def _stream(self):
         return _lib.stream_ptr(self.device)
 
+    def _mat(self, t2d):
+        """pgw_mat / pgw_matf of one of this env's [N, dim] buffers (its dtype;
+        None: the null matrix)."""
+        return (_lib.matf if self.dtype == torch.float32 else _lib.mat)(t2d)
+
+    def _kernel(self, name):
+        """The ABI entry for this env's storage dtype (name + "_f32" for fp32)."""
+        return getattr(_lib.lib(), name + ("_f32" if self.dtype == torch.float32 else ""))
+
     # ---- per-step host-cost caches ------------------------------------------
     # _bufv counts re-pointings of the env's device buffers (_adopt): cached
     # launch arguments that hold their pointers are rebuilt when it changes.

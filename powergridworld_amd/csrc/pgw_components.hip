@@ -65,8 +65,10 @@ __global__ void __launch_bounds__(kBlock) k_battery_step(pgw_battery_params p, i
 
 // ====================================================================== PV
 // One env's PVEnv obs (+ step when act.ptr): obs first (pre-advance, :143).
-__device__ __forceinline__ double pv_step_env(const pgw_pv_params& p, int64_t e, double pmax, const pgw_mat& act,
-                                              const double* __restrict__ vmin, const pgw_mat& obs) {
+// Mt = pgw_mat or pgw_matf (the _f32 entries: fp32 storage, fp64 arithmetic).
+template <class Mt>
+__device__ __forceinline__ double pv_step_env(const pgw_pv_params& p, int64_t e, double pmax, const Mt& act,
+                                              const double* __restrict__ vmin, const Mt& obs) {
   st(obs, e, 0, pv_obs(p, pmax));
   if (p.grid_aware) {
     double v = vmin[e];
@@ -75,21 +77,23 @@ __device__ __forceinline__ double pv_step_env(const pgw_pv_params& p, int64_t e,
   return act.ptr ? pv_real_power(p, ld(act, e, 0), pmax) : 0.0;
 }
 
-__global__ void __launch_bounds__(kBlock) k_pv(pgw_pv_params p, int64_t n, double pmax, pgw_mat act,
-                                               const double* __restrict__ vmin, pgw_mat obs,
-                                               double* __restrict__ rp) {
+template <class S, class Mt>
+__global__ void __launch_bounds__(kBlock) k_pv(pgw_pv_params p, int64_t n, double pmax, Mt act,
+                                               const double* __restrict__ vmin, Mt obs,
+                                               S* __restrict__ rp) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
   const double r = pv_step_env(p, e, pmax, act, vmin, obs);
-  if (rp) rp[e] = r;
+  if (rp) rp[e] = (S)r;
 }
 
 // ====================================================================== building
+template <class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p, pgw_building_exo ex0,
-                                                           int64_t n, double* __restrict__ x,
-                                                           double* __restrict__ pcons,
-                                                           double* __restrict__ rstate,
-                                                           pgw_building_ext ext, pgw_mat obs) {
+                                                           int64_t n, S* __restrict__ x,
+                                                           S* __restrict__ pcons,
+                                                           S* __restrict__ rstate,
+                                                           pgw_building_ext ext, Mt obs) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
   double xs[5], T[5];
@@ -110,25 +114,25 @@ __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p
   }
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
-    x[z * n + e] = xs[z];
+    x[z * n + e] = (S)xs[z];
     T[z] = p.C[z] * xs[z] + p.mean[z];               // temp_dynamics (dynamics.py:75-85)
   }
-  pcons[e] = 0.0;
+  pcons[e] = (S)0.0;
   BuildingExt xv = building_ext(ext, e);
   building_write_obs(p, T, ex0, 0.0, xv, [&](int j, double v) { st(obs, e, j, v); });
-  if (rstate) rstate[e] = building_reward(p, T, ex0.comfort_lb, ex0.comfort_ub, 0.0);
+  if (rstate) rstate[e] = (S)building_reward(p, T, ex0.comfort_lb, ex0.comfort_ub, 0.0);
 }
 
 // One env's FiveZoneROMEnv.step_ (:183-225); returns p_consumed (its real power).
 // STD: the reference's default model/obs layout (bld_is_std), via bld_std_step.
-template <bool STD>
+template <bool STD, class S = double, class Mt = pgw_mat>
 __device__ __forceinline__ double building_step_env(const pgw_building_params& p, const BldDerived& d,
                                                     const pgw_building_exo& ex,
                                                     const pgw_building_exo& exn, int64_t n, int64_t e,
-                                                    const pgw_mat& act, double* __restrict__ x,
-                                                    double* __restrict__ pcons, double* __restrict__ rout,
-                                                    double* __restrict__ rstate, int32_t lagged,
-                                                    const pgw_building_ext& ext, const pgw_mat& obs) {
+                                                    const Mt& act, S* __restrict__ x,
+                                                    S* __restrict__ pcons, S* __restrict__ rout,
+                                                    S* __restrict__ rstate, int32_t lagged,
+                                                    const pgw_building_ext& ext, const Mt& obs) {
   if constexpr (STD) {
     double av[6], xs[5], fresh;
 #pragma unroll
@@ -137,10 +141,10 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
     for (int z = 0; z < 5; ++z) xs[z] = x[z * n + e];
     const double pc = bld_std_step(p, d, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); });
 #pragma unroll
-    for (int z = 0; z < 5; ++z) x[z * n + e] = xs[z];
-    pcons[e] = pc;
-    if (rout) rout[e] = lagged ? rstate[e] : fresh;
-    if (rstate) rstate[e] = fresh;
+    for (int z = 0; z < 5; ++z) x[z * n + e] = (S)xs[z];
+    pcons[e] = (S)pc;
+    if (rout) rout[e] = lagged ? rstate[e] : (S)fresh;
+    if (rstate) rstate[e] = (S)fresh;
     return pc;
   }
   double a[6], xs[5], T[5];
@@ -160,54 +164,56 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
   building_state_update(p, ex, T, a, xs);
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
-    x[z * n + e] = xs[z];
+    x[z * n + e] = (S)xs[z];
     T[z] = p.C[z] * xs[z] + p.mean[z];
   }
   double pc = building_p_consumed(a, ex.T_oa);
-  pcons[e] = pc;
+  pcons[e] = (S)pc;
   double fresh = building_reward(p, T, exn.comfort_lb, exn.comfort_ub, pc);
-  if (rout) rout[e] = lagged ? rstate[e] : fresh;
-  if (rstate) rstate[e] = fresh;
+  if (rout) rout[e] = lagged ? rstate[e] : (S)fresh;
+  if (rstate) rstate[e] = (S)fresh;
   BuildingExt xv = building_ext(ext, e);
   building_write_obs(p, T, exn, pc, xv, [&](int j, double v) { st(obs, e, j, v); });
   return pc;
 }
 
-template <bool STD>
+template <bool STD, class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_building_step(pgw_building_params p_, BldDerived d,
                                                           pgw_building_exo ex,
-                                                          pgw_building_exo exn, int64_t n, pgw_mat act,
-                                                          double* __restrict__ x,
-                                                          double* __restrict__ pcons,
-                                                          double* __restrict__ rout,
-                                                          double* __restrict__ rstate, int32_t lagged,
-                                                          pgw_building_ext ext, pgw_mat obs) {
+                                                          pgw_building_exo exn, int64_t n, Mt act,
+                                                          S* __restrict__ x,
+                                                          S* __restrict__ pcons,
+                                                          S* __restrict__ rout,
+                                                          S* __restrict__ rstate, int32_t lagged,
+                                                          pgw_building_ext ext, Mt obs) {
   const pgw_building_params& p = PGW_KERNARG0(pgw_building_params);   // (no private copy)
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  (void)building_step_env<STD>(p, d, ex, exn, n, e, act, x, pcons, rout, rstate, lagged, ext, obs);
+  (void)building_step_env<STD, S, Mt>(p, d, ex, exn, n, e, act, x, pcons, rout, rstate, lagged, ext, obs);
 }
 
 // ====================================================================== EV
+template <class S>
 __global__ void __launch_bounds__(kBlock) k_ev_reset(int64_t n, int32_t V, int32_t W,
                                                      const double* __restrict__ req0,
-                                                     double* __restrict__ req,
+                                                     S* __restrict__ req,
                                                      uint64_t* __restrict__ chg) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  for (int v = 0; v < V; ++v) req[(int64_t)v * n + e] = req0[v];
+  for (int v = 0; v < V; ++v) req[(int64_t)v * n + e] = (S)req0[v];
   for (int w = 0; w < W; ++w) chg[(int64_t)w * n + e] = 0ull;
 }
 
 // randomize=True (ev_charging_env.py:154-156): every env restores its own
 // sampled vehicles' requirements.
+template <class S>
 __global__ void __launch_bounds__(kBlock) k_ev_reset_tables(int64_t n, int32_t V, int32_t W,
                                                             const double* __restrict__ req0,
-                                                            double* __restrict__ req,
+                                                            S* __restrict__ req,
                                                             uint64_t* __restrict__ chg) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  for (int v = 0; v < V; ++v) req[(int64_t)v * n + e] = req0[(int64_t)v * n + e];
+  for (int v = 0; v < V; ++v) req[(int64_t)v * n + e] = (S)req0[(int64_t)v * n + e];
   for (int w = 0; w < W; ++w) chg[(int64_t)w * n + e] = 0ull;
 }
 
@@ -220,12 +226,12 @@ __global__ void __launch_bounds__(kBlock) k_ev_reset_tables(int64_t n, int32_t V
 // 2 = time left divided in the kernel.  Instantiated per mode so the vehicle
 // loop carries no per-vehicle branch and no unused IEEE division.
 enum { kEvTable = 0, kEvPerEnv = 1, kEvDivide = 2 };
-template <int MODE>
+template <int MODE, class S, class Mt>
 __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
-                                             int64_t e, const pgw_mat& act, const double* __restrict__ endp,
-                                             double* __restrict__ req, uint64_t* __restrict__ chg,
-                                             const pgw_mat& obs, double* __restrict__ rp,
-                                             double* __restrict__ rew) {
+                                             int64_t e, const Mt& act, const double* __restrict__ endp,
+                                             S* __restrict__ req, uint64_t* __restrict__ chg,
+                                             const Mt& obs, S* __restrict__ rp,
+                                             S* __restrict__ rew) {
   double a = act.ptr ? ld(act, e, 0) : s.action_default;
   if (p.rescale) {
     oob_note(p.oob, oob_bad(a));
@@ -268,7 +274,7 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
       for (int i = 0; i < kEvChunk; ++i) {
         const int b = m ? __builtin_ctzll(m) : 0;    // past the chunk's end: a harmless reload
         const int v = w * 64 + b;
-        C.rs[i] = req[(int64_t)v * n + e];
+        C.rs[i] = (double)req[(int64_t)v * n + e];
         if constexpr (MODE == kEvPerEnv) {       // randomize: this env's own vehicle table
           const double en = s.env_endp[(int64_t)v * n + e];
           C.tls[i] = (en - s.time) / 60.0;
@@ -312,7 +318,7 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
         // under a branch leaves the compiler no static count of outstanding
         // memory operations, and it then waits for all of them (vmcnt(0)),
         // stores included, before every later load's use
-        if (in) req[(int64_t)v * n + e] = chg_now[i] ? r - cv[i] : r;
+        if (in) req[(int64_t)v * n + e] = (S)(chg_now[i] ? r - cv[i] : r);
       }
       m = C.bits;
 #pragma unroll
@@ -351,33 +357,35 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
   st_[3] = p.mult * demand;
   st_[4] = dcnt ? dsum / (double)dcnt : 0.0;
   st_[5] = unserved;
-  rp[e] = p.mult * consumed;                         // :255
+  rp[e] = (S)(p.mult * consumed);                    // :255
   // step_reward :135-142
   double ur = -p.u_pen * (st_[5] * st_[5]);
   double pk = pymax(0.0, st_[2] - p.thr);
   double pr = -p.p_pen * (pk * pk);
-  rew[e] = (ur + pr) / p.reward_scale;
+  rew[e] = (S)((ur + pr) / p.reward_scale);
 #pragma unroll
   for (int j = 0; j < 6; ++j)
     st(obs, e, j, p.rescale ? to_scaled(st_[j], p.obs_low[j], p.obs_high[j]) : st_[j]);
 }
 
+template <class S, class Mt>
 __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
-                                            int64_t e, const pgw_mat& act, const double* __restrict__ endp,
-                                            double* __restrict__ req, uint64_t* __restrict__ chg,
-                                            const pgw_mat& obs, double* __restrict__ rp,
-                                            double* __restrict__ rew) {
+                                            int64_t e, const Mt& act, const double* __restrict__ endp,
+                                            S* __restrict__ req, uint64_t* __restrict__ chg,
+                                            const Mt& obs, S* __restrict__ rp,
+                                            S* __restrict__ rew) {
   if (s.env_start) ev_step_mode<kEvPerEnv>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
   else if (s.tl_rcp) ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
   else ev_step_mode<kEvDivide>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
 }
 
+template <class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step_info s, int64_t n,
-                                                    pgw_mat act, const double* __restrict__ endp,
-                                                    double* __restrict__ req,
-                                                    uint64_t* __restrict__ chg, pgw_mat obs,
-                                                    double* __restrict__ rp,
-                                                    double* __restrict__ rew) {
+                                                    Mt act, const double* __restrict__ endp,
+                                                    S* __restrict__ req,
+                                                    uint64_t* __restrict__ chg, Mt obs,
+                                                    S* __restrict__ rp,
+                                                    S* __restrict__ rew) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
   ev_step_env(p, s, n, e, act, endp, req, chg, obs, rp, rew);
@@ -391,7 +399,7 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const pg
                                              const BldDerived& d, int64_t n, int64_t e) {
   switch (C.kind) {
     case PGW_MC_BUILDING:
-      (void)building_step_env<STD>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
+      (void)building_step_env<STD, double, pgw_mat>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
                                    C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
       break;
     case PGW_MC_PV:
@@ -481,7 +489,7 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_a
   if (e < n) {
     if (kind0 == PGW_MC_BUILDING) {
       const pgw_mc_component& C = a.comp[c0];
-      s_rp[c0][lane] = building_step_env<STD>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
+      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
                                               C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
       s_rew[c0][lane] = a.bld_reward_state[e];        // the fresh reward (MC semantics)
     } else if (kind0 == PGW_MC_EV) {
@@ -609,14 +617,29 @@ int32_t pgw_pv_obs(const pgw_pv_params* p, int64_t n, double pmax, const double*
   PGW_REQUIRE(p && obs.ptr && n >= 0, "pgw_pv_obs: null argument");
   PGW_REQUIRE(!p->grid_aware || min_voltage, "pgw_pv_obs: grid_aware needs min_voltage");
   pgw_mat none{nullptr, 0, 0};
-  PGW_LAUNCH(k_pv, n, stream, *p, n, pmax, none, min_voltage, obs, (double*)nullptr);
+  PGW_LAUNCH((k_pv<double, pgw_mat>), n, stream, *p, n, pmax, none, min_voltage, obs, (double*)nullptr);
+}
+
+int32_t pgw_pv_obs_f32(const pgw_pv_params* p, int64_t n, double pmax, const double* min_voltage,
+                       pgw_matf obs, void* stream) {
+  PGW_REQUIRE(p && obs.ptr && n >= 0, "pgw_pv_obs_f32: null argument");
+  PGW_REQUIRE(!p->grid_aware || min_voltage, "pgw_pv_obs_f32: grid_aware needs min_voltage");
+  pgw_matf none{nullptr, 0, 0};
+  PGW_LAUNCH((k_pv<float, pgw_matf>), n, stream, *p, n, pmax, none, min_voltage, obs, (float*)nullptr);
+}
+
+int32_t pgw_pv_step_f32(const pgw_pv_params* p, int64_t n, double pmax, pgw_matf action,
+                        const double* min_voltage, pgw_matf obs, float* real_power, void* stream) {
+  PGW_REQUIRE(p && action.ptr && obs.ptr && real_power && n >= 0, "pgw_pv_step_f32: null argument");
+  PGW_REQUIRE(!p->grid_aware || min_voltage, "pgw_pv_step_f32: grid_aware needs min_voltage");
+  PGW_LAUNCH((k_pv<float, pgw_matf>), n, stream, *p, n, pmax, action, min_voltage, obs, real_power);
 }
 
 int32_t pgw_pv_step(const pgw_pv_params* p, int64_t n, double pmax, pgw_mat action,
                     const double* min_voltage, pgw_mat obs, double* real_power, void* stream) {
   PGW_REQUIRE(p && action.ptr && obs.ptr && real_power && n >= 0, "pgw_pv_step: null argument");
   PGW_REQUIRE(!p->grid_aware || min_voltage, "pgw_pv_step: grid_aware needs min_voltage");
-  PGW_LAUNCH(k_pv, n, stream, *p, n, pmax, action, min_voltage, obs, real_power);
+  PGW_LAUNCH((k_pv<double, pgw_mat>), n, stream, *p, n, pmax, action, min_voltage, obs, real_power);
 }
 
 int32_t pgw_building_reset(const pgw_building_params* p, const pgw_building_exo* ex0, int64_t n,
@@ -624,7 +647,15 @@ int32_t pgw_building_reset(const pgw_building_params* p, const pgw_building_exo*
                            pgw_building_ext ext, pgw_mat obs, void* stream) {
   PGW_REQUIRE(p && ex0 && x && p_consumed && obs.ptr && n >= 0, "pgw_building_reset: null argument");
   PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_reset: bad n_obs");
-  PGW_LAUNCH(k_building_reset, n, stream, *p, *ex0, n, x, p_consumed, reward_state, ext, obs);
+  PGW_LAUNCH((k_building_reset<double, pgw_mat>), n, stream, *p, *ex0, n, x, p_consumed, reward_state, ext, obs);
+}
+
+int32_t pgw_building_reset_f32(const pgw_building_params* p, const pgw_building_exo* ex0, int64_t n,
+                               float* x, float* p_consumed, float* reward_state,
+                               pgw_building_ext ext, pgw_matf obs, void* stream) {
+  PGW_REQUIRE(p && ex0 && x && p_consumed && obs.ptr && n >= 0, "pgw_building_reset_f32: null argument");
+  PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_reset_f32: bad n_obs");
+  PGW_LAUNCH((k_building_reset<float, pgw_matf>), n, stream, *p, *ex0, n, x, p_consumed, reward_state, ext, obs);
 }
 
 int32_t pgw_building_step(const pgw_building_params* p, const pgw_building_exo* ex_t,
@@ -637,10 +668,26 @@ int32_t pgw_building_step(const pgw_building_params* p, const pgw_building_exo* 
   PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_step: bad n_obs");
   const BldDerived d = make_bld_derived(*p);
   if (bld_is_std(*p))
-    PGW_LAUNCH(k_building_step<true>, n, stream, *p, d, *ex_t, *ex_next, n, action, x, p_consumed,
-               reward_out, reward_state, lagged, ext, obs);
-  PGW_LAUNCH(k_building_step<false>, n, stream, *p, d, *ex_t, *ex_next, n, action, x, p_consumed,
-             reward_out, reward_state, lagged, ext, obs);
+    PGW_LAUNCH((k_building_step<true, double, pgw_mat>), n, stream, *p, d, *ex_t, *ex_next, n, action, x,
+               p_consumed, reward_out, reward_state, lagged, ext, obs);
+  PGW_LAUNCH((k_building_step<false, double, pgw_mat>), n, stream, *p, d, *ex_t, *ex_next, n, action, x,
+             p_consumed, reward_out, reward_state, lagged, ext, obs);
+}
+
+int32_t pgw_building_step_f32(const pgw_building_params* p, const pgw_building_exo* ex_t,
+                              const pgw_building_exo* ex_next, int64_t n, pgw_matf action, float* x,
+                              float* p_consumed, float* reward_out, float* reward_state,
+                              int32_t lagged, pgw_building_ext ext, pgw_matf obs, void* stream) {
+  PGW_REQUIRE(p && ex_t && ex_next && action.ptr && x && p_consumed && obs.ptr && n >= 0,
+              "pgw_building_step_f32: null argument");
+  PGW_REQUIRE(!lagged || reward_state, "pgw_building_step_f32: lagged reward needs reward_state");
+  PGW_REQUIRE(p->n_obs >= 0 && p->n_obs <= PGW_BLD_MAX_OBS, "pgw_building_step_f32: bad n_obs");
+  const BldDerived d = make_bld_derived(*p);
+  if (bld_is_std(*p))
+    PGW_LAUNCH((k_building_step<true, float, pgw_matf>), n, stream, *p, d, *ex_t, *ex_next, n, action, x,
+               p_consumed, reward_out, reward_state, lagged, ext, obs);
+  PGW_LAUNCH((k_building_step<false, float, pgw_matf>), n, stream, *p, d, *ex_t, *ex_next, n, action, x,
+             p_consumed, reward_out, reward_state, lagged, ext, obs);
 }
 
 int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, double* req,
@@ -649,7 +696,16 @@ int32_t pgw_ev_reset(const pgw_ev_params* p, int64_t n, const double* req0, doub
   PGW_REQUIRE(p->n_vehicles >= 0 && p->n_vehicles <= 64 * PGW_EV_MAX_WORDS,
               "pgw_ev_reset: too many vehicles");
   int32_t W = (p->n_vehicles + 63) / 64;
-  PGW_LAUNCH(k_ev_reset, n, stream, n, p->n_vehicles, W, req0, req, charging);
+  PGW_LAUNCH(k_ev_reset<double>, n, stream, n, p->n_vehicles, W, req0, req, charging);
+}
+
+int32_t pgw_ev_reset_f32(const pgw_ev_params* p, int64_t n, const double* req0, float* req,
+                         uint64_t* charging, void* stream) {
+  PGW_REQUIRE(p && req0 && req && charging && n >= 0, "pgw_ev_reset_f32: null argument");
+  PGW_REQUIRE(p->n_vehicles >= 0 && p->n_vehicles <= 64 * PGW_EV_MAX_WORDS,
+              "pgw_ev_reset_f32: too many vehicles");
+  int32_t W = (p->n_vehicles + 63) / 64;
+  PGW_LAUNCH(k_ev_reset<float>, n, stream, n, p->n_vehicles, W, req0, req, charging);
 }
 
 int32_t pgw_ev_reset_tables(const pgw_ev_params* p, int64_t n, const double* req0_env, double* req,
@@ -658,7 +714,16 @@ int32_t pgw_ev_reset_tables(const pgw_ev_params* p, int64_t n, const double* req
   PGW_REQUIRE(p->n_vehicles >= 0 && p->n_vehicles <= 64 * PGW_EV_MAX_WORDS,
               "pgw_ev_reset_tables: too many vehicles");
   const int32_t W = (p->n_vehicles + 63) / 64;
-  PGW_LAUNCH(k_ev_reset_tables, n, stream, n, p->n_vehicles, W, req0_env, req, charging);
+  PGW_LAUNCH(k_ev_reset_tables<double>, n, stream, n, p->n_vehicles, W, req0_env, req, charging);
+}
+
+int32_t pgw_ev_reset_tables_f32(const pgw_ev_params* p, int64_t n, const double* req0_env, float* req,
+                                uint64_t* charging, void* stream) {
+  PGW_REQUIRE(p && req0_env && req && charging && n >= 0, "pgw_ev_reset_tables_f32: null argument");
+  PGW_REQUIRE(p->n_vehicles >= 0 && p->n_vehicles <= 64 * PGW_EV_MAX_WORDS,
+              "pgw_ev_reset_tables_f32: too many vehicles");
+  const int32_t W = (p->n_vehicles + 63) / 64;
+  PGW_LAUNCH(k_ev_reset_tables<float>, n, stream, n, p->n_vehicles, W, req0_env, req, charging);
 }
 
 int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
@@ -670,7 +735,21 @@ int32_t pgw_ev_step(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n
               "pgw_ev_step: n_words does not match n_vehicles");
   PGW_REQUIRE(!s->env_start == !s->env_endp && (!s->env_start || !s->tl_rcp),
               "pgw_ev_step: per-env tables need env_start and env_endp, and no tl_rcp");
-  PGW_LAUNCH(k_ev_step, n, stream, *p, *s, n, action, endp, req, charging, obs, real_power, reward);
+  PGW_LAUNCH((k_ev_step<double, pgw_mat>), n, stream, *p, *s, n, action, endp, req, charging, obs, real_power,
+             reward);
+}
+
+int32_t pgw_ev_step_f32(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_matf action,
+                        const double* endp, float* req, uint64_t* charging, pgw_matf obs,
+                        float* real_power, float* reward, void* stream) {
+  PGW_REQUIRE(p && s && endp && req && charging && obs.ptr && real_power && reward && n >= 0,
+              "pgw_ev_step_f32: null argument");
+  PGW_REQUIRE(s->n_words == (p->n_vehicles + 63) / 64 && s->n_words <= PGW_EV_MAX_WORDS,
+              "pgw_ev_step_f32: n_words does not match n_vehicles");
+  PGW_REQUIRE(!s->env_start == !s->env_endp && (!s->env_start || !s->tl_rcp),
+              "pgw_ev_step_f32: per-env tables need env_start and env_endp, and no tl_rcp");
+  PGW_LAUNCH((k_ev_step<float, pgw_matf>), n, stream, *p, *s, n, action, endp, req, charging, obs, real_power,
+             reward);
 }
 
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {

@@ -147,7 +147,102 @@ def test_f32_refuses_non_standard_layout():
     with pytest.raises(ValueError):
         CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=8, device=DEV,
                                            dtype=torch.float32, fused=False)
-    with pytest.raises(NotImplementedError):
-        PVEnv(profile_csv="pv_profile.csv", num_envs=8, device=DEV, dtype=torch.float32)
+    from powergridworld_amd.base import MultiComponentEnv
+    with pytest.raises(NotImplementedError):          # the fused / generic MC step is fp64 only
+        MultiComponentEnv(name="mc", components=make_c4_config()["agents"][0]["config"]["components"],
+                          num_envs=8, device=DEV, dtype=torch.float32)
+    assert PVEnv(profile_csv="pv_profile.csv", num_envs=8, device=DEV, dtype=torch.float32).dtype == torch.float32
     with pytest.raises(Exception):
         EnergyStorageEnv(num_envs=8, device=DEV, dtype=torch.float16)
+
+
+def _c4_component(name):
+    from powergridworld_amd.scenarios.coordinated import make_c4_config
+    comps = make_c4_config()["agents"][0]["config"]["components"]
+    c = [x for x in comps if x["name"] == name][0]
+    return c["cls"], c["config"]
+
+
+def test_pv_f32_one_step():
+    """pgw_pv_*_f32: obs and real power = RN32 of the fp64 path's, every step."""
+    cls, cfg = _c4_component("pv")
+    n = 4096
+    e32 = cls(**cfg, num_envs=n, device=DEV, dtype=torch.float32)
+    e64 = cls(**cfg, num_envs=n, device=DEV)
+    e32.reset()
+    e64.reset()
+    gen = torch.Generator(DEV).manual_seed(11)
+    assert_f32(e32._obs, e64._obs, ulps=0)
+    for t in range(200):
+        a = (torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2).float()
+        o32, _, d32, _ = e32.step(a)
+        o64, _, d64, _ = e64.step(a.double())
+        assert o32.dtype == torch.float32
+        assert_f32(o32, o64, ulps=0)
+        assert_f32(e32.real_power, e64.real_power, ulps=0)
+        assert d32 == d64
+
+
+def test_building_f32_one_step_and_episode():
+    """pgw_building_*_f32 (fp32 x_k, p_consumed, rewards, obs; fp64 arithmetic):
+    from the same fp32 state (teacher forcing) every output is RN32 of the fp64
+    path's; a free-running episode stays within the north-star fp32 bound."""
+    cls, cfg = _c4_component("building")
+    n = 2048
+    e32 = cls(**cfg, num_envs=n, device=DEV, dtype=torch.float32)
+    e64 = cls(**cfg, num_envs=n, device=DEV)
+    free = cls(**cfg, num_envs=n, device=DEV)
+    for e in (e32, e64, free):
+        e.reset()
+    assert e32.x.dtype == torch.float32
+    gen = torch.Generator(DEV).manual_seed(12)
+    for t in range(250):
+        a = (torch.rand((n, 6), dtype=torch.float64, device=DEV, generator=gen) * 2.2 - 1.1).float()
+        e64.x.copy_(e32.x)
+        e64._reward_state.copy_(e32._reward_state)
+        o32, r32, d32, _ = e32.step(a)
+        o64, r64, d64, _ = e64.step(a.double())
+        free.step(a.double())
+        assert_f32(o32, o64, ulps=0)
+        assert_f32(e32.x, e64.x, ulps=0)
+        assert_f32(e32.p_consumed, e64.p_consumed, ulps=0)
+        assert_f32(r32, r64, ulps=0)
+        assert d32 == d64
+    np.testing.assert_allclose(e32.x.double().cpu().numpy(), free.x.cpu().numpy(), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("randomize", [False, True])
+def test_ev_f32_one_step_and_episode(randomize):
+    """pgw_ev_*_f32 (fp32 requirements, obs, real power, reward): from the same
+    fp32 requirements every output is RN32 of the fp64 path's; a free-running
+    episode stays within the fp32 bound."""
+    from powergridworld_amd.agents.vehicles import EVChargingEnv
+    cfg = dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7., peak_threshold=250.,
+               vehicle_multiplier=5., rescale_spaces=True, randomize=randomize)
+    n = 2048
+    envs = [EVChargingEnv(**cfg, num_envs=n, device=DEV, dtype=dt)
+            for dt in (torch.float32, torch.float64, torch.float64)]
+    for e in envs:
+        if randomize:
+            e.seed(5)
+        e.reset()
+    e32, e64, free = envs
+    assert e32.req.dtype == torch.float32
+    if not randomize:      # (reset = req0 stored, then the action-less step: two roundings)
+        assert_f32(e32.req, e64.req, ulps=1)
+    gen = torch.Generator(DEV).manual_seed(13)
+    for t in range(280):
+        a = (torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2.2 - 1.1).float()
+        e64.req.copy_(e32.req)
+        e64.charging.copy_(e32.charging)
+        o32, r32, d32, _ = e32.step(a)
+        o64, r64, d64, _ = e64.step(a.double())
+        free.step(a.double())
+        assert_f32(o32, o64, ulps=0)
+        assert_f32(r32, r64, ulps=0)
+        assert_f32(e32.real_power, e64.real_power, ulps=0)
+        assert_f32(e32.req, e64.req, ulps=0)
+        assert d32 == d64
+        if d32:
+            break
+    np.testing.assert_allclose(e32.req.double().cpu().numpy(), free.req.cpu().numpy(), rtol=1e-3, atol=1e-2)
