@@ -7,8 +7,9 @@
 // restated from OpenDSS's published RegControl / SolveSnap documentation in
 // oracle/pf_oracle.py (Feeder.solve_regulated), which the tests compare.
 //
-// Layout (gfx950): the factor is one wave per env -- lane j owns column j of
-// the augmented [I + D S | D] (r <= 24 rows, 2r <= 48 columns) in LDS,
+// Layout (gfx950): the factor is one wave per one or two envs -- lane j owns
+// column j of the env's augmented [I + D S | D] (r <= 24 rows, 2r <= 48
+// columns; two envs of 32 lanes each when 2r <= 32) in LDS,
 // Gauss-Jordan with partial pivoting, the pivot column read into registers
 // before the wave updates its columns; the control pass is one lane per env
 // (a handful of complex multiply-adds per RegControl).  Both are tiny next to
@@ -41,51 +42,66 @@ __device__ __forceinline__ void reg_taps(const pgw_reg_phase& ph, double tap, do
   t2 = ph.tap_winding == 2 ? tap : ph.tap2;
 }
 
+// EPB envs per 64-lane block (2 when 2 r <= 32: lanes 32 h + j serve env 2b + h,
+// column j), COLS = 64 / EPB columns per env; RMAX rows.
+template <int EPB>
 __global__ void __launch_bounds__(64) k_reg_factor(pgw_reg_params p_, int64_t n, const double* __restrict__ taps,
                                                    const int32_t* __restrict__ active, double* __restrict__ K) {
+  constexpr int COLS = 64 / EPB;
+  constexpr int RMAX = EPB == 2 ? 16 : kRegMax;
   const pgw_reg_params& p = PGW_KERNARG0(pgw_reg_params);
-  const int64_t e = blockIdx.x;
-  if (active && active[e] == 0) return;
-  const int r = p.r_reg, lane = threadIdx.x;
-  __shared__ c2 A[kRegMax * 64];        // row i, column `lane`
-  __shared__ c2 D[kRegMax * kRegMax];
-  for (int i = lane; i < r * r; i += 64) D[i] = {0.0, 0.0};
-  __syncthreads();
-  if (lane == 0) {                      // D = Y(t) - Y(DSS taps) over R, phase by phase
-    for (int q = 0; q < p.n_phase; ++q) {
-      const pgw_reg_phase& ph = p.phase[q];
-      double t1, t2;
-      reg_taps(ph, taps[(int64_t)ph.ctrl * n + e], t1, t2);
-      c2 aa, ab, bb, aa0, ab0, bb0;
-      reg_yprim(ph, t1, t2, aa, ab, bb);
-      reg_yprim(ph, ph.tap1, ph.tap2, aa0, ab0, bb0);
-      const int a = ph.a, b = ph.b;
-      D[a * r + a] = cadd(D[a * r + a], csub(aa, aa0));
-      D[a * r + b] = cadd(D[a * r + b], csub(ab, ab0));
-      D[b * r + a] = cadd(D[b * r + a], csub(ab, ab0));
-      D[b * r + b] = cadd(D[b * r + b], csub(bb, bb0));
-    }
-  }
-  __syncthreads();
+  const int lane = threadIdx.x, h = lane / COLS, jl = lane % COLS;
+  const int64_t e = (int64_t)blockIdx.x * EPB + h;
+  const bool live = e < n && (!active || active[e] != 0);
+  if (!__syncthreads_or(live)) return;      // (uniform: every lane of the block takes it)
+  const int64_t ec = e < n ? e : 0;
+  const int r = p.r_reg;
+  __shared__ c2 A[EPB * RMAX * COLS];        // env h: row i, column jl at A[(h RMAX + i) COLS + jl]
+  c2* Ah = A + h * RMAX * COLS;
+  // column jl of [I + D S | D] from the sparse D (a 2 x 2 block per regulated
+  // phase over its nodes a, b): (D S)[i][j] = sum over the phases holding i of
+  // D[i][a] S[a][j] + D[i][b] S[b][j]
   const c2* S = reinterpret_cast<const c2*>(p.S);
-  for (int i = 0; i < r; ++i) {
-    c2 v = {0.0, 0.0};
-    if (lane < r) {                     // (I + D S)[i][lane]
-      v = {i == lane ? 1.0 : 0.0, 0.0};
-      for (int l = 0; l < r; ++l) v = cadd(v, cmul(D[i * r + l], S[l * r + lane]));
-    } else if (lane < 2 * r) {
-      v = D[i * r + (lane - r)];
+  const int j = jl < r ? jl : jl - r;
+  const bool mcol = jl < r;
+  c2 col[RMAX];
+#pragma unroll
+  for (int i = 0; i < RMAX; ++i) col[i] = {(mcol && i == j) ? 1.0 : 0.0, 0.0};
+  for (int q = 0; q < p.n_phase; ++q) {
+    const pgw_reg_phase& ph = p.phase[q];
+    double t1, t2;
+    reg_taps(ph, taps[(int64_t)ph.ctrl * n + ec], t1, t2);
+    c2 aa, ab, bb, aa0, ab0, bb0;
+    reg_yprim(ph, t1, t2, aa, ab, bb);
+    reg_yprim(ph, ph.tap1, ph.tap2, aa0, ab0, bb0);
+    const c2 daa = csub(aa, aa0), dab = csub(ab, ab0), dbb = csub(bb, bb0);
+    const int a = ph.a, b = ph.b;
+    c2 ta, tb;                                          // this column's entries of rows a, b
+    if (mcol) {
+      const c2 sa = S[a * r + j], sb = S[b * r + j];
+      ta = cadd(cmul(daa, sa), cmul(dab, sb));
+      tb = cadd(cmul(dab, sa), cmul(dbb, sb));
+    } else {
+      ta = (j == a) ? daa : (j == b ? dab : c2{0.0, 0.0});
+      tb = (j == a) ? dab : (j == b ? dbb : c2{0.0, 0.0});
     }
-    A[i * 64 + lane] = v;
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i) {
+      col[i] = (i == a) ? cadd(col[i], ta) : col[i];
+      col[i] = (i == b) ? cadd(col[i], tb) : col[i];
+    }
   }
+#pragma unroll
+  for (int i = 0; i < RMAX; ++i)
+    if (i < r) Ah[i * COLS + jl] = (jl < 2 * r) ? col[i] : c2{0.0, 0.0};
   __syncthreads();
   bool singular = false;
   for (int c = 0; c < r; ++c) {
-    // pivot: the largest |A[i][c]|, i >= c (every lane finds the same row)
+    // pivot: the largest |A[i][c]|, i >= c (every lane of the env finds the same row)
     int pr = c;
     double best = -1.0;
     for (int i = c; i < r; ++i) {
-      const c2 v = A[i * 64 + c];
+      const c2 v = Ah[i * COLS + c];
       const double a2 = v.x * v.x + v.y * v.y;
       if (a2 > best) {
         best = a2;
@@ -93,55 +109,54 @@ __global__ void __launch_bounds__(64) k_reg_factor(pgw_reg_params p_, int64_t n,
       }
     }
     singular = singular || !(best > 0.0) || !isfinite(best);
-    c2 pc[kRegMax];                     // the pivot column, rows swapped
+    c2 pc[RMAX];                        // the pivot column, rows swapped
 #pragma unroll
-    for (int i = 0; i < kRegMax; ++i) {
+    for (int i = 0; i < RMAX; ++i) {
       const int src = (i == c) ? pr : (i == pr ? c : i);
-      pc[i] = i < r ? A[src * 64 + c] : c2{0.0, 0.0};
+      pc[i] = i < r ? Ah[src * COLS + c] : c2{0.0, 0.0};
     }
-    c2 rowc = A[pr * 64 + lane], rowp = A[c * 64 + lane];
+    const c2 rowc = Ah[pr * COLS + jl], rowp = Ah[c * COLS + jl];
     __syncthreads();                    // (all reads of column c done)
     // normalise the pivot row, eliminate the others (this lane's column)
     const c2 pv = pc[c];
     const double inv = 1.0 / (pv.x * pv.x + pv.y * pv.y);
     const c2 f = cmul(rowc, {pv.x * inv, -pv.y * inv});
 #pragma unroll
-    for (int i = 0; i < kRegMax; ++i) {
+    for (int i = 0; i < RMAX; ++i) {
       if (i < r) {
         c2 v;
         if (i == c) v = f;
         else {
-          const c2 old = (i == pr) ? rowp : A[i * 64 + lane];
+          const c2 old = (i == pr) ? rowp : Ah[i * COLS + jl];
           v = csub(old, cmul(pc[i], f));
         }
-        A[i * 64 + lane] = v;
+        Ah[i * COLS + jl] = v;
       }
     }
     __syncthreads();
   }
   // K rho: columns r .. 2r - 1 hold (I + D S)^-1 D
-  if (lane >= r && lane < 2 * r) {
-    const int j = lane - r;
-    const double rho = p.rho[j];
+  if (live && jl >= r && jl < 2 * r) {
+    const int jj = jl - r;
+    const double rho = p.rho[jj];
     for (int i = 0; i < r; ++i) {
-      const c2 v = A[i * 64 + lane];
-      const int64_t o = 2 * (((int64_t)i * r + j) * n + e);
+      const c2 v = Ah[i * COLS + jl];
+      const int64_t o = 2 * (((int64_t)i * r + jj) * n + e);
       K[o] = singular ? NAN : v.x * rho;
       K[o + 1] = singular ? NAN : v.y * rho;
     }
   }
 }
 
-// V at regulator node j: x_j rho_j - sum_l S_jl c_l.
+// V at regulator node j: x_j rho_j - sum_l S_jl c_l (c: the env's corrections, in registers).
 __device__ __forceinline__ c2 reg_node_v(const pgw_reg_params& p, int j, const double* __restrict__ rx,
-                                         const double* __restrict__ rc, int64_t n, int64_t e) {
+                                         const c2 (&c)[kRegMax], int64_t n, int64_t e) {
   const int r = p.r_reg;
   const c2* S = reinterpret_cast<const c2*>(p.S);
   c2 v = cscale({rx[2 * ((int64_t)j * n + e)], rx[2 * ((int64_t)j * n + e) + 1]}, p.rho[j]);
-  for (int l = 0; l < r; ++l) {
-    const c2 cl = {rc[2 * ((int64_t)l * n + e)], rc[2 * ((int64_t)l * n + e) + 1]};
-    v = csub(v, cmul(S[j * r + l], cl));
-  }
+#pragma unroll
+  for (int l = 0; l < kRegMax; ++l)
+    if (l < r) v = csub(v, cmul(S[j * r + l], c[l]));
   return v;
 }
 
@@ -153,6 +168,10 @@ __global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64
   if (e >= n) return;
   double want[PGW_REG_MAX_CTRL];
   double dmin = INFINITY;
+  c2 c[kRegMax];
+#pragma unroll
+  for (int l = 0; l < kRegMax; ++l)
+    c[l] = l < p.r_reg ? c2{rc[2 * ((int64_t)l * n + e)], rc[2 * ((int64_t)l * n + e) + 1]} : c2{0.0, 0.0};
   for (int g = 0; g < p.n_ctrl; ++g) {
     const pgw_reg_ctrl& C = p.ctrl[g];
     const double tap = taps[(int64_t)g * n + e];
@@ -160,7 +179,7 @@ __global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64
     // RegControl.Sample: the PT voltage on the 120-V base, less the line-drop
     // compensation (R + jX) I / CTprim with I the current the regulator delivers
     // from the monitored winding into its bus
-    const c2 vpt = reg_node_v(p, C.pt_node, rx, rc, n, e);
+    const c2 vpt = reg_node_v(p, C.pt_node, rx, c, n, e);
     c2 vc = cscale(vpt, 1.0 / C.ptratio);
     if (C.r_ldc != 0.0 || C.x_ldc != 0.0) {
       const pgw_reg_phase& ph = p.phase[C.pt_phase];
@@ -168,7 +187,7 @@ __global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64
       reg_taps(ph, tap, t1, t2);
       c2 yaa, yab, ybb;
       reg_yprim(ph, t1, t2, yaa, yab, ybb);
-      const c2 va = reg_node_v(p, ph.a, rx, rc, n, e), vb = reg_node_v(p, ph.b, rx, rc, n, e);
+      const c2 va = reg_node_v(p, ph.a, rx, c, n, e), vb = reg_node_v(p, ph.b, rx, c, n, e);
       const c2 i_in = C.winding == 2 ? cadd(cmul(yab, va), cmul(ybb, vb)) : cadd(cmul(yaa, va), cmul(yab, vb));
       const c2 i_out = cscale(i_in, -1.0 / C.ctprim);
       vc = csub(vc, cmul({C.r_ldc, C.x_ldc}, i_out));
@@ -236,8 +255,12 @@ int32_t pgw_reg_factor(const pgw_reg_params* p, int64_t n, const double* taps, c
   PGW_REQUIRE(taps && Kreg && n >= 0, "pgw_reg_factor: null argument");
   PGW_REQUIRE(2 * p->r_reg <= 64, "pgw_reg_factor: r_reg %d > 32", p->r_reg);
   if (n == 0) return PGW_OK;
-  hipLaunchKernelGGL(k_reg_factor, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, *p, n, taps, active,
-                     Kreg);
+  if (2 * p->r_reg <= 32)
+    hipLaunchKernelGGL(k_reg_factor<2>, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, (hipStream_t)stream, *p, n,
+                       taps, active, Kreg);
+  else
+    hipLaunchKernelGGL(k_reg_factor<1>, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, *p, n, taps, active,
+                       Kreg);
   return check_launch("k_reg_factor");
 }
 

@@ -591,11 +591,24 @@ class OpenDSSSolver(PowerFlowSolver):
                                              self._Kreg.data_ptr(), _lib.stream_ptr(self.device)))
 
     def _solve_regulated(self, fn, p, tables, cp, cq):
+        """The control loop.  Exact mode: a re-solve after a tap move starts from
+        the env's solution of the previous pass (U_init = U_out of the same
+        per-env buffer) -- the fixed point to tol in a few iterations instead of
+        ~11 from the direct solution; the result depends only on this call's
+        inputs and the taps it started from.  (OpenDSS mode keeps its
+        direct-solution start)"""
         n, st, lib = self.num_envs, _lib.stream_ptr(self.device), _lib.lib()
         t = type(tables).from_buffer_copy(tables)
         t.Kreg, t.reg_x, t.reg_c = self._Kreg.data_ptr(), self._reg_x.data_ptr(), self._reg_c.data_ptr()
+        warm = self.convergence == "exact"
+        if warm:
+            if getattr(self, "_reg_U", None) is None or self._reg_U.shape[1] != self.M:
+                self._reg_U = torch.zeros((n, self.M, 2), dtype=torch.float64, device=self.device)
+            t.U_out = self._reg_U.data_ptr()
         active = None
         for it in range(1, self.OPENDSS_MAX_CONTROL_ITER + 1):
+            if warm and it == 2:
+                t.U_init = self._reg_U.data_ptr()
             t.env_active = active
             _lib.check(fn(p, t, n, _lib.dptr(cp), _lib.dptr(cq), _lib.dptr(self.v_out),
                           _lib.dptr(self._iters), st))
