@@ -604,7 +604,13 @@ class OpenDSSSolver(PowerFlowSolver):
         if warm:
             if getattr(self, "_reg_U", None) is None or self._reg_U.shape[1] != self.M:
                 self._reg_U = torch.zeros((n, self.M, 2), dtype=torch.float64, device=self.device)
+                self._reg_U_valid = False
             t.U_out = self._reg_U.data_ptr()
+            if self.warm_start and self._reg_U_valid:
+                # warm_start=True: the first pass too starts from the env's last
+                # solution, as OpenDSS's snap solve does (history-dependent last bits)
+                t.U_init = self._reg_U.data_ptr()
+            self._reg_U_valid = True
         active = None
         for it in range(1, self.OPENDSS_MAX_CONTROL_ITER + 1):
             if warm and it == 2:

@@ -29,8 +29,10 @@ lib = _lib.lib()
 rng = np.random.default_rng(0)
 loads = [torch.tensor(rng.uniform(-300, 900, N), device=dev) for _ in range(8)]
 times = [pd.Timestamp("08-12-2021 %02d:00:00" % h) for h in range(24)]
-for label, path in (("RegControl", src), ("fixed taps", off)):
-    s = OpenDSSSolver(path, "ieee_13_dss/annual_hourly_load_profile.csv", num_envs=N, device=dev)
+for label, path, warm in (("RegControl", src, False), ("RegControl, warm_start", src, True),
+                          ("fixed taps", off, False)):
+    s = OpenDSSSolver(path, "ieee_13_dss/annual_hourly_load_profile.csv", num_envs=N, device=dev,
+                      warm_start=warm)
     for k in range(4):
         s.calculate_power_flow({"f1": loads[k % 8]}, None, current_time=times[k])
     torch.cuda.synchronize()
@@ -45,6 +47,6 @@ for label, path in (("RegControl", src), ("fixed taps", off)):
     tot, cnt = (ctypes.c_double * 8)(), (ctypes.c_int64 * 8)()
     _lib.check(lib.pgw_timing_stop(tot, cnt))
     it = s.iterations.float().abs().mean().item()
-    print("%-10s: %.1f us per calculate_power_flow, control passes %s, k_pf_general %.1f us x %d launches, "
+    print("%-22s: %.1f us per calculate_power_flow, control passes %s, k_pf_general %.1f us x %d launches, "
           "mean PF iterations (last solve) %.2f" % (label, dt * 1e6, sorted(set(passes)), tot[5] / max(cnt[5], 1) * 1e3,
                                                   cnt[5], it), flush=True)
