@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 20
+#define PGW_ABI_VERSION 21
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -723,6 +723,15 @@ typedef struct pgw_mc_component {
   double* real_power;     /* its real power (building: p_consumed)          */
 } pgw_mc_component;
 
+/* One episode step's shared values for a device-clocked step (below): the
+ * per-step fields of pgw_mc_step_args, one record per episode step in a device
+ * table. */
+typedef struct pgw_mc_step_dyn {
+  pgw_building_exo bld_ex_t, bld_ex_next;
+  pgw_ev_step_info ev_step;
+  double pv_pmax, pad_;
+} pgw_mc_step_dyn;
+
 typedef struct pgw_mc_step_args {
   int32_t n_comp, pad_;
   pgw_mc_component comp[4];
@@ -744,6 +753,17 @@ typedef struct pgw_mc_step_args {
   double* ev_reward;
   double* real_power;     /* agent sums (n)                                 */
   double* reward;
+  /* Device clock (optional, NULL = none; makes the launch's arguments the same
+   * at every step, so a captured hipGraph of it can be replayed step after
+   * step).  clock[0] = the episode step k, read at launch and advanced by one
+   * when the launch's last block retires; clock[1] = the retired-block count,
+   * 0 between launches.  With `dyn` (n_dyn records, built by the caller with
+   * the same values it would pass per step) the step's shared values come from
+   * dyn[min(k, n_dyn - 1)] instead of bld_ex_t / bld_ex_next / pv_pmax /
+   * ev_step; without it only the clock advances. */
+  const pgw_mc_step_dyn* dyn;
+  int32_t* clock;
+  int32_t n_dyn, pad2_;
 } pgw_mc_step_args;
 
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream);

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -191,6 +191,12 @@ class MCComponent(C.Structure):
     _fields_ = [("kind", i32), ("pad_", i32), ("action", Mat), ("obs", Mat), ("real_power", vp)]
 
 
+class MCStepDyn(C.Structure):
+    """pgw_mc_step_dyn: one episode step's shared values (device table record)."""
+    _fields_ = [("bld_ex_t", BuildingExo), ("bld_ex_next", BuildingExo), ("ev_step", EVStepInfo),
+                ("pv_pmax", f64), ("pad_", f64)]
+
+
 class MCStepArgs(C.Structure):
     _fields_ = [("n_comp", i32), ("pad_", i32), ("comp", MCComponent * 4),
                 ("bld", BuildingParams), ("bld_ex_t", BuildingExo), ("bld_ex_next", BuildingExo),
@@ -198,7 +204,8 @@ class MCStepArgs(C.Structure):
                 ("pv", PVParams), ("pv_pmax", f64), ("pv_min_voltage", vp),
                 ("bat", BatteryParams), ("bat_soc", vp),
                 ("ev", EVParams), ("ev_step", EVStepInfo), ("ev_endp", vp), ("ev_req", vp),
-                ("ev_charging", vp), ("ev_reward", vp), ("real_power", vp), ("reward", vp)]
+                ("ev_charging", vp), ("ev_reward", vp), ("real_power", vp), ("reward", vp),
+                ("dyn", vp), ("clock", vp), ("n_dyn", i32), ("pad2_", i32)]
 
 
 MA_MAX_SLOTS = 8
@@ -314,7 +321,7 @@ EXPORTED = sorted(_SIGS)
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
            CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32,
-           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams]
+           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams, MCStepDyn]
 
 _lib = None
 

@@ -335,6 +335,18 @@ class FiveZoneROMEnv(ComponentEnv):
         args.comp[slot].action = m
         return a, keep
 
+    def _mc_dyn_k(self):
+        return self.time_index
+
+    def _mc_dyn_len(self):
+        return len(self._exo) - 1
+
+    def _mc_dyn(self, rec, k):
+        rec.bld_ex_t, rec.bld_ex_next = self._exo[k], self._exo[k + 1]
+
+    def _mc_replayed(self):
+        pass
+
     def _mc_finish(self, obs_kwargs):
         self.time_index += 1
         return self._obs, self._reward_state, self.is_terminal(), {"p_consumed": self.p_consumed}

@@ -105,6 +105,18 @@ class PVEnv(ComponentEnv):
         args.comp[slot].action = m
         return a, vmin
 
+    def _mc_dyn_k(self):
+        return self.index
+
+    def _mc_dyn_len(self):
+        return len(self.data)
+
+    def _mc_dyn(self, rec, k):
+        rec.pv_pmax = float(self.data[k])
+
+    def _mc_replayed(self):
+        self._mc_pmax = float(self.data[self.index])
+
     def _mc_finish(self, kwargs):
         self.index += 1
         return self._obs, None, self.is_terminal(), {"real_power": -self._mc_pmax}

@@ -159,9 +159,15 @@ class EVChargingEnv(ComponentEnv):
         return c[0]
 
     def _build_step_info(self):
+        return self._step_info_at(self.time_index, self._prev_window)
+
+    def _step_info_at(self, ti, prev_window):
+        """(EVStepInfo, parked window) of the step at time index ti after a step
+        whose window was prev_window (None: the reset's action-less step)."""
         s = _lib.EVStepInfo()
-        s.time = float(self.time)
-        s.next_time = float(self.simulation_times[self.time_index + 1])
+        time = self.simulation_times[ti]
+        s.time = float(time)
+        s.next_time = float(self.simulation_times[ti + 1])
         s.action_default = float(self._action_space.low[0])                           # :178
         s.n_words = self._words
         if self.randomize:
@@ -171,9 +177,9 @@ class EVChargingEnv(ComponentEnv):
             for w, a in enumerate(_pack_bits(allv)):
                 s.scan[w] = a
             return s, allv
-        s.tl_rcp = self._tl_rcp[self.time_index].data_ptr() if self.num_vehicles else None
-        win = self._window(self.time)
-        prev = self._prev_window if self._prev_window is not None else np.zeros_like(win)
+        s.tl_rcp = self._tl_rcp[ti].data_ptr() if self.num_vehicles else None
+        win = self._window(time)
+        prev = prev_window if prev_window is not None else np.zeros_like(win)
         for w, (a, b) in enumerate(zip(_pack_bits(win), _pack_bits(win | prev))):
             s.window[w] = a
             s.scan[w] = b
@@ -208,6 +214,21 @@ class EVChargingEnv(ComponentEnv):
         self.time_index += 1
         self.time = self.simulation_times[self.time_index]
         return self._obs, self._reward, self.is_terminal(), {}
+
+    # ---- device-clocked fused step (graph.py): episode step k runs at time
+    # index k + 1 (the reset's action-less step took index 0)
+    def _mc_dyn_k(self):
+        return None if self.time_index is None else self.time_index - 1
+
+    def _mc_dyn_len(self):
+        return len(self.simulation_times) - 2
+
+    def _mc_dyn(self, rec, k):
+        prev = self._window(self.simulation_times[k]) if not self.randomize else None
+        rec.ev_step = self._step_info_at(k + 1, prev)[0]
+
+    def _mc_replayed(self):
+        self._step_info(True)          # the host's schedule state, as the eager step leaves it
 
     def seed(self, seed=None):
         """Seed the per-env vehicle sampling of randomize=True (the reference draws

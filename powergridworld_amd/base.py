@@ -327,7 +327,19 @@ class MultiComponentEnv(ComponentEnv):
         for e in self.envs:
             e.reset(**kwargs)
         self._real_power.zero_()
+        if self._mc_fusable():
+            # device clock of the fused step (graph.py): episode step 0
+            self._mc_clock().zero_()
+            self._ep_step = 0
         return self.get_obs(**kwargs)
+
+    def _mc_clock(self):
+        """[2] int32 device clock of the fused step (pgw_mc_step_args.clock)."""
+        c = self.__dict__.get("_clock")
+        if c is None:
+            c = self._clock = torch.zeros(2, dtype=torch.int32, device=self.device)
+            self._ep_step = 0
+        return c
 
     def _reduce(self):
         a = _lib.ReduceArgs()
@@ -367,6 +379,7 @@ class MultiComponentEnv(ComponentEnv):
                 for c, env in enumerate(self.envs):
                     env._mc_static(args, c)
                 args.real_power, args.reward = self._real_power.data_ptr(), self._reward.data_ptr()
+                args.clock = self._mc_clock().data_ptr()      # (advanced by every fused step)
                 self._mc_args, self._mc_args_key = args, key
                 self._mc_call = (_lib.lib().pgw_mc_agent_step, self.num_envs)
             keep = []
@@ -382,6 +395,7 @@ class MultiComponentEnv(ComponentEnv):
             rc = fn(args, n, self._stream())      # (the caller's current stream, every step)
             if rc:
                 _lib.check(rc)
+            self._ep_step += 1
             for env, env_kwargs in zip(self.envs, kws):
                 ob, _, done, meta = env._mc_finish(env_kwargs)
                 obs[env.name] = ob
@@ -396,6 +410,14 @@ class MultiComponentEnv(ComponentEnv):
             metas[env.name] = meta
         self._reduce()
         return obs, self._reward, any(dones), metas
+
+    def capture_step(self, action, steps=1, **kwargs):
+        """A StepGraph (graph.py) of the fused step reading `action` (a dict of
+        the components' [N, dim] device tensors, or a list of `steps` such
+        dicts): call it to run the captured step(s) with whatever the caller
+        wrote into those tensors."""
+        from powergridworld_amd.graph import StepGraph
+        return StepGraph(self, action, steps, kwargs)
 
     def step_reward(self, **kwargs):
         meta = {e.name: e.step_reward()[1] for e in self.envs}

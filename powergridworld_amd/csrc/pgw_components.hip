@@ -394,24 +394,43 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
 // ====================================================================== fused MC step
 // One component of an MC agent for env e; writes its real power (and its
 // reward where it has one) to the component's own buffers.
-template <bool STD>
-__device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const pgw_mc_component& C,
+// `V`: the step's shared values -- the launch's own fields (pgw_mc_step_args)
+// or a device-clocked record (pgw_mc_step_dyn); both name them alike.
+template <bool STD, class V>
+__device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const V& v, const pgw_mc_component& C,
                                              const BldDerived& d, int64_t n, int64_t e) {
   switch (C.kind) {
     case PGW_MC_BUILDING:
-      (void)building_step_env<STD, double, pgw_mat>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
+      (void)building_step_env<STD, double, pgw_mat>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action, a.bld_x,
                                    C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
       break;
     case PGW_MC_PV:
-      C.real_power[e] = pv_step_env(a.pv, e, a.pv_pmax, C.action, a.pv_min_voltage, C.obs);
+      C.real_power[e] = pv_step_env(a.pv, e, v.pv_pmax, C.action, a.pv_min_voltage, C.obs);
       break;
     case PGW_MC_STORAGE:
       C.real_power[e] = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
       break;
     default:
-      ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
+      ev_step_env(a.ev, v.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
                   C.real_power, a.ev_reward);
       break;
+  }
+}
+
+// Device clock (pgw_mc_step_args.clock): the episode step this launch runs,
+// read once at entry (an atomic load: never re-read after the tick below).
+__device__ __forceinline__ int clock_read(const int32_t* clk) {
+  return __hip_atomic_load(clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Called by one thread per block after the block's barrier (every thread of
+// the block has read the clock): the last block to retire advances it.  Plain
+// relaxed atomics -- no fence, nothing else is published through the clock
+// (the next launch sees the stores across the kernel boundary).
+__device__ __forceinline__ void clock_retire(int32_t* clk, int k) {
+  const unsigned prev = __hip_atomic_fetch_add((unsigned*)(clk + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev == gridDim.x - 1) {
+    __hip_atomic_store(clk + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(clk, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -431,22 +450,31 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const pg
 // component's real power and reward in LDS and, after the block barrier, wave 0
 // forms the sums in component order -- the same values and the same operation
 // order as one lane doing everything, without any cross-block synchronisation.
-template <bool STD>
+//
+// CLK (pgw_mc_step_args.clock): 0 none, 1 the clock only advances, 2 the
+// step's shared values also come from the device table dyn[k] -- the launch's
+// arguments are then the same at every step (hipGraph replay).
+template <bool STD, int CLK>
 __global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a_, BldDerived d, int64_t n) {
   const pgw_mc_step_args& a = PGW_KERNARG0(pgw_mc_step_args);
   __shared__ double s_rp[4][64], s_rew[4][64];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int k = CLK ? clock_read(a.clock) : 0;
   if (e < n) {
     const pgw_mc_component& C = a.comp[w];
-    mc_component<STD>(a, C, d, n, e);
+    if constexpr (CLK == 2)
+      mc_component<STD>(a, a.dyn[min(max(k, 0), a.n_dyn - 1)], C, d, n, e);
+    else
+      mc_component<STD>(a, a, C, d, n, e);
     const int kind = C.kind;
     s_rp[w][lane] = C.real_power[e];                 // this thread's own writes
     s_rew[w][lane] = kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
                      : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
   }
   __syncthreads();
+  if (CLK && threadIdx.x == 0) clock_retire(a.clock, k);
   if (w != 0 || e >= n) return;
   double rp_sum = 0.0, rew_sum = 0.0;
   for (int c = 0; c < a.n_comp; ++c) {
@@ -773,16 +801,19 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
                   !a->ev_step.env_start == !a->ev_step.env_endp &&
                   (!a->ev_step.env_start || !a->ev_step.tl_rcp), "pgw_mc_agent_step: EV buffers");
   }
+  PGW_REQUIRE(!a->dyn || (a->clock && a->n_dyn >= 1), "pgw_mc_agent_step: dyn needs clock and n_dyn >= 1");
   const BldDerived d = make_bld_derived(a->bld);
   bool std_bld = false;
   for (int c = 0; c < a->n_comp; ++c)
     if (a->comp[c].kind == PGW_MC_BUILDING) std_bld = bld_is_std(a->bld);
   if (n == 0) return PGW_OK;
   const dim3 grid((unsigned)((n + 63) / 64)), block(64u * (unsigned)a->n_comp);
+  const int clk = a->dyn ? 2 : a->clock ? 1 : 0;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
   if (std_bld)
-    hipLaunchKernelGGL(k_mc_step<true>, grid, block, 0, (hipStream_t)stream, *a, d, n);
+    clk == 2 ? go(k_mc_step<true, 2>) : clk == 1 ? go(k_mc_step<true, 1>) : go(k_mc_step<true, 0>);
   else
-    hipLaunchKernelGGL(k_mc_step<false>, grid, block, 0, (hipStream_t)stream, *a, d, n);
+    clk == 2 ? go(k_mc_step<false, 2>) : clk == 1 ? go(k_mc_step<false, 1>) : go(k_mc_step<false, 0>);
   return check_launch("k_mc_step");
 }
 

@@ -1,0 +1,181 @@
+"""Captured steps: a hipGraph of an env's step launch(es), replayed per step
+("hipGraph-captured step").
+
+A launch is worth capturing only when its arguments are the same at every
+step.  The fused MultiComponentEnv step (pgw_mc_agent_step) gets there through
+its device clock: the per-step values every env shares (the building's
+exogenous rows, the PV's profile value, the EV schedule) are written once per
+env into a device table of pgw_mc_step_dyn records, one per episode step, and
+the kernel reads record k = clock[0] and advances the clock when its last block
+retires.  The actions are read from the tensors given at capture: the caller
+writes each step's actions into them (a policy's static output buffers), then
+calls the graph.  EnergyStorageEnv's step has no per-step values at all.
+
+A graph of `steps` > 1 launches runs that many steps per call (one action
+buffer set per step; obs / reward are those of the last step) -- open-loop
+rollouts, where one graph launch replaces `steps` kernel launches.
+
+Host state (the components' clocks, the EV's schedule cache, `done`) advances
+in the call exactly as the eager step advances it, so captured and eager steps
+can be mixed freely; the results are bit-identical to the eager step's
+(tests/test_gpu_graph.py).
+"""
+import ctypes as C
+
+import torch
+
+from powergridworld_amd import _lib
+
+
+def _capture(device, launch):
+    """torch.cuda.CUDAGraph of launch() (our ctypes launches on torch's current
+    stream, which torch.cuda.graph makes its capture stream)."""
+    torch.cuda.synchronize(device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.device(device), torch.cuda.graph(g):
+        launch()
+    torch.cuda.synchronize(device)
+    return g
+
+
+def _in_place(env, action, dim):
+    """pgw_mat of an action tensor the kernel reads in place (a graph keeps the
+    pointer: a converted copy would be a dead temporary)."""
+    if not isinstance(action, torch.Tensor) or action.device != torch.device(env.device):
+        raise ValueError("capture_step: actions must be device tensors on %s" % (env.device,))
+    a, m = env._action_mat(action, dim)
+    if a.data_ptr() != action.data_ptr():
+        raise ValueError("capture_step: an action must be a float64 [N, %d] tensor the kernel can read "
+                         "in place (got %s %s)" % (dim, tuple(action.shape), action.dtype))
+    return m
+
+
+class StepGraph:
+    """Call it to run the captured step(s); returns what env.step returns."""
+
+    def __init__(self, env, action, steps, kwargs):
+        from powergridworld_amd.base import MultiComponentEnv
+        from powergridworld_amd.agents.energy_storage import EnergyStorageEnv
+        steps = int(steps)
+        if steps < 1:
+            raise ValueError("capture_step: steps >= 1")
+        actions = list(action) if isinstance(action, (list, tuple)) else [action] * steps
+        if len(actions) != steps:
+            raise ValueError("capture_step: %d action sets for %d steps" % (len(actions), steps))
+        self.env, self.steps, self._keep = env, steps, (actions, kwargs)
+        if isinstance(env, MultiComponentEnv):
+            self._init_mc(env, actions, kwargs)
+        elif type(env) is EnergyStorageEnv and env.dtype == torch.float64:
+            self._init_battery(env, actions)
+        else:
+            raise NotImplementedError("capture_step: MultiComponentEnv (fused) and EnergyStorageEnv (fp64)")
+
+    # ------------------------------------------------------------ battery
+    def _init_battery(self, env, actions):
+        if kwargs_given(self._keep[1]):
+            raise ValueError("capture_step: EnergyStorageEnv takes no observation inputs")
+        fn = _lib.lib().pgw_battery_step
+        mats = [_in_place(env, a, 1) for a in actions]
+        fixed = (C.c_void_p(env.soc.data_ptr()), env._mat(env._obs), C.c_void_p(env._real_power.data_ptr()))
+
+        def launch():
+            st = env._stream()
+            for m in mats:
+                _lib.check(fn(env.params, env.num_envs, m, *fixed, st))
+        self.graph = _capture(env.device, launch)
+        self._finish = self._finish_battery
+
+    def _finish_battery(self):
+        env = self.env
+        done = False
+        for _ in range(self.steps):
+            env.simulation_step += 1
+            done = done or env.is_terminal()
+        return env._obs, env._zero_reward, done, {"state_of_charge": env.soc.unsqueeze(1)}
+
+    # ------------------------------------------------------------ MC
+    def _init_mc(self, env, actions, kwargs):
+        if not env._mc_fusable():
+            raise NotImplementedError("capture_step: the agent's components are not all fused kinds "
+                                      "(pgw_mc_agent_step)")
+        env._mc_clock()
+        k0 = env._ep_step
+        for e in env.envs:
+            k = e._mc_dyn_k()
+            if k is not None and k != k0:
+                raise RuntimeError("capture_step: component %s is at episode step %s, the agent at %d "
+                                   "(step the agent, not its components)" % (e.name, k, k0))
+        self._dyn, self._n_dyn = _dyn_table(env)
+        kws = [{k: v for k, v in kwargs.items() if k in e.obs_labels} for e in env.envs]
+        self._kws = kws
+        arg_sets = []
+        for act in actions:
+            a = _lib.MCStepArgs()
+            a.n_comp = len(env.envs)
+            for c, e in enumerate(env.envs):
+                e._mc_static(a, c)
+                a.comp[c].action = _in_place(e, act[e.name], e.action_space.shape[0])
+                if e.mc_kind == 0 and kws[c]:
+                    a.bld_ext, keep = e._ext(kws[c])
+                    self._keep += (keep,)
+                if e.mc_kind == 1 and e.grid_aware:
+                    v = e._min_voltage(kws[c])
+                    self._keep += (v,)
+                    a.pv_min_voltage = v.data_ptr()
+            a.real_power, a.reward = env._real_power.data_ptr(), env._reward.data_ptr()
+            a.clock, a.dyn, a.n_dyn = env._clock.data_ptr(), self._dyn.data_ptr(), self._n_dyn
+            arg_sets.append(a)
+        self._args = arg_sets
+        fn, n = _lib.lib().pgw_mc_agent_step, env.num_envs
+
+        def launch():
+            st = env._stream()
+            for a in arg_sets:
+                _lib.check(fn(a, n, st))
+        self.graph = _capture(env.device, launch)
+        self._finish = self._finish_mc
+
+    def _finish_mc(self):
+        env = self.env
+        dones = []                      # (any step of the call reaching the end)
+        for _ in range(self.steps):
+            obs, metas = {}, {}
+            for e in env.envs:
+                e._mc_replayed()
+            env._ep_step += 1
+            for e, kw in zip(env.envs, self._kws):
+                ob, _, done, meta = e._mc_finish(kw)
+                obs[e.name] = ob
+                dones.append(done)
+                metas[e.name] = meta
+        return obs, env._reward, any(dones), metas
+
+    def __call__(self):
+        env = self.env
+        if hasattr(self, "_n_dyn") and env._ep_step + self.steps > self._n_dyn:
+            raise IndexError("capture_step: episode step %d + %d is past the %d steps of the episode "
+                             "tables (reset the env)" % (env._ep_step, self.steps, self._n_dyn))
+        self.graph.replay()
+        return self._finish()
+
+
+def kwargs_given(kwargs):
+    return any(v is not None for v in kwargs.values())
+
+
+def _dyn_table(env):
+    """(device uint8 tensor of pgw_mc_step_dyn[L], L): the agent's shared
+    per-step values for episode steps 0 .. L-1, built on the host once per env
+    from the same component code the eager step uses."""
+    c = env.__dict__.get("_dyn_cache")
+    if c is not None:
+        return c
+    lens = [n for n in (e._mc_dyn_len() for e in env.envs) if n is not None]
+    L = max(1, min(lens)) if lens else 1
+    recs = (_lib.MCStepDyn * L)()
+    for k in range(L):
+        for e in env.envs:
+            e._mc_dyn(recs[k], k)
+    buf = torch.frombuffer(bytearray(recs), dtype=torch.uint8).to(env.device)
+    env._dyn_cache = (buf, L)
+    return env._dyn_cache

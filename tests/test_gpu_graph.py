@@ -1,0 +1,169 @@
+"""Captured steps (powergridworld_amd/graph.py): a StepGraph replay is
+bit-identical to the eager step it stands for, across an episode boundary, in
+1- and multi-step graphs, mixed with eager steps, and for the EV's randomized
+schedule and a grid-aware PV.  Needs an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+N = 320                      # 5 blocks of 64 envs, the last one partial below
+
+
+def mc_env(n=N, randomize=False, grid_aware=False):
+    from powergridworld_amd import MultiComponentEnv
+    from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv, FiveZoneROMThermalEnergyEnv, PVEnv
+    comps = [
+        {"name": "building", "cls": FiveZoneROMThermalEnergyEnv, "config": {}},
+        {"name": "pv", "cls": PVEnv, "config": {"profile_csv": "pv_profile.csv", "scaling_factor": 40.,
+                                                "grid_aware": grid_aware}},
+        {"name": "storage", "cls": EnergyStorageEnv, "config": {}},
+        {"name": "ev", "cls": EVChargingEnv,
+         "config": dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7., peak_threshold=250.,
+                        vehicle_multiplier=5., rescale_spaces=True, randomize=randomize)},
+    ]
+    env = MultiComponentEnv(name="mc", components=comps, num_envs=n, device=DEV)
+    if randomize:
+        env.envs[3].seed(7)
+    return env
+
+
+DIMS = {"building": 6, "pv": 1, "storage": 1, "ev": 1}
+
+
+def actions(n, steps, seed):
+    g = torch.Generator(DEV).manual_seed(seed)
+    return [{c: torch.empty((n, d), dtype=torch.float64, device=DEV).uniform_(-1, 1, generator=g)
+             for c, d in DIMS.items()} for _ in range(steps)]
+
+
+def snap(env):
+    """Every output and state buffer of the agent, as host arrays."""
+    out = [env._reward, env._real_power]
+    for e in env.envs:
+        out.append(e._obs)
+        out.append(e._real_power if e.mc_kind != 0 else e.p_consumed)
+    b, s, v = env.envs[0], env.envs[2], env.envs[3]
+    out += [b.x, b._reward_state, s.soc, v.req, v.charging, v._reward]
+    return [t.detach().cpu().numpy().copy() for t in out]
+
+
+def same(a, b, what):
+    for i, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_array_equal(x, y, err_msg="%s: buffer %d" % (what, i))
+
+
+def reset(env, n=N):
+    init = torch.linspace(5.0, 45.0, n, dtype=torch.float64, device=DEV)
+    return env.reset(init_storage=init)
+
+
+@pytest.mark.parametrize("randomize", [False, True])
+def test_mc_graph_step_matches_eager_across_reset(randomize):
+    """One captured step replayed over 1.2 episodes (an episode is 287 steps
+    after the reset) == the eager fused step, every buffer after every step."""
+    ea, eb = mc_env(randomize=randomize), mc_env(randomize=randomize)
+    acts = actions(N, 16, 1)
+    reset(ea)
+    reset(eb)
+    buf = {c: torch.empty_like(t) for c, t in acts[0].items()}
+    g = eb.capture_step(buf)
+    steps = 0
+    for ep in range(2):
+        for t in range(340 if ep == 0 else 60):
+            a = acts[t % 16]
+            for c in buf:
+                buf[c].copy_(a[c])
+            _, ra, da, ma = ea.step(a)
+            _, rb, db, mb = g()
+            assert da == db
+            assert ma["pv"] == mb["pv"]
+            steps += 1
+            if t % 37 == 0 or da:
+                same(snap(ea), snap(eb), "step %d" % steps)
+            if da:
+                break
+        reset(ea)
+        reset(eb)
+    torch.cuda.synchronize()
+    same(snap(ea), snap(eb), "end")
+    assert eb._ep_step == ea._ep_step and int(eb._clock[0]) == eb._ep_step and int(eb._clock[1]) == 0
+
+
+def test_mc_graph_multi_step_and_mixed_with_eager():
+    """A 4-step graph (four action buffer sets) and eager steps interleaved ==
+    eager steps only; the clock keeps the episode step through both."""
+    ea, eb = mc_env(), mc_env()
+    acts = actions(N, 4, 2)
+    reset(ea)
+    reset(eb)
+    bufs = [{c: t.clone() for c, t in a.items()} for a in acts]
+    g4 = eb.capture_step(bufs, steps=4)
+    for r in range(10):
+        for a in acts:
+            ea.step(a)
+        if r % 3 == 1:
+            for a in acts:
+                eb.step(a)
+        else:
+            _, _, done, _ = g4()
+            assert not done
+        same(snap(ea), snap(eb), "round %d" % r)
+    assert int(eb._clock[0]) == eb._ep_step == 40
+
+
+def test_mc_graph_grid_aware_pv_reads_the_static_voltage():
+    ea, eb = mc_env(grid_aware=True), mc_env(grid_aware=True)
+    acts = actions(N, 1, 3)
+    vmin = torch.full((N,), 1.0, dtype=torch.float64, device=DEV)
+    gen = torch.Generator(DEV).manual_seed(4)
+    for e in (ea, eb):
+        e.reset(init_storage=torch.linspace(5.0, 45.0, N, dtype=torch.float64, device=DEV), min_voltage=vmin)
+    g = eb.capture_step(acts[0], min_voltage=vmin)
+    for t in range(20):
+        vmin.uniform_(0.92, 1.06, generator=gen)
+        ea.step(acts[0], min_voltage=vmin)
+        g()
+        same(snap(ea), snap(eb), "step %d" % t)
+
+
+def test_mc_graph_refuses_past_the_tables_and_copies():
+    env = mc_env(n=64)
+    reset(env, 64)
+    a = actions(64, 1, 5)[0]
+    with pytest.raises(ValueError):
+        env.capture_step({**a, "pv": a["pv"].float()})
+    g = env.capture_step(a)
+    env._ep_step = g._n_dyn            # (as if stepped to the tables' end)
+    with pytest.raises(IndexError):
+        g()
+
+
+def test_battery_graph_matches_eager():
+    from powergridworld_amd.agents import EnergyStorageEnv
+    n = 4096 + 17
+    ea, eb = EnergyStorageEnv(num_envs=n, device=DEV), EnergyStorageEnv(num_envs=n, device=DEV)
+    init = torch.linspace(3.0, 50.0, n, dtype=torch.float64, device=DEV)
+    ea.reset(init_storage=init)
+    eb.reset(init_storage=init)
+    gen = torch.Generator(DEV).manual_seed(6)
+    acts = [torch.empty((n, 1), dtype=torch.float64, device=DEV).uniform_(-1, 1, generator=gen) for _ in range(8)]
+    bufs, one = [a.clone() for a in acts], acts[0].clone()
+    g1, g8 = eb.capture_step(one), eb.capture_step(bufs, steps=8)
+    for r in range(40):
+        da = False
+        for a in acts:
+            da = ea.step(a)[2] or da       # (a graph call reports any of its steps' ends)
+        if r % 2:
+            _, _, db, _ = g8()
+        else:
+            db = False
+            for a in acts:
+                one.copy_(a)
+                db = g1()[2] or db
+        assert da == db
+        assert ea.simulation_step == eb.simulation_step
+        np.testing.assert_array_equal(ea.soc.cpu().numpy(), eb.soc.cpu().numpy())
+        np.testing.assert_array_equal(ea._obs.cpu().numpy(), eb._obs.cpu().numpy())
+        np.testing.assert_array_equal(ea._real_power.cpu().numpy(), eb._real_power.cpu().numpy())

@@ -6,8 +6,9 @@ heterogeneous.py) and HS = the Home-Steward house (base_hs.py) at 65536.  Each s
 with actions resident in HBM (a pool of pre-generated batches); episodes reset
 inside the timed region.  One JSON line per config.
 
-Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS] [--steps K] [--warmup W]
-(HETG: the heterogeneous scenario on the generic path, fused=False)
+Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS,C2G1,C2G8,C3G1,C3G8] [--steps K] [--warmup W]
+(HETG: the heterogeneous scenario on the generic path, fused=False; C2Gk / C3Gk:
+the step replayed from captured hipGraphs of k steps, powergridworld_amd/graph.py)
 """
 import argparse
 import json
@@ -37,7 +38,25 @@ def timed_loop(env, step, reset, steps, warmup):
     return time.perf_counter() - t0
 
 
-def bench_c2(dev, steps, warmup, n=4096, pool=64):
+def graph_steps(env, acts, per, reset):
+    """Captured steps (powergridworld_amd/graph.py) over the action pool: one
+    graph per pool entry (per = 1: as if the policy wrote into one of the pool's
+    buffers), or graphs of `per` consecutive pool entries (open-loop rollout).
+    Returns step() -> done, advancing `per` env steps per call."""
+    pool = len(acts)
+    graphs = [env.capture_step(acts[i] if per == 1 else [acts[(i + j) % pool] for j in range(per)], steps=per)
+              for i in range(0, pool, per)]
+    reset()
+    k = [0]
+
+    def step():
+        done = graphs[k[0] % len(graphs)]()[2]
+        k[0] += 1
+        return done
+    return step
+
+
+def bench_c2(dev, steps, warmup, n=4096, pool=64, graph=0):
     from powergridworld_amd.agents import EnergyStorageEnv
     env = EnergyStorageEnv(num_envs=n, device=dev)
     gen = torch.Generator(dev).manual_seed(0)
@@ -50,8 +69,15 @@ def bench_c2(dev, steps, warmup, n=4096, pool=64):
         k[0] += 1
         return done
 
-    dt = timed_loop(env, step, lambda: env.reset(init_storage=init), steps, warmup)
-    return dict(config="C2", workload="EnergyStorageEnv defaults", batch=n, agents=1, steps=steps, seconds=dt)
+    reset = lambda: env.reset(init_storage=init)
+    if graph:
+        step = graph_steps(env, list(acts), graph, reset)
+        steps, warmup = steps // graph, warmup // graph
+    dt = timed_loop(env, step, reset, steps, warmup)
+    steps *= max(graph, 1)
+    return dict(config="C2" + ("G%d" % graph if graph else ""),
+                workload="EnergyStorageEnv defaults" + (", %d-step captured graphs" % graph if graph else ""),
+                batch=n, agents=1, steps=steps, seconds=dt)
 
 
 def c3_env(dev, n, pool=16):
@@ -74,7 +100,7 @@ def c3_env(dev, n, pool=16):
     return env, acts
 
 
-def bench_c3(dev, steps, warmup, n=16384, pool=16):
+def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0):
     env, acts = c3_env(dev, n, pool)
     gen = torch.Generator(dev).manual_seed(1)
     init = torch.empty(n, dtype=torch.float64, device=dev).uniform_(3.0, 50.0, generator=gen)
@@ -85,9 +111,24 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16):
         k[0] += 1
         return done
 
-    dt = timed_loop(env, step, lambda: env.reset(init_storage=init), steps, warmup)
-    return dict(config="C3", workload="MC building+PV+storage+EV(100 vehicles)", batch=n, agents=1,
-                steps=steps, seconds=dt)
+    reset = lambda: env.reset(init_storage=init)
+    if graph:
+        # (the episode's 287 steps are not a multiple of `graph`: before a call
+        # that would pass the end, the env resets, as done would make it)
+        reset()
+        gstep = graph_steps(env, acts, graph, reset)
+
+        def step():
+            if env._ep_step + graph > 287:
+                reset()
+            return gstep()
+        steps, warmup = steps // graph, warmup // graph
+    dt = timed_loop(env, step, reset, steps, warmup)
+    steps *= max(graph, 1)
+    return dict(config="C3" + ("G%d" % graph if graph else ""),
+                workload="MC building+PV+storage+EV(100 vehicles)" + (
+                    ", %d-step captured graphs" % graph if graph else ""),
+                batch=n, agents=1, steps=steps, seconds=dt)
 
 
 def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto"):
@@ -144,15 +185,17 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     fns = {"C2": bench_c2, "C3": bench_c3, "HET": bench_het, "HS": bench_hs,
-           "HETG": lambda *a: bench_het(*a, fused=False)}
+           "HETG": lambda *a: bench_het(*a, fused=False),
+           "C2G1": lambda *a: bench_c2(*a, graph=1), "C2G8": lambda *a: bench_c2(*a, graph=8),
+           "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8)}
     for name in args.configs.split(","):
         r = fns[name](dev, args.steps, args.warmup)
         units = r["batch"] * r["agents"] * r["steps"]
         r["value"] = units / r["seconds"]
         r["unit"] = "agent-env-steps/s"
         r["us_per_step"] = r["seconds"] / r["steps"] * 1e6
-        if name in BYTES:
-            r["step_level_hbm_gbs"] = BYTES[name] * units / r["seconds"] / 1e9
+        if name[:2] in BYTES:
+            r["step_level_hbm_gbs"] = BYTES[name[:2]] * units / r["seconds"] / 1e9
         print(json.dumps(r), flush=True)
 
 
