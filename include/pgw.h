@@ -755,18 +755,32 @@ typedef struct pgw_mc_step_args {
   double* reward;
   /* Device clock (optional, NULL = none; makes the launch's arguments the same
    * at every step, so a captured hipGraph of it can be replayed step after
-   * step).  clock[0] = the episode step k, read at launch and advanced by one
-   * when the launch's last block retires; clock[1] = the retired-block count,
-   * 0 between launches.  With `dyn` (n_dyn records, built by the caller with
-   * the same values it would pass per step) the step's shared values come from
-   * dyn[min(k, n_dyn - 1)] instead of bld_ex_t / bld_ex_next / pv_pmax /
-   * ev_step; without it only the clock advances. */
+   * step): one int32 per block of 64 envs, clock[b] = the episode step k of
+   * block b, read at launch and advanced by one by that block.  The step's
+   * shared values then come from dyn[min(k, n_dyn - 1)] (n_dyn records, built
+   * by the caller with the values it would pass per step) instead of
+   * bld_ex_t / bld_ex_next / pv_pmax / ev_step.  clock and dyn are both given
+   * or both NULL. */
   const pgw_mc_step_dyn* dyn;
   int32_t* clock;
   int32_t n_dyn, pad2_;
 } pgw_mc_step_args;
 
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Captured launches (hipGraph; the reference has no equivalent -- its step is
+ * a Python call chain): every launch the library issues on `stream` between
+ * pgw_graph_begin and pgw_graph_end becomes one executable graph (*exec_out),
+ * replayed with pgw_graph_launch on any stream.  A launch's arguments are
+ * frozen at capture: capture steps whose arguments do not change per step
+ * (pgw_mc_step_args with clock / dyn, pgw_battery_step).  The stream must be a
+ * created stream (not the null stream); capture mode is thread-local.
+ * ---------------------------------------------------------------------- */
+int32_t pgw_graph_begin(void* stream);
+int32_t pgw_graph_end(void* stream, void** exec_out);
+int32_t pgw_graph_launch(void* exec, void* stream);
+int32_t pgw_graph_destroy(void* exec);
 
 /* ------------------------------------------------------------------------
  * Fused multi-agent step over MC-kind components (the heterogeneous scenario,

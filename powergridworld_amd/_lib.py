@@ -312,6 +312,10 @@ _SIGS = {
                                      CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
     "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
+    "pgw_graph_begin": (i32, [vp]),
+    "pgw_graph_end": (i32, [vp, P(vp)]),
+    "pgw_graph_launch": (i32, [vp, vp]),
+    "pgw_graph_destroy": (i32, [vp]),
     "pgw_hs_step": (i32, [P(HSParams), P(HSStepInfo), i64, HSBuffers, vp]),
     "pgw_ma_step": (i32, [P(MAStepArgs), P(PFParams), P(PFTables), i64, vp, vp, vp]),
 }

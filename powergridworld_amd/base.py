@@ -327,18 +327,17 @@ class MultiComponentEnv(ComponentEnv):
         for e in self.envs:
             e.reset(**kwargs)
         self._real_power.zero_()
-        if self._mc_fusable():
-            # device clock of the fused step (graph.py): episode step 0
-            self._mc_clock().zero_()
-            self._ep_step = 0
+        self._ep_step = 0                 # episode step (the captured steps' clock, graph.py)
         return self.get_obs(**kwargs)
 
     def _mc_clock(self):
-        """[2] int32 device clock of the fused step (pgw_mc_step_args.clock)."""
+        """Per-block device clocks of the captured fused step
+        (pgw_mc_step_args.clock, one int32 per 64 envs) and the host's record of
+        the episode step they hold (None: not known to match)."""
         c = self.__dict__.get("_clock")
         if c is None:
-            c = self._clock = torch.zeros(2, dtype=torch.int32, device=self.device)
-            self._ep_step = 0
+            c = self._clock = torch.zeros((self.num_envs + 63) // 64, dtype=torch.int32, device=self.device)
+            self._clock_k = None
         return c
 
     def _reduce(self):
@@ -379,7 +378,6 @@ class MultiComponentEnv(ComponentEnv):
                 for c, env in enumerate(self.envs):
                     env._mc_static(args, c)
                 args.real_power, args.reward = self._real_power.data_ptr(), self._reward.data_ptr()
-                args.clock = self._mc_clock().data_ptr()      # (advanced by every fused step)
                 self._mc_args, self._mc_args_key = args, key
                 self._mc_call = (_lib.lib().pgw_mc_agent_step, self.num_envs)
             keep = []
@@ -395,7 +393,7 @@ class MultiComponentEnv(ComponentEnv):
             rc = fn(args, n, self._stream())      # (the caller's current stream, every step)
             if rc:
                 _lib.check(rc)
-            self._ep_step += 1
+            self._ep_step = self.__dict__.get("_ep_step", 0) + 1
             for env, env_kwargs in zip(self.envs, kws):
                 ob, _, done, meta = env._mc_finish(env_kwargs)
                 obs[env.name] = ob

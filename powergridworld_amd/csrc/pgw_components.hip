@@ -417,23 +417,6 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const V&
   }
 }
 
-// Device clock (pgw_mc_step_args.clock): the episode step this launch runs,
-// read once at entry (an atomic load: never re-read after the tick below).
-__device__ __forceinline__ int clock_read(const int32_t* clk) {
-  return __hip_atomic_load(clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Called by one thread per block after the block's barrier (every thread of
-// the block has read the clock): the last block to retire advances it.  Plain
-// relaxed atomics -- no fence, nothing else is published through the clock
-// (the next launch sees the stores across the kernel boundary).
-__device__ __forceinline__ void clock_retire(int32_t* clk, int k) {
-  const unsigned prev = __hip_atomic_fetch_add((unsigned*)(clk + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev == gridDim.x - 1) {
-    __hip_atomic_store(clk + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(clk, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // MultiComponentEnv.step (base.py:114-139) of an agent made of building / PV /
 // storage / EV components (each at most once, any order): every component's
 // step in order, then real power and reward summed in order from 0 -- the
@@ -451,21 +434,37 @@ __device__ __forceinline__ void clock_retire(int32_t* clk, int k) {
 // forms the sums in component order -- the same values and the same operation
 // order as one lane doing everything, without any cross-block synchronisation.
 //
-// CLK (pgw_mc_step_args.clock): 0 none, 1 the clock only advances, 2 the
-// step's shared values also come from the device table dyn[k] -- the launch's
-// arguments are then the same at every step (hipGraph replay).
-template <bool STD, int CLK>
+// CLK (pgw_mc_step_args.clock != NULL): the step's shared values come from the
+// device table dyn[k], k = this block's clock -- the launch's arguments are
+// then the same at every step (hipGraph replay).  One clock per block: each is
+// read and advanced by its own block only (plain loads and stores, ordered by
+// the kernel boundary), so there is no cross-block count to contend on (one
+// counter advanced by the last block to retire cost 2.3 us per step: 256
+// serialised device-scope atomics).
+template <bool STD, bool CLK>
 __global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a_, BldDerived d, int64_t n) {
   const pgw_mc_step_args& a = PGW_KERNARG0(pgw_mc_step_args);
   __shared__ double s_rp[4][64], s_rew[4][64];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
-  const int k = CLK ? clock_read(a.clock) : 0;
+  // CLK: the step's record staged in LDS by the block (80 doubles): its
+  // fields are then read at fixed LDS addresses, with no pointer to keep live
+  // (a pointer into the table costs SGPRs the step does not have)
+  __shared__ pgw_mc_step_dyn s_dyn;
+  int k = 0;
+  if constexpr (CLK) {
+    constexpr int kWords = (int)(sizeof(pgw_mc_step_dyn) / sizeof(double));
+    k = a.clock[blockIdx.x];
+    const int r = min(max(k, 0), a.n_dyn - 1);
+    for (int i = threadIdx.x; i < kWords; i += blockDim.x)      // (a block is 1-4 waves)
+      reinterpret_cast<double*>(&s_dyn)[i] = reinterpret_cast<const double*>(a.dyn + r)[i];
+    __syncthreads();
+  }
   if (e < n) {
     const pgw_mc_component& C = a.comp[w];
-    if constexpr (CLK == 2)
-      mc_component<STD>(a, a.dyn[min(max(k, 0), a.n_dyn - 1)], C, d, n, e);
+    if constexpr (CLK)
+      mc_component<STD>(a, s_dyn, C, d, n, e);
     else
       mc_component<STD>(a, a, C, d, n, e);
     const int kind = C.kind;
@@ -474,7 +473,7 @@ __global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a_, BldDerived
                      : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
   }
   __syncthreads();
-  if (CLK && threadIdx.x == 0) clock_retire(a.clock, k);
+  if (CLK && threadIdx.x == 0) a.clock[blockIdx.x] = k + 1;    // (every wave read k before the barrier)
   if (w != 0 || e >= n) return;
   double rp_sum = 0.0, rew_sum = 0.0;
   for (int c = 0; c < a.n_comp; ++c) {
@@ -801,19 +800,19 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
                   !a->ev_step.env_start == !a->ev_step.env_endp &&
                   (!a->ev_step.env_start || !a->ev_step.tl_rcp), "pgw_mc_agent_step: EV buffers");
   }
-  PGW_REQUIRE(!a->dyn || (a->clock && a->n_dyn >= 1), "pgw_mc_agent_step: dyn needs clock and n_dyn >= 1");
+  PGW_REQUIRE(!a->clock == !a->dyn && (!a->dyn || a->n_dyn >= 1),
+              "pgw_mc_agent_step: clock and dyn go together, n_dyn >= 1");
   const BldDerived d = make_bld_derived(a->bld);
   bool std_bld = false;
   for (int c = 0; c < a->n_comp; ++c)
     if (a->comp[c].kind == PGW_MC_BUILDING) std_bld = bld_is_std(a->bld);
   if (n == 0) return PGW_OK;
   const dim3 grid((unsigned)((n + 63) / 64)), block(64u * (unsigned)a->n_comp);
-  const int clk = a->dyn ? 2 : a->clock ? 1 : 0;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
   if (std_bld)
-    clk == 2 ? go(k_mc_step<true, 2>) : clk == 1 ? go(k_mc_step<true, 1>) : go(k_mc_step<true, 0>);
+    a->clock ? go(k_mc_step<true, true>) : go(k_mc_step<true, false>);
   else
-    clk == 2 ? go(k_mc_step<false, 2>) : clk == 1 ? go(k_mc_step<false, 1>) : go(k_mc_step<false, 0>);
+    a->clock ? go(k_mc_step<false, true>) : go(k_mc_step<false, false>);
   return check_launch("k_mc_step");
 }
 

@@ -1,13 +1,14 @@
 """Captured steps: a hipGraph of an env's step launch(es), replayed per step
-("hipGraph-captured step").
+("hipGraph-captured step"; pgw_graph_* in include/pgw.h).
 
 A launch is worth capturing only when its arguments are the same at every
 step.  The fused MultiComponentEnv step (pgw_mc_agent_step) gets there through
-its device clock: the per-step values every env shares (the building's
+device clocks: the per-step values every env shares (the building's
 exogenous rows, the PV's profile value, the EV schedule) are written once per
 env into a device table of pgw_mc_step_dyn records, one per episode step, and
-the kernel reads record k = clock[0] and advances the clock when its last block
-retires.  The actions are read from the tensors given at capture: the caller
+each block of the kernel reads record k = its clock and advances the clock.
+The host sets the clocks to the episode step before a call when they may not
+hold it (after a reset or eager steps: the eager step does not touch them).  The actions are read from the tensors given at capture: the caller
 writes each step's actions into them (a policy's static output buffers), then
 calls the graph.  EnergyStorageEnv's step has no per-step values at all.
 
@@ -27,15 +28,40 @@ import torch
 from powergridworld_amd import _lib
 
 
+class _Graph:
+    """An executable hipGraph of the library's launches (pgw_graph_*): launch()
+    issues it on torch's current stream."""
+
+    def __init__(self, device, launch):
+        h = _lib.lib()
+        torch.cuda.synchronize(device)
+        side = torch.cuda.Stream(device)           # (capture needs a created stream)
+        ex = C.c_void_p()
+        with torch.cuda.device(device), torch.cuda.stream(side):
+            st = _lib.stream_ptr(device)
+            _lib.check(h.pgw_graph_begin(st))
+            try:
+                launch()
+            finally:
+                rc = h.pgw_graph_end(st, C.byref(ex))
+            _lib.check(rc)
+        torch.cuda.synchronize(device)
+        self._exec, self._device, self._launch = ex, device, h.pgw_graph_launch
+        self._destroy = h.pgw_graph_destroy
+
+    def launch(self, stream):
+        rc = self._launch(self._exec, stream)
+        if rc:
+            _lib.check(rc)
+
+    def __del__(self):
+        if getattr(self, "_exec", None):
+            self._destroy(self._exec)
+            self._exec = None
+
+
 def _capture(device, launch):
-    """torch.cuda.CUDAGraph of launch() (our ctypes launches on torch's current
-    stream, which torch.cuda.graph makes its capture stream)."""
-    torch.cuda.synchronize(device)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.device(device), torch.cuda.graph(g):
-        launch()
-    torch.cuda.synchronize(device)
-    return g
+    return _Graph(device, launch)
 
 
 def _in_place(env, action, dim):
@@ -51,7 +77,8 @@ def _in_place(env, action, dim):
 
 
 class StepGraph:
-    """Call it to run the captured step(s); returns what env.step returns."""
+    """Call it to run the captured step(s) on torch's current stream; returns
+    what env.step returns."""
 
     def __init__(self, env, action, steps, kwargs):
         from powergridworld_amd.base import MultiComponentEnv
@@ -99,7 +126,7 @@ class StepGraph:
             raise NotImplementedError("capture_step: the agent's components are not all fused kinds "
                                       "(pgw_mc_agent_step)")
         env._mc_clock()
-        k0 = env._ep_step
+        k0 = env.__dict__.setdefault("_ep_step", 0)
         for e in env.envs:
             k = e._mc_dyn_k()
             if k is not None and k != k0:
@@ -152,10 +179,15 @@ class StepGraph:
 
     def __call__(self):
         env = self.env
-        if hasattr(self, "_n_dyn") and env._ep_step + self.steps > self._n_dyn:
-            raise IndexError("capture_step: episode step %d + %d is past the %d steps of the episode "
-                             "tables (reset the env)" % (env._ep_step, self.steps, self._n_dyn))
-        self.graph.replay()
+        if hasattr(self, "_n_dyn"):
+            k = env._ep_step
+            if k + self.steps > self._n_dyn:
+                raise IndexError("capture_step: episode step %d + %d is past the %d steps of the episode "
+                                 "tables (reset the env)" % (k, self.steps, self._n_dyn))
+            if env._clock_k != k:          # (after a reset or eager steps: set the device clocks)
+                env._clock.fill_(k)
+            env._clock_k = k + self.steps
+        self.graph.launch(self.env._stream())
         return self._finish()
 
 
