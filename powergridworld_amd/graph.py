@@ -102,6 +102,7 @@ class StepGraph:
         if kwargs_given(self._keep[1]):
             raise ValueError("capture_step: EnergyStorageEnv takes no observation inputs")
         fn = _lib.lib().pgw_battery_step
+        self._parts, self._bufv = [env], [env._bufv]
         mats = [_in_place(env, a, 1) for a in actions]
         fixed = (C.c_void_p(env.soc.data_ptr()), env._mat(env._obs), C.c_void_p(env._real_power.data_ptr()))
 
@@ -133,6 +134,10 @@ class StepGraph:
                 raise RuntimeError("capture_step: component %s is at episode step %s, the agent at %d "
                                    "(step the agent, not its components)" % (e.name, k, k0))
         self._dyn, self._n_dyn = _dyn_table(env)
+        # the graph holds the buffers' pointers: a re-pointed buffer (a fused
+        # multi-agent env adopting the component) makes it stale
+        self._parts = env.envs
+        self._bufv = [e._bufv for e in env.envs]
         kws = [{k: v for k, v in kwargs.items() if k in e.obs_labels} for e in env.envs]
         self._kws = kws
         arg_sets = []
@@ -179,6 +184,8 @@ class StepGraph:
 
     def __call__(self):
         env = self.env
+        if [e._bufv for e in self._parts] != self._bufv:
+            raise RuntimeError("capture_step: the env's buffers moved since the capture (capture again)")
         if hasattr(self, "_n_dyn"):
             k = env._ep_step
             if k + self.steps > self._n_dyn:
