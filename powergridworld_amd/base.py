@@ -336,7 +336,7 @@ class MultiComponentEnv(ComponentEnv):
         the episode step they hold (None: not known to match)."""
         c = self.__dict__.get("_clock")
         if c is None:
-            c = self._clock = torch.zeros((self.num_envs + 63) // 64, dtype=torch.int32, device=self.device)
+            c = self._clock = torch.zeros(max(1, (self.num_envs + 63) // 64), dtype=torch.int32, device=self.device)
             self._clock_k = None
         return c
 

@@ -168,3 +168,31 @@ def test_battery_graph_matches_eager():
         np.testing.assert_array_equal(ea.soc.cpu().numpy(), eb.soc.cpu().numpy())
         np.testing.assert_array_equal(ea._obs.cpu().numpy(), eb._obs.cpu().numpy())
         np.testing.assert_array_equal(ea._real_power.cpu().numpy(), eb._real_power.cpu().numpy())
+
+
+def test_mc_graph_state_dict_round_trip():
+    """state_dict() after captured steps, loaded into a fresh env that then
+    captures its own graph: both continue bit-identically."""
+    ea, eb = mc_env(), mc_env()
+    acts = actions(N, 4, 11)
+    reset(ea)
+    buf = {c: t.clone() for c, t in acts[0].items()}
+    ga = ea.capture_step(buf)
+    for t in range(30):
+        for c in buf:
+            buf[c].copy_(acts[t % 4][c])
+        ga()
+    sd = ea.state_dict()
+    reset(eb)
+    eb.load_state_dict(sd)
+    bufb = {c: t.clone() for c, t in acts[0].items()}
+    gb = eb.capture_step(bufb)
+    for t in range(30, 60):
+        for c in buf:
+            buf[c].copy_(acts[t % 4][c])
+            bufb[c].copy_(acts[t % 4][c])
+        _, _, da, _ = ga()
+        _, _, db, _ = gb()
+        assert da == db
+    same(snap(ea), snap(eb), "after the round trip")
+    assert ea._ep_step == eb._ep_step == 60
