@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 21
+#define PGW_ABI_VERSION 22
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -490,10 +490,14 @@ typedef struct pgw_pfg_tables {
    * m + n_reg - 1: the rows' response to the correction currents c, pu per A) */
   const double* Greg;        /* x rows: n_reg x m complex (ld n_reg): G_R,k / (vb_k rho_j)  */
   const double* V0reg;       /* n_reg complex: V0_R / rho                                  */
-  const double* Kreg;        /* per env K(t) rho: r_reg^2 complex, [(j r_reg + l) n + e]   */
+  /* per env K(t), complex symmetric (D and S are), stored as its upper
+   * triangle: K[i][l], i <= l, at [(i r_reg - i (i - 1) / 2 + l - i) n + e],
+   * r_reg (r_reg + 1) / 2 complex */
+  const double* Kreg;
   double* reg_x;             /* out: x per env, r_reg complex, [j n + e] (pu of rho)       */
   double* reg_c;             /* out: c per env, r_reg complex, [j n + e] (A)               */
   const int32_t* env_active; /* optional: envs with 0 are left untouched (control loop)   */
+  const double* reg_rho;     /* r_reg (pgw_reg_params.rho): c = K (rho x)                */
 } pgw_pfg_tables;
 
 /* ctrl_p / ctrl_q: n_ctrl x n (NULL = 0); v_out: n_out x n (nullable); iters: n
@@ -539,7 +543,8 @@ typedef struct pgw_reg_params {
   const double* rho;         /* r_reg: the volts per unit of x (node bases), device  */
 } pgw_reg_params;
 
-/* K(t) rho for the envs with active[e] != 0 (NULL: all), from the taps
+/* K(t) (packed as pgw_pfg_tables.Kreg) for the envs with active[e] != 0
+ * (NULL: all), from the taps
  * (n_ctrl x n, the RegControls' present taps).  An env whose I + D S is
  * singular gets NaN in K, so its next solve reports unconverged. */
 int32_t pgw_reg_factor(const pgw_reg_params* p, int64_t n, const double* taps, const int32_t* active,

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -117,7 +117,7 @@ class PFGTables(C.Structure):
     _fields_ = [("elem", vp), ("W", vp), ("U0", vp), ("Gc", vp), ("V0c", vp), ("G", vp), ("V0", vp),
                 ("U_init", vp), ("U_out", vp), ("v_min_out", vp), ("v_max_out", vp),
                 ("Greg", vp), ("V0reg", vp), ("Kreg", vp), ("reg_x", vp), ("reg_c", vp),
-                ("env_active", vp)]
+                ("env_active", vp), ("reg_rho", vp)]
 
 
 PFG_MAX_REG, REG_MAX_PHASES, REG_MAX_CTRL = 24, 12, 12

@@ -288,18 +288,37 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
         for (int r = 0; r < kGR; ++r) s_x[(row0 + r) * 64 + lane] = make_double2(ar[r], ai[r]);
       }
       __syncthreads();
-      // ---- 1c. c = K x per env -> the correction columns of sJ
+      // ---- 1c. c = K (rho x) per env -> the correction columns of sJ (K
+      // symmetric, its upper triangle stored: row jr0 reads column jr0 below
+      // the diagonal).  A row's entries are loaded 8 at a time before their
+      // FMAs (one HBM round trip per 8 columns, not per column); the FMAs run
+      // in column order.
       const int rr = p.r_reg;
       for (int jr0 = wv; jr0 < rr; jr0 += kGW) {
         double cr_ = 0.0, ci_ = 0.0;
-        const double* kr = t.Kreg + 2 * ((int64_t)jr0 * rr * n + ec);
-        for (int l = 0; l < rr; ++l) {
-          const double2 x = s_x[l * 64 + lane];
-          const double kx = kr[2 * (int64_t)l * n], ky = kr[2 * (int64_t)l * n + 1];
-          cr_ = fma(kx, x.x, cr_);
-          cr_ = fma(-ky, x.y, cr_);
-          ci_ = fma(kx, x.y, ci_);
-          ci_ = fma(ky, x.x, ci_);
+        for (int l0 = 0; l0 < rr; l0 += 8) {
+          double kx[8], ky[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int l = min(l0 + u, rr - 1);          // (past the row: a valid address, value unused)
+            const int i0 = min(jr0, l), i1 = max(jr0, l);
+            const double* kp = t.Kreg + 2 * ((int64_t)(i0 * rr - i0 * (i0 - 1) / 2 + (i1 - i0)) * n + ec);
+            kx[u] = kp[0];
+            ky[u] = kp[1];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int l = l0 + u;
+            if (l < rr) {
+              const double2 xu = s_x[l * 64 + lane];
+              const double rl = t.reg_rho[l];
+              const double xr = xu.x * rl, xi = xu.y * rl;
+              cr_ = fma(kx[u], xr, cr_);
+              cr_ = fma(-ky[u], xi, cr_);
+              ci_ = fma(kx[u], xi, ci_);
+              ci_ = fma(ky[u], xr, ci_);
+            }
+          }
         }
         if (!done) sJ[(m + jr0) * 64 + lane] = make_double2(cr_, ci_);
       }
@@ -490,8 +509,8 @@ int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t 
                   p->r_reg <= p->n_reg && (p->n_reg == 0) == (p->r_reg == 0) &&
                   p->m + p->n_reg <= PGW_PFG_MAX_M,
               "pgw_pf_solve_general: bad n_reg %d / r_reg %d (m %d)", p->n_reg, p->r_reg, p->m);
-  PGW_REQUIRE(p->n_reg == 0 || (t->Greg && t->V0reg && t->Kreg && t->reg_x && t->reg_c),
-              "pgw_pf_solve_general: regulators need Greg / V0reg / Kreg / reg_x / reg_c");
+  PGW_REQUIRE(p->n_reg == 0 || (t->Greg && t->V0reg && t->Kreg && t->reg_x && t->reg_c && t->reg_rho),
+              "pgw_pf_solve_general: regulators need Greg / V0reg / Kreg / reg_x / reg_c / reg_rho");
   PGW_REQUIRE(p->n_reg == 0 || !c.agent_power, "pgw_pf_solve_general: regulators on the fused step");
   if (n == 0) return PGW_OK;
   hipStream_t st = (hipStream_t)stream;

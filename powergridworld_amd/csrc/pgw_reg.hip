@@ -135,15 +135,16 @@ __global__ void __launch_bounds__(64) k_reg_factor(pgw_reg_params p_, int64_t n,
     }
     __syncthreads();
   }
-  // K rho: columns r .. 2r - 1 hold (I + D S)^-1 D
+  // K: columns r .. 2r - 1 hold (I + D S)^-1 D, complex symmetric (D and S
+  // are); its upper triangle is stored (column jj: rows 0 .. jj), half the
+  // bytes every solve iteration re-reads
   if (live && jl >= r && jl < 2 * r) {
     const int jj = jl - r;
-    const double rho = p.rho[jj];
-    for (int i = 0; i < r; ++i) {
+    for (int i = 0; i <= jj; ++i) {
       const c2 v = Ah[i * COLS + jl];
-      const int64_t o = 2 * (((int64_t)i * r + jj) * n + e);
-      K[o] = singular ? NAN : v.x * rho;
-      K[o + 1] = singular ? NAN : v.y * rho;
+      const int64_t o = 2 * ((int64_t)(i * r - i * (i - 1) / 2 + (jj - i)) * n + e);
+      K[o] = singular ? NAN : v.x;
+      K[o + 1] = singular ? NAN : v.y;
     }
   }
 }

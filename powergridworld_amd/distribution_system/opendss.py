@@ -375,6 +375,7 @@ class OpenDSSSolver(PowerFlowSolver):
             t = self.tables
             t.Greg, t.V0reg = self._g_Greg.data_ptr(), self._g_V0reg.data_ptr()
             t.Kreg, t.reg_x, t.reg_c = self._Kreg.data_ptr(), self._reg_x.data_ptr(), self._reg_c.data_ptr()
+            t.reg_rho = self._reg_rho.data_ptr()
         self._cfg_version = getattr(self, "_cfg_version", 0) + 1
         self.tables_version = getattr(self, "tables_version", 0) + 1
         self._step_cache = {}
@@ -557,7 +558,8 @@ class OpenDSSSolver(PowerFlowSolver):
         reg, n, dev = self.regulators, self.num_envs, self.device
         r, nc = len(reg["nodes"]), len(reg["ctrls"])
         self.reg_taps = torch.tensor(np.repeat(reg["taps0"][:, None], n, 1), dtype=torch.float64, device=dev)
-        self._Kreg = torch.zeros((r * r, n, 2), dtype=torch.float64, device=dev)     # DSS taps: K = 0
+        # K per env, its upper triangle (pgw_pfg_tables.Kreg); DSS taps: K = 0
+        self._Kreg = torch.zeros((r * (r + 1) // 2, n, 2), dtype=torch.float64, device=dev)
         self._reg_x = torch.zeros((r, n, 2), dtype=torch.float64, device=dev)
         self._reg_c = torch.zeros((r, n, 2), dtype=torch.float64, device=dev)
         self._reg_active = torch.ones(n, dtype=torch.int32, device=dev)
@@ -600,6 +602,7 @@ class OpenDSSSolver(PowerFlowSolver):
         n, st, lib = self.num_envs, _lib.stream_ptr(self.device), _lib.lib()
         t = type(tables).from_buffer_copy(tables)
         t.Kreg, t.reg_x, t.reg_c = self._Kreg.data_ptr(), self._reg_x.data_ptr(), self._reg_c.data_ptr()
+        t.reg_rho = self._reg_rho.data_ptr()
         warm = self.convergence == "exact"
         if warm:
             if getattr(self, "_reg_U", None) is None or self._reg_U.shape[1] != self.M:
