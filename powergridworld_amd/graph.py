@@ -8,9 +8,13 @@ exogenous rows, the PV's profile value, the EV schedule) are written once per
 env into a device table of pgw_mc_step_dyn records, one per episode step, and
 each block of the kernel reads record k = its clock and advances the clock.
 The host sets the clocks to the episode step before a call when they may not
-hold it (after a reset or eager steps: the eager step does not touch them).  The actions are read from the tensors given at capture: the caller
-writes each step's actions into them (a policy's static output buffers), then
-calls the graph.  EnergyStorageEnv's step has no per-step values at all.
+hold it (after a reset or eager steps: the eager step does not touch them).
+The actions are read from the tensors given at capture: the caller writes each
+step's actions into them (a policy's static output buffers), then calls the
+graph.  EnergyStorageEnv's step has no per-step values at all.
+
+On this runtime a graph launch costs about twice an eager launch of host time
+(DESIGN.md section 7), so graphs of several steps are the ones that pay.
 
 A graph of `steps` > 1 launches runs that many steps per call (one action
 buffer set per step; obs / reward are those of the last step) -- open-loop
