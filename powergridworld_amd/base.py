@@ -409,13 +409,15 @@ class MultiComponentEnv(ComponentEnv):
         self._reduce()
         return obs, self._reward, any(dones), metas
 
-    def capture_step(self, action, steps=1, **kwargs):
+    def capture_step(self, action, steps=1, clocked=False, **kwargs):
         """A StepGraph (graph.py) of the fused step reading `action` (a dict of
         the components' [N, dim] device tensors, or a list of `steps` such
         dicts): call it to run the captured step(s) with whatever the caller
-        wrote into those tensors."""
+        wrote into those tensors.  Default: one graph per episode position,
+        captured on first use; clocked=True: one graph for every position, the
+        per-step values read through the device clocks."""
         from powergridworld_amd.graph import StepGraph
-        return StepGraph(self, action, steps, kwargs)
+        return StepGraph(self, action, steps, kwargs, clocked)
 
     def step_reward(self, **kwargs):
         meta = {e.name: e.step_reward()[1] for e in self.envs}

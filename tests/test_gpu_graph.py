@@ -59,16 +59,18 @@ def reset(env, n=N):
     return env.reset(init_storage=init)
 
 
-@pytest.mark.parametrize("randomize", [False, True])
-def test_mc_graph_step_matches_eager_across_reset(randomize):
+@pytest.mark.parametrize("randomize,clocked", [(False, True), (True, True), (False, False), (True, False)])
+def test_mc_graph_step_matches_eager_across_reset(randomize, clocked):
     """One captured step replayed over 1.2 episodes (an episode is 287 steps
-    after the reset) == the eager fused step, every buffer after every step."""
+    after the reset) == the eager fused step, every buffer after every step;
+    device-clocked, and captured per episode position."""
     ea, eb = mc_env(randomize=randomize), mc_env(randomize=randomize)
     acts = actions(N, 16, 1)
     reset(ea)
     reset(eb)
     buf = {c: torch.empty_like(t) for c, t in acts[0].items()}
-    g = eb.capture_step(buf)
+    g = eb.capture_step(buf, clocked=clocked)
+    assert g._clocked == clocked
     steps = 0
     for ep in range(2):
         for t in range(340 if ep == 0 else 60):
@@ -89,10 +91,14 @@ def test_mc_graph_step_matches_eager_across_reset(randomize):
     torch.cuda.synchronize()
     same(snap(ea), snap(eb), "end")
     assert eb._ep_step == ea._ep_step == 0
-    assert bool((eb._clock == eb._clock_k).all())      # (every block's clock, as the host records it)
+    if clocked:
+        assert bool((eb._clock == eb._clock_k).all())      # (every block's clock, as the host records it)
+    else:
+        assert len(g._pos_graphs) >= 280
 
 
-def test_mc_graph_multi_step_and_mixed_with_eager():
+@pytest.mark.parametrize("clocked", [True, False])
+def test_mc_graph_multi_step_and_mixed_with_eager(clocked):
     """A 4-step graph (four action buffer sets) and eager steps interleaved ==
     eager steps only (the host resets the device clocks after eager steps)."""
     ea, eb = mc_env(), mc_env()
@@ -100,7 +106,7 @@ def test_mc_graph_multi_step_and_mixed_with_eager():
     reset(ea)
     reset(eb)
     bufs = [{c: t.clone() for c, t in a.items()} for a in acts]
-    g4 = eb.capture_step(bufs, steps=4)
+    g4 = eb.capture_step(bufs, steps=4, clocked=clocked)
     for r in range(10):
         for a in acts:
             ea.step(a)
@@ -111,7 +117,9 @@ def test_mc_graph_multi_step_and_mixed_with_eager():
             _, _, done, _ = g4()
             assert not done
         same(snap(ea), snap(eb), "round %d" % r)
-    assert eb._ep_step == 40 and bool((eb._clock == 40).all())
+    assert eb._ep_step == 40
+    if clocked:
+        assert bool((eb._clock == 40).all())
 
 
 def test_mc_graph_grid_aware_pv_reads_the_static_voltage():

@@ -38,13 +38,14 @@ def timed_loop(env, step, reset, steps, warmup):
     return time.perf_counter() - t0
 
 
-def graph_steps(env, acts, per, reset):
+def graph_steps(env, acts, per, reset, clocked=False):
     """Captured steps (powergridworld_amd/graph.py) over the action pool: one
     graph per pool entry (per = 1: as if the policy wrote into one of the pool's
     buffers), or graphs of `per` consecutive pool entries (open-loop rollout).
     Returns step() -> done, advancing `per` env steps per call."""
     pool = len(acts)
-    graphs = [env.capture_step(acts[i] if per == 1 else [acts[(i + j) % pool] for j in range(per)], steps=per)
+    kw = {"clocked": True} if clocked else {}
+    graphs = [env.capture_step(acts[i] if per == 1 else [acts[(i + j) % pool] for j in range(per)], steps=per, **kw)
               for i in range(0, pool, per)]
     reset()
     k = [0]
@@ -100,7 +101,7 @@ def c3_env(dev, n, pool=16):
     return env, acts
 
 
-def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0):
+def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True):
     env, acts = c3_env(dev, n, pool)
     gen = torch.Generator(dev).manual_seed(1)
     init = torch.empty(n, dtype=torch.float64, device=dev).uniform_(3.0, 50.0, generator=gen)
@@ -116,18 +117,24 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0):
         # (the episode's 287 steps are not a multiple of `graph`: before a call
         # that would pass the end, the env resets, as done would make it)
         reset()
-        gstep = graph_steps(env, acts, graph, reset)
+        gstep = graph_steps(env, acts, graph, reset, clocked)
 
         def step():
             if env._ep_step + graph > 287:
                 reset()
             return gstep()
         steps, warmup = steps // graph, warmup // graph
+        if not clocked:
+            # every (graph, position) pair is captured on first use: warm up
+            # until the pool's graphs have met every position (the pool cycles
+            # with period len(graphs) calls, an episode is 287 // graph calls)
+            warmup = max(warmup, (pool // graph) * (287 // graph + 1))
     dt = timed_loop(env, step, reset, steps, warmup)
     steps *= max(graph, 1)
-    return dict(config="C3" + ("G%d" % graph if graph else ""),
+    return dict(config="C3" + (("G%d" if clocked else "P%d") % graph if graph else ""),
                 workload="MC building+PV+storage+EV(100 vehicles)" + (
-                    ", %d-step captured graphs" % graph if graph else ""),
+                    ", %d-step captured graphs%s" % (graph, "" if clocked else " per episode position")
+                    if graph else ""),
                 batch=n, agents=1, steps=steps, seconds=dt)
 
 
@@ -187,7 +194,9 @@ def main():
     fns = {"C2": bench_c2, "C3": bench_c3, "HET": bench_het, "HS": bench_hs,
            "HETG": lambda *a: bench_het(*a, fused=False),
            "C2G1": lambda *a: bench_c2(*a, graph=1), "C2G8": lambda *a: bench_c2(*a, graph=8),
-           "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8)}
+           "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8),
+           "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),
+           "C3P8": lambda *a: bench_c3(*a, graph=8, clocked=False)}
     for name in args.configs.split(","):
         r = fns[name](dev, args.steps, args.warmup)
         units = r["batch"] * r["agents"] * r["steps"]
