@@ -131,7 +131,7 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True):
             warmup = max(warmup, (pool // graph) * (287 // graph + 1))
     dt = timed_loop(env, step, reset, steps, warmup)
     steps *= max(graph, 1)
-    return dict(config="C3" + (("G%d" if clocked else "P%d") % graph if graph else ""),
+    return dict(config="C3" + ("L" if n != 16384 else "") + (("G%d" if clocked else "P%d") % graph if graph else ""),
                 workload="MC building+PV+storage+EV(100 vehicles)" + (
                     ", %d-step captured graphs%s" % (graph, "" if clocked else " per episode position")
                     if graph else ""),
@@ -196,7 +196,8 @@ def main():
            "C2G1": lambda *a: bench_c2(*a, graph=1), "C2G8": lambda *a: bench_c2(*a, graph=8),
            "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8),
            "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),
-           "C3P8": lambda *a: bench_c3(*a, graph=8, clocked=False)}
+           "C3P8": lambda *a: bench_c3(*a, graph=8, clocked=False),
+           "C3L": lambda *a: bench_c3(*a, n=65536)}
     for name in args.configs.split(","):
         r = fns[name](dev, args.steps, args.warmup)
         units = r["batch"] * r["agents"] * r["steps"]
