@@ -197,17 +197,19 @@ class HSMultiComponentEnv(MultiComponentEnv):
             s = self._info_cache[key] = self._make_info(ev_time, ev_next_time)
         return s
 
-    def _make_info(self, ev_time, ev_next_time):
+    def _make_info(self, ev_time, ev_next_time, rows=None):
+        """`rows` = (PV row, devices row, house time index); None: the present ones."""
         s = _lib.HSStepInfo()
-        pv = self._by_kind.get(0)
+        pv, dv = self._by_kind.get(0), self._by_kind.get(3)
+        pi, di, ti = rows if rows is not None else (pv.index if pv is not None else 0,
+                                                    dv.index if dv is not None else 0, self.time_index)
         if pv is not None:
-            s.pv_avail = float(pv.data[pv.index])
-        s.grid_cost = self._grid_cost_data[self.time_index]
-        dv = self._by_kind.get(3)
+            s.pv_avail = float(pv.data[pi])
+        s.grid_cost = self._grid_cost_data[ti]
         if dv is not None:
             for j, c in enumerate(dv._obs_labels):
-                s.dev_obs[j] = float(dv.data[dv.index][j]) if np.ndim(dv.data) > 1 else float(dv.data[dv.index])
-                s.dev_power[j] = float(self._dev_power[dv.index, j])
+                s.dev_obs[j] = float(dv.data[di][j]) if np.ndim(dv.data) > 1 else float(dv.data[di])
+                s.dev_power[j] = float(self._dev_power[di, j])
         ev = self._by_kind.get(2)
         if ev is not None:
             s.ev_time, s.ev_next_time = float(ev_time), float(ev_next_time)
@@ -297,16 +299,53 @@ class HSMultiComponentEnv(MultiComponentEnv):
     def step(self, action, **kwargs):
         """base_hs.py:114-180.  `action`: {component: [N, 1]} or one packed [N, n_comp]."""
         self._pack(action)
+        ev_time, ev_next = self._pre_step()
+        s = self._info(ev_time, ev_next)
+        self._bind_min_voltage(kwargs, stepping=True)
+        _lib.check(_lib.lib().pgw_hs_step(self.params, s, self.num_envs, self._bufs, self._stream()))
+        return self._post_step(ev_next)
+
+    def _pre_step(self):
+        """The step's host bookkeeping before the launch; (EV time, next time)."""
         self.meta_state["timestamp"] = self._timestamps[self.time_index]
         self.meta_state["grid_cost"] = self._grid_cost_data[self.time_index]
         self.meta_state["grid_power"] = self.max_grid_power
         ev = self._by_kind.get(2)
-        ev_time = ev_next = 0.0
+        if ev is None:
+            return 0.0, 0.0
+        return ev.time, ev.simulation_times[ev.time_index]
+
+    # ---- captured steps (graph.py): step j after a reset runs at PV / devices
+    # row j, house time index j and EV times (simulation_times[j], [j + 1])
+    def _hs_step_k(self):
+        return self.time_index
+
+    def _hs_steps(self):
+        """How many steps after a reset have data (the tables' length)."""
+        lens = [len(self._grid_cost_data)]
+        for k, e in self._by_kind.items():
+            if k in (0, 3):
+                lens.append(len(e.data))
+            elif k == 2:
+                lens.append(len(e.simulation_times) - 1)
+        return min(lens)
+
+    def _info_at(self, j):
+        ev = self._by_kind.get(2)
+        t0 = t1 = 0.0
         if ev is not None:
-            ev_time, ev_next = ev.time, ev.simulation_times[ev.time_index]
-        s = self._info(ev_time, ev_next)
-        self._bind_min_voltage(kwargs, stepping=True)
-        _lib.check(_lib.lib().pgw_hs_step(self.params, s, self.num_envs, self._bufs, self._stream()))
+            t0, t1 = float(ev.simulation_times[j]), float(ev.simulation_times[j + 1])
+        return self._make_info(t0, t1, rows=(j, j, j))
+
+    def capture_step(self, action, steps=1, **kwargs):
+        """A StepGraph (graph.py) of `steps` house steps reading `action` (a
+        packed [N, n_comp] fp64 device tensor, or a list of `steps` of them),
+        captured once per episode position on first use."""
+        from powergridworld_amd.graph import StepGraph
+        return StepGraph(self, action, steps, kwargs)
+
+    def _post_step(self, ev_next):
+        """The step's host bookkeeping after the launch (clocks, done, meta)."""
         dones = []
         for k, e in zip(self._kinds, self.envs):
             if k == 0:

@@ -165,7 +165,7 @@ def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto"):
                 batch=n, agents=3, steps=steps, seconds=dt)
 
 
-def bench_hs(dev, steps, warmup, n=65536, pool=16):
+def bench_hs(dev, steps, warmup, n=65536, pool=16, graph=0):
     from powergridworld_amd.base_hs import HSMultiComponentEnv
     from powergridworld_amd.scenarios.heterogeneous_hs import make_env_config
     env = HSMultiComponentEnv(**make_env_config(), num_envs=n, device=dev)
@@ -178,8 +178,23 @@ def bench_hs(dev, steps, warmup, n=65536, pool=16):
         k[0] += 1
         return done
 
+    if graph:
+        # per-position graphs of `graph` steps over the pool (as C3's); before
+        # a call that would pass the data's end the house resets
+        env.reset()
+        gstep = graph_steps(env, list(acts), graph, env.reset)
+        L = env._hs_steps()
+
+        def step():
+            if env._hs_step_k() + graph > L:
+                env.reset()
+            return gstep()
+        steps, warmup = steps // graph, max(warmup // graph, (pool // graph) * (L // graph + 1))
     dt = timed_loop(env, step, env.reset, steps, warmup)
-    return dict(config="HS", workload="Home-Steward house (PV, battery, EV, devices; shipped JSON scenario)",
+    steps *= max(graph, 1)
+    return dict(config="HS" + ("P%d" % graph if graph else ""),
+                workload="Home-Steward house (PV, battery, EV, devices; shipped JSON scenario)" + (
+                    ", %d-step captured graphs per episode position" % graph if graph else ""),
                 batch=n, agents=1, steps=steps, seconds=dt)
 
 
@@ -197,7 +212,8 @@ def main():
            "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8),
            "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),
            "C3P8": lambda *a: bench_c3(*a, graph=8, clocked=False),
-           "C3L": lambda *a: bench_c3(*a, n=65536)}
+           "C3L": lambda *a: bench_c3(*a, n=65536),
+           "HSP8": lambda *a: bench_hs(*a, graph=8)}
     for name in args.configs.split(","):
         r = fns[name](dev, args.steps, args.warmup)
         units = r["batch"] * r["agents"] * r["steps"]
