@@ -28,11 +28,24 @@ in the call exactly as the eager step advances it, so captured and eager steps
 can be mixed freely; the results are bit-identical to the eager step's
 (tests/test_gpu_graph.py).
 """
+import atexit
 import ctypes as C
+import weakref
 
 import torch
 
 from powergridworld_amd import _lib
+
+_LIVE = weakref.WeakSet()       # executable graphs still alive
+
+
+@atexit.register
+def _destroy_all():
+    """Destroy the graphs still alive at exit while the HIP runtime is (its
+    teardown runs after the interpreter's; a graph freed then would call
+    into a runtime that is gone)."""
+    for g in list(_LIVE):
+        g._release()
 
 
 class _Graph:
@@ -55,16 +68,22 @@ class _Graph:
         torch.cuda.synchronize(device)
         self._exec, self._device, self._launch = ex, device, h.pgw_graph_launch
         self._destroy = h.pgw_graph_destroy
+        _LIVE.add(self)
 
     def launch(self, stream):
+        if not self._exec:
+            raise RuntimeError("capture_step: the graph was released")
         rc = self._launch(self._exec, stream)
         if rc:
             _lib.check(rc)
 
-    def __del__(self):
+    def _release(self):
         if getattr(self, "_exec", None):
             self._destroy(self._exec)
             self._exec = None
+
+    def __del__(self):
+        self._release()
 
 
 def _capture(device, launch):
