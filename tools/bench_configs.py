@@ -6,9 +6,11 @@ heterogeneous.py) and HS = the Home-Steward house (base_hs.py) at 65536.  Each s
 with actions resident in HBM (a pool of pre-generated batches); episodes reset
 inside the timed region.  One JSON line per config.
 
-Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS,C2G1,C2G8,C3G1,C3G8] [--steps K] [--warmup W]
-(HETG: the heterogeneous scenario on the generic path, fused=False; C2Gk / C3Gk:
-the step replayed from captured hipGraphs of k steps, powergridworld_amd/graph.py)
+Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS,...] [--steps K] [--warmup W]
+(HETG: the heterogeneous scenario on the generic path, fused=False; C3L: C3 at
+65 536 envs; C2Gk / C3Gk: the step replayed from captured hipGraphs of k steps,
+C3 through the device clocks; C3Pk / HSPk: captured once per episode position,
+powergridworld_amd/graph.py)
 """
 import argparse
 import json
