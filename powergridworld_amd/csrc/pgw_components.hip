@@ -3,6 +3,7 @@
 // field is a contiguous, fully coalesced 512-B wave access.
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "pgw_common.h"
@@ -226,20 +227,59 @@ __global__ void __launch_bounds__(kBlock) k_ev_reset_tables(int64_t n, int32_t V
 // 2 = time left divided in the kernel.  Instantiated per mode so the vehicle
 // loop carries no per-vehicle branch and no unused IEEE division.
 enum { kEvTable = 0, kEvPerEnv = 1, kEvDivide = 2 };
-template <int MODE, class S, class Mt>
-__device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
-                                             int64_t e, const Mt& act, const double* __restrict__ endp,
-                                             S* __restrict__ req, uint64_t* __restrict__ chg,
-                                             const Mt& obs, S* __restrict__ rp,
-                                             S* __restrict__ rew) {
+// The vehicle walk's sums (demand, energy consumed, deficit sum, unserved) run
+// in kEvGroups groups of consecutive chunks: group g covers chunks [g K, g K + K)
+// of the step's scan, K = ceil(chunks / kEvGroups), each group summed from 0 in
+// vehicle order, the totals ((0 + p0) + p1) + p2 + p3.  One lane walking every
+// chunk folds at the group boundaries; k_mc_step's split EV waves (one group
+// each, below) fold the same partials after a block barrier -- so both forms are
+// bit-identical, whichever kernel steps the env.  (The reference's np.sum /
+// np.mean over the vehicles, ev_charging_env.py:245-252, is pairwise for 8 or
+// more elements: no form here is its order; the goldens compare at rtol 1e-12.)
+constexpr int kEvChunk = 8;
+constexpr int kEvGroups = 4;
+struct EvSums {
+  double demand, consumed, dsum, unserved;
+  int dcnt, nact;
+};
+__device__ __forceinline__ int ev_chunks(const pgw_ev_step_info& s) {       // uniform
+  int c = 0;
+  for (int w = 0; w < s.n_words; ++w) c += (__builtin_popcountll(s.scan[w]) + kEvChunk - 1) / kEvChunk;
+  return c;
+}
+__device__ __forceinline__ int ev_group_len(int chunks) { return max(1, (chunks + kEvGroups - 1) / kEvGroups); }
+// The one-lane walk's folded totals wait in LDS (indexed by thread; blocks are
+// at most 512 threads): four more doubles held in registers through the walk
+// took the EV kernels from 3 to 2 waves per SIMD.
+__shared__ double s_ev_fold[4][512];
+
+// The env's charge energy this step (:215-223); `note` counts an out-of-bounds
+// action (once per env: only one of the split waves notes it).
+template <class Mt>
+__device__ __forceinline__ double ev_kwh(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t e,
+                                         const Mt& act, bool note) {
   double a = act.ptr ? ld(act, e, 0) : s.action_default;
   if (p.rescale) {
-    oob_note(p.oob, oob_bad(a));
+    if (note) oob_note(p.oob, oob_bad(a));
     a = to_raw(a, 0.0, 1.0);
   }
-  double kwh = a * p.rate * p.hours_per_step;
-  double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
+  return a * p.rate * p.hours_per_step;
+}
+
+// Walks chunks [c_lo, c_hi) of the scan (:224-252).  SPLIT = false: the whole
+// scan in one lane, folding at the group boundaries, the charging bits stored
+// per word.  SPLIT = true: one group's chunks; the bits are ORed into the
+// block's s_bits[word][lane] and the group's partial sums returned unfolded.
+template <int MODE, bool SPLIT, class S>
+__device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+                                          int64_t e, double kwh, const double* __restrict__ endp,
+                                          S* __restrict__ req, uint64_t* __restrict__ chg, int c_lo,
+                                          int c_hi, int K, uint64_t* s_bits, int lane) {
+  double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;   // the current group's
   int dcnt = 0, nact = 0;
+  int ctr = 0, next_fold = K;                        // uniform chunk counter
+  bool folded = false;                               // (uniform) s_ev_fold holds a total
+  const int tid = threadIdx.x;
   // The scan mask is wave-uniform (scalar), so the vehicle loop is too.  The
   // vehicles go in chunks of kEvChunk: the chunk's requirements are loaded back
   // to back (one memory round trip per chunk, not per vehicle); then every
@@ -249,7 +289,6 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
   // vehicle at one wave per SIMD) -- and last the sums run over the chunk in
   // ascending vehicle order, by selects, exactly as one vehicle at a time.
   // Both passes walk the same chunk mask, so no index array is needed.
-  constexpr int kEvChunk = 8;
   struct Chunk {
     uint64_t bits;
     double rs[kEvChunk], tls[kEvChunk], rcs[kEvChunk];
@@ -263,6 +302,13 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
   };
   for (int w = 0; w < s.n_words; ++w) {
     uint64_t scan = s.scan[w];
+    const int base = ctr, nc = (__builtin_popcountll(scan) + kEvChunk - 1) / kEvChunk;
+    ctr += nc;
+    const int lo = max(base, c_lo), hi = min(base + nc, c_hi);
+    if (SPLIT && lo >= hi) continue;                 // (uniform) none of this group's chunks
+    for (int i = base; i < lo; ++i) (void)take(scan);
+    int budget = hi - lo, at = lo;
+    auto take_mine = [&]() -> uint64_t { return budget-- > 0 ? take(scan) : 0ull; };
     const uint64_t win = s.window[w];
     const uint64_t prev = chg[(int64_t)w * n + e];
     uint64_t now_bits = 0ull;
@@ -298,6 +344,17 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
       }
     };
     auto process = [&](const Chunk& C) {
+      if (!SPLIT && at == next_fold) {               // (uniform) a group boundary
+        // (the first total is the first group's sum: 0.0 + p0 == p0, a sum from
+        // +0.0 being never -0.0)
+        const double q[4] = {demand, consumed, dsum, unserved};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s_ev_fold[j][tid] = folded ? s_ev_fold[j][tid] + q[j] : q[j];
+        folded = true;
+        demand = consumed = dsum = unserved = 0.0;
+        next_fold += K;
+      }
+      ++at;
       double df[kEvChunk], cv[kEvChunk];
       bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk];
       uint64_t m = C.bits;
@@ -323,11 +380,11 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
       m = C.bits;
 #pragma unroll
       for (int i = 0; i < kEvChunk; ++i) {
-        const uint64_t lo = m & (0ull - m);          // the chunk's i-th vehicle bit (0 past its end)
+        const uint64_t lo_bit = m & (0ull - m);      // the chunk's i-th vehicle bit (0 past its end)
         m &= m - 1;
         demand = act[i] ? demand + C.rs[i] : demand;
         nact += act[i] ? 1 : 0;
-        now_bits |= act[i] ? lo : 0ull;
+        now_bits |= act[i] ? lo_bit : 0ull;
         dsum = chg_now[i] ? dsum + df[i] : dsum;
         consumed = chg_now[i] ? consumed + cv[i] : consumed;
         dcnt += chg_now[i] ? 1 : 0;
@@ -337,27 +394,49 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
     // two chunk buffers in turn: the next chunk's loads go out before the
     // current chunk's stores (a copy `cur = next` would wait for them)
     Chunk A, B;
-    A.bits = take(scan);
+    A.bits = take_mine();
     if (A.bits) load(A);
     while (A.bits) {
-      B.bits = take(scan);
+      B.bits = take_mine();
       if (B.bits) load(B);
       process(A);
       if (!B.bits) break;
-      A.bits = take(scan);
+      A.bits = take_mine();
       if (A.bits) load(A);
       process(B);
     }
-    chg[(int64_t)w * n + e] = now_bits;
+    if constexpr (SPLIT) {
+      if (now_bits) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[w * 64 + lane]),
+                             (unsigned long long)now_bits);
+    } else {
+      chg[(int64_t)w * n + e] = now_bits;
+    }
   }
+  EvSums t{demand, consumed, dsum, unserved, 0, 0};
+  if (!SPLIT && folded) {
+    t.demand = s_ev_fold[0][tid] + demand;
+    t.consumed = s_ev_fold[1][tid] + consumed;
+    t.dsum = s_ev_fold[2][tid] + dsum;
+    t.unserved = s_ev_fold[3][tid] + unserved;
+  }
+  t.dcnt = dcnt;
+  t.nact = nact;
+  return t;
+}
+
+// The step's state, reward and obs from the walk's totals (:253-262, :135-142).
+template <class S, class Mt>
+__device__ __forceinline__ void ev_finish(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t e,
+                                          const EvSums& t, const Mt& obs, S* __restrict__ rp,
+                                          S* __restrict__ rew) {
   double st_[6];
   st_[0] = s.next_time;
-  st_[1] = p.mult * (double)nact;
-  st_[2] = p.mult * consumed;
-  st_[3] = p.mult * demand;
-  st_[4] = dcnt ? dsum / (double)dcnt : 0.0;
-  st_[5] = unserved;
-  rp[e] = (S)(p.mult * consumed);                    // :255
+  st_[1] = p.mult * (double)t.nact;
+  st_[2] = p.mult * t.consumed;
+  st_[3] = p.mult * t.demand;
+  st_[4] = t.dcnt ? t.dsum / (double)t.dcnt : 0.0;
+  st_[5] = t.unserved;
+  rp[e] = (S)(p.mult * t.consumed);                  // :255
   // step_reward :135-142
   double ur = -p.u_pen * (st_[5] * st_[5]);
   double pk = pymax(0.0, st_[2] - p.thr);
@@ -366,6 +445,18 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
 #pragma unroll
   for (int j = 0; j < 6; ++j)
     st(obs, e, j, p.rescale ? to_scaled(st_[j], p.obs_low[j], p.obs_high[j]) : st_[j]);
+}
+
+template <int MODE, class S, class Mt>
+__device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+                                             int64_t e, const Mt& act, const double* __restrict__ endp,
+                                             S* __restrict__ req, uint64_t* __restrict__ chg,
+                                             const Mt& obs, S* __restrict__ rp,
+                                             S* __restrict__ rew) {
+  const double kwh = ev_kwh(p, s, e, act, true);
+  const int nc = ev_chunks(s);
+  const EvSums t = ev_walk<MODE, false>(p, s, n, e, kwh, endp, req, chg, 0, nc, ev_group_len(nc), nullptr, 0);
+  ev_finish(p, s, e, t, obs, rp, rew);
 }
 
 template <class S, class Mt>
@@ -377,6 +468,20 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
   if (s.env_start) ev_step_mode<kEvPerEnv>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
   else if (s.tl_rcp) ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
   else ev_step_mode<kEvDivide>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+}
+
+// Group g's part of the walk (k_mc_step's split EV waves).
+template <class Mt>
+__device__ __forceinline__ EvSums ev_step_group(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+                                                int64_t e, const Mt& act, const double* __restrict__ endp,
+                                                double* __restrict__ req, uint64_t* __restrict__ chg, int g,
+                                                uint64_t* s_bits, int lane) {
+  const double kwh = ev_kwh(p, s, e, act, g == 0);
+  const int nc = ev_chunks(s), K = ev_group_len(nc);
+  const int lo = min(g * K, nc), hi = min(lo + K, nc);
+  if (s.env_start) return ev_walk<kEvPerEnv, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
+  if (s.tl_rcp) return ev_walk<kEvTable, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
+  return ev_walk<kEvDivide, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
 }
 
 template <class S, class Mt>
@@ -441,13 +546,28 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const V&
 // the kernel boundary), so there is no cross-block count to contend on (one
 // counter advanced by the last block to retire cost 2.3 us per step: 256
 // serialised device-scope atomics).
+//
+// Split EV (blockDim.x > 64 n_comp: the launch added kEvGroups - 1 waves): the
+// EV slot's vehicle walk is shared by kEvGroups waves of the block, each over
+// one group of chunks (ev_walk), with the charging bits ORed in LDS; after a
+// block barrier the EV slot's wave folds the partial sums in group order and
+// finishes the EV step.  C3 runs one wave per SIMD and the EV wave's walk --
+// one memory round trip per chunk -- was the block's critical path.
 template <bool STD, bool CLK>
-__global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a_, BldDerived d, int64_t n) {
+__global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(pgw_mc_step_args a_, BldDerived d, int64_t n) {
   const pgw_mc_step_args& a = PGW_KERNARG0(pgw_mc_step_args);
   __shared__ double s_rp[4][64], s_rew[4][64];
+  __shared__ uint64_t s_bits[PGW_EV_MAX_WORDS * 64];
+  __shared__ double s_evs[kEvGroups][4][64];
+  __shared__ int s_evc[kEvGroups][2][64];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const bool split = (int)(blockDim.x >> 6) > a.n_comp;                   // (uniform)
+  int ev_slot = 0;
+  for (int c = 0; c < a.n_comp; ++c) ev_slot = a.comp[c].kind == PGW_MC_EV ? c : ev_slot;
+  if (split)
+    for (int i = threadIdx.x; i < PGW_EV_MAX_WORDS * 64; i += blockDim.x) s_bits[i] = 0ull;
   // CLK: the step's record staged in LDS by the block (80 doubles): its
   // fields are then read at fixed LDS addresses, with no pointer to keep live
   // (a pointer into the table costs SGPRs the step does not have)
@@ -457,20 +577,54 @@ __global__ void __launch_bounds__(256) k_mc_step(pgw_mc_step_args a_, BldDerived
     constexpr int kWords = (int)(sizeof(pgw_mc_step_dyn) / sizeof(double));
     k = a.clock[blockIdx.x];
     const int r = min(max(k, 0), a.n_dyn - 1);
-    for (int i = threadIdx.x; i < kWords; i += blockDim.x)      // (a block is 1-4 waves)
+    for (int i = threadIdx.x; i < kWords; i += blockDim.x)      // (a block is 1-7 waves)
       reinterpret_cast<double*>(&s_dyn)[i] = reinterpret_cast<const double*>(a.dyn + r)[i];
-    __syncthreads();
   }
+  if (CLK || split) __syncthreads();
+  const pgw_ev_step_info& evs = CLK ? s_dyn.ev_step : a.ev_step;
+  const bool ev_wave = split && (w >= a.n_comp || w == ev_slot);
   if (e < n) {
-    const pgw_mc_component& C = a.comp[w];
-    if constexpr (CLK)
-      mc_component<STD>(a, s_dyn, C, d, n, e);
-    else
-      mc_component<STD>(a, a, C, d, n, e);
-    const int kind = C.kind;
-    s_rp[w][lane] = C.real_power[e];                 // this thread's own writes
-    s_rew[w][lane] = kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
-                     : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
+    if (ev_wave) {
+      const int g = w >= a.n_comp ? w - a.n_comp + 1 : 0;
+      const EvSums t = ev_step_group(a.ev, evs, n, e, a.comp[ev_slot].action, a.ev_endp, a.ev_req,
+                                     a.ev_charging, g, s_bits, lane);
+      s_evs[g][0][lane] = t.demand;
+      s_evs[g][1][lane] = t.consumed;
+      s_evs[g][2][lane] = t.dsum;
+      s_evs[g][3][lane] = t.unserved;
+      s_evc[g][0][lane] = t.dcnt;
+      s_evc[g][1][lane] = t.nact;
+    } else {
+      const pgw_mc_component& C = a.comp[w];
+      if constexpr (CLK)
+        mc_component<STD>(a, s_dyn, C, d, n, e);
+      else
+        mc_component<STD>(a, a, C, d, n, e);
+      const int kind = C.kind;
+      s_rp[w][lane] = C.real_power[e];               // this thread's own writes
+      s_rew[w][lane] = kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
+                       : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
+    }
+  }
+  if (split) {
+    __syncthreads();
+    if (w == ev_slot && e < n) {
+      EvSums t{0.0, 0.0, 0.0, 0.0, 0, 0};
+#pragma unroll
+      for (int g = 0; g < kEvGroups; ++g) {
+        t.demand = t.demand + s_evs[g][0][lane];
+        t.consumed = t.consumed + s_evs[g][1][lane];
+        t.dsum = t.dsum + s_evs[g][2][lane];
+        t.unserved = t.unserved + s_evs[g][3][lane];
+        t.dcnt += s_evc[g][0][lane];
+        t.nact += s_evc[g][1][lane];
+      }
+      for (int j = 0; j < evs.n_words; ++j) a.ev_charging[(int64_t)j * n + e] = s_bits[j * 64 + lane];
+      const pgw_mc_component& C = a.comp[ev_slot];
+      ev_finish(a.ev, evs, e, t, C.obs, C.real_power, a.ev_reward);
+      s_rp[w][lane] = C.real_power[e];
+      s_rew[w][lane] = a.ev_reward[e];
+    }
   }
   __syncthreads();
   if (CLK && threadIdx.x == 0) a.clock[blockIdx.x] = k + 1;    // (every wave read k before the barrier)
@@ -807,7 +961,15 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   for (int c = 0; c < a->n_comp; ++c)
     if (a->comp[c].kind == PGW_MC_BUILDING) std_bld = bld_is_std(a->bld);
   if (n == 0) return PGW_OK;
-  const dim3 grid((unsigned)((n + 63) / 64)), block(64u * (unsigned)a->n_comp);
+  // the EV walk split over kEvGroups waves (k_mc_step) where the blocks are at
+  // most one per CU anyway: a 7-wave block of ~165 VGPRs fits once per CU, where
+  // 4-wave blocks fit 3 times
+  bool has_ev = false;
+  for (int c = 0; c < a->n_comp; ++c) has_ev = has_ev || a->comp[c].kind == PGW_MC_EV;
+  const int64_t blocks = (n + 63) / 64;
+  const char* force = getenv("PGW_MC_EV_SPLIT");
+  const bool split = has_ev && (force ? force[0] == '1' : blocks <= 256);
+  const dim3 grid((unsigned)blocks), block(64u * (unsigned)(a->n_comp + (split ? kEvGroups - 1 : 0)));
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
   if (std_bld)
     a->clock ? go(k_mc_step<true, true>) : go(k_mc_step<true, false>);

@@ -901,3 +901,51 @@ def test_pf_warm_start_multi_bus():
             close(vw[x], N(vc[x]), 1e-9, 0)
     assert it_w[0] == it_c[0]                                 # the first solve starts cold
     assert np.mean(it_w[1:]) < np.mean(it_c[1:]) - 1.0, (np.mean(it_w[1:]), np.mean(it_c[1:]))
+
+
+@pytest.mark.parametrize("randomize", [False, True])
+def test_mc_ev_split_walk_equals_one_lane_walk(randomize):
+    """k_mc_step's EV walk split over kEvGroups waves (below 257 blocks) against
+    the same kernel with the walk in one lane (PGW_MC_EV_SPLIT=0) and against
+    the generic k_ev_step, bit for bit, over a whole episode of 300 vehicles (5
+    scan words, up to ~40 chunks: every group boundary and word-crossing case)."""
+    import os
+    from powergridworld_amd import MultiComponentEnv
+    from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv
+    n = 2048
+    comps = [
+        {"name": "storage", "cls": EnergyStorageEnv, "config": {}},
+        {"name": "ev", "cls": EVChargingEnv,
+         "config": dict(num_vehicles=300, minutes_per_step=5, max_charge_rate_kw=7.,
+                        peak_threshold=250., vehicle_multiplier=5., rescale_spaces=True,
+                        randomize=randomize)},
+    ]
+    split, lane, generic = [MultiComponentEnv(name="mc", components=comps, num_envs=n, device=DEV)
+                            for _ in range(3)]
+    generic._mc_fuse = False
+    assert split._mc_fusable()
+    for e in (split, lane, generic):
+        if randomize:
+            e.env_dict["ev"].seed(7)
+        e.reset()
+    gen = torch.Generator(DEV).manual_seed(13)
+    for t in range(400):
+        act = {"storage": torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2 - 1,
+               "ev": torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2}
+        os_ = split.step(act)
+        os.environ["PGW_MC_EV_SPLIT"] = "0"
+        try:
+            ol = lane.step(act)
+        finally:
+            del os.environ["PGW_MC_EV_SPLIT"]
+        og = generic.step(act)
+        for o in (ol, og):
+            for c in ("storage", "ev"):
+                assert torch.equal(os_[0][c], o[0][c]), (t, c)
+            assert torch.equal(os_[1], o[1]), t
+            assert os_[2] == o[2]
+        for e in (lane, generic):
+            assert torch.equal(split.env_dict["ev"].real_power, e.env_dict["ev"].real_power), t
+        if os_[2]:
+            break
+    assert t > 250, t                                     # a whole episode
