@@ -968,7 +968,16 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   for (int c = 0; c < a->n_comp; ++c) has_ev = has_ev || a->comp[c].kind == PGW_MC_EV;
   const int64_t blocks = (n + 63) / 64;
   const char* force = getenv("PGW_MC_EV_SPLIT");
-  const bool split = has_ev && (force ? force[0] == '1' : blocks <= 256);
+  // ... and where the walk has more than one chunk: a one-chunk step is one
+  // group anyway and the split's barrier and LDS traffic only cost (C3's median
+  // step).  The clocked launch (graph replay) cannot see the step: split always.
+  int chunks = 2;
+  if (has_ev && !a->clock) {
+    chunks = 0;
+    for (int w = 0; w < a->ev_step.n_words; ++w)
+      chunks += (__builtin_popcountll(a->ev_step.scan[w]) + kEvChunk - 1) / kEvChunk;
+  }
+  const bool split = has_ev && (force ? force[0] == '1' : blocks <= 256 && chunks >= 2);
   const dim3 grid((unsigned)blocks), block(64u * (unsigned)(a->n_comp + (split ? kEvGroups - 1 : 0)));
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
   if (std_bld)

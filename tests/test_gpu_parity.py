@@ -905,8 +905,9 @@ def test_pf_warm_start_multi_bus():
 
 @pytest.mark.parametrize("randomize", [False, True])
 def test_mc_ev_split_walk_equals_one_lane_walk(randomize):
-    """k_mc_step's EV walk split over kEvGroups waves (below 257 blocks) against
-    the same kernel with the walk in one lane (PGW_MC_EV_SPLIT=0) and against
+    """k_mc_step's EV walk split over kEvGroups waves (PGW_MC_EV_SPLIT=1; the
+    default splits below 257 blocks on steps of 2+ chunks) against the same
+    kernel with the walk in one lane (PGW_MC_EV_SPLIT=0) and against
     the generic k_ev_step, bit for bit, over a whole episode of 300 vehicles (5
     scan words, up to ~40 chunks: every group boundary and word-crossing case)."""
     import os
@@ -924,17 +925,19 @@ def test_mc_ev_split_walk_equals_one_lane_walk(randomize):
                             for _ in range(3)]
     generic._mc_fuse = False
     assert split._mc_fusable()
+    init = torch.rand(n, dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(3)) * 60
     for e in (split, lane, generic):
         if randomize:
             e.env_dict["ev"].seed(7)
-        e.reset()
+        e.reset(init_storage=init)
     gen = torch.Generator(DEV).manual_seed(13)
     for t in range(400):
         act = {"storage": torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2 - 1,
                "ev": torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2}
-        os_ = split.step(act)
-        os.environ["PGW_MC_EV_SPLIT"] = "0"
         try:
+            os.environ["PGW_MC_EV_SPLIT"] = "1"
+            os_ = split.step(act)
+            os.environ["PGW_MC_EV_SPLIT"] = "0"
             ol = lane.step(act)
         finally:
             del os.environ["PGW_MC_EV_SPLIT"]
