@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 22
+#define PGW_ABI_VERSION 23
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -772,6 +772,14 @@ typedef struct pgw_mc_step_args {
 } pgw_mc_step_args;
 
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream);
+
+/* Test / A-B knob of pgw_mc_agent_step's EV walk (process-wide, not per call):
+ * -1 = automatic (the default: split over extra waves where the blocks are at
+ * most one per CU and the step's scan has 2+ chunks), 0 = always in one lane,
+ * 1 = always split.  Results are bit-identical in every mode.  The library
+ * reads PGW_MC_EV_SPLIT=0/1 once, at load, as the initial mode.  *previous
+ * (nullable) receives the mode it replaces. */
+int32_t pgw_mc_ev_split_mode(int32_t mode, int32_t* previous);
 
 /* ------------------------------------------------------------------------
  * Captured launches (hipGraph; the reference has no equivalent -- its step is

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -312,6 +312,7 @@ _SIGS = {
                                      CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
     "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
+    "pgw_mc_ev_split_mode": (i32, [i32, P(i32)]),
     "pgw_graph_begin": (i32, [vp]),
     "pgw_graph_end": (i32, [vp, P(vp)]),
     "pgw_graph_launch": (i32, [vp, vp]),

@@ -22,15 +22,22 @@ keyed by attribute path.  Cache-version counters and caches are skipped:
 they describe host-side tables, not the env's state.  ``load_state_dict``
 requires the same env configuration (same paths, shapes and dtypes) and
 raises otherwise.
+
+The voltage-history ring of ``MultiAgentEnv(record_history=True)`` (``_hist``,
+[cap, nodes, N] on the device: gigabytes at large N) is NOT saved, like the
+reference's own ``history`` lists it stands for
+(``multiagent_env.py:129,191-194``): a restore empties it (write index 0,
+lists cleared), so ``voltage_history()`` covers the steps after the restore.
 """
 import datetime
 import numbers
+import warnings
 
 import numpy as np
 import torch
 
 _SKIP_NAMES = ("version", "_ver", "cache", "_lib", "_memo")
-_SKIP_EXACT = ("history",)          # the reference-style history lists (views of the ring)
+_SKIP_EXACT = ("history", "_hist")  # the history lists and their device ring (emptied on load)
 _SCALARS = (bool, numbers.Number, str, type(None), datetime.datetime, datetime.date, np.generic)
 
 
@@ -119,6 +126,14 @@ def load_state_dict(env, sd, strict=False):
     if strict and (missing or extra):
         raise KeyError("state_dict does not match this env: missing %s, unexpected %s"
                        % (missing[:5], extra[:5]))
+    tmiss = [p for p, _, _, v in leaves if p not in sd and isinstance(v, torch.Tensor)]
+    textra = [p for p in extra if isinstance(sd[p], torch.Tensor)]
+    if tmiss or textra:
+        # lazily created buffers (first-step constants) exist on one side only;
+        # say which, since a tensor left out is device state not restored
+        warnings.warn("load_state_dict: tensors missing from the state_dict %s, not in this env %s"
+                      % (tmiss[:8], textra[:8]), stacklevel=2)
+    dev = getattr(env, "device", None)
     for p, owner, key, v in leaves:
         if p not in sd:
             continue
@@ -130,9 +145,23 @@ def load_state_dict(env, sd, strict=False):
         elif isinstance(v, torch.Generator):
             v.set_state(s[1])
         else:
-            val = s.copy() if isinstance(s, np.ndarray) else s
+            if isinstance(s, torch.Tensor):
+                # the live attribute is still unset (e.g. created on the first
+                # step): bind a private copy on the env's device, never the
+                # checkpoint's own tensor (the kernels get its pointer)
+                val = s.detach().clone().to(dev if dev is not None else s.device)
+            else:
+                val = s.copy() if isinstance(s, np.ndarray) else s
             if isinstance(owner, dict):
                 owner[key] = val
             else:
                 setattr(owner, key, val)
+    H = getattr(env, "_hist", None)
+    if isinstance(H, dict):
+        H["t"] = 0
+    hist = getattr(env, "history", None)
+    if isinstance(hist, dict):
+        for v in hist.values():
+            if isinstance(v, list):
+                v.clear()
     return env

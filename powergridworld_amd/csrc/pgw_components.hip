@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 
 #include "pgw_common.h"
 
@@ -233,9 +234,12 @@ enum { kEvTable = 0, kEvPerEnv = 1, kEvDivide = 2 };
 // vehicle order, the totals ((0 + p0) + p1) + p2 + p3.  One lane walking every
 // chunk folds at the group boundaries; k_mc_step's split EV waves (one group
 // each, below) fold the same partials after a block barrier -- so both forms are
-// bit-identical, whichever kernel steps the env.  (The reference's np.sum /
-// np.mean over the vehicles, ev_charging_env.py:245-252, is pairwise for 8 or
-// more elements: no form here is its order; the goldens compare at rtol 1e-12.)
+// bit-identical, whichever kernel steps the env.  (The reference sums demand,
+// consumed and unserved with sequential `+=` in the charging set's iteration
+// order, ev_charging_env.py:204-242; only the mean deficit is np.mean, :252,
+// pairwise from 8 elements on.  With more than one group the totals here are
+// ((p0 + p1) + p2) + p3 instead, a rounding difference of an ulp or so: the
+// goldens compare at rtol 1e-12, the north star allows 1e-6.)
 constexpr int kEvChunk = 8;
 constexpr int kEvGroups = 4;
 struct EvSums {
@@ -251,7 +255,13 @@ __device__ __forceinline__ int ev_group_len(int chunks) { return max(1, (chunks 
 // The one-lane walk's folded totals wait in LDS (indexed by thread; blocks are
 // at most 512 threads): four more doubles held in registers through the walk
 // took the EV kernels from 3 to 2 waves per SIMD.
-__shared__ double s_ev_fold[4][512];
+constexpr int kEvFoldThreads = 512;
+// every block that runs the one-lane walk must fit: k_ev_step (kBlock), k_mc_step
+// (64 x (4 components + kEvGroups - 1 split waves)), k_ma_step (64 x slots)
+static_assert(kBlock <= kEvFoldThreads, "s_ev_fold: k_ev_step block");
+static_assert(64 * (4 + kEvGroups - 1) <= kEvFoldThreads, "s_ev_fold: k_mc_step block");
+static_assert(64 * PGW_MA_MAX_SLOTS <= kEvFoldThreads, "s_ev_fold: k_ma_step block");
+__shared__ double s_ev_fold[4][kEvFoldThreads];
 
 // The env's charge energy this step (:215-223); `note` counts an out-of-bounds
 // action (once per env: only one of the split waves notes it).
@@ -754,7 +764,16 @@ __global__ void __launch_bounds__(kBlock) k_agent_reduce(pgw_reduce_args a, int6
 
 using namespace pgw;
 
-#define PGW_LAUNCH(kernel, n, stream, ...)                                             \
+// pgw_mc_ev_split_mode: -1 auto, 0 one lane, 1 split.  Initialised once at load
+// from PGW_MC_EV_SPLIT (A/B scripts); the step reads the atomic, never the
+// environment.
+static int initial_ev_split_mode() {
+  const char* v = getenv("PGW_MC_EV_SPLIT");
+  return (v && (v[0] == '0' || v[0] == '1')) ? v[0] - '0' : -1;
+}
+static std::atomic<int> g_mc_ev_split{initial_ev_split_mode()};
+
+#define PGW_LAUNCH(kernel, n, stream, ...)                                         \
   do {                                                                                 \
     if ((n) > 0)                                                                       \
       hipLaunchKernelGGL(kernel, dim3(grid_for(n)), dim3(kBlock), 0,                   \
@@ -933,6 +952,13 @@ int32_t pgw_ev_step_f32(const pgw_ev_params* p, const pgw_ev_step_info* s, int64
              reward);
 }
 
+int32_t pgw_mc_ev_split_mode(int32_t mode, int32_t* previous) {
+  PGW_REQUIRE(mode >= -1 && mode <= 1, "pgw_mc_ev_split_mode: mode must be -1, 0 or 1");
+  const int old = g_mc_ev_split.exchange(mode);
+  if (previous) *previous = old;
+  return PGW_OK;
+}
+
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   PGW_REQUIRE(a && n >= 0 && a->n_comp >= 1 && a->n_comp <= 4, "pgw_mc_agent_step: bad args");
   PGW_REQUIRE(a->real_power && a->reward, "pgw_mc_agent_step: null output");
@@ -967,7 +993,7 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   bool has_ev = false;
   for (int c = 0; c < a->n_comp; ++c) has_ev = has_ev || a->comp[c].kind == PGW_MC_EV;
   const int64_t blocks = (n + 63) / 64;
-  const char* force = getenv("PGW_MC_EV_SPLIT");
+  const int force = g_mc_ev_split.load(std::memory_order_relaxed);
   // ... and where the walk has more than one chunk: a one-chunk step is one
   // group anyway and the split's barrier and LDS traffic only cost (C3's median
   // step).  The clocked launch (graph replay) cannot see the step: split always.
@@ -977,7 +1003,7 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
     for (int w = 0; w < a->ev_step.n_words; ++w)
       chunks += (__builtin_popcountll(a->ev_step.scan[w]) + kEvChunk - 1) / kEvChunk;
   }
-  const bool split = has_ev && (force ? force[0] == '1' : blocks <= 256 && chunks >= 2);
+  const bool split = has_ev && (force >= 0 ? force == 1 : blocks <= 256 && chunks >= 2);
   const dim3 grid((unsigned)blocks), block(64u * (unsigned)(a->n_comp + (split ? kEvGroups - 1 : 0)));
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
   if (std_bld)

@@ -163,3 +163,69 @@ def test_checkpoint_regcontrol_solver():
     other = run(f)
     for x, y, z in zip(ref, again, other):
         assert torch.equal(x, y) and torch.equal(x, z)
+
+
+def test_checkpoint_hs_grid_aware_into_fresh_house():
+    """a grid-aware HS PV keeps the min_voltage of the house's first
+    step in state created lazily by that step (HSMultiComponentEnv._mv_state,
+    None before it).  Restoring into a fresh, only-reset house must bind a
+    private device copy (not the checkpoint's tensor, not a host tensor when
+    the checkpoint was mapped to the CPU) and replay bit for bit."""
+    from powergridworld_amd.base_hs import HSMultiComponentEnv
+    from powergridworld_amd.scenarios.heterogeneous_hs import make_env_config
+    n = 256
+    cfg = make_env_config()
+    by = {c["name"]: c for c in cfg["components"]}
+    by["pv"]["config"]["grid_aware"] = True
+    make = lambda: HSMultiComponentEnv(**cfg, num_envs=n, device=DEV)
+    names = [e.name for e in make().envs]
+    rng = np.random.default_rng(9)
+    acts = [torch.tensor(rng.uniform(-1.1, 1.1, (n, len(names))), device=DEV) for _ in range(20)]
+    mvs = [torch.tensor(rng.uniform(0.9, 1.1, n), device=DEV) for _ in range(20)]
+
+    def step(env, i):
+        o, r, d, m = env.step({nm: acts[i][:, j:j + 1] for j, nm in enumerate(names)}, min_voltage=mvs[i])
+        return o, r, d, env.real_power, m["pv_power"], m["es_power"], m["grid_power"]
+
+    env = make()
+    env.reset(min_voltage=mvs[0])
+    for i in range(5):
+        step(env, i)
+    sd = env.state_dict()
+    sd_cpu = {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in sd.items()}
+    ref = _replay(env, range(5, 20), step)
+    for s in (sd, sd_cpu):
+        fresh = make()
+        fresh.reset(min_voltage=mvs[0])
+        fresh.load_state_dict(s)
+        for k, v in vars(fresh).items():
+            if isinstance(v, torch.Tensor) and k in s and isinstance(s[k], torch.Tensor):
+                assert v.device == torch.device(DEV) and v.data_ptr() != s[k].data_ptr(), k
+        other = _replay(fresh, range(5, 20), step)
+        for t, (x, z) in enumerate(zip(ref, other)):
+            for i, (u, w) in enumerate(zip(x, z)):
+                assert torch.equal(u, w), "fresh house, step %d output %d" % (t, i)
+
+
+def test_checkpoint_history_ring_is_emptied():
+    """The voltage-history ring is not saved (it is GBs at large N
+    and its write index lives in a dict): a restore empties it, and the steps
+    recorded after the restore come back in order."""
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    n = 128
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, record_history=True)
+    env.reset()
+    g = torch.Generator(DEV).manual_seed(2)
+    acts = [torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=g) * 2 - 1 for _ in range(6)]
+    for a in acts[:3]:
+        env.step(a)
+    sd = env.state_dict()
+    assert not any(k.startswith("_hist") for k in sd)
+    env.step(acts[3])
+    env.load_state_dict(sd)
+    assert env.voltage_history()[0].shape[0] == 0 and env.history["voltage"] == []
+    for a in acts[3:]:
+        env.step(a)
+    v, p, names = env.voltage_history()
+    assert v.shape[0] == 3 and len(env.history["voltage"]) == 3
+    assert torch.equal(v[-1, names.index("675.3")], env.pf_solver.get_bus_voltage_by_name("675c"))

@@ -905,13 +905,12 @@ def test_pf_warm_start_multi_bus():
 
 @pytest.mark.parametrize("randomize", [False, True])
 def test_mc_ev_split_walk_equals_one_lane_walk(randomize):
-    """k_mc_step's EV walk split over kEvGroups waves (PGW_MC_EV_SPLIT=1; the
-    default splits below 257 blocks on steps of 2+ chunks) against the same
-    kernel with the walk in one lane (PGW_MC_EV_SPLIT=0) and against
+    """k_mc_step's EV walk split over kEvGroups waves (pgw_mc_ev_split_mode(1);
+    the default splits below 257 blocks on steps of 2+ chunks) against the same
+    kernel with the walk in one lane (pgw_mc_ev_split_mode(0)) and against
     the generic k_ev_step, bit for bit, over a whole episode of 300 vehicles (5
     scan words, up to ~40 chunks: every group boundary and word-crossing case)."""
-    import os
-    from powergridworld_amd import MultiComponentEnv
+    from powergridworld_amd import MultiComponentEnv, _lib
     from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv
     n = 2048
     comps = [
@@ -935,12 +934,12 @@ def test_mc_ev_split_walk_equals_one_lane_walk(randomize):
         act = {"storage": torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2 - 1,
                "ev": torch.rand((n, 1), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2}
         try:
-            os.environ["PGW_MC_EV_SPLIT"] = "1"
+            _lib.check(_lib.lib().pgw_mc_ev_split_mode(1, None))
             os_ = split.step(act)
-            os.environ["PGW_MC_EV_SPLIT"] = "0"
+            _lib.check(_lib.lib().pgw_mc_ev_split_mode(0, None))
             ol = lane.step(act)
         finally:
-            del os.environ["PGW_MC_EV_SPLIT"]
+            _lib.check(_lib.lib().pgw_mc_ev_split_mode(-1, None))
         og = generic.step(act)
         for o in (ol, og):
             for c in ("storage", "ev"):
