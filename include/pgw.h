@@ -42,8 +42,8 @@ const char* pgw_last_error(void);
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
  * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
  * mc_step_args, matf, coord_buffers_f32, ma_step_args, pfg_elem, pfg_params,
- * pfg_tables, reg_params -- lets a binding verify its layouts.  Writes
- * min(n, 27) values, returns 27. */
+ * pfg_tables, reg_params, mc_step_dyn, pf_od -- lets a binding verify its
+ * layouts.  Writes min(n, 29) values, returns 29. */
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -363,7 +363,50 @@ typedef struct pgw_pf_tables {
    * over the voltage dict (multiagent_env.py:107-113).  NULL = not written. */
   double* v_min_out;
   double* v_max_out;
+  /* OpenDSS's own snap solve on the fast kernels (HOST pointer, NULL = the
+   * exact fixed point): see pgw_pf_od below. */
+  const struct pgw_pf_od* od;
 } pgw_pf_tables;
+
+/* OpenDSS's snap solve (opendss.py:134 `Solve mode=snap`; Solution.pas
+ * SolveSnap -> DoNormalSolution, restated in oracle/pf_oracle.py
+ * Feeder.snap_opendss) on pgw_pf_solve / pgw_coord_step's one-lane-per-env
+ * kernels, for feeders of the fast shape (m = 14 constant-PQ elements, one
+ * voltage band, at most one controllable slot): the packed block holds the
+ * iteration matrix of Y + every load's nominal Yeq (W'' of that Y, u0 = the
+ * direct solution C Y^-1 I_src); element k's current is I'_k = (conj(S_k) g -
+ * y0'_k) u_k, y0' = the per-phase conj(S) whose Yeq sits in Y; the solve stops
+ * at the first iteration >= min_iter whose largest node-voltage magnitude
+ * change (pu of the node base) is <= tol, or at max_iter (-iterations).
+ *
+ * Node magnitudes: an element from a node to ground gives that node's |V| =
+ * |u_k| elem_scale[k] (0 = the element is not a node).  The other nodes are
+ * check rows (rows_V0 / rows_G: V = V0 + G I', pu of the node base against the
+ * scaled currents, the layout of pgw_pf_tables.G): rows [0, n_rep) are
+ * evaluated every iteration; rows [n_rep, n_rows) are bounded instead, members
+ * (electrically next to a row or an element node: |G_j - G_r| <= gamma per
+ * element, |V0_j - V0_r| <= eps) and source-side nodes (|G_j| <= gsrc per
+ * element), with gmax >= |G_r| per element of every row and element node; when
+ * a bound cannot decide an env's test, its wave re-runs the solve with every
+ * row evaluated, so the stopping iteration is always the exact rule's.
+ *
+ * start (device, this step's hour): the first iteration in closed form -- from
+ * the direct solution the currents are affine in the env's controllable
+ * (P, Q): u_1 = u1b + P u1P + Q u1Q (m complex each), then per row r
+ * V_1r = V1b + P V1P + Q V1Q: u1b, u1P, u1Q (m complex each), then per row
+ * (V1b, V1P, V1Q) complex. */
+#define PGW_PF_OD_MAX_ROWS 32
+typedef struct pgw_pf_od {
+  double tol;                        /* 1e-4 (ConvergenceTolerance)            */
+  double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M];   /* y0' per element (W, -var) */
+  double elem_scale[PGW_PF_MAX_M];   /* node |V| pu = |u_k| * scale; 0 = none   */
+  double gamma, eps, gmax, gsrc;     /* check-row bound constants (above)      */
+  int32_t min_iter;                  /* 2 (MinIterations)                      */
+  int32_t n_rep, n_rows, pad_;
+  const double* rows_V0;             /* n_rows complex (device)                */
+  const double* rows_G;              /* n_rows x m complex (device)            */
+  const double* start;               /* (6 m + 6 n_rows) doubles (device)      */
+} pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)
  * (opendss.py:107-129 then OpenDSS's per-phase WNominal).

@@ -98,7 +98,17 @@ class PFParams(C.Structure):
 class PFTables(C.Structure):
     _fields_ = [("block", vp), ("G", vp), ("V0", vp), ("U_pred", vp),
                 ("U_pred_meta", vp), ("U_init", vp), ("U_out", vp), ("sig_out", vp),
-                ("load_scale", vp), ("v_min_out", vp), ("v_max_out", vp)]
+                ("load_scale", vp), ("v_min_out", vp), ("v_max_out", vp), ("od", vp)]
+
+
+PF_OD_MAX_ROWS = 32
+
+
+class PFOD(C.Structure):
+    _fields_ = [("tol", f64), ("y0r", f64 * PF_MAX_M), ("y0i", f64 * PF_MAX_M),
+                ("elem_scale", f64 * PF_MAX_M), ("gamma", f64), ("eps", f64), ("gmax", f64),
+                ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("pad_", i32),
+                ("rows_V0", vp), ("rows_G", vp), ("start", vp)]
 
 
 class PFGElem(C.Structure):
@@ -326,7 +336,7 @@ EXPORTED = sorted(_SIGS)
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
            CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32,
-           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams, MCStepDyn]
+           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams, MCStepDyn, PFOD]
 
 _lib = None
 

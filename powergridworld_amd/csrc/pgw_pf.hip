@@ -278,6 +278,24 @@ template <int M, bool UB, bool GC> struct PFSolver {
     }
   }
 
+  // OpenDSS's compensation current (Load.CalcInjCurrentArray: the load's model-1
+  // current less its Yeq stamped in Y), in pu: I' = (conj(S) g - y0') u -- the
+  // operations and order of k_pf_general's model-1 path.
+  template <int K>
+  __device__ __forceinline__ void current_od(double y0r, double y0i, double& ir, double& ii) const {
+    double s_r, s_i;
+    pf_power<M, K>(s_r, s_i, sres, pc, qc);
+    double vlo2, vmn2, vmx2;
+    band<K>(vlo2, vmn2, vmx2);
+    const double m2 = fma(ui[K], ui[K], ur[K] * ur[K]);
+    double mc = fmin(fmax(m2, vmn2), vmx2);
+    mc = (m2 <= vlo2) ? 1.0 : mc;
+    const double g = fast_rcp(mc);
+    const double cr = fma(s_r, g, -y0r), ci = fma(s_i, g, -y0i);
+    ir = fma(cr, ur[K], -(ci * ui[K]));
+    ii = fma(cr, ui[K], ci * ur[K]);
+  }
+
   // Fixed-point iteration until max_k |du_k|^2 < tol^2 or max_iter.  The loop
   // is wave-uniform with the exec mask FULL: a lane disabled in EXEC is an
   // invalid DPP source, and every lane holds resident entries the others
@@ -996,6 +1014,338 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   }
 }
 
+// ============================================================ OpenDSS snap solve
+// (pgw_pf_od, include/pgw.h): the reference's own stopping rule on the fast
+// one-lane-per-env kernels.  Per env, from the direct solution u0:
+//   iteration 1   u_1 = u1b + P u1P + Q u1Q (the currents at u0 are affine in
+//                 the env's controllable P, Q: the host's per-hour table);
+//   iteration k   J = I'(u_{k-1}) (compensation currents), u_k = u0 + W'' J --
+//                 the resident DPP matvec of the exact solve;
+//   test          max over every node of | |V_k| - |V_{k-1}| | <= tol from
+//                 iteration min_iter on (Solution.pas Converged).
+// Node magnitudes: nodes that are an element's terminal come from |u|; the
+// others are check rows V = V0 + G J (LDS-staged, DPP row groups).  Only the
+// first n_rep rows are evaluated; the rest are bounded by the last two
+// iterations' current changes (pgw.h), and a wave whose bound cannot decide
+// some env re-runs the whole solve with every row evaluated -- so the stopping
+// iteration is always the exact rule's.  The previous magnitudes live in LDS.
+struct ODArgs {
+  double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M], esc[PGW_PF_MAX_M];
+  double tol, gamma, eps, gmax, gsrc;
+  const double* start;
+  const double* rows_V0;
+  const double* rows_G;
+  int32_t min_iter, n_rep, n_rows, max_iter;
+};
+constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
+constexpr int kOdOld = kOdRows + PGW_PF_MAX_M;   // LDS slots of previous magnitudes per lane
+
+static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
+  ODArgs o = {};
+  for (int k = 0; k < PGW_PF_MAX_M; ++k) {
+    o.y0r[k] = d.y0r[k];
+    o.y0i[k] = d.y0i[k];
+    o.esc[k] = d.elem_scale[k];
+  }
+  o.tol = d.tol;
+  o.gamma = d.gamma;
+  o.eps = d.eps;
+  o.gmax = d.gmax;
+  o.gsrc = d.gsrc;
+  o.start = d.start;
+  o.rows_V0 = d.rows_V0;
+  o.rows_G = d.rows_G;
+  o.min_iter = d.min_iter;
+  o.n_rep = d.n_rep;
+  o.n_rows = d.n_rows;
+  o.max_iter = max_iter;
+  return o;
+}
+
+// NaN-propagating max: an env whose change is NaN never passes the test.
+__device__ __forceinline__ double od_max(double a, double b) { return (b > a || b != b) ? b : a; }
+
+// Check rows into LDS in the resident row layout (pf_row_load / pf_row4_dpp).
+template <int M>
+__device__ __forceinline__ void od_rows_stage(const double* V0, const double* G, int rows, double* s) {
+  constexpr int S = 16 * PFRow<M>::kPairs;
+  for (int i = threadIdx.x; i < rows * S; i += kBlock) {
+    const int o = i / S, j = i - o * S;
+    double v = 0.0;
+    if (j < 2) v = V0[2 * o + j];
+    else if (j < 2 + M) v = G[2 * M * o + 2 * (j - 2)];
+    else if (j < 2 + 2 * M) v = G[2 * M * o + 2 * (j - 2 - M) + 1];
+    s[i] = v;
+  }
+}
+
+// Rows [0, R) from the currents J: err <- max | |V_r| - old_r |, amin <- min
+// old_r over the evaluated rows, old_r <- |V_r| unless the env has stopped.
+// Four rows per DPP group; every lane runs it (the broadcasts read all lanes).
+template <int M>
+__device__ __forceinline__ void od_rows(const double* s, double* s_old, int R, const double (&ir)[M],
+                                        const double (&ii)[M], bool done, double& err, double& amin) {
+  constexpr int P = PFRow<M>::kPairs;
+  const int tid = threadIdx.x;
+  const int last = R - 1;
+  for (int o = 0; o < R; o += 4) {
+    double wa[P], wb[P], wc[P], wd[P];
+    pf_row_load<M>(s, o, wa);
+    pf_row_load<M>(s, min(o + 1, last), wb);
+    pf_row_load<M>(s, min(o + 2, last), wc);
+    pf_row_load<M>(s, min(o + 3, last), wd);
+    double ar, ai, br, bi, cr, ci, dr, di;
+    pf_row4_dpp<M>(ar, ai, br, bi, cr, ci, dr, di, wa, wb, wc, wd, ir, ii);
+    const double mg[4] = {pf_mag<M>(ar, ai), pf_mag<M>(br, bi), pf_mag<M>(cr, ci), pf_mag<M>(dr, di)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (o + q < R) {                                  // (uniform)
+        double* op = s_old + (o + q) * kBlock + tid;
+        const double old = *op;
+        err = od_max(err, fabs(mg[q] - old));
+        amin = fmin(amin, old);
+        if (!done) *op = mg[q];
+      }
+    }
+  }
+}
+
+// The env's test after an iteration: lo = the exact changes (element nodes
+// and the evaluated rows), hi = lo plus the bounds of the unevaluated rows.
+// Returns 1 converged, 0 not, -1 undecided (the bounds straddle tol).
+__device__ __forceinline__ int od_decide(const ODArgs& o, bool full, int it, double lo, double amin,
+                                         double dsum, double jsum) {
+  if (it < o.min_iter || lo > o.tol || lo != lo) return 0;
+  if (full) return lo <= o.tol ? 1 : 0;
+  const double d = o.gmax * dsum;                       // >= |dV| of any evaluated node
+  if (!(amin - d > 0.0)) return -1;
+  // members: err_j <= err_r + |d_j - d_r| + 2 |V_j - V_r| |d_r| / (|V_r| - |d_r|)
+  const double delta = o.gamma * dsum + 2.0 * (o.eps + o.gamma * jsum) * d / (amin - d);
+  const double hi = fmax(lo + delta, o.gsrc * dsum);   // source side: err_j <= |d_j|
+  return hi <= o.tol ? 1 : -1;
+}
+
+// The whole snap solve of the lane's env (S: block, powers loaded).  lir / lii
+// end as the currents of the accepted iteration (the output rows' input).
+// Returns the iteration count, negative when stopped by max_iter.
+template <int M>
+__device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid, const double* s_rows,
+                        double* s_old, double (&lir)[M], double (&lii)[M]) {
+  const int tid = threadIdx.x;
+  for (int pass = 0;; ++pass) {                        // (uniform) fast, then full if undecided
+    const bool full = pass > 0 || o.n_rep >= o.n_rows;
+    const int R = full ? o.n_rows : o.n_rep;
+    // ---- iteration 1: J_0 = I'(u0) (kept: the change bound's previous
+    // currents), u_1 and the rows' V_1 from the affine table; previous
+    // magnitudes = the direct solution's
+    pf_u0<M>(S.ur, S.ui, S.w);
+    double dsum = 0.0, err = 0.0, amin = __builtin_huge_val();
+    static_for<0, M>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      S.template current_od<k>(o.y0r[k], o.y0i[k], lir[k], lii[k]);
+      dsum += fabs(lir[k]) + fabs(lii[k]);
+    });
+    const double* st = o.start;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      const double mo = sqrt(fma(S.ui[k], S.ui[k], S.ur[k] * S.ur[k])) * o.esc[k];
+      const double nr = fma(S.qc, st[2 * (2 * M + k)], fma(S.pc, st[2 * (M + k)], st[2 * k]));
+      const double ni = fma(S.qc, st[2 * (2 * M + k) + 1], fma(S.pc, st[2 * (M + k) + 1], st[2 * k + 1]));
+      S.ur[k] = nr;
+      S.ui[k] = ni;
+      const double mn = sqrt(fma(ni, ni, nr * nr)) * o.esc[k];
+      if (o.esc[k] > 0.0) {                           // (uniform) the element is a node
+        err = od_max(err, fabs(mn - mo));
+        amin = fmin(amin, mo);
+      }
+      s_old[(kOdRows + k) * kBlock + tid] = mn;
+    }
+    for (int r = 0; r < R; ++r) {                     // (uniform)
+      const double* v0 = s_rows + 16 * PFRow<M>::kPairs * r;   // staged V0 re, im
+      const double mo = sqrt(fma(v0[1], v0[1], v0[0] * v0[0]));
+      const double* q = st + 6 * M + 6 * r;
+      const double vr = fma(S.qc, q[4], fma(S.pc, q[2], q[0]));
+      const double vi = fma(S.qc, q[5], fma(S.pc, q[3], q[1]));
+      const double mn = sqrt(fma(vi, vi, vr * vr));
+      err = od_max(err, fabs(mn - mo));
+      amin = fmin(amin, mo);
+      s_old[r * kBlock + tid] = mn;
+    }
+    int it = 1, my_it = 1;
+    bool done = !valid, conv_ok = !valid, undecided = false;
+    {
+      const int d = od_decide(o, full, it, err, amin, dsum, 0.0);
+      undecided = !done && d < 0;
+      conv_ok = conv_ok || (!done && d > 0);
+      done = done || d > 0 || it >= o.max_iter;
+    }
+    if (__ballot(undecided) != 0ull) continue;
+    while (__ballot(!done) != 0ull) {
+      // ---- currents of u_{k-1} (kept, with the change sums), u_k by the matvec
+      double A[M], Bs[M], C[M];
+      pf_acc_init<M>(A, C, S.w);
+#pragma unroll
+      for (int i = 0; i < M; ++i) Bs[i] = 0.0;
+      dsum = 0.0;
+      double jsum = 0.0;
+      auto column = [&](auto kk, double ir, double ii) {
+        constexpr int k = decltype(kk)::value;
+        dsum += fabs(ir - lir[k]) + fabs(ii - lii[k]);
+        jsum += fabs(lir[k]) + fabs(lii[k]);
+        pf_column<M, k>(A, Bs, C, S.w, ir, ii, ir + ii);
+        lir[k] = done ? lir[k] : ir;
+        lii[k] = done ? lii[k] : ii;
+      };
+      static_for<0, M / 2>([&](auto h) {
+        constexpr int k0 = 2 * h, k1 = 2 * h + 1;
+        double ir0, ii0, ir1, ii1;
+        S.template current_od<k0>(o.y0r[k0], o.y0i[k0], ir0, ii0);
+        S.template current_od<k1>(o.y0r[k1], o.y0i[k1], ir1, ii1);
+        column(std::integral_constant<int, k0>{}, ir0, ii0);
+        column(std::integral_constant<int, k1>{}, ir1, ii1);
+      });
+      if constexpr (M % 2) {
+        double ir, ii;
+        S.template current_od<M - 1>(o.y0r[M - 1], o.y0i[M - 1], ir, ii);
+        column(std::integral_constant<int, M - 1>{}, ir, ii);
+      }
+      err = 0.0;
+      amin = __builtin_huge_val();
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const double nr = A[i] - Bs[i];
+        const double ni = (C[i] - A[i]) - Bs[i];
+        if (o.esc[i] > 0.0) {                         // (uniform)
+          double* op = s_old + (kOdRows + i) * kBlock + tid;
+          const double mo = *op, mn = sqrt(fma(ni, ni, nr * nr)) * o.esc[i];
+          err = od_max(err, fabs(mn - mo));
+          amin = fmin(amin, mo);
+          if (!done) *op = mn;
+        }
+        S.ur[i] = done ? S.ur[i] : nr;
+        S.ui[i] = done ? S.ui[i] : ni;
+      }
+      od_rows<M>(s_rows, s_old, R, lir, lii, done, err, amin);
+      ++it;
+      const int d = od_decide(o, full, it, err, amin, dsum, jsum);
+      undecided = !done && d < 0;
+      my_it = done ? my_it : it;
+      conv_ok = conv_ok || (!done && d > 0);
+      done = done || d > 0 || it >= o.max_iter;
+      if (__ballot(undecided) != 0ull) break;
+    }
+    if (__ballot(undecided) != 0ull) continue;     // (uniform) re-run with every row
+    return conv_ok ? my_it : -my_it;
+  }
+}
+
+// Fused C4 step, OpenDSS rule: k_coord_pf's prologue (agent powers -> bus
+// load) and epilogue (output row 0 = the coordinated bus, violation, reward),
+// the snap solve in between.
+template <int M, class Bufs>
+__global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
+                                                        int64_t n, Bufs b) {
+  using Sto = std::remove_pointer_t<decltype(b.reward)>;
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = e < n;
+  __shared__ double s_chk[kOdRows * 16 * PFRow<M>::kPairs];
+  __shared__ double s_old[kOdOld * kBlock];
+  od_rows_stage<M>(o.rows_V0, o.rows_G, o.n_rows, s_chk);
+  double rp[PGW_MAX_AGENTS];
+  const int64_t ec = valid ? e : 0;
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+    rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
+             ((valid && ag < c.n_agents) ? 1.0 : 0.0);
+  PFSolver<M, true, false> S;
+  S.load(a, t.block);
+  double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
+#pragma unroll
+  for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
+    cp[s] = 0.0;
+    cq[s] = 0.0;
+  }
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag) {
+    const int slot = ag < c.n_agents ? c.agent_ctrl[ag] : -1;
+#pragma unroll
+    for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
+  }
+  S.powers(a, cp, cq, 1.0);
+  __syncthreads();                                   // the staged check rows
+  double lir[M], lii[M];
+  const int it = od_solve<M>(S, o, valid, s_chk, s_old, lir, lii);
+  double v0r, v0i;
+  pf_node0<M>(v0r, v0i, S.w, lir, lii);
+  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  if (!valid) return;
+  if (b.v_out) b.v_out[e] = (Sto)v0;
+  if (b.iters) b.iters[e] = it;
+  if (c.coordinated) {
+    const double vv = pymax(pymax(0.0, c.vv_lo - v0), v0 - c.vv_hi);
+    if (b.vv) b.vv[e] = (Sto)vv;
+    const double share = (vv * c.vv_penalty) / (double)c.n_agents;
+#pragma unroll
+    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+      if (ag < c.n_agents)
+        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// pgw_pf_solve, OpenDSS rule: k_pf_solve's prologue (the env's controllable
+// powers) and outputs (every output row from the accepted iteration's currents,
+// extrema, element voltages), the snap solve in between.
+template <int M>
+__global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_pf_tables t, int64_t n,
+                                                        const double* __restrict__ ctrl_p,
+                                                        const double* __restrict__ ctrl_q,
+                                                        double* __restrict__ v_out,
+                                                        int32_t* __restrict__ iters) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = e < n;
+  __shared__ double s_chk[kOdRows * 16 * PFRow<M>::kPairs];
+  __shared__ double s_old[kOdOld * kBlock];
+  __shared__ double s_rows[kRowsLds];
+  od_rows_stage<M>(o.rows_V0, o.rows_G, o.n_rows, s_chk);
+  const bool rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
+  PFSolver<M, true, false> S;
+  S.load(a, t.block);
+  double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
+#pragma unroll
+  for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
+    cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
+    cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
+  }
+  S.powers(a, cp, cq, 1.0);
+  __syncthreads();                                   // the staged check and output rows
+  double lir[M], lii[M];
+  const int it = od_solve<M>(S, o, valid, s_chk, s_old, lir, lii);
+  double v0r, v0i;
+  pf_node0<M>(v0r, v0i, S.w, lir, lii);
+  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  if (valid && t.U_out) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      t.U_out[2 * (e * M + k)] = S.ur[k];
+      t.U_out[2 * (e * M + k) + 1] = S.ui[k];
+    }
+  }
+  double vmn = v0, vmx = v0;
+  pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, lir, lii, [&](int ro, double v) {
+    if (valid && v_out) v_out[(int64_t)ro * n + e] = v;
+    vmn = (v < vmn) ? v : vmn;
+    vmx = (v > vmx) ? v : vmx;
+  });
+  if (!valid) return;
+  if (a.n_out > 0) {
+    if (v_out) v_out[e] = v0;
+    if (t.v_min_out) t.v_min_out[e] = vmn;
+    if (t.v_max_out) t.v_max_out[e] = vmx;
+  }
+  if (iters) iters[e] = it;
+}
+
 // Stencil metadata of the predictor grid (one thread per segment): in a
 // segment whose two ends share the band signature the switch sits at t* = 1/2
 // (the nearest-point rule) and both sides use a 3-point stencil of that
@@ -1170,6 +1520,19 @@ __global__ void __launch_bounds__(kBlock) k_band_penalty(int64_t n, const double
   out[e] = -(y * y);
 }
 
+// OpenDSS rule on the fast kernels (pgw_pf_tables.od): the C4 shape only.
+static int32_t check_od(const pgw_pf_params& p, const pgw_pf_tables& t, const char* who) {
+  const pgw_pf_od* d = t.od;
+  PGW_REQUIRE(p.m == 14 && uniform_band(p) && p.n_ctrl <= 1 && !t.load_scale && !t.U_init,
+              "%s: the OpenDSS fast path needs m = 14, one voltage band, <= 1 controllable slot and no "
+              "load_scale / U_init (use pgw_pf_solve_general)", who);
+  PGW_REQUIRE(d->n_rows >= 0 && d->n_rows <= PGW_PF_OD_MAX_ROWS && d->n_rep >= 0 && d->n_rep <= d->n_rows,
+              "%s: od n_rep %d / n_rows %d (<= %d)", who, d->n_rep, d->n_rows, PGW_PF_OD_MAX_ROWS);
+  PGW_REQUIRE(d->start && (d->n_rows == 0 || (d->rows_V0 && d->rows_G)), "%s: od start / rows missing", who);
+  PGW_REQUIRE(d->min_iter >= 1 && p.max_iter >= 1 && d->tol >= 0.0, "%s: od min_iter / max_iter / tol", who);
+  return PGW_OK;
+}
+
 // Instantiated variants: IEEE-13 (m = 14) with a uniform band, at most one
 // controllable slot and no per-env load scale is the fast path (with one
 // output row accumulated inside the loop, or the last currents kept for any
@@ -1238,6 +1601,10 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   const bool std_layout = coord_is_std(*p);
   PGW_REQUIRE(std_layout || !kF32,
               "pgw_coord_step_f32: needs the standard C4 agent layout (building/pv/storage at 0/6/7)");
+  if (pft->od) {
+    const int32_t rc_od = check_od(*pf, *pft, "pgw_coord_step");
+    if (rc_od) return rc_od;
+  }
   // PVEnv.get_obs is the same for every env: evaluate it once here
   const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
                                         - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
@@ -1271,6 +1638,11 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
+  if (pft->od) {
+    launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs>, dim3(grid_for(n)), dim3(kBlock), st, c, a,
+                 make_od_args(*pft->od, pf->max_iter), *pft, n, b);
+    return check_launch("k_coord_pf_od");
+  }
   PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
 }
 
@@ -1429,8 +1801,17 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
   PGW_REQUIRE(p->n_out == 0 || v_out || t->v_min_out || t->v_max_out,
               "pgw_pf_solve: n_out > 0 but no output (v_out, v_min_out, v_max_out all NULL)");
   PGW_REQUIRE(p->max_iter >= 1, "pgw_pf_solve: max_iter < 1");
+  if (t->od) {
+    const int32_t rc = check_od(*p, *t, "pgw_pf_solve");
+    if (rc) return rc;
+  }
   if (n == 0) return PGW_OK;
   const PFArgs a = make_pf_args(*p, *t);
+  if (t->od) {
+    launch_timed(PGW_T_PF_SOLVE, k_pf_solve_od<14>, dim3(grid_for(n)), dim3(kBlock), (hipStream_t)stream, a,
+                 make_od_args(*t->od, p->max_iter), *t, n, ctrl_p, ctrl_q, v_out, iters);
+    return check_launch("k_pf_solve_od");
+  }
   PGW_PF_DISPATCH(*p, *t, launch_pf_solve, a, *t, n, ctrl_p, ctrl_q, v_out, iters, (hipStream_t)stream);
 }
 

@@ -87,9 +87,17 @@ class OpenDSSSolver(PowerFlowSolver):
         # the fast kernels hold up to PF_MAX_M constant-PQ elements; larger feeders,
         # other load models and OpenDSS's stopping rule run the general kernel
         self.regulators = None
-        self.general = (bool(general) or convergence == "opendss" or self.feeder.m > _lib.PF_MAX_M
-                        or bool((self.feeder.elem_model != 1).any())
-                        or bool(spec.get("regcontrols") and spec.get("controlmode", "static") != "off"))
+        f = self.feeder
+        regctl = bool(spec.get("regcontrols") and spec.get("controlmode", "static") != "off")
+        model1 = not bool((f.elem_model != 1).any())
+        # OpenDSS's rule on the fast kernels (pgw_pf_tables.od): the C4 shape --
+        # 14 constant-PQ elements in one voltage band, no RegControl; at most one
+        # controllable load (set_controllable_loads falls back beyond that)
+        self._od_fast = (convergence == "opendss" and not general and not regctl and model1 and
+                         f.m <= _lib.PF_MAX_M and int(_lib.lib().pgw_pf_padded_m(f.m)) == 14 and
+                         len({(a, b, c) for a, b, c in zip(f.elem_vmin, f.elem_vmax, f.elem_vlow)}) == 1)
+        self.general = (bool(general) or (convergence == "opendss" and not self._od_fast)
+                        or f.m > _lib.PF_MAX_M or not model1 or regctl)
         if self.feeder.m > _lib.PFG_MAX_M:
             raise ValueError("feeder has %d load phase elements (max %d)" % (self.feeder.m, _lib.PFG_MAX_M))
         if convergence == "opendss":
@@ -149,7 +157,9 @@ class OpenDSSSolver(PowerFlowSolver):
         idx = [f.node_index[n] for n in names]
         if self.general:
             return self._set_general_tables(idx)
-        M, W, U0, G, V0o = f.reduce(idx)
+        # OpenDSS rule: the reduction of its iteration matrix (Y + the loads' Yeq;
+        # U0 = the direct solution)
+        M, W, U0, G, V0o = (self._fd_iter if self._od_fast else f).reduce(idx)
         self.M = M
         self._base_params()
         dev = self.device
@@ -194,6 +204,139 @@ class OpenDSSSolver(PowerFlowSolver):
         self._pred_meta = torch.zeros((self.PREDICTOR_MAX_TABLES, n_pred - 1, 2), dtype=torch.float64,
                                       device=dev)
         self._pred_index = {}
+        if self._od_fast:
+            self._set_od_tables(W, U0, vb_elem)
+
+    # ------------------------------------------------------------ OpenDSS rule, fast kernels
+    OD_MAX_TABLES = 64            # hours of first-iteration tables kept on the device
+
+    def _set_od_tables(self, W, U0, vb_elem):
+        """pgw_pf_od (include/pgw.h): the loads' Yeq powers y0', the element-node
+        scales, the check rows -- every node that is not an element's terminal:
+        evaluated rows first, then members (electrically next to an evaluated
+        row or an element node) and source-side nodes, both bounded -- and the
+        bound constants.  OpenDSS's test runs over every node (Solution.pas
+        Converged); the bounds only decide which rows the kernel must evaluate."""
+        f, fi, M = self.feeder, self._fd_iter, self.M
+        m, n = f.m, f.n
+        vbn = f.kv_ln * 1000.0
+        _, _, Gall, V0all = fi.reduce_rows(list(range(n)))
+        Gs = np.zeros((n, M), complex)
+        Gs[:, :m] = (Gall / f.elem_vbase[None, :]) / vbn[:, None]
+        V0s = V0all / vbn
+        od = _lib.PFOD()
+        od.tol, od.min_iter = self.tol, self.min_iter
+        elem_nodes = []
+        for k in range(m):
+            li = f.elem_load[k]
+            od.y0r[k] = f.base_kw[li] * 1000.0 / f.elem_nph[k]
+            od.y0i[k] = -(f.base_kvar[li] * 1000.0 / f.elem_nph[k])
+            if f.elem_q[k] < 0:                      # phase node -> ground: the node itself
+                od.elem_scale[k] = f.elem_vbase[k] / vbn[f.elem_p[k]]
+                elem_nodes.append(int(f.elem_p[k]))
+        rowmax = np.abs(Gs).max(1)
+        others = [i for i in range(n) if i not in elem_nodes]
+        src = [i for i in others if rowmax[i] <= 1e-2 * rowmax.max()]
+        reps, members = [], []
+        for j in others:
+            if j in src:
+                continue
+            best = None
+            for r in elem_nodes + reps:
+                g = np.abs(Gs[j] - Gs[r]).max()
+                if g <= 1e-5 * rowmax[r] and abs(V0s[j] - V0s[r]) <= 1e-5 and (best is None or g < best[0]):
+                    best = (g, r)
+            if best is None:
+                reps.append(j)
+            else:
+                members.append((j, best[1]))
+        rows = reps + [j for j, _ in members] + src
+        if len(rows) > _lib.PF_OD_MAX_ROWS:
+            raise ValueError("%d check rows (max %d)" % (len(rows), _lib.PF_OD_MAX_ROWS))
+        od.n_rep, od.n_rows = len(reps), len(rows)
+        od.gamma = max([float(np.abs(Gs[j] - Gs[r]).max()) for j, r in members], default=0.0)
+        od.eps = max([float(abs(V0s[j] - V0s[r])) for j, r in members], default=0.0)
+        od.gmax = float(rowmax[elem_nodes + reps].max())
+        od.gsrc = float(rowmax[src].max()) if src else 0.0
+        dev = self.device
+        cdev = lambda a: torch.tensor(np.ascontiguousarray(a).view(np.float64).ravel(), dtype=torch.float64,
+                                      device=dev)
+        self._od_rows_V0 = cdev(V0s[rows] if rows else np.zeros(1, complex))
+        self._od_rows_G = cdev(Gs[rows] if rows else np.zeros((1, M), complex))
+        od.rows_V0, od.rows_G = self._od_rows_V0.data_ptr(), self._od_rows_G.data_ptr()
+        self._od_proto = od
+        self._od_rows = [f.node_names[i] for i in rows]
+        self._od_rowdata = (Gs[rows], V0s[rows])
+        self._od_W2 = W / (vb_elem[:, None] * vb_elem[None, :])
+        self._od_u0 = U0 / vb_elem
+        self._od_start = torch.zeros((self.OD_MAX_TABLES, 6 * M + 6 * max(len(rows), 1)), dtype=torch.float64,
+                                     device=dev)
+        self._od_index = {}
+        self._od_keep = {}
+
+    def _od_starts(self, hour):
+        """First-iteration tables (pgw_pf_od.start) of `hour` and the following
+        hours that have none: from the direct solution u0 the currents are affine
+        in the controllable (P, Q), so u_1 and the check rows' V_1 are too."""
+        hours, keys = [], []
+        for h in range(hour, min(hour + self.PREDICTOR_LOOKAHEAD, len(self.annual_hourly_load_profile))):
+            k = self._hour_key(h)
+            if k not in self._od_index and k not in keys:
+                hours.append(h)
+                keys.append(k)
+        if len(self._od_index) + len(keys) > self.OD_MAX_TABLES:
+            self._od_index, self._tables_cache, self._od_keep = {}, {}, {}
+            self.tables_version += 1
+        idx0 = len(self._od_index)
+        M, od = self.M, self._od_proto
+        W2, u0 = self._od_W2, self._od_u0
+        Gr, V0r = self._od_rowdata
+        p0 = self.params
+        nph = np.array(p0.nph[:M])
+        ctrl0 = np.array(p0.elem_ctrl[:M]) == 0
+        fr = np.where(ctrl0, 1000.0 / nph, 0.0)
+        fi = np.where(ctrl0, -1000.0 / nph, 0.0)
+        y0 = np.array(od.y0r[:M]) + 1j * np.array(od.y0i[:M])
+        m2 = np.abs(u0) ** 2
+        lo2, mn2, mx2 = p0.vlow[0] ** 2, p0.vmin[0] ** 2, p0.vmax[0] ** 2
+        g = 1.0 / np.where(m2 <= lo2, 1.0, np.clip(m2, mn2, mx2))
+        jP, jQ = fr * g * u0, 1j * fi * g * u0
+        u1P, u1Q = W2 @ jP, W2 @ jQ
+        V1P, V1Q = Gr @ jP, Gr @ jQ
+        recs = np.zeros((len(hours), self._od_start.shape[1]))
+        for q, h in enumerate(hours):
+            p = self._params_for_hour(h)
+            s0 = (np.array(p.base_kw[:M]) * 1000.0) / nph - 1j * ((np.array(p.base_kvar[:M]) * 1000.0) / nph)
+            J0 = (s0 * g - y0) * u0
+            u = np.concatenate([u0 + W2 @ J0, u1P, u1Q])
+            rowsv = np.stack([V0r + Gr @ J0, V1P, V1Q], 1).ravel() if len(V0r) else np.zeros(3, complex)
+            rec = np.concatenate([u, rowsv]).view(np.float64)
+            recs[q, :rec.size] = rec
+        for j, k in enumerate(keys):
+            self._od_index[k] = idx0 + j
+        if hours:
+            self._od_start[idx0:idx0 + len(hours)].copy_(torch.from_numpy(recs), non_blocking=False)
+
+    def _od_tables(self, hour):
+        key = (hour, self._cfg_version)
+        t = self._tables_cache.get(key)
+        if t is not None:
+            return t
+        idx = self._od_index.get(self._hour_key(hour))
+        if idx is None:
+            self._od_starts(hour)
+            idx = self._od_index[self._hour_key(hour)]
+        od = _lib.PFOD.from_buffer_copy(self._od_proto)
+        od.start = self._od_start[idx].data_ptr()
+        t = _lib.PFTables.from_buffer_copy(self.tables)
+        t.od = _lib.C.addressof(od)
+        t._od_ref = od                     # the struct lives as long as these tables
+        if len(self._tables_cache) > 4096:
+            self._tables_cache.clear()
+            self._od_keep.clear()
+        self._tables_cache[key] = t
+        self._od_keep[key] = od            # the tables hold its address
+        return t
 
     # ------------------------------------------------------------ general kernel
     def _set_general_tables(self, idx):
@@ -325,7 +468,12 @@ class OpenDSSSolver(PowerFlowSolver):
         if names != self._ctrl_names:
             self._ctrl_names = names
             self._seen_keys = None
-            self._base_params()
+            if self._od_fast and len(names) > 1:
+                # the fast OpenDSS kernels take one controllable slot: the general kernel
+                self._od_fast, self.general = False, True
+                self.set_output_nodes(self.output_names)
+            else:
+                self._base_params()
 
     def _base_params(self):
         if self.general:
@@ -351,6 +499,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self._step_cache = {}
         self._tables_cache = {}
         self._pred_index = {}
+        self._od_index, self._od_keep = {}, {}     # (first-iteration tables depend on the slots)
         self._warm = None              # (cold, warm) PFTables over the previous solutions
 
     def _base_params_general(self):
@@ -430,6 +579,8 @@ class OpenDSSSolver(PowerFlowSolver):
         PREDICTOR_LOOKAHEAD - 1 hours in ONE launch (the hours differ only by
         the loadshape coefficient, passed as a per-env load scale), so an
         episode pays for about one table solve.  Otherwise the cold-start tables."""
+        if self._od_fast:
+            return self._od_tables(self.hour_of(current_time))
         if self.general or not (self.use_predictor and len(self._ctrl_names) == 1):
             return self.tables
         hour = self.hour_of(current_time)
@@ -636,7 +787,7 @@ class OpenDSSSolver(PowerFlowSolver):
         """The PFTables a solve at `current_time` uses: the hour's predictor tables
         (one controllable load), else the cold-start tables -- or, with
         warm_start, the ones over each env's previous solution."""
-        tables = self.step_tables(current_time) if controllable else self.tables
+        tables = self.step_tables(current_time) if (controllable or self._od_fast) else self.tables
         if controllable and self.warm_start and tables is self.tables:
             tables = self._warm_tables()
         return tables

@@ -89,7 +89,7 @@ def test_opendss_semantics_ieee13_vs_oracle():
     restatement of OpenDSS's snap solve -- the same iteration count for every
     env, every node within 1e-9 rel -- and measurably not the fixed point."""
     K = 4096
-    s = _solver(IEEE13, system_load_rescale_factor=1.2, num_envs=K, convergence="opendss")
+    s = _solver(IEEE13, system_load_rescale_factor=1.2, num_envs=K, convergence="opendss", general=True)
     assert s.general and s.tol == 1e-4 and s.max_iter == 15 and s.min_iter == 2
     g, o, git, oit = _run(s, _oracle(IEEE13, 1.2), TIMES, "675c", -400.0, 900.0, K,
                           np.random.default_rng(2), "opendss")
@@ -253,9 +253,11 @@ def test_general_kernel_multi_bus_warm_start():
 
 
 def _c4_pair(n, convergence):
+    """(fused, generic) C4 envs on the GENERAL power flow (the fast kernels'
+    OpenDSS rule: tests/test_gpu_pf_od.py)."""
     from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
-    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=convergence), num_envs=n,
-                                               device=DEV, fused=f) for f in (True, False)]
+    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=convergence, pf_general=True),
+                                               num_envs=n, device=DEV, fused=f) for f in (True, False)]
     return envs
 
 

@@ -1,0 +1,203 @@
+"""OpenDSS's snap-solve rule on the fast one-lane-per-env kernels
+(pgw_pf_tables.od; csrc/pgw_pf.hip k_pf_solve_od / k_coord_pf_od): the C4
+shape (IEEE-13, one controllable load).  Needs an MI355X.
+
+PF parity is unpinned (no OpenDSS in this image): the results are
+checked against the oracle's NumPy restatement of OpenDSS's snap solve,
+oracle/pf_oracle.py Feeder.snap_opendss (the loads' Yeq in Y at the DSS
+file's kW, direct-solution start, every node's magnitude change <= 1e-4 from
+iteration 2, at most 15) -- equal iteration counts for every env, every node
+within 1e-9 rel -- and against the general kernel's implementation of the same
+rule.  The fast kernels evaluate only some check rows and bound the others;
+the tests pin that this never changes a result: bounded (fast) == every row
+(full) == every wave re-run, bit for bit.
+"""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HERE = os.path.dirname(os.path.abspath(__file__))
+IEEE13 = "ieee_13_dss/IEEE13Nodeckt.dss"
+SHAPE = "ieee_13_dss/annual_hourly_load_profile.csv"
+TIMES = [pd.Timestamp("08-12-2021 %02d:10:00" % h) for h in (3, 11, 17, 20)]
+
+
+def _solver(**kw):
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    return OpenDSSSolver(IEEE13, SHAPE, device=DEV, system_load_rescale_factor=1.2, convergence="opendss", **kw)
+
+
+def _loads(K, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in TIMES:
+        p = rng.uniform(-400.0, 900.0, K)
+        q = rng.uniform(-0.3, 0.5, K) * np.abs(p)
+        out.append((p, q))
+    return out
+
+
+def _solve_all(s, loads):
+    """[T, n_nodes, K] pu and [T, K] iterations of s over TIMES."""
+    v, it = [], []
+    for t, (p, q) in zip(TIMES, loads):
+        s.calculate_power_flow({"675c": torch.tensor(p, device=DEV)}, {"675c": torch.tensor(q, device=DEV)},
+                               current_time=t)
+        bv = s.get_bus_voltages()
+        v.append(torch.stack([bv[nm] for nm in s.feeder.node_names]).clone())
+        it.append(s.iterations.clone())
+    torch.cuda.synchronize()
+    return torch.stack(v), torch.stack(it)
+
+
+def test_od_fast_kernel_selected():
+    s = _solver(num_envs=8)
+    assert s._od_fast and not s.general and s.M == 14
+    od = s._od_proto
+    assert 0 < od.n_rep < od.n_rows <= 32 and od.min_iter == 2 and od.tol == 1e-4
+    # every node is covered exactly once: an element's terminal or a check row
+    elem = {s.feeder.node_names[s.feeder.elem_p[k]] for k in range(s.feeder.m) if s.feeder.elem_q[k] < 0}
+    assert sorted(elem | set(s._od_rows)) == sorted(s.feeder.node_names) and not (elem & set(s._od_rows))
+    s.set_controllable_loads(["675a", "675c"])           # two slots: the general kernel
+    assert s.general and not s._od_fast
+    g = _solver(num_envs=8, general=True)
+    assert g.general and not g._od_fast
+
+
+def test_od_ieee13_vs_oracle_and_general_kernel():
+    """The fast kernel's stopped iterate equals the oracle's restatement of
+    OpenDSS's snap solve (same iterations, every node within 1e-9 rel) and the
+    general kernel's (same iterations, 1e-11 rel)."""
+    from oracle.pf_oracle import BatchedPF
+    K = 4096
+    loads = _loads(K, 2)
+    v, it = _solve_all(_solver(num_envs=K), loads)
+    vg, itg = _solve_all(_solver(num_envs=K, general=True), loads)
+    assert torch.equal(it, itg)
+    torch.testing.assert_close(v, vg, rtol=1e-11, atol=0)
+    o = BatchedPF(system_load_rescale_factor=1.2)
+    f = o.feeder
+    for i, (t, (p, q)) in enumerate(zip(TIMES, loads)):
+        kw, kvar = o.loads(t, {"675c": p}, {"675c": q}, K=K)
+        V, oit = f.snap_opendss(kw, kvar, f.base_kw, f.base_kvar)
+        np.testing.assert_array_equal(it[i].cpu().numpy(), oit)
+        np.testing.assert_allclose(v[i].cpu().numpy().T, f.pu(V), rtol=1e-9, atol=0)
+    assert set(np.unique(it.cpu().numpy())) <= set(range(2, 16))
+
+
+def test_od_bounded_rows_equal_every_row_and_rerun():
+    """The bounded check rows never change a result: the fast kernel equals
+    the same solve with every row evaluated (n_rep = n_rows), and a solve whose
+    bounds can never decide (every wave re-runs with every row) -- bit for bit,
+    iteration counts included."""
+    K = 4096
+    loads = _loads(K, 3)
+    ref = _solve_all(_solver(num_envs=K), loads)
+    for change in (dict(n_rep=None), dict(gsrc=1e9)):
+        s = _solver(num_envs=K)
+        if change.get("n_rep", 0) is None:
+            s._od_proto.n_rep = s._od_proto.n_rows
+        else:
+            s._od_proto.gsrc = change["gsrc"]
+        s._tables_cache.clear()
+        got = _solve_all(s, loads)
+        assert torch.equal(got[1], ref[1]), change
+        assert torch.equal(got[0], ref[0]), change
+
+
+def test_od_c4_fused_equals_generic_and_oracle():
+    """C4 with convergence="opendss" on the fast kernels: the fused step
+    (pgw_coord_step + k_coord_pf_od) is bit-identical to the generic path
+    (component kernels + k_pf_solve_od) and matches the NumPy C4 oracle with
+    OpenDSS's snap semantics: rewards, violation, V675.3, iteration counts."""
+    from oracle.ma_oracle import CoordinatedOracle
+    from oracle.pf_oracle import BatchedPF
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    n = 256
+    fused, generic = [CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence="opendss"), num_envs=n,
+                                                         device=DEV, fused=f) for f in (True, False)]
+    assert fused._fused is not None and fused._fused["kernel"] == "pgw_coord_step" and fused.pf_solver._od_fast
+    assert generic._fused is None and generic.pf_solver._od_fast
+    rng = np.random.default_rng(11)
+    init = rng.uniform(5.0, 45.0, size=(5, n))
+    for env in (fused, generic):
+        env.reset()
+        for ai, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=torch.tensor(init[ai], device=DEV))
+        env.load_component_state()
+    ora = CoordinatedOracle(n)
+    ora.pf = BatchedPF(system_load_rescale_factor=1.2, semantics="opendss")
+    ora.reset(init)
+    for t in range(40):
+        act = rng.uniform(-1, 1, size=(5, n, 8))
+        a_t = torch.tensor(act, device=DEV)
+        of, rf, _, mf = fused.step(a_t)
+        og, rg, _, mg = generic.step({a.name: {"building": a_t[i, :, :6], "pv": a_t[i, :, 6:7],
+                                               "storage": a_t[i, :, 7:8]} for i, a in enumerate(generic.agents)})
+        o_obs, o_rew, o_vv = ora.step(act)
+        torch.cuda.synchronize()
+        assert torch.equal(mf["voltage_violation"], mg["voltage_violation"])
+        for a in fused.agents:
+            assert torch.equal(rf[a.name], rg[a.name])
+        assert torch.equal(fused.pf_solver.iterations, generic.pf_solver.iterations)
+        np.testing.assert_allclose(fused.packed_obs().cpu().numpy(), o_obs, rtol=1e-9, atol=1e-9)
+        r = np.stack([rf[a.name].cpu().numpy() for a in fused.agents])
+        np.testing.assert_allclose(r, o_rew, rtol=1e-7, atol=1e-7)
+        np.testing.assert_allclose(fused.pf_solver.get_bus_voltage_by_name("675c").cpu().numpy(), ora.v,
+                                   rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(fused.pf_solver.iterations.cpu().numpy(), ora.pf.last_iters)
+    v_f, v_g = fused.voltages, generic.voltages
+    for nm in ("632.1", "671.2", "652.1", "675.3"):
+        assert torch.equal(v_f[nm], v_g[nm])
+
+
+def test_od_c4_two_episodes_tiled_full_batch():
+    """The BASELINE batch (65,536 envs, fused, OpenDSS rule) on the
+    c4_two_episodes golden action streams tiled over the batch, against the C4
+    oracle with OpenDSS's snap solve run on the golden envs: every env's
+    iteration count equal at every step of both episodes, V675.3 within 1e-10
+    rel, violation within 1e-11, rewards within 1e-7 (errors accumulated on the
+    device, one check per episode)."""
+    from oracle.ma_oracle import CoordinatedOracle
+    from oracle.pf_oracle import BatchedPF
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    g = np.load(os.path.join(HERE, "golden", "c4_two_episodes.npz"))
+    E, Tn, NA, K, _ = g["actions"].shape
+    n = 65536
+    idx = torch.arange(n, device=DEV) % K
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence="opendss"), num_envs=n, device=DEV,
+                                             fused=True)
+    assert env._fused["kernel"] == "pgw_coord_step" and env.pf_solver._od_fast
+    T = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device=DEV)
+    acts = T(g["actions"])[:, :, :, idx]
+    ora = CoordinatedOracle(K)
+    ora.pf = BatchedPF(system_load_rescale_factor=1.2, semantics="opendss")
+    hist = {2: 0, 3: 0, 4: 0, 5: 0}
+    for e in range(E):
+        err = torch.zeros(4, dtype=torch.float64, device=DEV)
+        env.reset()
+        for a, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=T(g["init_storage"][e, a])[idx])
+        ora.reset(g["init_storage"][e])
+        for t in range(Tn):
+            _, rew, dones, meta = env.step(acts[e, t])
+            _, o_rew, o_vv = ora.step(g["actions"][e, t])
+            want_it = T(ora.pf.last_iters.astype(np.float64))[idx]
+            for i in np.unique(ora.pf.last_iters):
+                hist[int(i)] = hist.get(int(i), 0) + 1
+            r = torch.stack([rew[a.name] for a in env.agents])
+            wr = T(o_rew)[:, idx]
+            err[0] = torch.maximum(err[0], ((r - wr).abs() / (1e-7 + 1e-7 * wr.abs())).max())
+            err[1] = torch.maximum(err[1], (meta["voltage_violation"] - T(o_vv)[idx]).abs().max())
+            v = env.pf_solver.get_bus_voltage_by_name("675c")
+            err[2] = torch.maximum(err[2], ((v - T(ora.v)[idx]).abs() / T(ora.v)[idx]).max())
+            err[3] = err[3] + (env.pf_solver.iterations.double() != want_it).sum()
+            assert dones["__all__"] == bool(g["done"][e, t, 0])
+        err = err.cpu().numpy()
+        assert err[0] <= 1 and err[1] < 1e-11 and err[2] < 1e-10 and err[3] == 0, (e, err)
+    assert hist[3] + hist[4] > 0, hist

@@ -1,0 +1,63 @@
+"""C4 at 65,536 envs: exact fixed point vs OpenDSS rule (fast kernels) vs
+OpenDSS rule (general kernel) -- us/step over a driver-shaped region and the
+PF kernel's event-timed mean.  Usage: python tools/gpu/od_probe.py [--steps 200]"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from powergridworld_amd import _lib  # noqa: E402
+from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config  # noqa
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=200)
+ap.add_argument("--n", type=int, default=65536)
+ap.add_argument("--modes", default="exact,opendss,opendss_general")
+ap.add_argument("--rows", default="", help="opendss only: 'none' (no check row evaluated; results wrong) "
+                                         "or 'all' (every row every iteration), for phase costs")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+n = a.n
+gen = torch.Generator(dev).manual_seed(0)
+pool = torch.empty((16, 5, 8, n), dtype=torch.float64, device=dev).uniform_(-1, 1, generator=gen).transpose(2, 3)
+for mode in a.modes.split(","):
+    conv = "exact" if mode == "exact" else "opendss"
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv, pf_general=mode.endswith("general")),
+                                             num_envs=n, device=dev, fused=True)
+    if a.rows and mode == "opendss":
+        od = env.pf_solver._od_proto
+        od.n_rep = 0 if a.rows == "none" else od.n_rows
+        if a.rows == "none":
+            od.n_rows = 0
+        env.pf_solver._tables_cache.clear()
+        env._fused["step_cache"].clear()
+    env.reset()
+    k = [0]
+
+    def run(m):
+        for _ in range(m):
+            _, _, d, _ = env.step(pool[k[0] % 16])
+            k[0] += 1
+            if d["__all__"]:
+                env.reset()
+    run(30)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(a.steps)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / a.steps * 1e6
+    _lib.check(_lib.lib().pgw_timing_start(1))
+    run(64)
+    torch.cuda.synchronize()
+    tot = (_lib.C.c_double * 6)()
+    cnt = (_lib.C.c_int64 * 6)()
+    _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
+    ks = {nm: round(tot[i] / cnt[i] * 1e3, 2) for i, nm in enumerate(("agents", "coord_pf", "pf_solve", "-", "ma", "pf_general")) if cnt[i]}
+    it = env.pf_solver.iterations.abs()
+    print("%-16s %7.2f us/step  kernels %s  iters mean %.3f max %d  kernel=%s" %
+          (mode + ("/" + a.rows if a.rows and mode == "opendss" else ""), us, ks, it.double().mean().item(), it.max().item(), env._fused["kernel"]), flush=True)
+    del env
+    torch.cuda.synchronize()
