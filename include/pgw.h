@@ -383,29 +383,29 @@ typedef struct pgw_pf_tables {
  * |u_k| elem_scale[k] (0 = the element is not a node).  The other nodes are
  * check rows (rows_V0 / rows_G: V = V0 + G I', pu of the node base against the
  * scaled currents, the layout of pgw_pf_tables.G): rows [0, n_rep) are
- * evaluated every iteration; rows [n_rep, n_rows) are bounded instead, members
- * (electrically next to a row or an element node: |G_j - G_r| <= gamma per
- * element, |V0_j - V0_r| <= eps) and source-side nodes (|G_j| <= gsrc per
+ * evaluated when a test needs them; rows [n_rep, n_rows) are bounded instead,
+ * members (electrically next to a row or an element node: |G_j - G_r| <= gamma
+ * per element, |V0_j - V0_r| <= eps) and source-side nodes (|G_j| <= gsrc per
  * element), with gmax >= |G_r| per element of every row and element node; when
  * a bound cannot decide an env's test, its wave re-runs the solve with every
- * row evaluated, so the stopping iteration is always the exact rule's.
+ * row evaluated, so the stopping iteration is always the exact rule's.  The
+ * rows are evaluated only in iterations where some env of the wave has no
+ * element node whose change is surely above tol (min_iter >= 2).
  *
  * start (device, this step's hour): the first iteration in closed form -- from
  * the direct solution the currents are affine in the env's controllable
- * (P, Q): u_1 = u1b + P u1P + Q u1Q (m complex each), then per row r
- * V_1r = V1b + P V1P + Q V1Q: u1b, u1P, u1Q (m complex each), then per row
- * (V1b, V1P, V1Q) complex. */
-#define PGW_PF_OD_MAX_ROWS 32
+ * (P, Q): u_1 = u1b + P u1P + Q u1Q; u1b, u1P, u1Q (m complex each). */
+#define PGW_PF_OD_MAX_ROWS 28
 typedef struct pgw_pf_od {
   double tol;                        /* 1e-4 (ConvergenceTolerance)            */
   double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M];   /* y0' per element (W, -var) */
   double elem_scale[PGW_PF_MAX_M];   /* node |V| pu = |u_k| * scale; 0 = none   */
   double gamma, eps, gmax, gsrc;     /* check-row bound constants (above)      */
-  int32_t min_iter;                  /* 2 (MinIterations)                      */
+  int32_t min_iter;                  /* 2 (MinIterations); >= 2                */
   int32_t n_rep, n_rows, pad_;
   const double* rows_V0;             /* n_rows complex (device)                */
   const double* rows_G;              /* n_rows x m complex (device)            */
-  const double* start;               /* (6 m + 6 n_rows) doubles (device)      */
+  const double* start;               /* 6 m doubles (device)                   */
 } pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

@@ -101,7 +101,7 @@ class PFTables(C.Structure):
                 ("load_scale", vp), ("v_min_out", vp), ("v_max_out", vp), ("od", vp)]
 
 
-PF_OD_MAX_ROWS = 32
+PF_OD_MAX_ROWS = 28
 
 
 class PFOD(C.Structure):

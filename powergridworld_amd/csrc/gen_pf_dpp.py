@@ -181,6 +181,25 @@ def gen_power(M, k, ns):
             % (M, k, ns, asm_stmt(lines, outs, ins)))
 
 
+def gen_od_elem(M, k):
+    """The OpenDSS solve's per-element Yeq powers from its resident table y (2
+    pairs: y0' re, y0' im; entry k in lane k % 16): y0r, y0i of element k."""
+    lines = ["v_mov_b64_dpp %%%d, %%2 row_newbcast:%d %s" % (0, k % 16, DPP),
+             "v_mov_b64_dpp %%%d, %%3 row_newbcast:%d %s" % (1, k % 16, DPP)]
+    outs = ['"=&v"(y0r)', '"=&v"(y0i)']
+    ins = ['"v"(y[0])', '"v"(y[1])']
+    return ("template <> __device__ __forceinline__ void pf_od_elem<%d, %d>(\n"
+            "    double& y0r, double& y0i, const double (&y)[2]) {\n%s}\n"
+            % (M, k, asm_stmt(lines, outs, ins)))
+
+
+def gen_bc16(k):
+    """Entry k of a 16-entry resident pair (lane k % 16 of each row)."""
+    lines = ["v_mov_b64_dpp %%0, %%1 row_newbcast:%d %s" % (k, DPP)]
+    return ("template <> __device__ __forceinline__ double pf_bc16<%d>(double y) {\n  double r;\n%s  return r;\n}\n"
+            % (k, asm_stmt(lines, ['"=&v"(r)'], ['"v"(y)'])))
+
+
 def gen_band(M, k, nr):
     L = block_layout(M)
     es = [L["lo2"] + k, L["mn2"] + k, L["mx2"] + k]
@@ -274,10 +293,15 @@ def main():
            "    double& di, const double (&wa)[PFRow<M>::kPairs], const double (&wb)[PFRow<M>::kPairs],",
            "    const double (&wc)[PFRow<M>::kPairs], const double (&wd)[PFRow<M>::kPairs],",
            "    const double (&ir)[M], const double (&ii)[M]);",
+           "template <int M, int K> __device__ __forceinline__ void pf_od_elem(",
+           "    double& y0r, double& y0i, const double (&y)[2]);",
+           "template <int K> __device__ __forceinline__ double pf_bc16(double y);",
            "template <int M> __device__ __forceinline__ void pf_row1_dpp(",
            "    double& ar, double& ai, const double (&wa)[PFRow<M>::kPairs], const double (&ir)[M],",
            "    const double (&ii)[M]);",
            ""]
+    for k in range(16):
+        out.append(gen_bc16(k))
     for M in SIZES:
         L = block_layout(M)
         nr = (L["size"] + 15) // 16
@@ -292,6 +316,7 @@ def main():
             out.append(gen_column_v(M, k))
             out.append(gen_power(M, k, ns))
             out.append(gen_band(M, k, nr))
+            out.append(gen_od_elem(M, k))
     sys.stdout.write("\n".join(out))
 
 

@@ -1028,7 +1028,8 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
 // first n_rep rows are evaluated; the rest are bounded by the last two
 // iterations' current changes (pgw.h), and a wave whose bound cannot decide
 // some env re-runs the whole solve with every row evaluated -- so the stopping
-// iteration is always the exact rule's.  The previous magnitudes live in LDS.
+// iteration is always the exact rule's.  A wave evaluates the rows only in an
+// iteration where the element nodes alone do not already fail every env.
 struct ODArgs {
   double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M], esc[PGW_PF_MAX_M];
   double tol, gamma, eps, gmax, gsrc;
@@ -1036,9 +1037,21 @@ struct ODArgs {
   const double* rows_V0;
   const double* rows_G;
   int32_t min_iter, n_rep, n_rows, max_iter;
+  int32_t node_mask;                              // bit k: element k is a node (esc[k] > 0)
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
-constexpr int kOdOld = kOdRows + PGW_PF_MAX_M;   // LDS slots of previous magnitudes per lane
+// LDS of the OpenDSS solve, per block of kBlock lanes (one env each):
+//   rows  the check rows in the resident row layout (pf_row_load)
+//   J     per lane, by iteration parity: iteration k's currents I'(u_{k-1})
+//         go to J[k & 1], so the last two iterations' are always there (a lane
+//         that stops keeps both: the accepted iteration's are the outputs'
+//         input).  During an exact test the previous iteration's buffer, once
+//         read, holds the rows' previous magnitudes (two rows per slot).
+template <int M> struct ODShared {
+  double rows[kOdRows * 16 * PFRow<M>::kPairs];
+  double st[6 * M];                                 // pgw_pf_od.start (broadcast reads)
+  double2 J[2][M * kBlock];
+};
 
 static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   ODArgs o = {};
@@ -1059,53 +1072,106 @@ static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   o.n_rep = d.n_rep;
   o.n_rows = d.n_rows;
   o.max_iter = max_iter;
+  for (int k = 0; k < PGW_PF_MAX_M; ++k)
+    if (d.elem_scale[k] > 0.0) o.node_mask |= 1 << k;
   return o;
 }
 
 // NaN-propagating max: an env whose change is NaN never passes the test.
 __device__ __forceinline__ double od_max(double a, double b) { return (b > a || b != b) ? b : a; }
 
-// Check rows into LDS in the resident row layout (pf_row_load / pf_row4_dpp).
-template <int M>
-__device__ __forceinline__ void od_rows_stage(const double* V0, const double* G, int rows, double* s) {
-  constexpr int S = 16 * PFRow<M>::kPairs;
-  for (int i = threadIdx.x; i < rows * S; i += kBlock) {
-    const int o = i / S, j = i - o * S;
-    double v = 0.0;
-    if (j < 2) v = V0[2 * o + j];
-    else if (j < 2 + M) v = G[2 * M * o + 2 * (j - 2)];
-    else if (j < 2 + 2 * M) v = G[2 * M * o + 2 * (j - 2 - M) + 1];
-    s[i] = v;
-  }
+// |z| from m2 = |z|^2 for the convergence test: v_rsq_f64 and two Goldschmidt
+// steps (~1 ulp for the pu magnitudes here, m2 in [1e-6, 1e6]; 0 for 0) --
+// about half the VALU of the IEEE sqrt sequence, which also handles denormals
+// and infinities the test never sees.  Every path (fused, generic, fast and
+// full row sets) uses it, so they stay bit-identical to each other.
+__device__ __forceinline__ double od_mag(double m2) {
+  const double r = __builtin_amdgcn_rsq(m2);
+  double g = m2 * r, h = 0.5 * r;
+  double e = fma(-g, h, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  const double d = fma(-g, g, m2);
+  g = fma(d, h, g);
+  return m2 > 0.0 ? g : 0.0;
 }
 
-// Rows [0, R) from the currents J: err <- max | |V_r| - old_r |, amin <- min
-// old_r over the evaluated rows, old_r <- |V_r| unless the env has stopped.
-// Four rows per DPP group; every lane runs it (the broadcasts read all lanes).
+// The check rows (resident row layout) and the first-iteration table into
+// LDS; the block synchronises before use.
 template <int M>
-__device__ __forceinline__ void od_rows(const double* s, double* s_old, int R, const double (&ir)[M],
-                                        const double (&ii)[M], bool done, double& err, double& amin) {
+__device__ __forceinline__ void od_stage(const ODArgs& o, ODShared<M>& sh) {
+  constexpr int S = 16 * PFRow<M>::kPairs;
+  const int rows = o.n_rows;
+  for (int i = threadIdx.x; i < rows * S; i += kBlock) {
+    const int r = i / S, j = i - r * S;
+    double v = 0.0;
+    if (j < 2) v = o.rows_V0[2 * r + j];
+    else if (j < 2 + M) v = o.rows_G[2 * M * r + 2 * (j - 2)];
+    else if (j < 2 + 2 * M) v = o.rows_G[2 * M * r + 2 * (j - 2 - M) + 1];
+    sh.rows[i] = v;
+  }
+  for (int i = threadIdx.x; i < 6 * M; i += kBlock) sh.st[i] = o.start[i];
+}
+
+// Rows [0, R) from the currents in `cur` (the lane's slots).  CMP = false:
+// their magnitudes replace the currents in `cur` (rows 2s, 2s+1 in slot s;
+// the currents are all read first) unless the env has stopped.  CMP = true:
+// err <- max | |V_r| - prev_r |, amin <- min prev_r against the magnitudes
+// in `prev`.  Four rows per DPP group, the next group's operands loaded while
+// this one computes; every lane runs it (the broadcasts read all lanes).
+template <int M, bool CMP>
+__device__ __forceinline__ void od_rows(const ODShared<M>& sh, double2* cur, const double2* prev, int R,
+                                        bool done, double& err, double& amin) {
   constexpr int P = PFRow<M>::kPairs;
   const int tid = threadIdx.x;
   const int last = R - 1;
+  double ir[M], ii[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double2 j = cur[k * kBlock + tid];
+    ir[k] = j.x;
+    ii[k] = j.y;
+  }
+  double wa[P], wb[P], wc[P], wd[P];
+  pf_row_load<M>(sh.rows, 0, wa);
+  pf_row_load<M>(sh.rows, min(1, last), wb);
+  pf_row_load<M>(sh.rows, min(2, last), wc);
+  pf_row_load<M>(sh.rows, min(3, last), wd);
   for (int o = 0; o < R; o += 4) {
-    double wa[P], wb[P], wc[P], wd[P];
-    pf_row_load<M>(s, o, wa);
-    pf_row_load<M>(s, min(o + 1, last), wb);
-    pf_row_load<M>(s, min(o + 2, last), wc);
-    pf_row_load<M>(s, min(o + 3, last), wd);
+    double na[P], nb[P], nc[P], nd[P];
+    pf_row_load<M>(sh.rows, min(o + 4, last), na);     // the next group in flight
+    pf_row_load<M>(sh.rows, min(o + 5, last), nb);
+    pf_row_load<M>(sh.rows, min(o + 6, last), nc);
+    pf_row_load<M>(sh.rows, min(o + 7, last), nd);
+    double2 p0, p1;
+    if constexpr (CMP) {
+      p0 = prev[(o / 2) * kBlock + tid];
+      p1 = prev[(o / 2 + 1) * kBlock + tid];
+    }
+    __builtin_amdgcn_sched_barrier(0);
     double ar, ai, br, bi, cr, ci, dr, di;
     pf_row4_dpp<M>(ar, ai, br, bi, cr, ci, dr, di, wa, wb, wc, wd, ir, ii);
-    const double mg[4] = {pf_mag<M>(ar, ai), pf_mag<M>(br, bi), pf_mag<M>(cr, ci), pf_mag<M>(dr, di)};
+    const double mg[4] = {od_mag(fma(ai, ai, ar * ar)), od_mag(fma(bi, bi, br * br)),
+                          od_mag(fma(ci, ci, cr * cr)), od_mag(fma(di, di, dr * dr))};
+    if constexpr (CMP) {
+      const double om[4] = {p0.x, p0.y, p1.x, p1.y};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (o + q < R) {                                  // (uniform)
-        double* op = s_old + (o + q) * kBlock + tid;
-        const double old = *op;
-        err = od_max(err, fabs(mg[q] - old));
-        amin = fmin(amin, old);
-        if (!done) *op = mg[q];
+      for (int q = 0; q < 4; ++q) {
+        if (o + q < R) {                                // (uniform)
+          err = od_max(err, fabs(mg[q] - om[q]));
+          amin = fmin(amin, om[q]);
+        }
       }
+    } else if (!done) {
+      cur[(o / 2) * kBlock + tid] = make_double2(mg[0], mg[1]);
+      cur[(o / 2 + 1) * kBlock + tid] = make_double2(mg[2], mg[3]);
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      wa[p] = na[p];
+      wb[p] = nb[p];
+      wc[p] = nc[p];
+      wd[p] = nd[p];
     }
   }
 }
@@ -1125,109 +1191,152 @@ __device__ __forceinline__ int od_decide(const ODArgs& o, bool full, int it, dou
   return hi <= o.tol ? 1 : -1;
 }
 
-// The whole snap solve of the lane's env (S: block, powers loaded).  lir / lii
-// end as the currents of the accepted iteration (the output rows' input).
-// Returns the iteration count, negative when stopped by max_iter.
+// The currents of the accepted iteration `it` (od_solve's return).
 template <int M>
-__device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid, const double* s_rows,
-                        double* s_old, double (&lir)[M], double (&lii)[M]) {
+__device__ __forceinline__ void od_load_J(const ODShared<M>& sh, int it, double (&ir)[M], double (&ii)[M]) {
+  const double2* J = sh.J[abs(it) & 1];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double2 j = J[k * kBlock + threadIdx.x];
+    ir[k] = j.x;
+    ii[k] = j.y;
+  }
+}
+
+// The whole snap solve of the lane's env (S: block, powers loaded; sh staged
+// and synchronised; min_iter >= 2, check_od).  Returns the iteration count,
+// negative when stopped by max_iter; the accepted currents are in
+// sh.J[|count| & 1].
+//   iteration 1  u_1 from the affine table; no test (it < min_iter).
+//   iteration k  currents and matvec; then, without a square root, a lower
+//                bound of every element node's change (|a| + |b| <= (a^2 +
+//                b^2)/2 + 1): above tol for some node means not converged,
+//                exactly.  Only when some lane of the wave is left (k >=
+//                min_iter, no node above tol) does the wave run the exact test:
+//                element nodes, then the rows' previous magnitudes from the
+//                previous currents and the new ones from this iteration's.
+template <int M>
+__device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid, ODShared<M>& sh) {
+  static_assert(kOdRows <= 2 * M, "od_rows keeps two row magnitudes per current slot");
   const int tid = threadIdx.x;
+  // per-element constants resident for DPP: y0' (re, im) and the node scale
+  double yres[2], eres;
+  {
+    const int l = threadIdx.x & 15;
+    const bool in = l < M;
+    yres[0] = in ? o.y0r[l] : 0.0;
+    yres[1] = in ? o.y0i[l] : 0.0;
+    eres = in ? o.esc[l] : 0.0;
+  }
+  // |a| - |b| > tol for sure when |a^2 - b^2| > tol_lo ((a^2 + b^2)/2 + 1)
+  const double tol_lo = o.tol * (1.0 + 0x1p-30);
   for (int pass = 0;; ++pass) {                        // (uniform) fast, then full if undecided
     const bool full = pass > 0 || o.n_rep >= o.n_rows;
     const int R = full ? o.n_rows : o.n_rep;
-    // ---- iteration 1: J_0 = I'(u0) (kept: the change bound's previous
-    // currents), u_1 and the rows' V_1 from the affine table; previous
-    // magnitudes = the direct solution's
+    // ---- iteration 1: its currents I'(u0) (the next test's previous ones);
+    // u_1 from the affine table
     pf_u0<M>(S.ur, S.ui, S.w);
-    double dsum = 0.0, err = 0.0, amin = __builtin_huge_val();
     static_for<0, M>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
-      S.template current_od<k>(o.y0r[k], o.y0i[k], lir[k], lii[k]);
-      dsum += fabs(lir[k]) + fabs(lii[k]);
+      double jr, ji, y0r, y0i;
+      pf_od_elem<M, k>(y0r, y0i, yres);
+      S.template current_od<k>(y0r, y0i, jr, ji);
+      sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
     });
-    const double* st = o.start;
+    const double* st = sh.st;
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-      const double mo = sqrt(fma(S.ui[k], S.ui[k], S.ur[k] * S.ur[k])) * o.esc[k];
-      const double nr = fma(S.qc, st[2 * (2 * M + k)], fma(S.pc, st[2 * (M + k)], st[2 * k]));
-      const double ni = fma(S.qc, st[2 * (2 * M + k) + 1], fma(S.pc, st[2 * (M + k) + 1], st[2 * k + 1]));
-      S.ur[k] = nr;
-      S.ui[k] = ni;
-      const double mn = sqrt(fma(ni, ni, nr * nr)) * o.esc[k];
-      if (o.esc[k] > 0.0) {                           // (uniform) the element is a node
-        err = od_max(err, fabs(mn - mo));
-        amin = fmin(amin, mo);
-      }
-      s_old[(kOdRows + k) * kBlock + tid] = mn;
-    }
-    for (int r = 0; r < R; ++r) {                     // (uniform)
-      const double* v0 = s_rows + 16 * PFRow<M>::kPairs * r;   // staged V0 re, im
-      const double mo = sqrt(fma(v0[1], v0[1], v0[0] * v0[0]));
-      const double* q = st + 6 * M + 6 * r;
-      const double vr = fma(S.qc, q[4], fma(S.pc, q[2], q[0]));
-      const double vi = fma(S.qc, q[5], fma(S.pc, q[3], q[1]));
-      const double mn = sqrt(fma(vi, vi, vr * vr));
-      err = od_max(err, fabs(mn - mo));
-      amin = fmin(amin, mo);
-      s_old[r * kBlock + tid] = mn;
+      S.ur[k] = fma(S.qc, st[2 * (2 * M + k)], fma(S.pc, st[2 * (M + k)], st[2 * k]));
+      S.ui[k] = fma(S.qc, st[2 * (2 * M + k) + 1], fma(S.pc, st[2 * (M + k) + 1], st[2 * k + 1]));
     }
     int it = 1, my_it = 1;
-    bool done = !valid, conv_ok = !valid, undecided = false;
-    {
-      const int d = od_decide(o, full, it, err, amin, dsum, 0.0);
-      undecided = !done && d < 0;
-      conv_ok = conv_ok || (!done && d > 0);
-      done = done || d > 0 || it >= o.max_iter;
-    }
-    if (__ballot(undecided) != 0ull) continue;
+    bool done = !valid || o.max_iter <= 1, conv_ok = !valid, undecided = false;
     while (__ballot(!done) != 0ull) {
-      // ---- currents of u_{k-1} (kept, with the change sums), u_k by the matvec
+      ++it;
+      double2* const cur = sh.J[it & 1];
+      double2* const prv = sh.J[(it & 1) ^ 1];
+      // ---- currents of u_{k-1} (into LDS), u_k by the matvec
       double A[M], Bs[M], C[M];
       pf_acc_init<M>(A, C, S.w);
 #pragma unroll
       for (int i = 0; i < M; ++i) Bs[i] = 0.0;
-      dsum = 0.0;
-      double jsum = 0.0;
       auto column = [&](auto kk, double ir, double ii) {
         constexpr int k = decltype(kk)::value;
-        dsum += fabs(ir - lir[k]) + fabs(ii - lii[k]);
-        jsum += fabs(lir[k]) + fabs(lii[k]);
         pf_column<M, k>(A, Bs, C, S.w, ir, ii, ir + ii);
-        lir[k] = done ? lir[k] : ir;
-        lii[k] = done ? lii[k] : ii;
+        if (!done) cur[k * kBlock + tid] = make_double2(ir, ii);
       };
       static_for<0, M / 2>([&](auto h) {
         constexpr int k0 = 2 * h, k1 = 2 * h + 1;
-        double ir0, ii0, ir1, ii1;
-        S.template current_od<k0>(o.y0r[k0], o.y0i[k0], ir0, ii0);
-        S.template current_od<k1>(o.y0r[k1], o.y0i[k1], ir1, ii1);
+        double ir0, ii0, ir1, ii1, y0r0, y0i0, y0r1, y0i1;
+        pf_od_elem<M, k0>(y0r0, y0i0, yres);
+        pf_od_elem<M, k1>(y0r1, y0i1, yres);
+        S.template current_od<k0>(y0r0, y0i0, ir0, ii0);
+        S.template current_od<k1>(y0r1, y0i1, ir1, ii1);
         column(std::integral_constant<int, k0>{}, ir0, ii0);
         column(std::integral_constant<int, k1>{}, ir1, ii1);
       });
       if constexpr (M % 2) {
-        double ir, ii;
-        S.template current_od<M - 1>(o.y0r[M - 1], o.y0i[M - 1], ir, ii);
+        double ir, ii, y0r, y0i;
+        pf_od_elem<M, M - 1>(y0r, y0i, yres);
+        S.template current_od<M - 1>(y0r, y0i, ir, ii);
         column(std::integral_constant<int, M - 1>{}, ir, ii);
       }
-      err = 0.0;
-      amin = __builtin_huge_val();
+      double nr[M], ni[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) {
-        const double nr = A[i] - Bs[i];
-        const double ni = (C[i] - A[i]) - Bs[i];
-        if (o.esc[i] > 0.0) {                         // (uniform)
-          double* op = s_old + (kOdRows + i) * kBlock + tid;
-          const double mo = *op, mn = sqrt(fma(ni, ni, nr * nr)) * o.esc[i];
-          err = od_max(err, fabs(mn - mo));
-          amin = fmin(amin, mo);
-          if (!done) *op = mn;
-        }
-        S.ur[i] = done ? S.ur[i] : nr;
-        S.ui[i] = done ? S.ui[i] : ni;
+        nr[i] = A[i] - Bs[i];
+        ni[i] = (C[i] - A[i]) - Bs[i];
       }
-      od_rows<M>(s_rows, s_old, R, lir, lii, done, err, amin);
-      ++it;
-      const int d = od_decide(o, full, it, err, amin, dsum, jsum);
+      // ---- the square-root-free lower bound over the element nodes
+      bool hit = false;
+      static_for<0, M>([&](auto kk) {
+        constexpr int i = decltype(kk)::value;
+        if ((o.node_mask >> i) & 1) {                 // (uniform) the element is a node
+          const double e = pf_bc16<i % 16>(eres), e2 = e * e;
+          const double a2 = fma(ni[i], ni[i], nr[i] * nr[i]) * e2;
+          const double b2 = fma(S.ui[i], S.ui[i], S.ur[i] * S.ur[i]) * e2;
+          hit = hit || fabs(a2 - b2) > tol_lo * fma(0.5, a2 + b2, 1.0);
+        }
+      });
+      const bool need = !done && it >= o.min_iter && !hit;
+      const bool exact = __ballot(need) != 0ull;      // (uniform)
+      double err = 0.0, amin = __builtin_huge_val();
+      if (exact) {
+        static_for<0, M>([&](auto kk) {
+          constexpr int i = decltype(kk)::value;
+          if ((o.node_mask >> i) & 1) {               // (uniform)
+            const double e = pf_bc16<i % 16>(eres);
+            const double mo = od_mag(fma(S.ui[i], S.ui[i], S.ur[i] * S.ur[i])) * e;
+            const double mn = od_mag(fma(ni[i], ni[i], nr[i] * nr[i])) * e;
+            err = od_max(err, fabs(mn - mo));
+            amin = fmin(amin, mo);
+          }
+        });
+      }
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        S.ur[i] = done ? S.ur[i] : nr[i];
+        S.ui[i] = done ? S.ui[i] : ni[i];
+      }
+      int d = 0;
+      if (exact) {
+        // the change bound's sums: this iteration's currents against the
+        // previous ones (the rounding, ~1e-15 relative, as slack)
+        double dsum = 0.0, jsum = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          const double2 c = cur[k * kBlock + tid], p = prv[k * kBlock + tid];
+          dsum += fabs(c.x - p.x) + fabs(c.y - p.y);
+          jsum += fabs(p.x) + fabs(p.y);
+        }
+        dsum = fma(0x1p-40, jsum + dsum, dsum);
+        jsum = fma(0x1p-40, jsum, jsum);
+        if (R > 0) {                                  // (uniform)
+          od_rows<M, false>(sh, prv, nullptr, R, done, err, amin);
+          od_rows<M, true>(sh, cur, prv, R, done, err, amin);
+        }
+        d = od_decide(o, full, it, err, amin, dsum, jsum);
+      }
       undecided = !done && d < 0;
       my_it = done ? my_it : it;
       conv_ok = conv_ok || (!done && d > 0);
@@ -1248,9 +1357,8 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   using Sto = std::remove_pointer_t<decltype(b.reward)>;
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
-  __shared__ double s_chk[kOdRows * 16 * PFRow<M>::kPairs];
-  __shared__ double s_old[kOdOld * kBlock];
-  od_rows_stage<M>(o.rows_V0, o.rows_G, o.n_rows, s_chk);
+  __shared__ ODShared<M> sh;
+  od_stage<M>(o, sh);
   double rp[PGW_MAX_AGENTS];
   const int64_t ec = valid ? e : 0;
 #pragma unroll
@@ -1273,10 +1381,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   }
   S.powers(a, cp, cq, 1.0);
   __syncthreads();                                   // the staged check rows
-  double lir[M], lii[M];
-  const int it = od_solve<M>(S, o, valid, s_chk, s_old, lir, lii);
-  double v0r, v0i;
-  pf_node0<M>(v0r, v0i, S.w, lir, lii);
+  const int it = od_solve<M>(S, o, valid, sh);
+  double ir[M], ii[M], v0r, v0i;
+  od_load_J<M>(sh, it, ir, ii);
+  pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if (!valid) return;
   if (b.v_out) b.v_out[e] = (Sto)v0;
@@ -1294,7 +1402,8 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
 }
 
 // pgw_pf_solve, OpenDSS rule: k_pf_solve's prologue (the env's controllable
-// powers) and outputs (every output row from the accepted iteration's currents,
+// powers) and outputs (every output row from the accepted iteration's currents
+// -- through the scalar cache: the solve's LDS leaves no room to stage them --,
 // extrema, element voltages), the snap solve in between.
 template <int M>
 __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_pf_tables t, int64_t n,
@@ -1304,11 +1413,8 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
                                                         int32_t* __restrict__ iters) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
-  __shared__ double s_chk[kOdRows * 16 * PFRow<M>::kPairs];
-  __shared__ double s_old[kOdOld * kBlock];
-  __shared__ double s_rows[kRowsLds];
-  od_rows_stage<M>(o.rows_V0, o.rows_G, o.n_rows, s_chk);
-  const bool rows_lds = pf_rows_stage<M>(t, a.n_out, s_rows);
+  __shared__ ODShared<M> sh;
+  od_stage<M>(o, sh);
   PFSolver<M, true, false> S;
   S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
@@ -1318,11 +1424,11 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
   S.powers(a, cp, cq, 1.0);
-  __syncthreads();                                   // the staged check and output rows
-  double lir[M], lii[M];
-  const int it = od_solve<M>(S, o, valid, s_chk, s_old, lir, lii);
-  double v0r, v0i;
-  pf_node0<M>(v0r, v0i, S.w, lir, lii);
+  __syncthreads();                                   // the staged check rows
+  const int it = od_solve<M>(S, o, valid, sh);
+  double ir[M], ii[M], v0r, v0i;
+  od_load_J<M>(sh, it, ir, ii);
+  pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if (valid && t.U_out) {
 #pragma unroll
@@ -1332,7 +1438,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     }
   }
   double vmn = v0, vmx = v0;
-  pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, lir, lii, [&](int ro, double v) {
+  pf_rows_out<M>(t, false, nullptr, a.n_out, ir, ii, [&](int ro, double v) {
     if (valid && v_out) v_out[(int64_t)ro * n + e] = v;
     vmn = (v < vmn) ? v : vmn;
     vmx = (v > vmx) ? v : vmx;
@@ -1529,7 +1635,7 @@ static int32_t check_od(const pgw_pf_params& p, const pgw_pf_tables& t, const ch
   PGW_REQUIRE(d->n_rows >= 0 && d->n_rows <= PGW_PF_OD_MAX_ROWS && d->n_rep >= 0 && d->n_rep <= d->n_rows,
               "%s: od n_rep %d / n_rows %d (<= %d)", who, d->n_rep, d->n_rows, PGW_PF_OD_MAX_ROWS);
   PGW_REQUIRE(d->start && (d->n_rows == 0 || (d->rows_V0 && d->rows_G)), "%s: od start / rows missing", who);
-  PGW_REQUIRE(d->min_iter >= 1 && p.max_iter >= 1 && d->tol >= 0.0, "%s: od min_iter / max_iter / tol", who);
+  PGW_REQUIRE(d->min_iter >= 2 && p.max_iter >= 1 && d->tol >= 0.0, "%s: od min_iter / max_iter / tol", who);
   return PGW_OK;
 }
 

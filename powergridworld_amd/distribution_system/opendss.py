@@ -94,6 +94,7 @@ class OpenDSSSolver(PowerFlowSolver):
         # 14 constant-PQ elements in one voltage band, no RegControl; at most one
         # controllable load (set_controllable_loads falls back beyond that)
         self._od_fast = (convergence == "opendss" and not general and not regctl and model1 and
+                         self.OPENDSS_MIN_ITER >= 2 and
                          f.m <= _lib.PF_MAX_M and int(_lib.lib().pgw_pf_padded_m(f.m)) == 14 and
                          len({(a, b, c) for a, b, c in zip(f.elem_vmin, f.elem_vmax, f.elem_vlow)}) == 1)
         self.general = (bool(general) or (convergence == "opendss" and not self._od_fast)
@@ -266,18 +267,16 @@ class OpenDSSSolver(PowerFlowSolver):
         od.rows_V0, od.rows_G = self._od_rows_V0.data_ptr(), self._od_rows_G.data_ptr()
         self._od_proto = od
         self._od_rows = [f.node_names[i] for i in rows]
-        self._od_rowdata = (Gs[rows], V0s[rows])
         self._od_W2 = W / (vb_elem[:, None] * vb_elem[None, :])
         self._od_u0 = U0 / vb_elem
-        self._od_start = torch.zeros((self.OD_MAX_TABLES, 6 * M + 6 * max(len(rows), 1)), dtype=torch.float64,
-                                     device=dev)
+        self._od_start = torch.zeros((self.OD_MAX_TABLES, 6 * M), dtype=torch.float64, device=dev)
         self._od_index = {}
         self._od_keep = {}
 
     def _od_starts(self, hour):
         """First-iteration tables (pgw_pf_od.start) of `hour` and the following
         hours that have none: from the direct solution u0 the currents are affine
-        in the controllable (P, Q), so u_1 and the check rows' V_1 are too."""
+        in the controllable (P, Q), so u_1 is too."""
         hours, keys = [], []
         for h in range(hour, min(hour + self.PREDICTOR_LOOKAHEAD, len(self.annual_hourly_load_profile))):
             k = self._hour_key(h)
@@ -290,7 +289,6 @@ class OpenDSSSolver(PowerFlowSolver):
         idx0 = len(self._od_index)
         M, od = self.M, self._od_proto
         W2, u0 = self._od_W2, self._od_u0
-        Gr, V0r = self._od_rowdata
         p0 = self.params
         nph = np.array(p0.nph[:M])
         ctrl0 = np.array(p0.elem_ctrl[:M]) == 0
@@ -302,16 +300,12 @@ class OpenDSSSolver(PowerFlowSolver):
         g = 1.0 / np.where(m2 <= lo2, 1.0, np.clip(m2, mn2, mx2))
         jP, jQ = fr * g * u0, 1j * fi * g * u0
         u1P, u1Q = W2 @ jP, W2 @ jQ
-        V1P, V1Q = Gr @ jP, Gr @ jQ
         recs = np.zeros((len(hours), self._od_start.shape[1]))
         for q, h in enumerate(hours):
             p = self._params_for_hour(h)
             s0 = (np.array(p.base_kw[:M]) * 1000.0) / nph - 1j * ((np.array(p.base_kvar[:M]) * 1000.0) / nph)
             J0 = (s0 * g - y0) * u0
-            u = np.concatenate([u0 + W2 @ J0, u1P, u1Q])
-            rowsv = np.stack([V0r + Gr @ J0, V1P, V1Q], 1).ravel() if len(V0r) else np.zeros(3, complex)
-            rec = np.concatenate([u, rowsv]).view(np.float64)
-            recs[q, :rec.size] = rec
+            recs[q] = np.concatenate([u0 + W2 @ J0, u1P, u1Q]).view(np.float64)
         for j, k in enumerate(keys):
             self._od_index[k] = idx0 + j
         if hours:

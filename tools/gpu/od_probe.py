@@ -16,6 +16,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--n", type=int, default=65536)
 ap.add_argument("--modes", default="exact,opendss,opendss_general")
+ap.add_argument("--max-iter", type=int, default=0, help="opendss only: cap the iterations (results "
+                                                          "change), for the per-iteration cost")
+ap.add_argument("--nobound", action="store_true", help="opendss only: zero bound constants (timing only)")
+ap.add_argument("--hist", type=int, default=0, help="after timing: per-step max iterations over HIST steps")
 ap.add_argument("--rows", default="", help="opendss only: 'none' (no check row evaluated; results wrong) "
                                          "or 'all' (every row every iteration), for phase costs")
 a = ap.parse_args()
@@ -33,6 +37,18 @@ for mode in a.modes.split(","):
         if a.rows == "none":
             od.n_rows = 0
         env.pf_solver._tables_cache.clear()
+        env._fused["step_cache"].clear()
+    if a.nobound and mode == "opendss":      # bounds that always decide (timing only)
+        od = env.pf_solver._od_proto
+        od.gmax = od.gamma = od.gsrc = od.eps = 0.0
+        env.pf_solver._tables_cache.clear()
+        env._fused["step_cache"].clear()
+    if a.max_iter and mode == "opendss":
+        s = env.pf_solver
+        s.params.max_iter = s.max_iter = a.max_iter
+        s._step_cache.clear()
+        s._tables_cache.clear()
+        s.tables_version += 1
         env._fused["step_cache"].clear()
     env.reset()
     k = [0]
@@ -57,7 +73,17 @@ for mode in a.modes.split(","):
     _lib.check(_lib.lib().pgw_timing_stop(tot, cnt))
     ks = {nm: round(tot[i] / cnt[i] * 1e3, 2) for i, nm in enumerate(("agents", "coord_pf", "pf_solve", "-", "ma", "pf_general")) if cnt[i]}
     it = env.pf_solver.iterations.abs()
+    if a.hist:            # per-step max / mean iterations over a pass (one sync per step)
+        hist = {}
+        for _ in range(a.hist):
+            run(1)
+            mx = int(env.pf_solver.iterations.abs().max())
+            hist[mx] = hist.get(mx, 0) + 1
+        print("  per-step max iterations over %d steps: %s" % (a.hist, dict(sorted(hist.items()))))
+    tag = mode + ("/" + a.rows if a.rows and mode == "opendss" else "") + \
+        ("/max%d" % a.max_iter if a.max_iter and mode == "opendss" else "") + \
+        ("/nobound" if a.nobound and mode == "opendss" else "")
     print("%-16s %7.2f us/step  kernels %s  iters mean %.3f max %d  kernel=%s" %
-          (mode + ("/" + a.rows if a.rows and mode == "opendss" else ""), us, ks, it.double().mean().item(), it.max().item(), env._fused["kernel"]), flush=True)
+          (tag, us, ks, it.double().mean().item(), it.max().item(), env._fused["kernel"]), flush=True)
     del env
     torch.cuda.synchronize()
