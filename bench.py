@@ -3,9 +3,11 @@ with the IEEE-13 power flow (BASELINE.json config C4), batch 65,536 per GPU.
 
 One "step" = one MultiAgentEnv.step of the whole batch through the public API
 (fused path: one pgw_coord_step call = k_coord_agents_std (5 x [building, PV,
-storage] per env) + k_coord_pf (power flow + coordinated reward); about once
-per episode also the predictor-table solve for the next 24 simulated hours),
-actions already resident in HBM.  Episodes (286 steps) end with done["__all__"]; the following env.reset()
+storage] per env) + the power flow with the coordinated reward: by default
+k_coord_pf_od, OpenDSS's snap-solve rule as the reference runs it (about once
+per episode also the first-iteration tables of the next 24 simulated hours);
+--pf-convergence exact: k_coord_pf, the exact fixed point with its predictor
+tables), actions already resident in HBM.  Episodes (286 steps) end with done["__all__"]; the following env.reset()
 is inside the timed region.  Kernel durations come from HIP events the library
 records around every --time-every-th launch, on the launch's stream.
 
@@ -55,13 +57,30 @@ PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
 M_ELEM = 14
 PF_FLOPS_ITER = 8 * M_ELEM ** 2 + 12 * M_ELEM + 6 * M_ELEM
 PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
-# k_pf_general in OpenDSS mode (m = 16 padded element rows, 40 padded check rows =
-# every node): per iteration 8 x 16 x (16 + 40) complex-MAC flops + the current
-# law, per env the output row
-PFG_FLOPS_ITER = 8 * 16 * (16 + 40) + 14 * 16
-PF_KERNEL = "k_coord_pf<14,true,false,false>"
-# PGW_T_* order (include/pgw.h); slot 3 is unused (the one-launch C4 step of
-# round 3 measured slower: profiles/r03/coop_dropped.txt)
+# k_coord_pf_od (OpenDSS rule, fast kernel): per compensation iteration after the
+# first 8 m^2 (matvec) + 14 m (current law with the Yeq term) + 6 m (the
+# square-root-free element test); once per env the exact test of the accepted
+# iteration -- element magnitudes (2 x 8 per node) and the n_rep = 11 evaluated
+# check rows twice (previous and new: 8 m + 4 each) -- the first iteration (14 m
+# currents + 4 m affine u_1), one output row (8 m + 4) and the reward
+OD_REP_ROWS = 11
+OD_FLOPS_ITER = 8 * M_ELEM ** 2 + 14 * M_ELEM + 6 * M_ELEM
+OD_FLOPS_ENV = 16 * M_ELEM + 2 * OD_REP_ROWS * (8 * M_ELEM + 4) + 18 * M_ELEM + 8 * M_ELEM + 4 + 10
+PF_KERNEL_NAME = {"exact": "k_coord_pf<14,true,false,false>", "opendss": "k_coord_pf_od<14>"}
+PF_KERNEL = "k_coord_pf"              # PGW_T_COORD_PF: whichever PF kernel the step's mode runs
+
+
+def pf_roofline(conv, avg_us, mean_it, n):
+    """Achieved fp64 TF/s of the step's PF kernel from its algorithmic flops."""
+    if conv == "exact":
+        flops = PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV
+    else:
+        flops = OD_FLOPS_ITER * max(mean_it - 1.0, 0.0) + OD_FLOPS_ENV
+    tfs = flops * n / (avg_us * 1e-6) / 1e12
+    return {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
+            "flops_per_env": flops}
+
+
 KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "(unused)", "k_ma_step", "k_pf_general")
 
 
@@ -83,19 +102,23 @@ def parse():
     ap.add_argument("--time-steps", type=int, default=64,
                     help="steps of the kernel-timing pass after the timed region (every launch "
                          "HIP-event-timed; at least 8, at most --steps)")
+    ap.add_argument("--pf-convergence", choices=("opendss", "exact"), default="opendss",
+                    help="the headline's power-flow stopping rule: OpenDSS's snap solve (the "
+                         "reference's: loads' Yeq in Y, node-magnitude test 1e-4, 2..15 iterations) "
+                         "or the exact fixed point; the other runs as variants.*_pf")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the fp32-storage variant line (N=1 only; never the headline)")
     return ap.parse_args()
 
 
-def f32_variant(n, steps, warmup, pool_size, seed, dev):
+def f32_variant(conv, n, steps, warmup, pool_size, seed, dev):
     """The same C4 workload on the fp32-storage fused path (pgw_coord_step_f32:
     fp32 state/actions/outputs, fp64 arithmetic).  Reported beside
     the fp64 headline, never as it: the reference computes in fp64."""
     from powergridworld_amd import _lib
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
-    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=dev,
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n, device=dev,
                                              dtype=torch.float32)
     gen = torch.Generator(dev).manual_seed(seed)
     pool = torch.empty((pool_size, N_AGENTS, ACT_DIM, n), dtype=torch.float32, device=dev)
@@ -150,15 +173,14 @@ def timed_pass(run, steps):
     return tot, cnt
 
 
-def opendss_variant(n, steps, warmup, pool, dev):
-    """The same C4 workload with OpenDSSSolver(convergence="opendss") -- OpenDSS's
-    own snap-solve stopping rule (loads' Yeq in Y, direct-solution start, node
-    magnitude test at 1e-4, 2..15 iterations), on the fused general-PF step
-    (pgw_coord_step_general).  Reported beside the headline: the default
-    solver converges every env to the fixed point."""
+def pf_variant(conv, n, steps, warmup, pool, dev):
+    """The same C4 workload (same action pool) with the other power-flow stopping
+    rule on the fused step: OpenDSS's snap solve (the reference's,
+    opendss.py:131-135; pgw_coord_step + k_coord_pf_od) or the exact fixed point
+    (k_coord_pf + its predictor).  Reported beside the headline."""
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
-    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence="opendss"), num_envs=n,
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n,
                                              device=dev, fused=True)
     P = pool.shape[0]
     env.reset()
@@ -178,15 +200,15 @@ def opendss_variant(n, steps, warmup, pool, dev):
     dt = time.perf_counter() - t0
     tot, cnt = timed_pass(run, 64)
     it = env.pf_solver.iterations.abs().double()
-    g_us = tot[5] / cnt[5] * 1e3 if cnt[5] else None
-    out = {"pf_convergence": "opendss", "value": N_AGENTS * n * steps / dt, "unit": "agent-env-steps/s",
+    p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
+    out = {"pf_convergence": conv, "value": N_AGENTS * n * steps / dt, "unit": "agent-env-steps/s",
            "ms_per_step": dt / steps * 1e3, "steps": steps, "pf_iterations_mean": float(it.mean()),
+           "pf_iterations_max": int(it.max()),
            "k_coord_agents_std_avg_us": tot[0] / cnt[0] * 1e3 if cnt[0] else None,
-           "k_pf_general": {"avg_us": g_us, "bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFS,
-                            "note": "fp64 VALU; 38 node rows checked every iteration"}}
-    if g_us:
-        tfs = (PFG_FLOPS_ITER * float(it.mean())) * n / (g_us * 1e-6) / 1e12
-        out["k_pf_general"].update(achieved=tfs, frac=tfs / FP64_PEAK_TFS)
+           "pf_kernel": {"name": PF_KERNEL_NAME[conv] if env.pf_solver._od_fast or conv == "exact"
+                         else "k_pf_general", "avg_us": p_us, "bound": "mfma"}}
+    if p_us:
+        out["pf_kernel"].update(pf_roofline(conv, p_us, float(it.mean()), n))
     del env
     return out
 
@@ -330,7 +352,11 @@ def main():
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     n = args.batch
-    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=dev, fused=True)
+    conv = args.pf_convergence
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n, device=dev,
+                                             fused=True)
+    if conv == "opendss" and not env.pf_solver._od_fast:
+        raise RuntimeError("bench.py: the C4 feeder did not select the fast OpenDSS-rule kernel")
     for i, agent in enumerate(env.agents):         # per-rank seed offset
         agent.env_dict["storage"].seed(pgd.rank_seed(0, rank, i))
     gen = torch.Generator(dev).manual_seed(pgd.rank_seed(0, rank))     # seed 0 at rank 0
@@ -403,6 +429,10 @@ def main():
             break
     torch.cuda.synchronize()
     ep_elapsed = pgd.max_over_ranks(time.perf_counter() - ep0, dev)
+    # per-env statistics of the episode's last step, all-gathered in global env
+    # order once per episode, outside every timed region (RCCL at N>1)
+    ep_stats = pgd.gather_episode_stats(torch.stack(
+        [iters_last.double(), env.pf_solver.get_bus_voltage_by_name("675c").double()], 1))
     total_envs = n * world
     value = N_AGENTS * total_envs * args.steps / elapsed
     if rank == 0:
@@ -425,14 +455,13 @@ def main():
                                    "bytes_per_launch": AGENT_BYTES * N_AGENTS * n,
                                    "traffic": traffic.get(KERNELS[0])}
         if p_us:
-            tfs = (PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV) * n / (p_us * 1e-6) / 1e12
-            kernels[KERNELS[1]] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
-                                   "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); "
-                                           "latency-bound; one wave per SIMD at 65,536 envs",
-                                   "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                                   "frac": tfs / FP64_PEAK_TFS,
-                                   "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
-                                   "traffic": traffic.get(KERNELS[1])}
+            pk = PF_KERNEL_NAME[conv]
+            kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
+                           "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); issue-bound "
+                                   "DPP FMAs, one wave per SIMD at 65,536 envs",
+                           "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
+                           "traffic": traffic.get(pk)}
+            kernels[pk].update(pf_roofline(conv, p_us, mean_it, n))
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "
@@ -471,6 +500,7 @@ def main():
                     "exogenous building data, IEEE-13 feeder + 8760-h loadshape)",
             "config": {"workload": "C4: 5-agent coordinated buildings (building+PV+storage) "
                                    "+ IEEE-13 power flow + voltage-violation reward",
+                       "pf_convergence": conv,
                        "batch_per_gpu": n, "global_batch": total_envs, "episode_steps": 286,
                        "parallelism": "env-sharded x%d (no collective on the step path)" % world},
             "roofline": roof,
@@ -486,16 +516,18 @@ def main():
             "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist,
                               "unconverged_envs": unconverged},
             "episode": {"steps": ep_steps, "ms_per_step": ep_elapsed / ep_steps * 1e3,
+                        "gathered_env_stats": int(ep_stats.shape[0]),
                         "value": N_AGENTS * total_envs * ep_steps / ep_elapsed,
                         "note": "one whole episode after the timed region: its %d steps and the "
                                 "env.reset() that ends it (reset kernels, predictor tables of the "
                                 "next hours), no events" % ep_steps},
         }
         if world == 1 and not args.no_variants:
-            out["variants"] = {"f32": f32_variant(n, min(args.steps, 286), args.warmup, P,
+            other = "exact" if conv == "opendss" else "opendss"
+            out["variants"] = {"f32": f32_variant(conv, n, min(args.steps, 286), args.warmup, P,
                                                   pgd.rank_seed(0, rank), dev),
-                               "opendss_pf": opendss_variant(n, min(args.steps, 286), args.warmup, packed,
-                                                             dev)}
+                               other + "_pf": pf_variant(other, n, min(args.steps, 286), args.warmup, packed,
+                                                         dev)}
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out))

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 23
+#define PGW_ABI_VERSION 24
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -387,8 +387,8 @@ typedef struct pgw_pf_tables {
  * members (electrically next to a row or an element node: |G_j - G_r| <= gamma
  * per element, |V0_j - V0_r| <= eps) and source-side nodes (|G_j| <= gsrc per
  * element), with gmax >= |G_r| per element of every row and element node; when
- * a bound cannot decide an env's test, its wave re-runs the solve with every
- * row evaluated, so the stopping iteration is always the exact rule's.  The
+ * a bound cannot decide an env's test, its wave evaluates the bounded rows too
+ * (that iteration), so the stopping iteration is always the exact rule's.  The
  * rows are evaluated only in iterations where some env of the wave has no
  * element node whose change is surely above tol (min_iter >= 2).
  *
@@ -753,6 +753,21 @@ int32_t pgw_coord_step_general(const pgw_coord_params* p, const pgw_pfg_params* 
 int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
                            const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                            pgw_coord_buffers_f32 b, void* stream);
+
+/* pgw_coord_step / _f32 with the power flow on a second stream: the agents'
+ * kernel on `stream`; pf_stream then waits for it (an event recorded inside the
+ * call) and runs the PF kernel.  So the PF of step t can run beside the agents'
+ * kernel of step t+1 (C4's observations do not read voltages).  The caller
+ * orders everything else: later reads of the PF outputs (reward, v_out, vv,
+ * iters) after pf_stream, and the next writes of agent_power / reward after the
+ * PF that reads / adds to them (e.g. two buffer sets, alternating).
+ * pf_stream == stream is pgw_coord_step. */
+int32_t pgw_coord_step_overlap(const pgw_coord_params* p, const pgw_pf_params* pf,
+                               const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                               pgw_coord_buffers b, void* stream, void* pf_stream);
+int32_t pgw_coord_step_f32_overlap(const pgw_coord_params* p, const pgw_pf_params* pf,
+                                   const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                                   pgw_coord_buffers_f32 b, void* stream, void* pf_stream);
 
 /* ------------------------------------------------------------------------
  * Fused MultiComponentEnv step (SURVEY 8(b) pgw_mc_agent_step): one agent of

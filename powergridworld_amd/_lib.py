@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -318,6 +318,10 @@ _SIGS = {
                              CoordBuffers, vp]),
     "pgw_coord_step_f32": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
                                  CoordBuffersF32, vp]),
+    "pgw_coord_step_overlap": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
+                                     CoordBuffers, vp, vp]),
+    "pgw_coord_step_f32_overlap": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
+                                         CoordBuffersF32, vp, vp]),
     "pgw_coord_step_general": (i32, [P(CoordParams), P(PFGParams), P(PFGTables), P(CoordStepInfo), i64,
                                      CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),

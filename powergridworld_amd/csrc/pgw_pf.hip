@@ -31,6 +31,7 @@
 #include <cmath>
 #include <type_traits>
 
+#include <mutex>
 #include "pgw_common.h"
 
 namespace pgw {
@@ -1027,7 +1028,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
 // others are check rows V = V0 + G J (LDS-staged, DPP row groups).  Only the
 // first n_rep rows are evaluated; the rest are bounded by the last two
 // iterations' current changes (pgw.h), and a wave whose bound cannot decide
-// some env re-runs the whole solve with every row evaluated -- so the stopping
+// some env evaluates them too, in the same iteration -- so the stopping
 // iteration is always the exact rule's.  A wave evaluates the rows only in an
 // iteration where the element nodes alone do not already fail every env.
 struct ODArgs {
@@ -1040,17 +1041,21 @@ struct ODArgs {
   int32_t node_mask;                              // bit k: element k is a node (esc[k] > 0)
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
+constexpr int kOdChunk = 12;                      // check rows per previous-magnitude pass
 // LDS of the OpenDSS solve, per block of kBlock lanes (one env each):
 //   rows  the check rows in the resident row layout (pf_row_load)
+//   st    pgw_pf_od.start (broadcast reads)
 //   J     per lane, by iteration parity: iteration k's currents I'(u_{k-1})
 //         go to J[k & 1], so the last two iterations' are always there (a lane
 //         that stops keeps both: the accepted iteration's are the outputs'
-//         input).  During an exact test the previous iteration's buffer, once
-//         read, holds the rows' previous magnitudes (two rows per slot).
+//         input)
+//   old   per lane: the previous magnitudes of up to kOdChunk check rows
+//         during an exact test
 template <int M> struct ODShared {
   double rows[kOdRows * 16 * PFRow<M>::kPairs];
-  double st[6 * M];                                 // pgw_pf_od.start (broadcast reads)
+  double st[6 * M];
   double2 J[2][M * kBlock];
+  double old[kOdChunk * kBlock];
 };
 
 static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
@@ -1113,58 +1118,56 @@ __device__ __forceinline__ void od_stage(const ODArgs& o, ODShared<M>& sh) {
   for (int i = threadIdx.x; i < 6 * M; i += kBlock) sh.st[i] = o.start[i];
 }
 
-// Rows [0, R) from the currents in `cur` (the lane's slots).  CMP = false:
-// their magnitudes replace the currents in `cur` (rows 2s, 2s+1 in slot s;
-// the currents are all read first) unless the env has stopped.  CMP = true:
-// err <- max | |V_r| - prev_r |, amin <- min prev_r against the magnitudes
-// in `prev`.  Four rows per DPP group, the next group's operands loaded while
-// this one computes; every lane runs it (the broadcasts read all lanes).
+// Rows [r0, r1) (r1 - r0 <= kOdChunk) from the currents in J (the lane's
+// slots).  CMP = false: their magnitudes into old[r - r0].  CMP = true:
+// err <- max | |V_r| - old |, amin <- min old.  Four rows per DPP group, the
+// next group's operands loaded while this one computes; every lane runs it
+// (the broadcasts read all lanes).
 template <int M, bool CMP>
-__device__ __forceinline__ void od_rows(const ODShared<M>& sh, double2* cur, const double2* prev, int R,
-                                        bool done, double& err, double& amin) {
+__device__ __forceinline__ void od_rows(const ODShared<M>& sh, const double2* J, double* old, int r0, int r1,
+                                        double& err, double& amin) {
   constexpr int P = PFRow<M>::kPairs;
   const int tid = threadIdx.x;
-  const int last = R - 1;
+  const int last = r1 - 1;
   double ir[M], ii[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    const double2 j = cur[k * kBlock + tid];
+    const double2 j = J[k * kBlock + tid];
     ir[k] = j.x;
     ii[k] = j.y;
   }
   double wa[P], wb[P], wc[P], wd[P];
-  pf_row_load<M>(sh.rows, 0, wa);
-  pf_row_load<M>(sh.rows, min(1, last), wb);
-  pf_row_load<M>(sh.rows, min(2, last), wc);
-  pf_row_load<M>(sh.rows, min(3, last), wd);
-  for (int o = 0; o < R; o += 4) {
+  pf_row_load<M>(sh.rows, r0, wa);
+  pf_row_load<M>(sh.rows, min(r0 + 1, last), wb);
+  pf_row_load<M>(sh.rows, min(r0 + 2, last), wc);
+  pf_row_load<M>(sh.rows, min(r0 + 3, last), wd);
+  for (int o = r0; o < r1; o += 4) {
     double na[P], nb[P], nc[P], nd[P];
     pf_row_load<M>(sh.rows, min(o + 4, last), na);     // the next group in flight
     pf_row_load<M>(sh.rows, min(o + 5, last), nb);
     pf_row_load<M>(sh.rows, min(o + 6, last), nc);
     pf_row_load<M>(sh.rows, min(o + 7, last), nd);
-    double2 p0, p1;
+    double* const ol = old + (o - r0) * kBlock + tid;
+    double om[4];
     if constexpr (CMP) {
-      p0 = prev[(o / 2) * kBlock + tid];
-      p1 = prev[(o / 2 + 1) * kBlock + tid];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) om[q] = ol[min(q, last - o) * kBlock];
     }
     __builtin_amdgcn_sched_barrier(0);
     double ar, ai, br, bi, cr, ci, dr, di;
     pf_row4_dpp<M>(ar, ai, br, bi, cr, ci, dr, di, wa, wb, wc, wd, ir, ii);
     const double mg[4] = {od_mag(fma(ai, ai, ar * ar)), od_mag(fma(bi, bi, br * br)),
                           od_mag(fma(ci, ci, cr * cr)), od_mag(fma(di, di, dr * dr))};
-    if constexpr (CMP) {
-      const double om[4] = {p0.x, p0.y, p1.x, p1.y};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (o + q < R) {                                // (uniform)
+    for (int q = 0; q < 4; ++q) {
+      if (o + q < r1) {                                 // (uniform)
+        if constexpr (CMP) {
           err = od_max(err, fabs(mg[q] - om[q]));
           amin = fmin(amin, om[q]);
+        } else {
+          ol[q * kBlock] = mg[q];
         }
       }
-    } else if (!done) {
-      cur[(o / 2) * kBlock + tid] = make_double2(mg[0], mg[1]);
-      cur[(o / 2 + 1) * kBlock + tid] = make_double2(mg[2], mg[3]);
     }
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -1173,6 +1176,18 @@ __device__ __forceinline__ void od_rows(const ODShared<M>& sh, double2* cur, con
       wc[p] = nc[p];
       wd[p] = nd[p];
     }
+  }
+}
+
+// Rows [r0, r1) of an exact test: previous magnitudes from the previous
+// iteration's currents, new ones from this iteration's, kOdChunk rows at a time.
+template <int M>
+__device__ __forceinline__ void od_check_rows(ODShared<M>& sh, const double2* cur, const double2* prv, int r0,
+                                              int r1, double& err, double& amin) {
+  for (int c = r0; c < r1; c += kOdChunk) {            // (uniform)
+    const int e = min(c + kOdChunk, r1);
+    od_rows<M, false>(sh, prv, sh.old, c, e, err, amin);
+    od_rows<M, true>(sh, cur, sh.old, c, e, err, amin);
   }
 }
 
@@ -1214,7 +1229,9 @@ __device__ __forceinline__ void od_load_J(const ODShared<M>& sh, int it, double 
 //                exactly.  Only when some lane of the wave is left (k >=
 //                min_iter, no node above tol) does the wave run the exact test:
 //                element nodes, then the rows' previous magnitudes from the
-//                previous currents and the new ones from this iteration's.
+//                previous currents and the new ones from this iteration's --
+//                the first n_rep rows, the bounded ones only when some env's
+//                bounds cannot decide (it then takes the exact decision).
 template <int M>
 __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid, ODShared<M>& sh) {
   static_assert(kOdRows <= 2 * M, "od_rows keeps two row magnitudes per current slot");
@@ -1230,122 +1247,119 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid
   }
   // |a| - |b| > tol for sure when |a^2 - b^2| > tol_lo ((a^2 + b^2)/2 + 1)
   const double tol_lo = o.tol * (1.0 + 0x1p-30);
-  for (int pass = 0;; ++pass) {                        // (uniform) fast, then full if undecided
-    const bool full = pass > 0 || o.n_rep >= o.n_rows;
-    const int R = full ? o.n_rows : o.n_rep;
-    // ---- iteration 1: its currents I'(u0) (the next test's previous ones);
-    // u_1 from the affine table
-    pf_u0<M>(S.ur, S.ui, S.w);
-    static_for<0, M>([&](auto kk) {
+  const bool bounded = o.n_rep < o.n_rows;
+  // ---- iteration 1: its currents I'(u0) (the next test's previous ones);
+  // u_1 from the affine table
+  pf_u0<M>(S.ur, S.ui, S.w);
+  static_for<0, M>([&](auto kk) {
+    constexpr int k = decltype(kk)::value;
+    double jr, ji, y0r, y0i;
+    pf_od_elem<M, k>(y0r, y0i, yres);
+    S.template current_od<k>(y0r, y0i, jr, ji);
+    sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
+  });
+  const double* st = sh.st;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    S.ur[k] = fma(S.qc, st[2 * (2 * M + k)], fma(S.pc, st[2 * (M + k)], st[2 * k]));
+    S.ui[k] = fma(S.qc, st[2 * (2 * M + k) + 1], fma(S.pc, st[2 * (M + k) + 1], st[2 * k + 1]));
+  }
+  int it = 1, my_it = 1;
+  bool done = !valid || o.max_iter <= 1, conv_ok = !valid;
+  while (__ballot(!done) != 0ull) {
+    ++it;
+    double2* const cur = sh.J[it & 1];
+    const double2* const prv = sh.J[(it & 1) ^ 1];
+    // ---- currents of u_{k-1} (into LDS), u_k by the matvec
+    double A[M], Bs[M], C[M];
+    pf_acc_init<M>(A, C, S.w);
+#pragma unroll
+    for (int i = 0; i < M; ++i) Bs[i] = 0.0;
+    auto column = [&](auto kk, double ir, double ii) {
       constexpr int k = decltype(kk)::value;
-      double jr, ji, y0r, y0i;
-      pf_od_elem<M, k>(y0r, y0i, yres);
-      S.template current_od<k>(y0r, y0i, jr, ji);
-      sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
+      pf_column<M, k>(A, Bs, C, S.w, ir, ii, ir + ii);
+      if (!done) cur[k * kBlock + tid] = make_double2(ir, ii);
+    };
+    static_for<0, M / 2>([&](auto h) {
+      constexpr int k0 = 2 * h, k1 = 2 * h + 1;
+      double ir0, ii0, ir1, ii1, y0r0, y0i0, y0r1, y0i1;
+      pf_od_elem<M, k0>(y0r0, y0i0, yres);
+      pf_od_elem<M, k1>(y0r1, y0i1, yres);
+      S.template current_od<k0>(y0r0, y0i0, ir0, ii0);
+      S.template current_od<k1>(y0r1, y0i1, ir1, ii1);
+      column(std::integral_constant<int, k0>{}, ir0, ii0);
+      column(std::integral_constant<int, k1>{}, ir1, ii1);
     });
-    const double* st = sh.st;
-#pragma unroll
-    for (int k = 0; k < M; ++k) {
-      S.ur[k] = fma(S.qc, st[2 * (2 * M + k)], fma(S.pc, st[2 * (M + k)], st[2 * k]));
-      S.ui[k] = fma(S.qc, st[2 * (2 * M + k) + 1], fma(S.pc, st[2 * (M + k) + 1], st[2 * k + 1]));
+    if constexpr (M % 2) {
+      double ir, ii, y0r, y0i;
+      pf_od_elem<M, M - 1>(y0r, y0i, yres);
+      S.template current_od<M - 1>(y0r, y0i, ir, ii);
+      column(std::integral_constant<int, M - 1>{}, ir, ii);
     }
-    int it = 1, my_it = 1;
-    bool done = !valid || o.max_iter <= 1, conv_ok = !valid, undecided = false;
-    while (__ballot(!done) != 0ull) {
-      ++it;
-      double2* const cur = sh.J[it & 1];
-      double2* const prv = sh.J[(it & 1) ^ 1];
-      // ---- currents of u_{k-1} (into LDS), u_k by the matvec
-      double A[M], Bs[M], C[M];
-      pf_acc_init<M>(A, C, S.w);
+    double nr[M], ni[M];
 #pragma unroll
-      for (int i = 0; i < M; ++i) Bs[i] = 0.0;
-      auto column = [&](auto kk, double ir, double ii) {
-        constexpr int k = decltype(kk)::value;
-        pf_column<M, k>(A, Bs, C, S.w, ir, ii, ir + ii);
-        if (!done) cur[k * kBlock + tid] = make_double2(ir, ii);
-      };
-      static_for<0, M / 2>([&](auto h) {
-        constexpr int k0 = 2 * h, k1 = 2 * h + 1;
-        double ir0, ii0, ir1, ii1, y0r0, y0i0, y0r1, y0i1;
-        pf_od_elem<M, k0>(y0r0, y0i0, yres);
-        pf_od_elem<M, k1>(y0r1, y0i1, yres);
-        S.template current_od<k0>(y0r0, y0i0, ir0, ii0);
-        S.template current_od<k1>(y0r1, y0i1, ir1, ii1);
-        column(std::integral_constant<int, k0>{}, ir0, ii0);
-        column(std::integral_constant<int, k1>{}, ir1, ii1);
-      });
-      if constexpr (M % 2) {
-        double ir, ii, y0r, y0i;
-        pf_od_elem<M, M - 1>(y0r, y0i, yres);
-        S.template current_od<M - 1>(y0r, y0i, ir, ii);
-        column(std::integral_constant<int, M - 1>{}, ir, ii);
+    for (int i = 0; i < M; ++i) {
+      nr[i] = A[i] - Bs[i];
+      ni[i] = (C[i] - A[i]) - Bs[i];
+    }
+    // ---- the square-root-free lower bound over the element nodes
+    bool hit = false;
+    static_for<0, M>([&](auto kk) {
+      constexpr int i = decltype(kk)::value;
+      if ((o.node_mask >> i) & 1) {                   // (uniform) the element is a node
+        const double e = pf_bc16<i % 16>(eres), e2 = e * e;
+        const double a2 = fma(ni[i], ni[i], nr[i] * nr[i]) * e2;
+        const double b2 = fma(S.ui[i], S.ui[i], S.ur[i] * S.ur[i]) * e2;
+        hit = hit || fabs(a2 - b2) > tol_lo * fma(0.5, a2 + b2, 1.0);
       }
-      double nr[M], ni[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        nr[i] = A[i] - Bs[i];
-        ni[i] = (C[i] - A[i]) - Bs[i];
-      }
-      // ---- the square-root-free lower bound over the element nodes
-      bool hit = false;
+    });
+    const bool need = !done && it >= o.min_iter && !hit;
+    const bool exact = __ballot(need) != 0ull;        // (uniform)
+    double err = 0.0, amin = __builtin_huge_val();
+    if (exact) {
       static_for<0, M>([&](auto kk) {
         constexpr int i = decltype(kk)::value;
-        if ((o.node_mask >> i) & 1) {                 // (uniform) the element is a node
-          const double e = pf_bc16<i % 16>(eres), e2 = e * e;
-          const double a2 = fma(ni[i], ni[i], nr[i] * nr[i]) * e2;
-          const double b2 = fma(S.ui[i], S.ui[i], S.ur[i] * S.ur[i]) * e2;
-          hit = hit || fabs(a2 - b2) > tol_lo * fma(0.5, a2 + b2, 1.0);
+        if ((o.node_mask >> i) & 1) {                 // (uniform)
+          const double e = pf_bc16<i % 16>(eres);
+          const double mo = od_mag(fma(S.ui[i], S.ui[i], S.ur[i] * S.ur[i])) * e;
+          const double mn = od_mag(fma(ni[i], ni[i], nr[i] * nr[i])) * e;
+          err = od_max(err, fabs(mn - mo));
+          amin = fmin(amin, mo);
         }
       });
-      const bool need = !done && it >= o.min_iter && !hit;
-      const bool exact = __ballot(need) != 0ull;      // (uniform)
-      double err = 0.0, amin = __builtin_huge_val();
-      if (exact) {
-        static_for<0, M>([&](auto kk) {
-          constexpr int i = decltype(kk)::value;
-          if ((o.node_mask >> i) & 1) {               // (uniform)
-            const double e = pf_bc16<i % 16>(eres);
-            const double mo = od_mag(fma(S.ui[i], S.ui[i], S.ur[i] * S.ur[i])) * e;
-            const double mn = od_mag(fma(ni[i], ni[i], nr[i] * nr[i])) * e;
-            err = od_max(err, fabs(mn - mo));
-            amin = fmin(amin, mo);
-          }
-        });
-      }
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        S.ur[i] = done ? S.ur[i] : nr[i];
-        S.ui[i] = done ? S.ui[i] : ni[i];
-      }
-      int d = 0;
-      if (exact) {
-        // the change bound's sums: this iteration's currents against the
-        // previous ones (the rounding, ~1e-15 relative, as slack)
-        double dsum = 0.0, jsum = 0.0;
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-          const double2 c = cur[k * kBlock + tid], p = prv[k * kBlock + tid];
-          dsum += fabs(c.x - p.x) + fabs(c.y - p.y);
-          jsum += fabs(p.x) + fabs(p.y);
-        }
-        dsum = fma(0x1p-40, jsum + dsum, dsum);
-        jsum = fma(0x1p-40, jsum, jsum);
-        if (R > 0) {                                  // (uniform)
-          od_rows<M, false>(sh, prv, nullptr, R, done, err, amin);
-          od_rows<M, true>(sh, cur, prv, R, done, err, amin);
-        }
-        d = od_decide(o, full, it, err, amin, dsum, jsum);
-      }
-      undecided = !done && d < 0;
-      my_it = done ? my_it : it;
-      conv_ok = conv_ok || (!done && d > 0);
-      done = done || d > 0 || it >= o.max_iter;
-      if (__ballot(undecided) != 0ull) break;
     }
-    if (__ballot(undecided) != 0ull) continue;     // (uniform) re-run with every row
-    return conv_ok ? my_it : -my_it;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      S.ur[i] = done ? S.ur[i] : nr[i];
+      S.ui[i] = done ? S.ui[i] : ni[i];
+    }
+    int d = 0;
+    if (exact) {
+      // the change bound's sums: this iteration's currents against the
+      // previous ones (the rounding, ~1e-15 relative, as slack)
+      double dsum = 0.0, jsum = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const double2 c = cur[k * kBlock + tid], p = prv[k * kBlock + tid];
+        dsum += fabs(c.x - p.x) + fabs(c.y - p.y);
+        jsum += fabs(p.x) + fabs(p.y);
+      }
+      dsum = fma(0x1p-40, jsum + dsum, dsum);
+      jsum = fma(0x1p-40, jsum, jsum);
+      od_check_rows<M>(sh, cur, prv, 0, o.n_rep, err, amin);
+      d = od_decide(o, !bounded, it, err, amin, dsum, jsum);
+      // an env whose bounds cannot decide: its wave evaluates the bounded
+      // rows too, in this iteration, and the env takes the exact decision
+      if (__ballot(!done && d < 0) != 0ull) {
+        od_check_rows<M>(sh, cur, prv, o.n_rep, o.n_rows, err, amin);
+        d = d < 0 ? od_decide(o, true, it, err, amin, dsum, jsum) : d;
+      }
+    }
+    my_it = done ? my_it : it;
+    conv_ok = conv_ok || (!done && d > 0);
+    done = done || d > 0 || it >= o.max_iter;
   }
+  return conv_ok ? my_it : -my_it;
 }
 
 // Fused C4 step, OpenDSS rule: k_coord_pf's prologue (agent powers -> bus
@@ -1676,9 +1690,22 @@ static int32_t launch_coord_agents(const pgw_coord_params& p, const pgw_coord_st
   return check_launch("k_coord_agents");
 }
 
+// The event that orders a second-stream power flow after the agents' kernel
+// (pgw_coord_step_overlap): recorded and waited on within one call, so one per
+// process suffices.
+static hipEvent_t coord_agents_event() {
+  static std::once_flag once;
+  static hipEvent_t ev = nullptr;
+  std::call_once(once, [] { (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming); });
+  return ev;
+}
+
+// pf_stream == stream: one stream (pgw_coord_step); otherwise the PF kernel
+// runs on pf_stream after the agents' kernel (pgw_coord_step_overlap).
 template <class Bufs>
 static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
-                          const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream) {
+                          const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream,
+                          void* pf_stream) {
   constexpr bool kF32 = std::is_same<Bufs, pgw_coord_buffers_f32>::value;
   PGW_REQUIRE(p && pf && pft && s && n >= 0, "pgw_coord_step: null argument");
   PGW_REQUIRE(p->n_agents >= 1 && p->n_agents <= PGW_MAX_AGENTS, "pgw_coord_step: bad n_agents");
@@ -1744,12 +1771,18 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
+  hipStream_t pst = (hipStream_t)pf_stream;
+  if (pst != st) {
+    hipEvent_t ev = coord_agents_event();
+    PGW_REQUIRE(ev && hipEventRecord(ev, st) == hipSuccess && hipStreamWaitEvent(pst, ev, 0) == hipSuccess,
+                "pgw_coord_step_overlap: stream ordering failed");
+  }
   if (pft->od) {
-    launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs>, dim3(grid_for(n)), dim3(kBlock), st, c, a,
+    launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs>, dim3(grid_for(n)), dim3(kBlock), pst, c, a,
                  make_od_args(*pft->od, pf->max_iter), *pft, n, b);
     return check_launch("k_coord_pf_od");
   }
-  PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, st);
+  PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, pst);
 }
 
 // pgw_coord_step_general: the agents' kernel, then the general power flow with
@@ -1923,13 +1956,25 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
                        const pgw_coord_step_info* s, int64_t n, pgw_coord_buffers b, void* stream) {
-  return coord_step(p, pf, pft, s, n, b, stream);
+  return coord_step(p, pf, pft, s, n, b, stream, stream);
 }
 
 int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
                            const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                            pgw_coord_buffers_f32 b, void* stream) {
-  return coord_step(p, pf, pft, s, n, b, stream);
+  return coord_step(p, pf, pft, s, n, b, stream, stream);
+}
+
+int32_t pgw_coord_step_overlap(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
+                               const pgw_coord_step_info* s, int64_t n, pgw_coord_buffers b, void* stream,
+                               void* pf_stream) {
+  return coord_step(p, pf, pft, s, n, b, stream, pf_stream);
+}
+
+int32_t pgw_coord_step_f32_overlap(const pgw_coord_params* p, const pgw_pf_params* pf,
+                                   const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
+                                   pgw_coord_buffers_f32 b, void* stream, void* pf_stream) {
+  return coord_step(p, pf, pft, s, n, b, stream, pf_stream);
 }
 
 }  // extern "C"

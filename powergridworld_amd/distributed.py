@@ -74,6 +74,9 @@ def gather_episode_stats(stats: torch.Tensor) -> torch.Tensor:
     episode, never on the step path."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return stats
+    if dist.get_backend() == "gloo" and stats.device.type != "cpu":
+        # gloo collectives run on host tensors: stage through the CPU
+        return gather_episode_stats(stats.cpu()).to(stats.device)
     world = dist.get_world_size()
     n = torch.tensor([stats.shape[0]], dtype=torch.int64, device=stats.device)
     counts = [torch.zeros_like(n) for _ in range(world)]

@@ -652,6 +652,7 @@ class OpenDSSSolver(PowerFlowSolver):
     # ------------------------------------------------------------ reference API
     def calculate_power_flow(self, p_controllable_consumed: dict = None,
                              q_controllable_consumed: dict = None, current_time: str = None) -> None:
+        self._join()
         n = self.num_envs
         if p_controllable_consumed is not None:
             kt = (tuple(p_controllable_consumed), tuple(q_controllable_consumed or ()))
@@ -806,6 +807,21 @@ class OpenDSSSolver(PowerFlowSolver):
             self._warm, self._warm_valid = (cold, warm), False
         return self._warm[1] if self._warm_valid else self._warm[0]
 
+    def _join(self):
+        """Order the caller's stream after a power flow still running on another
+        stream (set by MultiAgentEnv(overlap_pf=True)); a no-op otherwise."""
+
+    @property
+    def iterations(self):
+        """[N] int32 iteration count of the last solve per env (-max_iter =
+        stopped unconverged)."""
+        self._join()
+        return self._iterations
+
+    @iterations.setter
+    def iterations(self, v):
+        self._iterations = v
+
     def unconverged(self) -> int:
         """Envs whose last solve stopped at max_iter without meeting tol (the
         kernels report their count as -iterations).  Synchronises; never
@@ -843,6 +859,7 @@ class OpenDSSSolver(PowerFlowSolver):
 
     def voltage_extrema(self):
         """(min, max) over all output nodes per env, once per solve (multiagent_env.py:107-113)."""
+        self._join()
         if self._extrema is None:
             if self._all_nodes and self.bus_voltages is self._bv:
                 v = self.v_out[:len(self.output_names)]
@@ -852,9 +869,11 @@ class OpenDSSSolver(PowerFlowSolver):
         return self._extrema
 
     def get_bus_voltages(self) -> dict:
+        self._join()
         return self.bus_voltages
 
     def get_bus_voltage_by_name(self, bus_name: str) -> Union[torch.Tensor, List[torch.Tensor]]:
+        self._join()
         nodes = bus_name_to_nodes(bus_name)
         if len(nodes) == 1:
             return self.bus_voltages[nodes[0]]

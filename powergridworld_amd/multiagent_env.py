@@ -56,7 +56,7 @@ class MultiAgentEnv(Env):
     def __init__(self, common_config: dict = {}, pf_config: dict = {}, agents: list = None,
                  max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
                  device=None, fused: Union[bool, str] = "auto", record_history: bool = False,
-                 dtype=None, history_capacity: int = None, **kwargs):
+                 dtype=None, history_capacity: int = None, overlap_pf: bool = False, **kwargs):
         self.common_config = common_config
         self.rescale_spaces = rescale_spaces
         assert len(agents) > 0, "need at least one agent!"
@@ -133,6 +133,8 @@ class MultiAgentEnv(Env):
         self._hist = None
         if self.record_history:
             self._init_history(history_capacity)
+        if overlap_pf:
+            self._setup_overlap()
 
     # ================================================================ hooks
     @abstractmethod
@@ -177,6 +179,7 @@ class MultiAgentEnv(Env):
 
     def reset(self) -> Dict[str, any]:
         """multiagent_env.py:125-140"""
+        self._pf_join()
         self.episode_step = 0
         oob_poll(self.oob_count)
         self.time = self._time_at(0)
@@ -894,8 +897,24 @@ class MultiAgentEnv(Env):
         if H is not None:            # outputs straight into this step's history slot
             s_ = H["t"] % H["cap"]
             bufs.v_out, bufs.agent_power = H["v"][s_].data_ptr(), H["p"][s_].data_ptr()
-        rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
-                                              self.num_envs, bufs, _lib.stream_ptr(self.device))
+        O = F.get("overlap")
+        if O is None:
+            rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
+                                                  self.num_envs, bufs, _lib.stream_ptr(self.device))
+        else:
+            # the PF of this step on the second stream beside the next step's
+            # agents; this step's buffer set waits for the PF of two steps ago
+            slot = O["slot"]
+            main = torch.cuda.current_stream(self.device)
+            main.wait_event(O["ev"][slot])
+            bufs.reward, bufs.agent_power = O["reward_ptr"][slot], O["power_ptr"][slot]
+            rc = getattr(_lib.lib(), F["kernel"] + "_overlap")(F["params"], pfp, pft, info, self.num_envs, bufs,
+                                                             main.cuda_stream, O["stream"].cuda_stream)
+            O["ev"][slot].record(O["stream"])
+            O["pending"] = O["ev"][slot]
+            O["slot"] = slot ^ 1
+            for ai, agent in enumerate(self.agents):
+                agent._reward, agent._real_power = O["reward"][slot][ai], O["power"][slot][ai]
         if rc:
             _lib.check(rc)
         self.pf_solver.iterations = F["iters"]
@@ -923,6 +942,8 @@ class MultiAgentEnv(Env):
         d = any(e.is_terminal() for e in F["agent0_envs"])
         if H is not None:
             self._record(None)
+        if O is not None:
+            return (F["obs_dict"], O["rew_dict"][slot], F["done_true"] if d else F["done_false"], O["meta"])
         return F["obs_dict"], F["rew_dict"], F["done_true"] if d else F["done_false"], F["meta"]
 
     def _step_entry(self, skey):
@@ -930,6 +951,7 @@ class MultiAgentEnv(Env):
         PV index, time, tables version): exogenous rows, PV value, PF parameters
         and tables of the hour; cached per key (every episode repeats them)."""
         F, solver = self._fused, self.pf_solver
+        self._pf_join()              # the table uploads below must not pass a running PF
         t, p, time = skey[0], skey[1], skey[2]
         bld, pv = F["bld0"], F["pv0"]
         info = _lib.CoordStepInfo()
@@ -973,16 +995,79 @@ class MultiAgentEnv(Env):
         """The env's whole state (device tensors, generator states, clocks):
         powergridworld_amd.checkpoint.state_dict."""
         from powergridworld_amd.checkpoint import state_dict
+        self._pf_join()
         return state_dict(self)
 
     def load_state_dict(self, sd, strict=False):
         """Restore a state_dict() of an env of the same configuration (in place)."""
         from powergridworld_amd.checkpoint import load_state_dict
+        self._pf_join()
         return load_state_dict(self, sd, strict)
 
     def packed_obs(self):
         """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""
         return self._fused["obs"].transpose(1, 2)
+
+    # ================================================================ PF beside the next step
+    def _setup_overlap(self):
+        """overlap_pf=True (fused C4 path, pgw_coord_step_overlap): step t's power
+        flow runs on a second stream beside step t+1's agents' kernel -- C4's
+        observations do not read voltages (multiagent_env.py:165-189), so only
+        the rewards, the violation and the voltages wait for it.  Two buffer sets
+        (rewards, agent powers) alternate by step.  The rewards / meta mappings a
+        step returns, env.voltages, the solver's outputs, reset(), state_dict()
+        and every host-side table update make the caller's current stream wait
+        for the pending power flow first (_pf_join), so every value read through
+        them is the synchronous step's, bit for bit."""
+        F = self._fused
+        if F is None or F["kernel"] not in ("pgw_coord_step", "pgw_coord_step_f32"):
+            raise ValueError("overlap_pf needs the fused C4 step (pgw_coord_step); this env runs %s"
+                             % (F["kernel"] if F else "the generic / multi-agent path"))
+        if self._hist is not None:
+            raise ValueError("overlap_pf: record_history is not supported")
+        dev = self.device
+        rew = [F["reward"], torch.zeros_like(F["reward"])]
+        pwr = [F["agent_power"], torch.zeros_like(F["agent_power"])]
+        O = dict(slot=0, pending=None, stream=torch.cuda.Stream(dev),
+                 ev=[torch.cuda.Event(), torch.cuda.Event()], reward=rew, power=pwr,
+                 reward_ptr=[r.data_ptr() for r in rew], power_ptr=[q.data_ptr() for q in pwr])
+        O["rew_dict"] = [_JoinedMapping(self, {a.name: r[ai] for ai, a in enumerate(self.agents)}) for r in rew]
+        O["meta"] = _JoinedMapping(self, F["meta"])
+        F["overlap"] = O
+        self.pf_solver._join = self._pf_join
+
+    def _pf_join(self):
+        """The current stream waits for the pending overlapped power flow."""
+        F = self._fused
+        O = F.get("overlap") if F is not None else None
+        if O is not None and O["pending"] is not None:
+            torch.cuda.current_stream(self.device).wait_event(O["pending"])
+            O["pending"] = None
+
+
+class _JoinedMapping(Mapping):
+    """A step's rewards / meta under overlap_pf: the mapping of the synchronous
+    step, whose every read first joins the pending power flow."""
+    __slots__ = ("_env", "_d")
+
+    def __init__(self, env, d):
+        self._env, self._d = env, d
+
+    def __getitem__(self, k):
+        self._env._pf_join()
+        return self._d[k]
+
+    def __iter__(self):
+        return iter(self._d)
+
+    def __len__(self):
+        return len(self._d)
+
+    def __contains__(self, k):
+        return k in self._d
+
+    def copy(self):
+        return dict(self.items())
 
 
 class _FusedVoltages(Mapping):
@@ -1003,6 +1088,7 @@ class _FusedVoltages(Mapping):
         return self._full
 
     def __getitem__(self, node):
+        self._env._pf_join()
         v = self._fast.get(node)
         return v if v is not None else self._all()[node]
 

@@ -12,6 +12,13 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    # multi-process GPU tests fork their ranks from a forkserver started here,
+    # before this process touches the GPU: no rank is a fork or an exec of a
+    # GPU-initialised process
+    mark = (config.option.markexpr or "").strip()
+    if mark == "gpu" or (mark and "not gpu" not in mark and "gpu" in mark):
+        import multiprocessing.forkserver as fs
+        fs.ensure_running()
 
 
 def golden_path(name):
