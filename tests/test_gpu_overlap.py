@@ -27,15 +27,17 @@ def test_overlap_equals_synchronous_step(conv):
     rng = np.random.default_rng(5)
     init = torch.tensor(rng.uniform(5.0, 45.0, size=(5, n)), device=DEV)
     acts = torch.tensor(rng.uniform(-1, 1, size=(steps, 5, n, 8)), device=DEV)
-    for env in (sync, ov):
+    def start(env):
         env.reset()
         for ai, agent in enumerate(env.agents):
             agent.env_dict["storage"].reset(init_storage=init[ai])
         env.load_component_state()
+    for env in (sync, ov):
+        start(env)
     for t in range(steps):
         if t == 25:                                  # a reset in the middle of the stream
             for env in (sync, ov):
-                env.reset()
+                start(env)
         out = []
         for env in (sync, ov):
             obs, rew, done, meta = env.step(acts[t])
@@ -48,6 +50,7 @@ def test_overlap_equals_synchronous_step(conv):
     # the state after the stream (device copies), and stepping on from a restore
     sd = ov.state_dict()
     ov2 = _pair(conv, n)[1]
+    ov2.reset()
     ov2.load_state_dict(sd)
     _, r1, _, _ = ov.step(acts[0])
     _, r2, _, _ = ov2.step(acts[0])
