@@ -394,7 +394,8 @@ typedef struct pgw_pf_tables {
  *
  * start (device, this step's hour): the first iteration in closed form -- from
  * the direct solution the currents are affine in the env's controllable
- * (P, Q): u_1 = u1b + P u1P + Q u1Q; u1b, u1P, u1Q (m complex each). */
+ * (P, Q): u_1 = u1b + P u1P + Q u1Q and J_1 = J1b + P J1P + Q J1Q; u1b, u1P,
+ * u1Q, J1b, J1P, J1Q (m complex each). */
 #define PGW_PF_OD_MAX_ROWS 28
 typedef struct pgw_pf_od {
   double tol;                        /* 1e-4 (ConvergenceTolerance)            */
@@ -405,7 +406,7 @@ typedef struct pgw_pf_od {
   int32_t n_rep, n_rows, pad_;
   const double* rows_V0;             /* n_rows complex (device)                */
   const double* rows_G;              /* n_rows x m complex (device)            */
-  const double* start;               /* 6 m doubles (device)                   */
+  const double* start;               /* 12 m doubles (device)                  */
 } pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

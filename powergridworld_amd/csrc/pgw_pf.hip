@@ -941,6 +941,9 @@ template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
                                                      int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;   // double, or float (_f32)
+  // issue priority over a co-resident agents' kernel (pgw_coord_step_overlap):
+  // this kernel is issue-bound, the agents' one memory-bound
+  __builtin_amdgcn_s_setprio(3);
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   // read once: a reload per phase would put an L2 round trip on the chain
@@ -1053,7 +1056,7 @@ constexpr int kOdChunk = 12;                      // check rows per previous-mag
 //         during an exact test
 template <int M> struct ODShared {
   double rows[kOdRows * 16 * PFRow<M>::kPairs];
-  double st[6 * M];
+  double st[12 * M];
   double2 J[2][M * kBlock];
   double old[kOdChunk * kBlock];
 };
@@ -1115,7 +1118,7 @@ __device__ __forceinline__ void od_stage(const ODArgs& o, ODShared<M>& sh) {
     else if (j < 2 + 2 * M) v = o.rows_G[2 * M * r + 2 * (j - 2 - M) + 1];
     sh.rows[i] = v;
   }
-  for (int i = threadIdx.x; i < 6 * M; i += kBlock) sh.st[i] = o.start[i];
+  for (int i = threadIdx.x; i < 12 * M; i += kBlock) sh.st[i] = o.start[i];
 }
 
 // Rows [r0, r1) (r1 - r0 <= kOdChunk) from the currents in J (the lane's
@@ -1248,21 +1251,19 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid
   // |a| - |b| > tol for sure when |a^2 - b^2| > tol_lo ((a^2 + b^2)/2 + 1)
   const double tol_lo = o.tol * (1.0 + 0x1p-30);
   const bool bounded = o.n_rep < o.n_rows;
-  // ---- iteration 1: its currents I'(u0) (the next test's previous ones);
-  // u_1 from the affine table
-  pf_u0<M>(S.ur, S.ui, S.w);
-  static_for<0, M>([&](auto kk) {
-    constexpr int k = decltype(kk)::value;
-    double jr, ji, y0r, y0i;
-    pf_od_elem<M, k>(y0r, y0i, yres);
-    S.template current_od<k>(y0r, y0i, jr, ji);
-    sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
-  });
+  // ---- iteration 1 from the affine tables: its currents I'(u0) (the next
+  // test's previous ones) and u_1
   const double* st = sh.st;
+  auto affine = [&](int c, double& re, double& im) {    // table entry c (of 3 M)
+    re = fma(S.qc, st[2 * (2 * M + c)], fma(S.pc, st[2 * (M + c)], st[2 * c]));
+    im = fma(S.qc, st[2 * (2 * M + c) + 1], fma(S.pc, st[2 * (M + c) + 1], st[2 * c + 1]));
+  };
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    S.ur[k] = fma(S.qc, st[2 * (2 * M + k)], fma(S.pc, st[2 * (M + k)], st[2 * k]));
-    S.ui[k] = fma(S.qc, st[2 * (2 * M + k) + 1], fma(S.pc, st[2 * (M + k) + 1], st[2 * k + 1]));
+    double jr, ji;
+    affine(3 * M + k, jr, ji);
+    sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
+    affine(k, S.ur[k], S.ui[k]);
   }
   int it = 1, my_it = 1;
   bool done = !valid || o.max_iter <= 1, conv_ok = !valid;
@@ -1369,6 +1370,7 @@ template <int M, class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
                                                         int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;
+  __builtin_amdgcn_s_setprio(3);                     // (as k_coord_pf)
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   __shared__ ODShared<M> sh;

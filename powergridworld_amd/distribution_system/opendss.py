@@ -269,14 +269,14 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_rows = [f.node_names[i] for i in rows]
         self._od_W2 = W / (vb_elem[:, None] * vb_elem[None, :])
         self._od_u0 = U0 / vb_elem
-        self._od_start = torch.zeros((self.OD_MAX_TABLES, 6 * M), dtype=torch.float64, device=dev)
+        self._od_start = torch.zeros((self.OD_MAX_TABLES, 12 * M), dtype=torch.float64, device=dev)
         self._od_index = {}
         self._od_keep = {}
 
     def _od_starts(self, hour):
         """First-iteration tables (pgw_pf_od.start) of `hour` and the following
         hours that have none: from the direct solution u0 the currents are affine
-        in the controllable (P, Q), so u_1 is too."""
+        in the controllable (P, Q), so they and u_1 are tabulated as affine maps."""
         hours, keys = [], []
         for h in range(hour, min(hour + self.PREDICTOR_LOOKAHEAD, len(self.annual_hourly_load_profile))):
             k = self._hour_key(h)
@@ -305,7 +305,7 @@ class OpenDSSSolver(PowerFlowSolver):
             p = self._params_for_hour(h)
             s0 = (np.array(p.base_kw[:M]) * 1000.0) / nph - 1j * ((np.array(p.base_kvar[:M]) * 1000.0) / nph)
             J0 = (s0 * g - y0) * u0
-            recs[q] = np.concatenate([u0 + W2 @ J0, u1P, u1Q]).view(np.float64)
+            recs[q] = np.concatenate([u0 + W2 @ J0, u1P, u1Q, J0, jP, jQ]).view(np.float64)
         for j, k in enumerate(keys):
             self._od_index[k] = idx0 + j
         if hours:

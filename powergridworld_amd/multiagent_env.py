@@ -1028,7 +1028,8 @@ class MultiAgentEnv(Env):
         dev = self.device
         rew = [F["reward"], torch.zeros_like(F["reward"])]
         pwr = [F["agent_power"], torch.zeros_like(F["agent_power"])]
-        O = dict(slot=0, pending=None, stream=torch.cuda.Stream(dev),
+        # high priority: its kernel dispatches ahead of the next step's agents
+        O = dict(slot=0, pending=None, stream=torch.cuda.Stream(dev, priority=-1),
                  ev=[torch.cuda.Event(), torch.cuda.Event()], reward=rew, power=pwr,
                  reward_ptr=[r.data_ptr() for r in rew], power_ptr=[q.data_ptr() for q in pwr])
         O["rew_dict"] = [_JoinedMapping(self, {a.name: r[ai] for ai, a in enumerate(self.agents)}) for r in rew]

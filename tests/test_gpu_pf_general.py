@@ -307,14 +307,17 @@ def test_c4_opendss_fused_equals_generic_and_oracle():
 
 def test_het_opendss_fused_equals_generic():
     """The heterogeneous scenario with convergence="opendss": pgw_ma_step's
-    agents + the general PF (extrema epilogue for the PV farm's min_voltage)
-    bit-identical to the generic path over a stretch of the episode."""
+    agents + the OpenDSS-rule PF (fast or general kernel; extrema epilogue for
+    the PV farm's min_voltage) bit-identical to the generic path over a stretch
+    of the episode."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     n = 512
     envs = [MultiAgentEnv(**make_env_config(pf_convergence="opendss"), num_envs=n, device=DEV, fused=f)
             for f in ("auto", False)]
-    assert envs[0]._ma is not None and envs[0]._ma["general"] is not None and envs[1]._ma is None
+    assert envs[0]._ma is not None and envs[1]._ma is None
+    # one controllable bus: the fast OpenDSS-rule kernel (k_pf_solve_od); more: the general one
+    assert (envs[0]._ma["general"] is None) == envs[0].pf_solver._od_fast
     rng = np.random.default_rng(12)
     for e in envs:
         for k, a in enumerate(e.agents):
