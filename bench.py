@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="(internal) print the cpu_baseline JSON and exit; bench.py runs this as a "
                          "child process so the oracle's imports stay out of the timed process")
-    ap.add_argument("--time-steps", type=int, default=64,
+    ap.add_argument("--time-steps", type=int, default=286,
                     help="steps of the kernel-timing pass after the timed region (every launch "
                          "HIP-event-timed; at least 8, at most --steps)")
     ap.add_argument("--pf-convergence", choices=("opendss", "exact"), default="opendss",

@@ -10,6 +10,7 @@ import os
 import sys
 
 NAMES = {"k_coord_agents_std": "k_coord_agents_std",
+         "k_coord_pf_od<14": "k_coord_pf_od<14>",
          "k_coord_pf<14, true, false, false": "k_coord_pf<14,true,false,false>",
          "k_coord_pf_split": "k_coord_pf_split",
          "k_pf_solve<14, true, false, false>": "k_pf_solve<14,true,false,false>"}
@@ -32,11 +33,23 @@ def main():
     base = os.path.join("gpurun_out", "pmc", tag)
     fetch = per_kernel(os.path.join(base, "p3"), "FETCH_SIZE")
     write = per_kernel(os.path.join(base, "p4"), "WRITE_SIZE")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), run " + tag,
+    path = os.path.join("profiles", "pmc_traffic.json")
+    old = json.load(open(path)) if os.path.exists(path) else {}
+    runs = dict(old.get("runs", {}))
+    for k in old.get("bytes_per_launch", {}):             # kernels this run did not launch keep theirs
+        runs.setdefault(k, old.get("source", "").split()[-1])
+    for k in fetch:
+        runs[k] = tag
+    bpl = dict(old.get("bytes_per_launch", {}))
+    bpl.update({k: (2 * fetch[k] + write.get(k, 0.0)) * 1024 for k in fetch})
+    fk = dict(old.get("fetch_kb", {}))
+    fk.update(fetch)
+    wk = dict(old.get("write_kb", {}))
+    wk.update(write)
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), run per kernel in `runs`",
            "formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes, mean per dispatch",
-           "bytes_per_launch": {k: (2 * fetch[k] + write.get(k, 0.0)) * 1024 for k in fetch},
-           "fetch_kb": fetch, "write_kb": write}
-    with open(os.path.join("profiles", "pmc_traffic.json"), "w") as f:
+           "runs": runs, "bytes_per_launch": bpl, "fetch_kb": fk, "write_kb": wk}
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["bytes_per_launch"]))
 
