@@ -1251,27 +1251,35 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid
   // |a| - |b| > tol for sure when |a^2 - b^2| > tol_lo ((a^2 + b^2)/2 + 1)
   const double tol_lo = o.tol * (1.0 + 0x1p-30);
   const bool bounded = o.n_rep < o.n_rows;
-  // ---- iteration 1 from the affine tables: its currents I'(u0) (the next
-  // test's previous ones) and u_1
+  // ---- iteration 1 from the affine tables: u_1 now; its currents I'(u0)
+  // (an exact test's previous ones at iteration 2, or the outputs when
+  // max_iter = 1) only when needed
   const double* st = sh.st;
   auto affine = [&](int c, double& re, double& im) {    // table entry c (of 3 M)
     re = fma(S.qc, st[2 * (2 * M + c)], fma(S.pc, st[2 * (M + c)], st[2 * c]));
     im = fma(S.qc, st[2 * (2 * M + c) + 1], fma(S.pc, st[2 * (M + c) + 1], st[2 * c + 1]));
   };
+  auto currents_1 = [&]() {
 #pragma unroll
-  for (int k = 0; k < M; ++k) {
-    double jr, ji;
-    affine(3 * M + k, jr, ji);
-    sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
-    affine(k, S.ur[k], S.ui[k]);
-  }
+    for (int k = 0; k < M; ++k) {
+      double jr, ji;
+      affine(3 * M + k, jr, ji);
+      sh.J[1][k * kBlock + tid] = make_double2(jr, ji);
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < M; ++k) affine(k, S.ur[k], S.ui[k]);
+  if (o.max_iter <= 1) currents_1();                 // (uniform)
   int it = 1, my_it = 1;
   bool done = !valid || o.max_iter <= 1, conv_ok = !valid;
   while (__ballot(!done) != 0ull) {
     ++it;
     double2* const cur = sh.J[it & 1];
     const double2* const prv = sh.J[(it & 1) ^ 1];
-    // ---- currents of u_{k-1} (into LDS), u_k by the matvec
+    // ---- currents of u_{k-1} (into LDS), u_k by the matvec.  (Interleaving
+    // element k+1's current law between slices of column k's FMAs measured no
+    // faster -- profiles/r04/ab_pipelined_column_loop.txt: the wave is bound by
+    // its DPP issue rate, not by the chain's latency.)
     double A[M], Bs[M], C[M];
     pf_acc_init<M>(A, C, S.w);
 #pragma unroll
@@ -1336,6 +1344,7 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid
     }
     int d = 0;
     if (exact) {
+      if (it == 2) currents_1();                     // (uniform)
       // the change bound's sums: this iteration's currents against the
       // previous ones (the rounding, ~1e-15 relative, as slack)
       double dsum = 0.0, jsum = 0.0;
