@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 24
+#define PGW_ABI_VERSION 25
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -831,6 +831,47 @@ typedef struct pgw_mc_step_args {
 } pgw_mc_step_args;
 
 int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream);
+
+/* fp32 storage variant: the same fields, every per-env buffer
+ * (state, obs, actions, real powers, rewards) fp32; fp64 arithmetic, each value
+ * rounded once at its store, the agent sums formed in fp64 from the
+ * components' stored values (what pgw_agent_reduce would read).  ev_endp,
+ * ev_charging and pv_min_voltage keep their types.  Layout-identical to
+ * pgw_mc_step_args. */
+typedef struct pgw_mc_component_f32 {
+  int32_t kind, pad_;
+  pgw_matf action;
+  pgw_matf obs;
+  float* real_power;
+} pgw_mc_component_f32;
+
+typedef struct pgw_mc_step_args_f32 {
+  int32_t n_comp, pad_;
+  pgw_mc_component_f32 comp[4];
+  pgw_building_params bld;
+  pgw_building_exo bld_ex_t, bld_ex_next;
+  pgw_building_ext bld_ext;
+  float* bld_x;
+  float* bld_reward_state;
+  pgw_pv_params pv;
+  double pv_pmax;
+  const double* pv_min_voltage;
+  pgw_battery_params bat;
+  float* bat_soc;
+  pgw_ev_params ev;
+  pgw_ev_step_info ev_step;
+  const double* ev_endp;
+  float* ev_req;
+  uint64_t* ev_charging;
+  float* ev_reward;
+  float* real_power;
+  float* reward;
+  const pgw_mc_step_dyn* dyn;
+  int32_t* clock;
+  int32_t n_dyn, pad2_;
+} pgw_mc_step_args_f32;
+
+int32_t pgw_mc_agent_step_f32(const pgw_mc_step_args_f32* a, int64_t n, void* stream);
 
 /* Test / A-B knob of pgw_mc_agent_step's EV walk (process-wide, not per call):
  * -1 = automatic (the default: split over extra waves where the blocks are at

@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -219,6 +219,16 @@ class MCStepArgs(C.Structure):
                 ("dyn", vp), ("clock", vp), ("n_dyn", i32), ("pad2_", i32)]
 
 
+class MCComponentF32(C.Structure):
+    _fields_ = [("kind", i32), ("pad_", i32), ("action", Matf), ("obs", Matf), ("real_power", vp)]
+
+
+class MCStepArgsF32(C.Structure):
+    """pgw_mc_step_args_f32: pgw_mc_step_args with fp32 per-env buffers (the same
+    field names, so the components' _mc_static / _mc_prepare fill it unchanged)."""
+    _fields_ = [(nm, MCComponentF32 * 4) if nm == "comp" else (nm, tp) for nm, tp in MCStepArgs._fields_]
+
+
 MA_MAX_SLOTS = 8
 
 
@@ -327,6 +337,7 @@ _SIGS = {
                                      CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),
     "pgw_mc_agent_step": (i32, [P(MCStepArgs), i64, vp]),
+    "pgw_mc_agent_step_f32": (i32, [P(MCStepArgsF32), i64, vp]),
     "pgw_mc_ev_split_mode": (i32, [i32, P(i32)]),
     "pgw_graph_begin": (i32, [vp]),
     "pgw_graph_end": (i32, [vp, P(vp)]),
@@ -341,7 +352,7 @@ EXPORTED = sorted(_SIGS)
 STRUCTS = [Mat, BatteryParams, PVParams, BuildingParams, BuildingExo, BuildingExt, EVParams,
            EVStepInfo, ReduceArgs, PFParams, PFTables, FeederElem, CoordParams, CoordBuffers,
            CoordStepInfo, PredMeta, HSParams, HSStepInfo, HSBuffers, MCStepArgs, Matf, CoordBuffersF32,
-           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams, MCStepDyn, PFOD]
+           MAStepArgs, PFGElem, PFGParams, PFGTables, RegParams, MCStepDyn, PFOD, MCStepArgsF32]
 
 _lib = None
 

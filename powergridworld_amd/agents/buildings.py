@@ -318,7 +318,7 @@ class FiveZoneROMEnv(ComponentEnv):
         args.bld, args.bld_ext = self.params, _lib.BuildingExt()
         args.bld_x, args.bld_reward_state = self.x.data_ptr(), self._reward_state.data_ptr()
         c = args.comp[slot]
-        c.kind, c.obs, c.real_power = 0, _lib.mat(self._obs), self.p_consumed.data_ptr()
+        c.kind, c.obs, c.real_power = 0, self._mat(self._obs), self.p_consumed.data_ptr()
 
     def _mc_prepare(self, args, slot, action, obs_kwargs):
         a, m = self._action_mat(action, 6)

@@ -147,7 +147,7 @@ class EnergyStorageEnv(ComponentEnv):
     def _mc_static(self, args, slot):
         args.bat, args.bat_soc = self.params, self.soc.data_ptr()
         c = args.comp[slot]
-        c.kind, c.obs, c.real_power = 2, _lib.mat(self._obs), self._real_power.data_ptr()
+        c.kind, c.obs, c.real_power = 2, self._mat(self._obs), self._real_power.data_ptr()
 
     def _mc_prepare(self, args, slot, action, kwargs):
         a, args.comp[slot].action = self._action_mat(action, 1)

@@ -91,7 +91,7 @@ class PVEnv(ComponentEnv):
         f = self._mc_pv_fields if hasattr(args, "pv2_pmax") else PVEnv._mc_pv_fields
         setattr(args, f[0], self.params)
         c = args.comp[slot]
-        c.kind, c.obs, c.real_power = 1, _lib.mat(self._obs), self._real_power.data_ptr()
+        c.kind, c.obs, c.real_power = 1, self._mat(self._obs), self._real_power.data_ptr()
 
     def _mc_prepare(self, args, slot, action, kwargs):
         a, m = self._action_mat(action, 1)

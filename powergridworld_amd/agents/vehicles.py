@@ -203,7 +203,7 @@ class EVChargingEnv(ComponentEnv):
         args.ev_endp, args.ev_req = self._endp_dev.data_ptr(), self.req.data_ptr()
         args.ev_charging, args.ev_reward = self.charging.data_ptr(), self._reward.data_ptr()
         c = args.comp[slot]
-        c.kind, c.obs, c.real_power = 3, _lib.mat(self._obs), self._real_power.data_ptr()
+        c.kind, c.obs, c.real_power = 3, self._mat(self._obs), self._real_power.data_ptr()
 
     def _mc_prepare(self, args, slot, action, kwargs):
         args.ev_step = self._step_info(action is not None)

@@ -194,7 +194,7 @@ class ComponentEnv(spaces.Env, ABC):
                     # (pointer + strides), never a reference that would pin the
                     # allocation
                     return action, hit
-        a = as_action(action, self.num_envs, dim, self.device)
+        a = as_action(action, self.num_envs, dim, self.device, self.dtype)
         m = self._act_mat(a)
         if key is not None and a is action:
             c = self.__dict__.get("_am_c")
@@ -290,7 +290,11 @@ def register_env(cls):
 class MultiComponentEnv(ComponentEnv):
     """Single agent composed of several component envs (gridworld/base.py:74-182):
     the action/observation spaces are the union, real power and reward the sum
-    over components (reward recomputed after all components stepped, base.py:137)."""
+    over components (reward recomputed after all components stepped, base.py:137).
+    dtype=torch.float32: fp32 storage for every component (fp64 arithmetic),
+    stepped by pgw_mc_agent_step_f32; the fused component kinds only."""
+
+    supported_dtypes = (torch.float64, torch.float32)
 
     def __init__(self, name: str = None, components: List[dict] = None, num_envs: int = 1,
                  device=None, **kwargs):
@@ -298,11 +302,14 @@ class MultiComponentEnv(ComponentEnv):
         self.envs = []
         for c in components:
             cls = resolve_env_class(c["cls"])
-            env = cls(name=c["name"], num_envs=self.num_envs, device=self.device, **c["config"])
+            cfg = dict(c["config"])
+            if self.dtype != torch.float64:
+                cfg.setdefault("dtype", self.dtype)
+            env = cls(name=c["name"], num_envs=self.num_envs, device=self.device, **cfg)
             env._in_multicomponent = True
             if env.dtype != self.dtype:
-                raise NotImplementedError("MultiComponentEnv steps fp64 components only "
-                                          "(component %s is %s)" % (env.name, env.dtype))
+                raise NotImplementedError("MultiComponentEnv: component %s is %s, the agent %s"
+                                          % (env.name, env.dtype, self.dtype))
             self.envs.append(env)
         self._bind_oob(self.oob_count)
         self.observation_space = spaces.Dict({e.name: e.observation_space for e in self.envs})
@@ -312,9 +319,12 @@ class MultiComponentEnv(ComponentEnv):
         for e in self.envs:
             obs_labels += e.obs_labels
         self._obs_labels = list(set(obs_labels))
-        self._reward = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._reward = torch.zeros(self.num_envs, dtype=self.dtype, device=self.device)
         if len(self.envs) > _lib.MAX_COMP:
             raise ValueError("at most %d components per agent" % _lib.MAX_COMP)
+        if self.dtype != torch.float64 and not self._mc_fusable():
+            raise NotImplementedError("MultiComponentEnv dtype=%s needs every component to be a fused kind "
+                                      "(pgw_mc_agent_step_f32)" % self.dtype)
 
     def _bind_oob(self, counter):
         super()._bind_oob(counter)
@@ -373,13 +383,15 @@ class MultiComponentEnv(ComponentEnv):
             key = (self._real_power.data_ptr(), self._reward.data_ptr(), [e._bufv for e in self.envs])
             args = self.__dict__.get("_mc_args")
             if args is None or self._mc_args_key != key:
-                args = _lib.MCStepArgs()
+                f32 = self.dtype == torch.float32
+                args = (_lib.MCStepArgsF32 if f32 else _lib.MCStepArgs)()
                 args.n_comp = len(self.envs)
                 for c, env in enumerate(self.envs):
                     env._mc_static(args, c)
                 args.real_power, args.reward = self._real_power.data_ptr(), self._reward.data_ptr()
                 self._mc_args, self._mc_args_key = args, key
-                self._mc_call = (_lib.lib().pgw_mc_agent_step, self.num_envs)
+                self._mc_call = (_lib.lib().pgw_mc_agent_step_f32 if f32 else _lib.lib().pgw_mc_agent_step,
+                                 self.num_envs)
             keep = []
             if kwargs:
                 kws = [{k: v for k, v in kwargs.items() if k in env.obs_labels} for env in self.envs]

@@ -481,10 +481,10 @@ __device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev
 }
 
 // Group g's part of the walk (k_mc_step's split EV waves).
-template <class Mt>
+template <class S, class Mt>
 __device__ __forceinline__ EvSums ev_step_group(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
                                                 int64_t e, const Mt& act, const double* __restrict__ endp,
-                                                double* __restrict__ req, uint64_t* __restrict__ chg, int g,
+                                                S* __restrict__ req, uint64_t* __restrict__ chg, int g,
                                                 uint64_t* s_bits, int lane) {
   const double kwh = ev_kwh(p, s, e, act, g == 0);
   const int nc = ev_chunks(s), K = ev_group_len(nc);
@@ -511,19 +511,32 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
 // reward where it has one) to the component's own buffers.
 // `V`: the step's shared values -- the launch's own fields (pgw_mc_step_args)
 // or a device-clocked record (pgw_mc_step_dyn); both name them alike.
-template <bool STD, class V>
-__device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const V& v, const pgw_mc_component& C,
+// Args: pgw_mc_step_args (fp64 storage) or pgw_mc_step_args_f32 (fp32 storage).
+template <class Args> struct McStore {
+  using S = double;
+  using Mt = pgw_mat;
+};
+template <> struct McStore<pgw_mc_step_args_f32> {
+  using S = float;
+  using Mt = pgw_matf;
+};
+static_assert(sizeof(pgw_mc_step_args_f32) == sizeof(pgw_mc_step_args), "pgw_mc_step_args_f32 layout");
+
+template <bool STD, class Args, class V, class Comp>
+__device__ __forceinline__ void mc_component(const Args& a, const V& v, const Comp& C,
                                              const BldDerived& d, int64_t n, int64_t e) {
+  using S = typename McStore<Args>::S;
+  using Mt = typename McStore<Args>::Mt;
   switch (C.kind) {
     case PGW_MC_BUILDING:
-      (void)building_step_env<STD, double, pgw_mat>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action, a.bld_x,
-                                   C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
+      (void)building_step_env<STD, S, Mt>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action, a.bld_x,
+                                          C.real_power, (S*)nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
       break;
     case PGW_MC_PV:
-      C.real_power[e] = pv_step_env(a.pv, e, v.pv_pmax, C.action, a.pv_min_voltage, C.obs);
+      C.real_power[e] = (S)pv_step_env(a.pv, e, v.pv_pmax, C.action, a.pv_min_voltage, C.obs);
       break;
     case PGW_MC_STORAGE:
-      C.real_power[e] = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
+      C.real_power[e] = (S)battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
       break;
     default:
       ev_step_env(a.ev, v.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
@@ -563,9 +576,10 @@ __device__ __forceinline__ void mc_component(const pgw_mc_step_args& a, const V&
 // block barrier the EV slot's wave folds the partial sums in group order and
 // finishes the EV step.  C3 runs one wave per SIMD and the EV wave's walk --
 // one memory round trip per chunk -- was the block's critical path.
-template <bool STD, bool CLK>
-__global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(pgw_mc_step_args a_, BldDerived d, int64_t n) {
-  const pgw_mc_step_args& a = PGW_KERNARG0(pgw_mc_step_args);
+template <class Args, bool STD, bool CLK>
+__global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, BldDerived d, int64_t n) {
+  using S = typename McStore<Args>::S;
+  const Args& a = PGW_KERNARG0(Args);
   __shared__ double s_rp[4][64], s_rew[4][64];
   __shared__ uint64_t s_bits[PGW_EV_MAX_WORDS * 64];
   __shared__ double s_evs[kEvGroups][4][64];
@@ -605,7 +619,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(pgw_mc_ste
       s_evc[g][0][lane] = t.dcnt;
       s_evc[g][1][lane] = t.nact;
     } else {
-      const pgw_mc_component& C = a.comp[w];
+      const auto& C = a.comp[w];
       if constexpr (CLK)
         mc_component<STD>(a, s_dyn, C, d, n, e);
       else
@@ -630,7 +644,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(pgw_mc_ste
         t.nact += s_evc[g][1][lane];
       }
       for (int j = 0; j < evs.n_words; ++j) a.ev_charging[(int64_t)j * n + e] = s_bits[j * 64 + lane];
-      const pgw_mc_component& C = a.comp[ev_slot];
+      const auto& C = a.comp[ev_slot];
       ev_finish(a.ev, evs, e, t, C.obs, C.real_power, a.ev_reward);
       s_rp[w][lane] = C.real_power[e];
       s_rew[w][lane] = a.ev_reward[e];
@@ -644,8 +658,8 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(pgw_mc_ste
     rp_sum = rp_sum + s_rp[c][lane];
     rew_sum = rew_sum + s_rew[c][lane];
   }
-  a.real_power[e] = rp_sum;
-  a.reward[e] = rew_sum;
+  a.real_power[e] = (S)rp_sum;
+  a.reward[e] = (S)rew_sum;
 }
 
 // ====================================================================== fused multi-agent step
@@ -959,12 +973,15 @@ int32_t pgw_mc_ev_split_mode(int32_t mode, int32_t* previous) {
   return PGW_OK;
 }
 
-int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
+}  // extern "C"
+
+template <class Args>
+static int32_t mc_agent_step(const Args* a, int64_t n, void* stream) {
   PGW_REQUIRE(a && n >= 0 && a->n_comp >= 1 && a->n_comp <= 4, "pgw_mc_agent_step: bad args");
   PGW_REQUIRE(a->real_power && a->reward, "pgw_mc_agent_step: null output");
   int seen = 0;
   for (int c = 0; c < a->n_comp; ++c) {
-    const pgw_mc_component& C = a->comp[c];
+    const auto& C = a->comp[c];
     PGW_REQUIRE(C.kind >= 0 && C.kind <= 3 && !(seen & (1 << C.kind)),
                 "pgw_mc_agent_step: component kinds must be distinct PGW_MC_* values");
     seen |= 1 << C.kind;
@@ -1007,10 +1024,20 @@ int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
   const dim3 grid((unsigned)blocks), block(64u * (unsigned)(a->n_comp + (split ? kEvGroups - 1 : 0)));
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
   if (std_bld)
-    a->clock ? go(k_mc_step<true, true>) : go(k_mc_step<true, false>);
+    a->clock ? go(k_mc_step<Args, true, true>) : go(k_mc_step<Args, true, false>);
   else
-    a->clock ? go(k_mc_step<false, true>) : go(k_mc_step<false, false>);
+    a->clock ? go(k_mc_step<Args, false, true>) : go(k_mc_step<Args, false, false>);
   return check_launch("k_mc_step");
+}
+
+extern "C" {
+
+int32_t pgw_mc_agent_step(const pgw_mc_step_args* a, int64_t n, void* stream) {
+  return mc_agent_step(a, n, stream);
+}
+
+int32_t pgw_mc_agent_step_f32(const pgw_mc_step_args_f32* a, int64_t n, void* stream) {
+  return mc_agent_step(a, n, stream);
 }
 
 int32_t pgw_ma_step(const pgw_ma_step_args* a, const pgw_pf_params* pf, const pgw_pf_tables* pft,

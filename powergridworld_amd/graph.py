@@ -227,8 +227,9 @@ class StepGraph:
         kws = [{k: v for k, v in kwargs.items() if k in e.obs_labels} for e in env.envs]
         self._kws = kws
         arg_sets = []
+        f32 = env.dtype == torch.float32
         for act in actions:
-            a = _lib.MCStepArgs()
+            a = (_lib.MCStepArgsF32 if f32 else _lib.MCStepArgs)()
             a.n_comp = len(env.envs)
             for c, e in enumerate(env.envs):
                 e._mc_static(a, c)
@@ -256,7 +257,8 @@ class StepGraph:
 
     def _capture_mc(self, arg_sets):
         env = self.env
-        fn, n = _lib.lib().pgw_mc_agent_step, env.num_envs
+        fn = _lib.lib().pgw_mc_agent_step_f32 if env.dtype == torch.float32 else _lib.lib().pgw_mc_agent_step
+        n = env.num_envs
 
         def launch():
             st = env._stream()

@@ -148,8 +148,17 @@ def test_f32_refuses_non_standard_layout():
         CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=8, device=DEV,
                                            dtype=torch.float32, fused=False)
     from powergridworld_amd.base import MultiComponentEnv
-    with pytest.raises(NotImplementedError):          # the fused / generic MC step is fp64 only
-        MultiComponentEnv(name="mc", components=make_c4_config()["agents"][0]["config"]["components"],
+    # an fp32 MC agent runs pgw_mc_agent_step_f32: its components must all be fused kinds
+    m = MultiComponentEnv(name="mc", components=make_c4_config()["agents"][0]["config"]["components"],
+                          num_envs=8, device=DEV, dtype=torch.float32)
+    assert m.dtype == torch.float32 and m._mc_fusable()
+
+    class OwnStepPV(PVEnv):
+        def step(self, *a, **k):
+            return super().step(*a, **k)
+    with pytest.raises(NotImplementedError):
+        MultiComponentEnv(name="mc", components=[{"name": "pv", "cls": OwnStepPV,
+                                                  "config": {"profile_csv": "pv_profile.csv"}}],
                           num_envs=8, device=DEV, dtype=torch.float32)
     assert PVEnv(profile_csv="pv_profile.csv", num_envs=8, device=DEV, dtype=torch.float32).dtype == torch.float32
     with pytest.raises(Exception):
@@ -246,3 +255,63 @@ def test_ev_f32_one_step_and_episode(randomize):
         if d32:
             break
     np.testing.assert_allclose(e32.req.double().cpu().numpy(), free.req.cpu().numpy(), rtol=1e-3, atol=1e-2)
+
+
+def test_mc_f32_c3_one_step_and_episode():
+    """pgw_mc_agent_step_f32 (the C3 agent: building + PV + storage + EV(100),
+    fp32 state / obs / actions / powers / rewards, fp64 arithmetic): from the
+    same fp32 state every component output is RN32 of the fp64 fused step's;
+    the agent sums are formed from the stored fp32 component values (so within
+    2^-23 (sum |terms| + |sum|)); a free-running episode stays within the
+    north-star fp32 bound."""
+    from powergridworld_amd import MultiComponentEnv
+    from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv, FiveZoneROMThermalEnergyEnv, PVEnv
+    n = 16384
+    comps = [
+        {"name": "building", "cls": FiveZoneROMThermalEnergyEnv, "config": {}},
+        {"name": "pv", "cls": PVEnv, "config": {"profile_csv": "pv_profile.csv", "scaling_factor": 40.}},
+        {"name": "storage", "cls": EnergyStorageEnv, "config": {}},
+        {"name": "ev", "cls": EVChargingEnv,
+         "config": dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7.,
+                        peak_threshold=250., vehicle_multiplier=5., rescale_spaces=True)},
+    ]
+    m32 = MultiComponentEnv(name="mc", components=comps, num_envs=n, device=DEV, dtype=torch.float32)
+    m64, free = [MultiComponentEnv(name="mc", components=comps, num_envs=n, device=DEV) for _ in range(2)]
+    assert m32._mc_fusable() and all(e.dtype == torch.float32 for e in m32.envs)
+    init = (torch.rand(n, dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(11)) * 60)
+    init = init.float().double()
+    m32.reset(init_storage=init.float())
+    for e in (m64, free):
+        e.reset(init_storage=init)
+    b32, s32, v32 = m32.env_dict["building"], m32.env_dict["storage"], m32.env_dict["ev"]
+    b64, s64, v64 = m64.env_dict["building"], m64.env_dict["storage"], m64.env_dict["ev"]
+    assert b32.x.dtype == s32.soc.dtype == v32.req.dtype == m32.real_power.dtype == torch.float32
+    gen = torch.Generator(DEV).manual_seed(12)
+    dims = {"building": 6, "pv": 1, "storage": 1, "ev": 1}
+    for t in range(280):
+        act = {c: (torch.rand((n, d), dtype=torch.float64, device=DEV, generator=gen) * 2.4 - 1.2).float()
+               for c, d in dims.items()}
+        b64.x.copy_(b32.x)
+        b64._reward_state.copy_(b32._reward_state)
+        s64.soc.copy_(s32.soc)
+        v64.req.copy_(v32.req)
+        v64.charging.copy_(v32.charging)
+        o32, r32, d32, _ = m32.step(act)
+        o64, r64, d64, _ = m64.step({c: a.double() for c, a in act.items()})
+        free.step({c: a.double() for c, a in act.items()})
+        for c in dims:
+            assert_f32(o32[c], o64[c], ulps=0)
+            assert_f32(m32.env_dict[c].real_power, m64.env_dict[c].real_power, ulps=0)
+        # the sums add the stored (rounded) terms: each term and the sum are off
+        # by <= half an fp32 ulp, so the bound is 2^-24 (sum |terms| + |sum|), x2
+        big = torch.stack([m64.env_dict[c].real_power.abs() for c in dims]).sum(0)
+        assert_f32(m32.real_power, m64.real_power, ulps=0, atol=F32_ULP * (big + m64.real_power.abs()))
+        rbig = b64._reward_state.abs() + v64._reward.abs()
+        assert_f32(r32, r64, ulps=0, atol=F32_ULP * (rbig + r64.abs()))
+        assert d32 == d64
+        if d32:
+            break
+    np.testing.assert_allclose(b32.x.double().cpu().numpy(), free.env_dict["building"].x.cpu().numpy(),
+                               rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(s32.soc.double().cpu().numpy(), free.env_dict["storage"].soc.cpu().numpy(),
+                               rtol=1e-3, atol=1e-2)
