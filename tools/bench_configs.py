@@ -7,7 +7,8 @@ with actions resident in HBM (a pool of pre-generated batches); episodes reset
 inside the timed region.  One JSON line per config.
 
 Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS,...] [--steps K] [--warmup W]
-(HETG: the heterogeneous scenario on the generic path, fused=False; C3L: C3 at
+(HETG: the heterogeneous scenario on the generic path, fused=False; C3F / C3G8F:
+C3 with fp32 storage (pgw_mc_agent_step_f32); C3L: C3 at
 65 536 envs; C2Gk / C3Gk: the step replayed from captured hipGraphs of k steps,
 C3 through the device clocks; C3Pk / HSPk: captured once per episode position,
 powergridworld_amd/graph.py)
@@ -83,7 +84,7 @@ def bench_c2(dev, steps, warmup, n=4096, pool=64, graph=0):
                 batch=n, agents=1, steps=steps, seconds=dt)
 
 
-def c3_env(dev, n, pool=16):
+def c3_env(dev, n, pool=16, dtype=torch.float64):
     """The C3 agent and a pool of pre-generated action dicts (HBM resident)."""
     from powergridworld_amd import MultiComponentEnv
     from powergridworld_amd.agents import EnergyStorageEnv, EVChargingEnv, FiveZoneROMThermalEnergyEnv, PVEnv
@@ -95,18 +96,18 @@ def c3_env(dev, n, pool=16):
          "config": dict(num_vehicles=100, minutes_per_step=5, max_charge_rate_kw=7.,
                         peak_threshold=250., vehicle_multiplier=5., rescale_spaces=True)},
     ]
-    env = MultiComponentEnv(name="mc", components=comps, num_envs=n, device=dev)
+    env = MultiComponentEnv(name="mc", components=comps, num_envs=n, device=dev, dtype=dtype)
     gen = torch.Generator(dev).manual_seed(0)
     dims = {"building": 6, "pv": 1, "storage": 1, "ev": 1}
-    acts = [{c: torch.empty((n, d), dtype=torch.float64, device=dev).uniform_(-1, 1, generator=gen)
+    acts = [{c: torch.empty((n, d), dtype=dtype, device=dev).uniform_(-1, 1, generator=gen)
              for c, d in dims.items()} for _ in range(pool)]
     return env, acts
 
 
-def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True):
-    env, acts = c3_env(dev, n, pool)
+def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True, dtype=torch.float64):
+    env, acts = c3_env(dev, n, pool, dtype)
     gen = torch.Generator(dev).manual_seed(1)
-    init = torch.empty(n, dtype=torch.float64, device=dev).uniform_(3.0, 50.0, generator=gen)
+    init = torch.empty(n, dtype=dtype, device=dev).uniform_(3.0, 50.0, generator=gen)
     k = [0]
 
     def step():
@@ -133,7 +134,8 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True):
             warmup = max(warmup, (pool // graph) * (287 // graph + 1))
     dt = timed_loop(env, step, reset, steps, warmup)
     steps *= max(graph, 1)
-    return dict(config="C3" + ("L" if n != 16384 else "") + (("G%d" if clocked else "P%d") % graph if graph else ""),
+    return dict(config="C3" + ("L" if n != 16384 else "") + (("G%d" if clocked else "P%d") % graph if graph else "")
+                + ("F" if dtype == torch.float32 else ""),
                 workload="MC building+PV+storage+EV(100 vehicles)" + (
                     ", %d-step captured graphs%s" % (graph, "" if clocked else " per episode position")
                     if graph else ""),
@@ -215,6 +217,8 @@ def main():
            "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),
            "C3P8": lambda *a: bench_c3(*a, graph=8, clocked=False),
            "C3L": lambda *a: bench_c3(*a, n=65536),
+           "C3F": lambda *a: bench_c3(*a, dtype=torch.float32),
+           "C3G8F": lambda *a: bench_c3(*a, graph=8, dtype=torch.float32),
            "HSP8": lambda *a: bench_hs(*a, graph=8)}
     for name in args.configs.split(","):
         r = fns[name](dev, args.steps, args.warmup)
