@@ -74,12 +74,15 @@ for mode in a.modes.split(","):
     ks = {nm: round(tot[i] / cnt[i] * 1e3, 2) for i, nm in enumerate(("agents", "coord_pf", "pf_solve", "-", "ma", "pf_general")) if cnt[i]}
     it = env.pf_solver.iterations.abs()
     if a.hist:            # per-step max / mean iterations over a pass (one sync per step)
-        hist = {}
+        hist, seq = {}, []
         for _ in range(a.hist):
             run(1)
-            mx = int(env.pf_solver.iterations.abs().max())
+            its = env.pf_solver.iterations.abs()
+            mx, mn = int(its.max()), int(its.min())
             hist[mx] = hist.get(mx, 0) + 1
+            seq.append("%d%d" % (mn, mx))
         print("  per-step max iterations over %d steps: %s" % (a.hist, dict(sorted(hist.items()))))
+        print("  per-step (min, max) iterations in order: " + " ".join(seq))
     tag = mode + ("/" + a.rows if a.rows and mode == "opendss" else "") + \
         ("/max%d" % a.max_iter if a.max_iter and mode == "opendss" else "") + \
         ("/nobound" if a.nobound and mode == "opendss" else "")
