@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 25
+#define PGW_ABI_VERSION 26
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -390,7 +390,10 @@ typedef struct pgw_pf_tables {
  * a bound cannot decide an env's test, its wave evaluates the bounded rows too
  * (that iteration), so the stopping iteration is always the exact rule's.  The
  * rows are evaluated only in iterations where some env of the wave has no
- * element node whose change is surely above tol (min_iter >= 2).
+ * element node whose change is surely above tol (min_iter >= 2).  A wave with
+ * at most sparse_envs envs to test evaluates their rows one env at a time
+ * (one lane per row) instead of as every lane's row groups -- same values,
+ * bit for bit; sparse_envs 0 = the default (4), < 0 = never.
  *
  * start (device, this step's hour): the first iteration in closed form -- from
  * the direct solution the currents are affine in the env's controllable
@@ -403,7 +406,8 @@ typedef struct pgw_pf_od {
   double elem_scale[PGW_PF_MAX_M];   /* node |V| pu = |u_k| * scale; 0 = none   */
   double gamma, eps, gmax, gsrc;     /* check-row bound constants (above)      */
   int32_t min_iter;                  /* 2 (MinIterations); >= 2                */
-  int32_t n_rep, n_rows, pad_;
+  int32_t n_rep, n_rows;
+  int32_t sparse_envs;               /* 0 = default (4); < 0 never; <= 64     */
   const double* rows_V0;             /* n_rows complex (device)                */
   const double* rows_G;              /* n_rows x m complex (device)            */
   const double* start;               /* 12 m doubles (device)                  */

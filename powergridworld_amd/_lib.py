@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -108,7 +108,7 @@ PF_OD_MAX_ROWS = 28
 class PFOD(C.Structure):
     _fields_ = [("tol", f64), ("y0r", f64 * PF_MAX_M), ("y0i", f64 * PF_MAX_M),
                 ("elem_scale", f64 * PF_MAX_M), ("gamma", f64), ("eps", f64), ("gmax", f64),
-                ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("pad_", i32),
+                ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("sparse_envs", i32),
                 ("rows_V0", vp), ("rows_G", vp), ("start", vp)]
 
 

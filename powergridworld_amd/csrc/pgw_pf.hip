@@ -1041,12 +1041,21 @@ struct ODArgs {
   const double* rows_V0;
   const double* rows_G;
   int32_t min_iter, n_rep, n_rows, max_iter;
+  int32_t sparse;                                 // envs a wave's exact test takes one at a time
   int32_t node_mask;                              // bit k: element k is a node (esc[k] > 0)
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
 constexpr int kOdChunk = 12;                      // check rows per previous-magnitude pass
+constexpr int kOdSparse = 4;                      // pgw_pf_od.sparse_envs's default
+static_assert(kOdRows <= 32, "od_rows_sparse: one lane pair per row");
+// Check-row stride in LDS: the resident row layout plus one pad slot, so that
+// od_rows_sparse's lanes (one row each) read 32 rows without bank conflicts.
+template <int M> struct ODRow {
+  static constexpr int kStride = 16 * PFRow<M>::kPairs + 1;
+};
 // LDS of the OpenDSS solve, per block of kBlock lanes (one env each):
-//   rows  the check rows in the resident row layout (pf_row_load)
+//   rows  the check rows in the resident row layout (od_row_load), row
+//         stride ODRow<M>::kStride
 //   st    pgw_pf_od.start (broadcast reads)
 //   J     per lane, by iteration parity: iteration k's currents I'(u_{k-1})
 //         go to J[k & 1], so the last two iterations' are always there (a lane
@@ -1055,7 +1064,7 @@ constexpr int kOdChunk = 12;                      // check rows per previous-mag
 //   old   per lane: the previous magnitudes of up to kOdChunk check rows
 //         during an exact test
 template <int M> struct ODShared {
-  double rows[kOdRows * 16 * PFRow<M>::kPairs];
+  double rows[kOdRows * ODRow<M>::kStride];
   double st[12 * M];
   double2 J[2][M * kBlock];
   double old[kOdChunk * kBlock];
@@ -1080,6 +1089,7 @@ static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   o.n_rep = d.n_rep;
   o.n_rows = d.n_rows;
   o.max_iter = max_iter;
+  o.sparse = d.sparse_envs == 0 ? kOdSparse : d.sparse_envs < 0 ? 0 : min(d.sparse_envs, 64);
   for (int k = 0; k < PGW_PF_MAX_M; ++k)
     if (d.elem_scale[k] > 0.0) o.node_mask |= 1 << k;
   return o;
@@ -1108,7 +1118,7 @@ __device__ __forceinline__ double od_mag(double m2) {
 // LDS; the block synchronises before use.
 template <int M>
 __device__ __forceinline__ void od_stage(const ODArgs& o, ODShared<M>& sh) {
-  constexpr int S = 16 * PFRow<M>::kPairs;
+  constexpr int S = ODRow<M>::kStride;
   const int rows = o.n_rows;
   for (int i = threadIdx.x; i < rows * S; i += kBlock) {
     const int r = i / S, j = i - r * S;
@@ -1119,6 +1129,13 @@ __device__ __forceinline__ void od_stage(const ODArgs& o, ODShared<M>& sh) {
     sh.rows[i] = v;
   }
   for (int i = threadIdx.x; i < 12 * M; i += kBlock) sh.st[i] = o.start[i];
+}
+
+template <int M>
+__device__ __forceinline__ void od_row_load(const double* s, int o, double (&w)[PFRow<M>::kPairs]) {
+  const double* r = s + ODRow<M>::kStride * o + (threadIdx.x & 15);
+#pragma unroll
+  for (int p = 0; p < PFRow<M>::kPairs; ++p) w[p] = r[16 * p];
 }
 
 // Rows [r0, r1) (r1 - r0 <= kOdChunk) from the currents in J (the lane's
@@ -1140,16 +1157,16 @@ __device__ __forceinline__ void od_rows(const ODShared<M>& sh, const double2* J,
     ii[k] = j.y;
   }
   double wa[P], wb[P], wc[P], wd[P];
-  pf_row_load<M>(sh.rows, r0, wa);
-  pf_row_load<M>(sh.rows, min(r0 + 1, last), wb);
-  pf_row_load<M>(sh.rows, min(r0 + 2, last), wc);
-  pf_row_load<M>(sh.rows, min(r0 + 3, last), wd);
+  od_row_load<M>(sh.rows, r0, wa);
+  od_row_load<M>(sh.rows, min(r0 + 1, last), wb);
+  od_row_load<M>(sh.rows, min(r0 + 2, last), wc);
+  od_row_load<M>(sh.rows, min(r0 + 3, last), wd);
   for (int o = r0; o < r1; o += 4) {
     double na[P], nb[P], nc[P], nd[P];
-    pf_row_load<M>(sh.rows, min(o + 4, last), na);     // the next group in flight
-    pf_row_load<M>(sh.rows, min(o + 5, last), nb);
-    pf_row_load<M>(sh.rows, min(o + 6, last), nc);
-    pf_row_load<M>(sh.rows, min(o + 7, last), nd);
+    od_row_load<M>(sh.rows, min(o + 4, last), na);     // the next group in flight
+    od_row_load<M>(sh.rows, min(o + 5, last), nb);
+    od_row_load<M>(sh.rows, min(o + 6, last), nc);
+    od_row_load<M>(sh.rows, min(o + 7, last), nd);
     double* const ol = old + (o - r0) * kBlock + tid;
     double om[4];
     if constexpr (CMP) {
@@ -1191,6 +1208,54 @@ __device__ __forceinline__ void od_check_rows(ODShared<M>& sh, const double2* cu
     const int e = min(c + kOdChunk, r1);
     od_rows<M, false>(sh, prv, sh.old, c, e, err, amin);
     od_rows<M, true>(sh, cur, sh.old, c, e, err, amin);
+  }
+}
+
+// Rows [r0, r1) (<= 32) of an exact test for the few envs of the wave in
+// `envs` (lane bits), one env at a time, transposed: lane 2 q evaluates row
+// r0 + q from the env's previous currents, lane 2 q + 1 from its current ones
+// -- each with pf_node_pu's operations in od_rows's order, so the magnitudes
+// are bit-identical --, and a butterfly reduces the row changes and previous
+// magnitudes onto the env's lane.  For a wave where one env or a few need the
+// test, instead of every lane's DPP row groups.
+template <int M>
+__device__ __forceinline__ void od_rows_sparse(const ODShared<M>& sh, const double2* cur, const double2* prv,
+                                               int r0, int r1, uint64_t envs, double& err, double& amin) {
+  if (r0 >= r1) return;                              // (uniform)
+  const int lane = threadIdx.x & 63;
+  const int row = min(r0 + (lane >> 1), r1 - 1);
+  const bool on = r0 + (lane >> 1) < r1;
+  const double* R = sh.rows + ODRow<M>::kStride * row;
+  const double2* J = (lane & 1) ? cur : prv;
+  const int wave0 = threadIdx.x & ~63;
+  while (envs) {                                     // (uniform)
+    const int L = __builtin_ctzll(envs);
+    envs &= envs - 1;
+    const double2* Je = J + wave0 + L;
+    double vr = R[0], vi = R[1];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      const double gr = R[2 + k], gi = R[2 + M + k];
+      const double2 j = Je[k * kBlock];
+      vr = fma(gr, j.x, vr);
+      vi = fma(gr, j.y, vi);
+      vr = fma(-gi, j.y, vr);
+      vi = fma(gi, j.x, vi);
+    }
+    const double mg = od_mag(fma(vi, vi, vr * vr));
+    const double mn = __shfl_xor(mg, 1);             // even lanes: the new magnitude
+    const bool prev_lane = on && !(lane & 1);
+    double we = prev_lane ? fabs(mn - mg) : 0.0;
+    double wa = prev_lane ? mg : __builtin_huge_val();
+#pragma unroll
+    for (int x = 1; x < 64; x <<= 1) {
+      we = od_max(we, __shfl_xor(we, x));
+      wa = fmin(wa, __shfl_xor(wa, x));
+    }
+    if (lane == L) {
+      err = od_max(err, we);
+      amin = fmin(amin, wa);
+    }
   }
 }
 
@@ -1323,7 +1388,8 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid
       }
     });
     const bool need = !done && it >= o.min_iter && !hit;
-    const bool exact = __ballot(need) != 0ull;        // (uniform)
+    const uint64_t needs = __ballot(need);
+    const bool exact = needs != 0ull;                 // (uniform)
     double err = 0.0, amin = __builtin_huge_val();
     if (exact) {
       static_for<0, M>([&](auto kk) {
@@ -1356,12 +1422,19 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid
       }
       dsum = fma(0x1p-40, jsum + dsum, dsum);
       jsum = fma(0x1p-40, jsum, jsum);
-      od_check_rows<M>(sh, cur, prv, 0, o.n_rep, err, amin);
+      // (an env that is not tested here already fails at an element node
+      // or is below min_iter: its decision does not read the rows)
+      if (__popcll(needs) <= o.sparse) od_rows_sparse<M>(sh, cur, prv, 0, o.n_rep, needs, err, amin);
+      else od_check_rows<M>(sh, cur, prv, 0, o.n_rep, err, amin);
       d = od_decide(o, !bounded, it, err, amin, dsum, jsum);
       // an env whose bounds cannot decide: its wave evaluates the bounded
       // rows too, in this iteration, and the env takes the exact decision
-      if (__ballot(!done && d < 0) != 0ull) {
-        od_check_rows<M>(sh, cur, prv, o.n_rep, o.n_rows, err, amin);
+      const uint64_t undecided = __ballot(!done && d < 0);
+      if (undecided != 0ull) {
+        if (__popcll(undecided) <= o.sparse)
+          od_rows_sparse<M>(sh, cur, prv, o.n_rep, o.n_rows, undecided, err, amin);
+        else
+          od_check_rows<M>(sh, cur, prv, o.n_rep, o.n_rows, err, amin);
         d = d < 0 ? od_decide(o, true, it, err, amin, dsum, jsum) : d;
       }
     }

@@ -98,12 +98,19 @@ def test_od_bounded_rows_equal_every_row_and_rerun():
     K = 4096
     loads = _loads(K, 3)
     ref = _solve_all(_solver(num_envs=K), loads)
-    for change in (dict(n_rep=None), dict(gsrc=1e9)):
+    # also: every wave's rows as row groups (sparse_envs < 0) and every
+    # tested env's rows one env at a time (64), with and without bounds that
+    # decide -- the transposed evaluation (od_rows_sparse) against the DPP row
+    # groups, bit for bit
+    for change in (dict(n_rep=None), dict(gsrc=1e9), dict(sparse_envs=-1), dict(sparse_envs=64),
+                   dict(sparse_envs=64, gsrc=1e9), dict(sparse_envs=-1, gsrc=1e9)):
         s = _solver(num_envs=K)
         if change.get("n_rep", 0) is None:
             s._od_proto.n_rep = s._od_proto.n_rows
-        else:
+        if "gsrc" in change:
             s._od_proto.gsrc = change["gsrc"]
+        if "sparse_envs" in change:
+            s._od_proto.sparse_envs = change["sparse_envs"]
         s._tables_cache.clear()
         got = _solve_all(s, loads)
         assert torch.equal(got[1], ref[1]), change

@@ -22,6 +22,8 @@ ap.add_argument("--nobound", action="store_true", help="opendss only: zero bound
 ap.add_argument("--hist", type=int, default=0, help="after timing: per-step max iterations over HIST steps")
 ap.add_argument("--rows", default="", help="opendss only: 'none' (no check row evaluated; results wrong) "
                                          "or 'all' (every row every iteration), for phase costs")
+ap.add_argument("--sparse", type=int, default=None, help="opendss only: pgw_pf_od.sparse_envs (0 default, "
+                                                         "-1 never, 64 always)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 n = a.n
@@ -36,6 +38,10 @@ for mode in a.modes.split(","):
         od.n_rep = 0 if a.rows == "none" else od.n_rows
         if a.rows == "none":
             od.n_rows = 0
+        env.pf_solver._tables_cache.clear()
+        env._fused["step_cache"].clear()
+    if a.sparse is not None and mode == "opendss":
+        env.pf_solver._od_proto.sparse_envs = a.sparse
         env.pf_solver._tables_cache.clear()
         env._fused["step_cache"].clear()
     if a.nobound and mode == "opendss":      # bounds that always decide (timing only)
