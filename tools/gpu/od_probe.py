@@ -80,15 +80,19 @@ for mode in a.modes.split(","):
     ks = {nm: round(tot[i] / cnt[i] * 1e3, 2) for i, nm in enumerate(("agents", "coord_pf", "pf_solve", "-", "ma", "pf_general")) if cnt[i]}
     it = env.pf_solver.iterations.abs()
     if a.hist:            # per-step max / mean iterations over a pass (one sync per step)
-        hist, seq = {}, []
+        hist, seq, seq2 = {}, [], []
         for _ in range(a.hist):
             run(1)
             its = env.pf_solver.iterations.abs()
             mx, mn = int(its.max()), int(its.min())
             hist[mx] = hist.get(mx, 0) + 1
             seq.append("%d%d" % (mn, mx))
+            early = (its < mx).view(-1, 64).sum(1)           # per wave: envs stopping before the step's max
+            seq2.append("%d/%d" % (int((early > 0).sum()), int(early.max())))
         print("  per-step max iterations over %d steps: %s" % (a.hist, dict(sorted(hist.items()))))
         print("  per-step (min, max) iterations in order: " + " ".join(seq))
+        print("  per-step waves with an env stopping before the max / most such envs in one wave: " +
+              " ".join(seq2))
     tag = mode + ("/" + a.rows if a.rows and mode == "opendss" else "") + \
         ("/max%d" % a.max_iter if a.max_iter and mode == "opendss" else "") + \
         ("/nobound" if a.nobound and mode == "opendss" else "")
