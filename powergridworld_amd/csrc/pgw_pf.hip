@@ -528,7 +528,6 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   long long* const trace = g_pf_trace;
-  pf_trace(trace, 0);
   constexpr bool kKeep = KEEP || !UB || GC;   // general variants always keep the currents
   __shared__ double s_rows[kKeep ? kRowsLds : 1];
   bool rows_lds = false;
@@ -536,6 +535,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
   S.load(a, t.block);
+  pf_trace(trace, 0);                          // (behind the loads: see k_coord_pf)
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
@@ -948,7 +948,6 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   const bool valid = e < n;
   // read once: a reload per phase would put an L2 round trip on the chain
   long long* const trace = g_pf_trace;
-  pf_trace(trace, 0);
   // HBM first: the agent powers gate the predictor.  The loads are
   // unconditional (clamped indices, then scaled by 1 or 0 -- a select would be
   // sunk back into a branch around the load) so that all of them issue back
@@ -968,6 +967,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
   // every lane stays to the end of the solve: the DPP broadcasts read all lanes
   PFSolver<M, UB, GC> S;
   S.load(a, t.block);
+  // phase 0 is stamped once the prologue's loads are in flight: the trace
+  // pointer's test waits for its load, which at the kernel's first instruction
+  // put a whole dependent L2 round trip ahead of the agent-power loads
+  pf_trace(trace, 0);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
@@ -1115,20 +1118,59 @@ __device__ __forceinline__ double od_mag(double m2) {
 }
 
 // The check rows (resident row layout) and the first-iteration table into
-// LDS; the block synchronises before use.
+// LDS, in two halves so that every load of the stage is in flight at once and
+// the kernel's own prologue loads go out behind them: od_stage_load issues
+// them (a fixed count per lane, no branches: one L2 round trip instead of one
+// per 256 entries), od_stage_store writes LDS; the block synchronises before
+// use.  (The rolled loop waited for each load before the next: ~5 dependent
+// round trips ahead of the solve.)
+template <int M> struct ODStage {
+  static constexpr int kRowQ = (kOdRows * ODRow<M>::kStride + kBlock - 1) / kBlock;
+  static constexpr int kStQ = (12 * M + kBlock - 1) / kBlock;
+  double v[kRowQ + kStQ];
+  double y0r, y0i, esc;                            // od_solve's resident element constants
+};
+
 template <int M>
-__device__ __forceinline__ void od_stage(const ODArgs& o, ODShared<M>& sh) {
+__device__ __forceinline__ void od_stage_load(const ODArgs& o, ODStage<M>& g) {
   constexpr int S = ODRow<M>::kStride;
-  const int rows = o.n_rows;
-  for (int i = threadIdx.x; i < rows * S; i += kBlock) {
+  const int total = o.n_rows * S;
+#pragma unroll
+  for (int q = 0; q < ODStage<M>::kRowQ; ++q) {
+    const int i = threadIdx.x + q * kBlock;
     const int r = i / S, j = i - r * S;
-    double v = 0.0;
-    if (j < 2) v = o.rows_V0[2 * r + j];
-    else if (j < 2 + M) v = o.rows_G[2 * M * r + 2 * (j - 2)];
-    else if (j < 2 + 2 * M) v = o.rows_G[2 * M * r + 2 * (j - 2 - M) + 1];
-    sh.rows[i] = v;
+    // the entry's source (any in-bounds address when it has none)
+    const bool has = i < total && j < 2 + 2 * M;
+    const double* p = j < 2 ? o.rows_V0 + (2 * r + j)
+                            : o.rows_G + (2 * M * r + (j < 2 + M ? 2 * (j - 2) : 2 * (j - 2 - M) + 1));
+    g.v[q] = has ? *p : 0.0;
   }
-  for (int i = threadIdx.x; i < 12 * M; i += kBlock) sh.st[i] = o.start[i];
+#pragma unroll
+  for (int q = 0; q < ODStage<M>::kStQ; ++q) {
+    const int i = threadIdx.x + q * kBlock;
+    g.v[ODStage<M>::kRowQ + q] = i < 12 * M ? o.start[i] : 0.0;
+  }
+  const int l = threadIdx.x & 15;
+  const bool in = l < M;
+  g.y0r = in ? o.y0r[l] : 0.0;
+  g.y0i = in ? o.y0i[l] : 0.0;
+  g.esc = in ? o.esc[l] : 0.0;
+}
+
+template <int M>
+__device__ __forceinline__ void od_stage_store(const ODArgs& o, const ODStage<M>& g, ODShared<M>& sh) {
+  constexpr int S = ODRow<M>::kStride;
+  const int total = o.n_rows * S;
+#pragma unroll
+  for (int q = 0; q < ODStage<M>::kRowQ; ++q) {
+    const int i = threadIdx.x + q * kBlock;
+    if (i < total) sh.rows[i] = g.v[q];
+  }
+#pragma unroll
+  for (int q = 0; q < ODStage<M>::kStQ; ++q) {
+    const int i = threadIdx.x + q * kBlock;
+    if (i < 12 * M) sh.st[i] = g.v[ODStage<M>::kRowQ + q];
+  }
 }
 
 template <int M>
@@ -1301,18 +1343,14 @@ __device__ __forceinline__ void od_load_J(const ODShared<M>& sh, int it, double 
 //                the first n_rep rows, the bounded ones only when some env's
 //                bounds cannot decide (it then takes the exact decision).
 template <int M>
-__device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, bool valid, ODShared<M>& sh) {
+__device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, const ODStage<M>& g, bool valid,
+                        ODShared<M>& sh) {
   static_assert(kOdRows <= 2 * M, "od_rows keeps two row magnitudes per current slot");
   const int tid = threadIdx.x;
   // per-element constants resident for DPP: y0' (re, im) and the node scale
-  double yres[2], eres;
-  {
-    const int l = threadIdx.x & 15;
-    const bool in = l < M;
-    yres[0] = in ? o.y0r[l] : 0.0;
-    yres[1] = in ? o.y0i[l] : 0.0;
-    eres = in ? o.esc[l] : 0.0;
-  }
+  // (loaded with the stage)
+  double yres[2] = {g.y0r, g.y0i};
+  const double eres = g.esc;
   // |a| - |b| > tol for sure when |a^2 - b^2| > tol_lo ((a^2 + b^2)/2 + 1)
   const double tol_lo = o.tol * (1.0 + 0x1p-30);
   const bool bounded = o.n_rep < o.n_rows;
@@ -1456,7 +1494,8 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   __shared__ ODShared<M> sh;
-  od_stage<M>(o, sh);
+  ODStage<M> stg;
+  od_stage_load<M>(o, stg);                          // in flight with the loads below
   double rp[PGW_MAX_AGENTS];
   const int64_t ec = valid ? e : 0;
 #pragma unroll
@@ -1478,8 +1517,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
     for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
   S.powers(a, cp, cq, 1.0);
+  od_stage_store<M>(o, stg, sh);
   __syncthreads();                                   // the staged check rows
-  const int it = od_solve<M>(S, o, valid, sh);
+  const int it = od_solve<M>(S, o, stg, valid, sh);
   double ir[M], ii[M], v0r, v0i;
   od_load_J<M>(sh, it, ir, ii);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
@@ -1512,7 +1552,8 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   __shared__ ODShared<M> sh;
-  od_stage<M>(o, sh);
+  ODStage<M> stg;
+  od_stage_load<M>(o, stg);                          // in flight with the loads below
   PFSolver<M, true, false> S;
   S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
@@ -1522,8 +1563,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
   S.powers(a, cp, cq, 1.0);
+  od_stage_store<M>(o, stg, sh);
   __syncthreads();                                   // the staged check rows
-  const int it = od_solve<M>(S, o, valid, sh);
+  const int it = od_solve<M>(S, o, stg, valid, sh);
   double ir[M], ii[M], v0r, v0i;
   od_load_J<M>(sh, it, ir, ii);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
