@@ -145,8 +145,11 @@ def f32_variant(conv, n, steps, warmup, pool_size, seed, dev):
     p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
     out = {"dtype": "f32 storage, f64 arithmetic", "value": N_AGENTS * n * steps / dt,
            "unit": "agent-env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
-           "parity": "tests/test_gpu_f32.py: one step = fp64 result rounded once; episode within "
-                     "1e-3 rel of fp64",
+           "parity": "tests/test_gpu_f32.py::test_c4_f32_one_step_parity[%s] (one step = fp64 result "
+                     "rounded once) and ::test_c4_f32_episode_within_bound[%s] (episode within 1e-3 rel "
+                     "of fp64), both on this variant's kernels (pgw_coord_step_f32: %s)"
+                     % (conv, conv, "k_coord_pf_od<14, pgw_coord_buffers_f32>" if conv == "opendss"
+                        else "k_coord_pf<14,true,false,false, pgw_coord_buffers_f32>"),
            "k_coord_agents_std": {"avg_us": a_us, "bytes_per_launch": AGENT_BYTES_F32 * N_AGENTS * n,
                                   "achieved": (AGENT_BYTES_F32 * N_AGENTS * n / (a_us * 1e-6) / 1e9
                                                if a_us else None),
@@ -206,7 +209,7 @@ def pf_variant(conv, n, steps, warmup, pool, dev):
            "pf_iterations_max": int(it.max()),
            "k_coord_agents_std_avg_us": tot[0] / cnt[0] * 1e3 if cnt[0] else None,
            "pf_kernel": {"name": PF_KERNEL_NAME[conv] if env.pf_solver._od_fast or conv == "exact"
-                         else "k_pf_general", "avg_us": p_us, "bound": "mfma"}}
+                         else "k_pf_general", "avg_us": p_us, "bound": "fp64 valu"}}
     if p_us:
         out["pf_kernel"].update(pf_roofline(conv, p_us, float(it.mean()), n))
     del env
@@ -456,9 +459,9 @@ def main():
                                    "traffic": traffic.get(KERNELS[0])}
         if p_us:
             pk = PF_KERNEL_NAME[conv]
-            kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "mfma",
-                           "note": "fp64 VALU (MI355X fp64 vector peak = matrix peak); issue-bound "
-                                   "DPP FMAs, one wave per SIMD at 65,536 envs",
+            kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "fp64 valu",
+                           "note": "fp64 VALU DPP FMAs, no MFMA (MI355X fp64 vector peak = matrix "
+                                   "peak); issue-bound, one wave per SIMD at 65,536 envs",
                            "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
                            "traffic": traffic.get(pk)}
             kernels[pk].update(pf_roofline(conv, p_us, mean_it, n))

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 26
+#define PGW_ABI_VERSION 27
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -42,8 +42,10 @@ const char* pgw_last_error(void);
  * reduce_args, pf_params, pf_tables, feeder_elem, coord_params, coord_buffers,
  * coord_step_info, pred_meta, hs_params, hs_step_info, hs_buffers,
  * mc_step_args, matf, coord_buffers_f32, ma_step_args, pfg_elem, pfg_params,
- * pfg_tables, reg_params, mc_step_dyn, pf_od -- lets a binding verify its
- * layouts.  Writes min(n, 29) values, returns 29. */
+ * pfg_tables, reg_params, mc_step_dyn, pf_od, mc_step_args_f32 -- lets a
+ * binding verify its layouts.  Writes min(n, PGW_N_STRUCT_SIZES) values,
+ * returns PGW_N_STRUCT_SIZES. */
+#define PGW_N_STRUCT_SIZES 30
 int32_t pgw_struct_sizes(int64_t* out, int32_t n);
 
 /* A [n_envs x dim] fp64 matrix in device memory: element (e, j) at
@@ -758,21 +760,6 @@ int32_t pgw_coord_step_general(const pgw_coord_params* p, const pgw_pfg_params* 
 int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
                            const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                            pgw_coord_buffers_f32 b, void* stream);
-
-/* pgw_coord_step / _f32 with the power flow on a second stream: the agents'
- * kernel on `stream`; pf_stream then waits for it (an event recorded inside the
- * call) and runs the PF kernel.  So the PF of step t can run beside the agents'
- * kernel of step t+1 (C4's observations do not read voltages).  The caller
- * orders everything else: later reads of the PF outputs (reward, v_out, vv,
- * iters) after pf_stream, and the next writes of agent_power / reward after the
- * PF that reads / adds to them (e.g. two buffer sets, alternating).
- * pf_stream == stream is pgw_coord_step. */
-int32_t pgw_coord_step_overlap(const pgw_coord_params* p, const pgw_pf_params* pf,
-                               const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
-                               pgw_coord_buffers b, void* stream, void* pf_stream);
-int32_t pgw_coord_step_f32_overlap(const pgw_coord_params* p, const pgw_pf_params* pf,
-                                   const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
-                                   pgw_coord_buffers_f32 b, void* stream, void* pf_stream);
 
 /* ------------------------------------------------------------------------
  * Fused MultiComponentEnv step (SURVEY 8(b) pgw_mc_agent_step): one agent of

@@ -351,10 +351,13 @@ from oracle.pf_oracle import BatchedPF  # noqa: E402
 
 
 class OraclePowerFlowSolver(PowerFlowSolver):
-    """The oracle PF behind the reference's PowerFlowSolver ABC (OpenDSS is absent)."""
+    """The oracle PF behind the reference's PowerFlowSolver ABC (OpenDSS is absent).
+    semantics: "exact" (the fixed point) or "opendss" (OpenDSS's stopped snap
+    iterate, Feeder.snap_opendss -- the rule the reference's OpenDSSSolver runs,
+    opendss.py:131-135)."""
 
-    def __init__(self, system_load_rescale_factor=1.0, **kwargs):
-        self.pf = BatchedPF(system_load_rescale_factor=system_load_rescale_factor)
+    def __init__(self, system_load_rescale_factor=1.0, semantics="exact", **kwargs):
+        self.pf = BatchedPF(system_load_rescale_factor=system_load_rescale_factor, semantics=semantics)
         self.bus_voltages = {}
         self.trace = []
 
@@ -396,7 +399,7 @@ class CoordinatedEnv(MultiAgentEnv):
         return max([0.0, self.VOLTAGE_LIMITS[0] - v, v - self.VOLTAGE_LIMITS[1]])
 
 
-def gen_c4():
+def gen_c4(semantics="exact"):
     rng = np.random.default_rng(606)
     K, NA = 2, 5
     T = 286
@@ -404,7 +407,8 @@ def gen_c4():
                           pv_config={"profile_csv": "pv_profile.csv", "scaling_factor": 40.},
                           storage_config={"max_power": 15., "storage_range": (3., 50.)},
                           system_load_rescale_factor=1.2, num_buildings=NA)
-    cfg["pf_config"] = {"cls": OraclePowerFlowSolver, "config": {"system_load_rescale_factor": 1.2}}
+    cfg["pf_config"] = {"cls": OraclePowerFlowSolver,
+                        "config": {"system_load_rescale_factor": 1.2, "semantics": semantics}}
     acts = rng.uniform(-1, 1, size=(T, NA, K, 8))
     mask = rng.random(acts.shape) < 0.03
     acts[mask] *= 1.2
@@ -431,20 +435,24 @@ def gen_c4():
             done[t, k] = d["__all__"]
             v675[t + 1, k] = env.pf_solver.get_bus_voltage_by_name("675c")
     assert done[-1].all() and not done[:-1].any()
-    _save("c4_coordinated", actions=acts, obs=obs, reward=rew, voltage_violation=vv, done=done,
-          init_storage=soc0, v675=v675)
+    _save("c4_coordinated" + _SUFFIX[semantics], actions=acts, obs=obs, reward=rew, voltage_violation=vv,
+          done=done, init_storage=soc0, v675=v675)
 
 
-def _c4_cfg():
+_SUFFIX = {"exact": "", "opendss": "_od"}
+
+
+def _c4_cfg(semantics="exact"):
     cfg = make_env_config(building_config={},
                           pv_config={"profile_csv": "pv_profile.csv", "scaling_factor": 40.},
                           storage_config={"max_power": 15., "storage_range": (3., 50.)},
                           system_load_rescale_factor=1.2, num_buildings=5)
-    cfg["pf_config"] = {"cls": OraclePowerFlowSolver, "config": {"system_load_rescale_factor": 1.2}}
+    cfg["pf_config"] = {"cls": OraclePowerFlowSolver,
+                        "config": {"system_load_rescale_factor": 1.2, "semantics": semantics}}
     return cfg
 
 
-def gen_c4_episodes():
+def gen_c4_episodes(semantics="exact"):
     """C4 across the episode boundary: two full episodes per env, with the SoC
     the reference draws at each reset (energy_storage_env.py:80-95) and every
     building's x_k (persists across reset, five_zone_rom_env.py:147-176;
@@ -458,7 +466,7 @@ def gen_c4_episodes():
     done = np.zeros((E, T, K), bool); soc0 = np.zeros((E, NA, K)); v675 = np.zeros((E, T + 1, K))
     xk = np.zeros((E, T + 1, NA, K, 5))
     for k in range(K):
-        env = CoordinatedEnv(**copy.deepcopy(_c4_cfg()))
+        env = CoordinatedEnv(**copy.deepcopy(_c4_cfg(semantics)))
         names = [a.name for a in env.agents]
 
         def snap(e, t):
@@ -488,8 +496,8 @@ def gen_c4_episodes():
                 done[e, t, k] = d["__all__"]
                 snap(e, t + 1)
     assert done[:, -1].all() and not done[:, :-1].any()
-    _save("c4_two_episodes", actions=acts, obs=obs, reward=rew, voltage_violation=vv, done=done,
-          init_storage=soc0, v675=v675, x_k=xk)
+    _save("c4_two_episodes" + _SUFFIX[semantics], actions=acts, obs=obs, reward=rew, voltage_violation=vv,
+          done=done, init_storage=soc0, v675=v675, x_k=xk)
 
 
 # --------------------------------------------------------------------------
@@ -499,12 +507,12 @@ def gen_c4_episodes():
 from gridworld.scenarios.heterogeneous import make_env_config as make_het_config  # noqa: E402
 
 
-def gen_het():
+def gen_het(semantics="exact"):
     rng = np.random.default_rng(707)
     K = 2
     cfg = make_het_config()
     cfg["pf_config"] = {"cls": OraclePowerFlowSolver,
-                        "config": {"system_load_rescale_factor": 0.65}}
+                        "config": {"system_load_rescale_factor": 0.65, "semantics": semantics}}
     rows = []
     for k in range(K):
         env = MultiAgentEnv(**copy.deepcopy(cfg))
@@ -533,7 +541,7 @@ def gen_het():
     flat_act = lambda a: np.concatenate([a["building"]["building"], a["building"]["pv"],
                                          a["building"]["storage"], a["pv"], a["ev-charging"]])
     agents = ["building", "pv", "ev-charging"]
-    _save("het_scenario",
+    _save("het_scenario" + _SUFFIX[semantics],
           init_storage=np.array([r["soc0"] for r in rows]),
           actions=np.stack([[flat_act(r["acts"][t]) for r in rows] for t in range(T)]),
           obs=np.stack([[flat_obs(r["obs"][t]) for r in rows] for t in range(T + 1)]),
@@ -664,7 +672,12 @@ def gen_hs_order():
 
 
 GENERATORS = {"battery": gen_battery, "pv": gen_pv, "building": gen_building,
-              "ev": gen_ev, "evrand": gen_ev_random, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes, "het": gen_het, "hs": gen_hs, "hs_order": gen_hs_order}
+              "ev": gen_ev, "evrand": gen_ev_random, "mc": gen_mc, "c4": gen_c4, "c4ep": gen_c4_episodes,
+              "het": gen_het, "hs": gen_hs, "hs_order": gen_hs_order,
+              # the reference's own power-flow rule (OpenDSS's snap solve, opendss.py:131-135)
+              # through the reference's MultiAgentEnv: the same seeded action streams
+              "c4_od": lambda: gen_c4("opendss"), "c4ep_od": lambda: gen_c4_episodes("opendss"),
+              "het_od": lambda: gen_het("opendss")}
 
 
 def main():

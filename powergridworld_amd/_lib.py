@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 26
+ABI_VERSION = 27
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -329,10 +329,6 @@ _SIGS = {
                              CoordBuffers, vp]),
     "pgw_coord_step_f32": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
                                  CoordBuffersF32, vp]),
-    "pgw_coord_step_overlap": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
-                                     CoordBuffers, vp, vp]),
-    "pgw_coord_step_f32_overlap": (i32, [P(CoordParams), P(PFParams), P(PFTables), P(CoordStepInfo), i64,
-                                         CoordBuffersF32, vp, vp]),
     "pgw_coord_step_general": (i32, [P(CoordParams), P(PFGParams), P(PFGTables), P(CoordStepInfo), i64,
                                      CoordBuffers, vp]),
     "pgw_hs_reset": (i32, [P(HSParams), P(HSStepInfo), i64, vp, HSBuffers, vp]),

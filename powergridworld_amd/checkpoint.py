@@ -18,8 +18,10 @@ buffers) and records
   timestamps) and small NumPy arrays (e.g. the EV's previous parking window);
   scalars inside dicts and lists are keys and indices, not state,
 
-keyed by attribute path.  Cache-version counters and caches are skipped:
-they describe host-side tables, not the env's state.  ``load_state_dict``
+keyed by attribute path.  Cache-version counters, caches and the tensors a
+solver keeps alive for an in-flight table upload are skipped: they describe
+host-side tables, not the env's state; so are the {node: voltage} mappings,
+views of the solver's output buffers (saved under the buffers' own names).  ``load_state_dict``
 requires the same env configuration (same paths, shapes and dtypes) and
 raises otherwise.
 
@@ -36,8 +38,10 @@ import warnings
 import numpy as np
 import torch
 
-_SKIP_NAMES = ("version", "_ver", "cache", "_lib", "_memo")
-_SKIP_EXACT = ("history", "_hist")  # the history lists and their device ring (emptied on load)
+# caches, host-table keep-alives and the voltage mappings (views of buffers saved
+# under their own names; MultiAgentEnv.load_state_dict re-arms them)
+_SKIP_NAMES = ("version", "_ver", "cache", "_lib", "_memo", "keepalive", "voltages")
+_SKIP_EXACT = ("history", "_hist", "_bv")  # the history lists and their device ring (emptied on load)
 _SCALARS = (bool, numbers.Number, str, type(None), datetime.datetime, datetime.date, np.generic)
 
 

@@ -269,7 +269,7 @@ void put(double* dst, const cplx* src, size_t count) {
 extern "C" {
 
 int32_t pgw_struct_sizes(int64_t* out, int32_t n) {
-  const int64_t sz[30] = {
+  const int64_t sz[PGW_N_STRUCT_SIZES] = {
       (int64_t)sizeof(pgw_mat),           (int64_t)sizeof(pgw_battery_params),
       (int64_t)sizeof(pgw_pv_params),     (int64_t)sizeof(pgw_building_params),
       (int64_t)sizeof(pgw_building_exo),  (int64_t)sizeof(pgw_building_ext),
@@ -285,8 +285,8 @@ int32_t pgw_struct_sizes(int64_t* out, int32_t n) {
       (int64_t)sizeof(pgw_pfg_params),     (int64_t)sizeof(pgw_pfg_tables),
       (int64_t)sizeof(pgw_reg_params),    (int64_t)sizeof(pgw_mc_step_dyn),
       (int64_t)sizeof(pgw_pf_od),         (int64_t)sizeof(pgw_mc_step_args_f32)};
-  for (int i = 0; i < n && i < 30; ++i) out[i] = sz[i];
-  return 30;
+  for (int i = 0; i < n && i < PGW_N_STRUCT_SIZES; ++i) out[i] = sz[i];
+  return PGW_N_STRUCT_SIZES;
 }
 
 int32_t pgw_feeder_build(const pgw_feeder_elem* elems, int32_t n_elems, int32_t n_nodes, double* Y,

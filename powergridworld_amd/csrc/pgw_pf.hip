@@ -31,7 +31,6 @@
 #include <cmath>
 #include <type_traits>
 
-#include <mutex>
 #include "pgw_common.h"
 
 namespace pgw {
@@ -941,9 +940,6 @@ template <int M, bool UB, bool GC, bool KEEP, class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pgw_pf_tables t,
                                                      int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;   // double, or float (_f32)
-  // issue priority over a co-resident agents' kernel (pgw_coord_step_overlap):
-  // this kernel is issue-bound, the agents' one memory-bound
-  __builtin_amdgcn_s_setprio(3);
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   // read once: a reload per phase would put an L2 round trip on the chain
@@ -1139,10 +1135,13 @@ __device__ __forceinline__ void od_stage_load(const ODArgs& o, ODStage<M>& g) {
   for (int q = 0; q < ODStage<M>::kRowQ; ++q) {
     const int i = threadIdx.x + q * kBlock;
     const int r = i / S, j = i - r * S;
-    // the entry's source (any in-bounds address when it has none)
+    // the entry's source; an entry that has none reads row min(r, n_rows - 1),
+    // slot min(j, 2M + 1) -- in bounds (the host passes one dummy row when
+    // n_rows = 0), so the load may issue unconditionally
     const bool has = i < total && j < 2 + 2 * M;
-    const double* p = j < 2 ? o.rows_V0 + (2 * r + j)
-                            : o.rows_G + (2 * M * r + (j < 2 + M ? 2 * (j - 2) : 2 * (j - 2 - M) + 1));
+    const int rc = min(r, max(o.n_rows - 1, 0)), jc = min(j, 1 + 2 * M);
+    const double* p = jc < 2 ? o.rows_V0 + (2 * rc + jc)
+                             : o.rows_G + (2 * M * rc + (jc < 2 + M ? 2 * (jc - 2) : 2 * (jc - 2 - M) + 1));
     g.v[q] = has ? *p : 0.0;
   }
 #pragma unroll
@@ -1462,6 +1461,9 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, const ODSt
       jsum = fma(0x1p-40, jsum, jsum);
       // (an env that is not tested here already fails at an element node
       // or is below min_iter: its decision does not read the rows)
+      // od_rows_sparse reads other lanes' current slots written above in this
+      // iteration: make the cross-lane LDS dependency explicit
+      __builtin_amdgcn_wave_barrier();
       if (__popcll(needs) <= o.sparse) od_rows_sparse<M>(sh, cur, prv, 0, o.n_rep, needs, err, amin);
       else od_check_rows<M>(sh, cur, prv, 0, o.n_rep, err, amin);
       d = od_decide(o, !bounded, it, err, amin, dsum, jsum);
@@ -1490,7 +1492,6 @@ template <int M, class Bufs>
 __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
                                                         int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;
-  __builtin_amdgcn_s_setprio(3);                     // (as k_coord_pf)
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
   __shared__ ODShared<M> sh;
@@ -1524,11 +1525,18 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   od_load_J<M>(sh, it, ir, ii);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  // rows 1.. (a history slot holds every node): through the scalar cache, as
+  // k_pf_solve_od, in pf_node_pu's operation order (bit-identical per node)
+  double vsel = v0;
+  pf_rows_out<M>(t, false, nullptr, a.n_out, ir, ii, [&](int ro, double v) {
+    if (valid && b.v_out) b.v_out[(int64_t)ro * n + e] = (Sto)v;
+    vsel = (ro == c.vv_row) ? v : vsel;
+  });
   if (!valid) return;
   if (b.v_out) b.v_out[e] = (Sto)v0;
   if (b.iters) b.iters[e] = it;
   if (c.coordinated) {
-    const double vv = pymax(pymax(0.0, c.vv_lo - v0), v0 - c.vv_hi);
+    const double vv = pymax(pymax(0.0, c.vv_lo - vsel), vsel - c.vv_hi);
     if (b.vv) b.vv[e] = (Sto)vv;
     const double share = (vv * c.vv_penalty) / (double)c.n_agents;
 #pragma unroll
@@ -1816,22 +1824,11 @@ static int32_t launch_coord_agents(const pgw_coord_params& p, const pgw_coord_st
   return check_launch("k_coord_agents");
 }
 
-// The event that orders a second-stream power flow after the agents' kernel
-// (pgw_coord_step_overlap): recorded and waited on within one call, so one per
-// process suffices.
-static hipEvent_t coord_agents_event() {
-  static std::once_flag once;
-  static hipEvent_t ev = nullptr;
-  std::call_once(once, [] { (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming); });
-  return ev;
-}
-
-// pf_stream == stream: one stream (pgw_coord_step); otherwise the PF kernel
-// runs on pf_stream after the agents' kernel (pgw_coord_step_overlap).
+// The agents' kernel, then the power flow with the coordinated prologue and
+// epilogue, on one stream.
 template <class Bufs>
 static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
-                          const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream,
-                          void* pf_stream) {
+                          const pgw_coord_step_info* s, int64_t n, const Bufs& b, void* stream) {
   constexpr bool kF32 = std::is_same<Bufs, pgw_coord_buffers_f32>::value;
   PGW_REQUIRE(p && pf && pft && s && n >= 0, "pgw_coord_step: null argument");
   PGW_REQUIRE(p->n_agents >= 1 && p->n_agents <= PGW_MAX_AGENTS, "pgw_coord_step: bad n_agents");
@@ -1897,12 +1894,7 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
-  hipStream_t pst = (hipStream_t)pf_stream;
-  if (pst != st) {
-    hipEvent_t ev = coord_agents_event();
-    PGW_REQUIRE(ev && hipEventRecord(ev, st) == hipSuccess && hipStreamWaitEvent(pst, ev, 0) == hipSuccess,
-                "pgw_coord_step_overlap: stream ordering failed");
-  }
+  hipStream_t pst = st;
   if (pft->od) {
     launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs>, dim3(grid_for(n)), dim3(kBlock), pst, c, a,
                  make_od_args(*pft->od, pf->max_iter), *pft, n, b);
@@ -2082,25 +2074,13 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
                        const pgw_coord_step_info* s, int64_t n, pgw_coord_buffers b, void* stream) {
-  return coord_step(p, pf, pft, s, n, b, stream, stream);
+  return coord_step(p, pf, pft, s, n, b, stream);
 }
 
 int32_t pgw_coord_step_f32(const pgw_coord_params* p, const pgw_pf_params* pf,
                            const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
                            pgw_coord_buffers_f32 b, void* stream) {
-  return coord_step(p, pf, pft, s, n, b, stream, stream);
-}
-
-int32_t pgw_coord_step_overlap(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,
-                               const pgw_coord_step_info* s, int64_t n, pgw_coord_buffers b, void* stream,
-                               void* pf_stream) {
-  return coord_step(p, pf, pft, s, n, b, stream, pf_stream);
-}
-
-int32_t pgw_coord_step_f32_overlap(const pgw_coord_params* p, const pgw_pf_params* pf,
-                                   const pgw_pf_tables* pft, const pgw_coord_step_info* s, int64_t n,
-                                   pgw_coord_buffers_f32 b, void* stream, void* pf_stream) {
-  return coord_step(p, pf, pft, s, n, b, stream, pf_stream);
+  return coord_step(p, pf, pft, s, n, b, stream);
 }
 
 }  // extern "C"

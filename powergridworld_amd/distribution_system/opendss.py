@@ -66,16 +66,17 @@ class OpenDSSSolver(PowerFlowSolver):
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = None, max_iter: int = None,
                  output_nodes=None, predictor: bool = True, warm_start: bool = False,
-                 convergence: str = "exact", general: bool = None, **kwargs):
-        """convergence: "exact" -- every env's solve iterates to the fixed point
-        (max |dU| < tol = 1e-10 pu), history-free and reproducible; "opendss" --
-        OpenDSS's own snap solve as the reference runs it (opendss.py:134):
+                 convergence: str = "opendss", general: bool = None, **kwargs):
+        """convergence: "opendss" (the default) -- OpenDSS's own snap solve as
+        the reference runs it (opendss.py:134):
         loads' nominal admittances in Y, start from the direct solution, stop at
         the first iteration >= 2 whose largest node-voltage magnitude change is
-        <= tol = 1e-4 pu, at most 15 (DESIGN.md section 2 measures the
-        difference).  Feeders with more than 16 load phase elements and the
-        "opendss" mode run the general kernel (pgw_pf_solve_general); general=True
-        forces it for the exact mode too (tests, measurements)."""
+        <= tol = 1e-4 pu, at most 15; "exact" (opt-in) -- every env's solve
+        iterates to the fixed point (max |dU| < tol = 1e-10 pu), history-free
+        and reproducible (DESIGN.md section 2 measures the difference).
+        Feeders with more than 16 load phase elements, other load models or
+        RegControls run the general kernel (pgw_pf_solve_general); general=True
+        forces it (tests, measurements)."""
         super().__init__(**kwargs)
         if convergence not in ("exact", "opendss"):
             raise ValueError("convergence must be 'exact' or 'opendss', got %r" % (convergence,))
@@ -652,7 +653,6 @@ class OpenDSSSolver(PowerFlowSolver):
     # ------------------------------------------------------------ reference API
     def calculate_power_flow(self, p_controllable_consumed: dict = None,
                              q_controllable_consumed: dict = None, current_time: str = None) -> None:
-        self._join()
         n = self.num_envs
         if p_controllable_consumed is not None:
             kt = (tuple(p_controllable_consumed), tuple(q_controllable_consumed or ()))
@@ -807,15 +807,10 @@ class OpenDSSSolver(PowerFlowSolver):
             self._warm, self._warm_valid = (cold, warm), False
         return self._warm[1] if self._warm_valid else self._warm[0]
 
-    def _join(self):
-        """Order the caller's stream after a power flow still running on another
-        stream (set by MultiAgentEnv(overlap_pf=True)); a no-op otherwise."""
-
     @property
     def iterations(self):
         """[N] int32 iteration count of the last solve per env (-max_iter =
         stopped unconverged)."""
-        self._join()
         return self._iterations
 
     @iterations.setter
@@ -859,7 +854,6 @@ class OpenDSSSolver(PowerFlowSolver):
 
     def voltage_extrema(self):
         """(min, max) over all output nodes per env, once per solve (multiagent_env.py:107-113)."""
-        self._join()
         if self._extrema is None:
             if self._all_nodes and self.bus_voltages is self._bv:
                 v = self.v_out[:len(self.output_names)]
@@ -869,11 +863,9 @@ class OpenDSSSolver(PowerFlowSolver):
         return self._extrema
 
     def get_bus_voltages(self) -> dict:
-        self._join()
         return self.bus_voltages
 
     def get_bus_voltage_by_name(self, bus_name: str) -> Union[torch.Tensor, List[torch.Tensor]]:
-        self._join()
         nodes = bus_name_to_nodes(bus_name)
         if len(nodes) == 1:
             return self.bus_voltages[nodes[0]]

@@ -56,7 +56,7 @@ class MultiAgentEnv(Env):
     def __init__(self, common_config: dict = {}, pf_config: dict = {}, agents: list = None,
                  max_episode_steps: int = None, rescale_spaces: bool = True, num_envs: int = 1,
                  device=None, fused: Union[bool, str] = "auto", record_history: bool = False,
-                 dtype=None, history_capacity: int = None, overlap_pf: bool = False, **kwargs):
+                 dtype=None, history_capacity: int = None, **kwargs):
         self.common_config = common_config
         self.rescale_spaces = rescale_spaces
         assert len(agents) > 0, "need at least one agent!"
@@ -108,6 +108,7 @@ class MultiAgentEnv(Env):
         self._fused = None
         self._ma = None              # fused multi-agent path (pgw_ma_step), see _setup_ma
         self._fused_steps = 0
+        self._at_reset = False       # the last call was reset() (env.voltages: the reset solve)
         # every agent reports the base class's reactive power (its zero buffer)
         self._q_zero = all(type(a).reactive_power is ComponentEnv.reactive_power for a in self.agents)
         if fused:
@@ -133,8 +134,6 @@ class MultiAgentEnv(Env):
         self._hist = None
         if self.record_history:
             self._init_history(history_capacity)
-        if overlap_pf:
-            self._setup_overlap()
 
     # ================================================================ hooks
     @abstractmethod
@@ -179,7 +178,6 @@ class MultiAgentEnv(Env):
 
     def reset(self) -> Dict[str, any]:
         """multiagent_env.py:125-140"""
-        self._pf_join()
         self.episode_step = 0
         oob_poll(self.oob_count)
         self.time = self._time_at(0)
@@ -191,6 +189,7 @@ class MultiAgentEnv(Env):
                 for ai, agent in enumerate(self.agents):
                     agent._real_power = self._fused["agent_power"][ai]
         self.pf_solver.calculate_power_flow(current_time=self.time)
+        self._at_reset = True
         self.voltages = self.pf_solver.get_bus_voltages()
         if self._fused is not None and len(self.pf_solver.output_names) < self.pf_solver.feeder.n:
             # the reset solve's rows, every other node solved on first access
@@ -228,6 +227,7 @@ class MultiAgentEnv(Env):
         [n_agents, N, act_dim] (any strides; zero-copy)."""
         self.episode_step += 1
         self.time = self._time_at(self.episode_step)
+        self._at_reset = False
         self.obs_dict = {}
         if self._fused is not None:
             obs, rew, done, meta = self._step_fused(action)
@@ -897,24 +897,8 @@ class MultiAgentEnv(Env):
         if H is not None:            # outputs straight into this step's history slot
             s_ = H["t"] % H["cap"]
             bufs.v_out, bufs.agent_power = H["v"][s_].data_ptr(), H["p"][s_].data_ptr()
-        O = F.get("overlap")
-        if O is None:
-            rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
-                                                  self.num_envs, bufs, _lib.stream_ptr(self.device))
-        else:
-            # the PF of this step on the second stream beside the next step's
-            # agents; this step's buffer set waits for the PF of two steps ago
-            slot = O["slot"]
-            main = torch.cuda.current_stream(self.device)
-            main.wait_event(O["ev"][slot])
-            bufs.reward, bufs.agent_power = O["reward_ptr"][slot], O["power_ptr"][slot]
-            rc = getattr(_lib.lib(), F["kernel"] + "_overlap")(F["params"], pfp, pft, info, self.num_envs, bufs,
-                                                             main.cuda_stream, O["stream"].cuda_stream)
-            O["ev"][slot].record(O["stream"])
-            O["pending"] = O["ev"][slot]
-            O["slot"] = slot ^ 1
-            for ai, agent in enumerate(self.agents):
-                agent._reward, agent._real_power = O["reward"][slot][ai], O["power"][slot][ai]
+        rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
+                                              self.num_envs, bufs, _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
         self.pf_solver.iterations = F["iters"]
@@ -942,8 +926,6 @@ class MultiAgentEnv(Env):
         d = any(e.is_terminal() for e in F["agent0_envs"])
         if H is not None:
             self._record(None)
-        if O is not None:
-            return (F["obs_dict"], O["rew_dict"][slot], F["done_true"] if d else F["done_false"], O["meta"])
         return F["obs_dict"], F["rew_dict"], F["done_true"] if d else F["done_false"], F["meta"]
 
     def _step_entry(self, skey):
@@ -951,7 +933,6 @@ class MultiAgentEnv(Env):
         PV index, time, tables version): exogenous rows, PV value, PF parameters
         and tables of the hour; cached per key (every episode repeats them)."""
         F, solver = self._fused, self.pf_solver
-        self._pf_join()              # the table uploads below must not pass a running PF
         t, p, time = skey[0], skey[1], skey[2]
         bld, pv = F["bld0"], F["pv0"]
         info = _lib.CoordStepInfo()
@@ -995,80 +976,42 @@ class MultiAgentEnv(Env):
         """The env's whole state (device tensors, generator states, clocks):
         powergridworld_amd.checkpoint.state_dict."""
         from powergridworld_amd.checkpoint import state_dict
-        self._pf_join()
         return state_dict(self)
 
     def load_state_dict(self, sd, strict=False):
-        """Restore a state_dict() of an env of the same configuration (in place)."""
+        """Restore a state_dict() of an env of the same configuration (in place),
+        then point the {node: voltage} mapping at the restored step's outputs."""
         from powergridworld_amd.checkpoint import load_state_dict
-        self._pf_join()
-        return load_state_dict(self, sd, strict)
+        load_state_dict(self, sd, strict)
+        self._rearm_voltages()
+        return self
+
+    def _rearm_voltages(self):
+        """env.voltages / solver.bus_voltages for the restored state: the solver's
+        output rows, and on the fused paths the other nodes solved on first
+        access for the restored step (or reset) number."""
+        solver = self.pf_solver
+        if not hasattr(solver, "_prepare_bus_voltages"):
+            return
+        H = self._hist
+        if H is not None or (self._fused is None and self._ma is None):
+            solver._prepare_bus_voltages()
+            self.voltages = solver.bus_voltages
+            return
+        if self._at_reset or self._fused_steps == 0:
+            solver._prepare_bus_voltages()
+            self.voltages = solver.bus_voltages
+            if self._fused is not None and len(solver.output_names) < solver.feeder.n:
+                self.voltages = solver.bus_voltages = _FusedVoltages(self, solver.bus_voltages,
+                                                                     self._fused_steps, reset=True)
+            return
+        lazy = (self._fused or self._ma)["lazy_v"]
+        lazy._step, lazy._reset, lazy._full = self._fused_steps, False, None
+        self.voltages = solver.bus_voltages = lazy
 
     def packed_obs(self):
         """Fused path: the [n_agents, N, obs_dim] observation view (list-interface order)."""
         return self._fused["obs"].transpose(1, 2)
-
-    # ================================================================ PF beside the next step
-    def _setup_overlap(self):
-        """overlap_pf=True (fused C4 path, pgw_coord_step_overlap): step t's power
-        flow runs on a second stream beside step t+1's agents' kernel -- C4's
-        observations do not read voltages (multiagent_env.py:165-189), so only
-        the rewards, the violation and the voltages wait for it.  Two buffer sets
-        (rewards, agent powers) alternate by step.  The rewards / meta mappings a
-        step returns, env.voltages, the solver's outputs, reset(), state_dict()
-        and every host-side table update make the caller's current stream wait
-        for the pending power flow first (_pf_join), so every value read through
-        them is the synchronous step's, bit for bit."""
-        F = self._fused
-        if F is None or F["kernel"] not in ("pgw_coord_step", "pgw_coord_step_f32"):
-            raise ValueError("overlap_pf needs the fused C4 step (pgw_coord_step); this env runs %s"
-                             % (F["kernel"] if F else "the generic / multi-agent path"))
-        if self._hist is not None:
-            raise ValueError("overlap_pf: record_history is not supported")
-        dev = self.device
-        rew = [F["reward"], torch.zeros_like(F["reward"])]
-        pwr = [F["agent_power"], torch.zeros_like(F["agent_power"])]
-        # high priority: its kernel dispatches ahead of the next step's agents
-        O = dict(slot=0, pending=None, stream=torch.cuda.Stream(dev, priority=-1),
-                 ev=[torch.cuda.Event(), torch.cuda.Event()], reward=rew, power=pwr,
-                 reward_ptr=[r.data_ptr() for r in rew], power_ptr=[q.data_ptr() for q in pwr])
-        O["rew_dict"] = [_JoinedMapping(self, {a.name: r[ai] for ai, a in enumerate(self.agents)}) for r in rew]
-        O["meta"] = _JoinedMapping(self, F["meta"])
-        F["overlap"] = O
-        self.pf_solver._join = self._pf_join
-
-    def _pf_join(self):
-        """The current stream waits for the pending overlapped power flow."""
-        F = self._fused
-        O = F.get("overlap") if F is not None else None
-        if O is not None and O["pending"] is not None:
-            torch.cuda.current_stream(self.device).wait_event(O["pending"])
-            O["pending"] = None
-
-
-class _JoinedMapping(Mapping):
-    """A step's rewards / meta under overlap_pf: the mapping of the synchronous
-    step, whose every read first joins the pending power flow."""
-    __slots__ = ("_env", "_d")
-
-    def __init__(self, env, d):
-        self._env, self._d = env, d
-
-    def __getitem__(self, k):
-        self._env._pf_join()
-        return self._d[k]
-
-    def __iter__(self):
-        return iter(self._d)
-
-    def __len__(self):
-        return len(self._d)
-
-    def __contains__(self, k):
-        return k in self._d
-
-    def copy(self):
-        return dict(self.items())
 
 
 class _FusedVoltages(Mapping):
@@ -1089,7 +1032,6 @@ class _FusedVoltages(Mapping):
         return self._full
 
     def __getitem__(self, node):
-        self._env._pf_join()
         v = self._fast.get(node)
         return v if v is not None else self._all()[node]
 

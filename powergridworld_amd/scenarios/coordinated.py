@@ -40,10 +40,11 @@ class CoordinatedMultiBuildingControlEnv(MultiAgentEnv):
                              v - self.VOLTAGE_LIMITS[1])
 
 
-def make_c4_config(num_buildings=5, sys_load=1.2, pf_convergence="exact", pf_general=False):
+def make_c4_config(num_buildings=5, sys_load=1.2, pf_convergence="opendss", pf_general=False):
     """The BASELINE C4 scenario: make_env (train.py:165-188) with 5 buildings.
     pf_convergence: the power flow's stopping rule (OpenDSSSolver convergence:
-    "exact" fixed point, or "opendss" -- OpenDSS's own snap iterate);
+    "opendss" -- OpenDSS's own snap iterate, the reference's; or the opt-in
+    "exact" fixed point);
     pf_general=True forces the general kernel (tests, measurements)."""
     cfg = make_env_config(
         building_config={},
@@ -51,8 +52,7 @@ def make_c4_config(num_buildings=5, sys_load=1.2, pf_convergence="exact", pf_gen
         storage_config={"max_power": 15., "storage_range": (3., 50.)},
         system_load_rescale_factor=sys_load,
         num_buildings=num_buildings)
-    if pf_convergence != "exact":
-        cfg["pf_config"]["config"]["convergence"] = pf_convergence
+    cfg["pf_config"]["config"]["convergence"] = pf_convergence
     if pf_general:
         cfg["pf_config"]["config"]["general"] = True
     return cfg

@@ -45,7 +45,7 @@ class ThisPVEnv(PVEnv):
         return self._band_rew, {}
 
 
-def make_env_config(system_load_rescale_factor=0.65, rescale_spaces=True, pf_convergence="exact"):
+def make_env_config(system_load_rescale_factor=0.65, rescale_spaces=True, pf_convergence="opendss"):
     """heterogeneous.py:13-112 (the building's reward_structure kwarg is passed
     on unchanged; the reference's FiveZoneROMThermalEnergyEnv ignores it)."""
     building_components = [
@@ -69,8 +69,9 @@ def make_env_config(system_load_rescale_factor=0.65, rescale_spaces=True, pf_con
             "system_load_rescale_factor": system_load_rescale_factor,
         },
     }
-    if pf_convergence != "exact":          # OpenDSSSolver(convergence=...): "opendss" = OpenDSS's snap iterate
-        pf_config["config"]["convergence"] = pf_convergence
+    # OpenDSSSolver(convergence=...): "opendss" = OpenDSS's snap iterate (the
+    # reference's rule, the default), "exact" = the fixed point (opt-in)
+    pf_config["config"]["convergence"] = pf_convergence
     agents = [
         {"name": "building", "bus": "675c", "cls": MultiComponentEnv,
          "config": {"components": building_components}},

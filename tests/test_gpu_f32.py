@@ -61,13 +61,15 @@ def test_battery_f32_one_step_and_episode():
     np.testing.assert_allclose(e32.soc.double().cpu().numpy(), free.soc.cpu().numpy(), rtol=1e-3, atol=1e-3)
 
 
-def _c4_pair(n, seed):
+def _c4_pair(n, seed, semantics):
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
-    e32 = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV,
-                                             dtype=torch.float32)
-    e64 = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
+    cfg = make_c4_config(pf_convergence=semantics)
+    e32 = CoordinatedMultiBuildingControlEnv(**cfg, num_envs=n, device=DEV, dtype=torch.float32)
+    e64 = CoordinatedMultiBuildingControlEnv(**cfg, num_envs=n, device=DEV, fused=True)
     assert e32._fused is not None and e32._fused["kernel"] == "pgw_coord_step_f32"
+    # OpenDSS's rule: k_coord_pf_od<14, pgw_coord_buffers_f32>; the fixed point: k_coord_pf
+    assert e32.pf_solver._od_fast == (semantics == "opendss") and not e32.pf_solver.general
     gen = torch.Generator(DEV).manual_seed(seed)
     init = (torch.rand((5, n), dtype=torch.float64, device=DEV, generator=gen) * 50.0).float().double()
     for e in (e32, e64):
@@ -78,14 +80,21 @@ def _c4_pair(n, seed):
     return e32, e64, gen
 
 
-def test_c4_f32_one_step_parity():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_c4_f32_one_step_parity(semantics):
     """Teacher-forced: each step starts the fp64 fused env from the fp32 env's
-    state; every fp32 output is the fp64 output rounded once."""
+    state; every fp32 output is the fp64 output rounded once.  Under OpenDSS's
+    rule the power flow stops at an iteration count, which the fp32-rounded
+    agent powers (the same values summed in fp64) can move by one for an env
+    within ~1e-5 kW of a stopping threshold: such envs (their count differs from
+    the fp64 path's, at most a 1e-4 fraction) are excluded from the PF / reward
+    comparison of that step."""
     n = 8192
-    e32, e64, gen = _c4_pair(n, 5)
+    e32, e64, gen = _c4_pair(n, 5, semantics)
     assert_f32(e32.packed_obs(), e64.packed_obs(), ulps=0)
     F32, F64 = e32._fused, e64._fused
     names = [a.name for a in e32.agents]
+    flips = 0
     for t in range(40):
         F64["x"].copy_(F32["x"])
         F64["soc"].copy_(F32["soc"])
@@ -97,14 +106,20 @@ def test_c4_f32_one_step_parity():
         assert_f32(F32["soc"], F64["soc"], ulps=0)
         assert_f32(F32["agent_power"], F64["agent_power"], ulps=0)
         # PF from the fp32-rounded agent powers (same values, summed in fp64)
-        assert_f32(F32["v_out"][0], F64["v_out"][0], ulps=1)
-        assert_f32(m32["voltage_violation"], m64["voltage_violation"], ulps=1, atol=1e-9)
+        same = F32["iters"] == F64["iters"]
+        flips += int((~same).sum())
+        assert_f32(F32["v_out"][0][same], F64["v_out"][0][same], ulps=1)
+        assert_f32(m32["voltage_violation"][same], m64["voltage_violation"][same], ulps=1, atol=1e-9)
         for nm in names:
-            assert_f32(r32[nm], r64[nm], ulps=2, atol=1e-6)
+            assert_f32(r32[nm][same], r64[nm][same], ulps=2, atol=1e-6)
         assert d32["__all__"] == d64["__all__"]
+    assert flips <= 1e-4 * 40 * n, flips
+    if semantics == "exact":
+        assert flips == 0
 
 
-def test_c4_f32_episode_within_bound():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_c4_f32_episode_within_bound(semantics):
     """Free-running full episode (286 steps + the next reset) at batch 4096
     against the fp64 path: observations within 1e-3 relative (north star).
     The reward contains the reference's discontinuous battery clamp
@@ -112,7 +127,7 @@ def test_c4_f32_episode_within_bound():
     the voltage penalty, so a state 1 fp32 ulp from a clamp threshold can take
     the other branch; rewards are held to the bound on all but a 1e-4 fraction."""
     n = 4096
-    e32, e64, gen = _c4_pair(n, 9)
+    e32, e64, gen = _c4_pair(n, 9, semantics)
     names = [a.name for a in e32.agents]
     bad_r, tot_r = 0, 0
     steps = 0

@@ -227,14 +227,17 @@ def test_battery_c2_vs_oracle():
 
 
 # ------------------------------------------------------------------ power flow
-def test_pf_vs_oracle():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_pf_vs_oracle(semantics):
+    """Two controllable loads (the general kernel under OpenDSS's rule, the
+    fast one for the fixed point) against the oracle with the same rule."""
     from oracle.pf_oracle import BatchedPF
     from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
     n = 1024
     rng = np.random.default_rng(11)
     pf = OpenDSSSolver("ieee_13_dss/IEEE13Nodeckt.dss", "ieee_13_dss/annual_hourly_load_profile.csv",
-                       system_load_rescale_factor=1.2, num_envs=n, device=DEV)
-    orc = BatchedPF(system_load_rescale_factor=1.2)
+                       system_load_rescale_factor=1.2, num_envs=n, device=DEV, convergence=semantics)
+    orc = BatchedPF(system_load_rescale_factor=1.2, semantics=semantics)
     for ts in ["2021-08-12 00:05", "2021-08-12 15:00", "2021-01-01 05:00"]:
         p675 = rng.uniform(-300, 600, n)
         q675 = rng.uniform(-50, 50, n)
@@ -248,7 +251,8 @@ def test_pf_vs_oracle():
         assert (N(pf.iterations) == orc.last_iters).mean() > 0.99
 
 
-def test_pf_regcap_feeder_vs_oracle():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_pf_regcap_feeder_vs_oracle(semantics):
     """A feeder beyond IEEE-13 (tests/data/regcap_feeder.dss: fixed-tap
     regulators, capacitors, model-2 loads; parity unpinned, no OpenDSS) through
     the batched solver against the oracle, two controllable loads."""
@@ -261,9 +265,9 @@ def test_pf_regcap_feeder_vs_oracle():
     n = 512
     rng = np.random.default_rng(12)
     pf = OpenDSSSolver(path, "ieee_13_dss/annual_hourly_load_profile.csv", system_load_rescale_factor=1.1,
-                       num_envs=n, device=DEV)
+                       num_envs=n, device=DEV, convergence=semantics)
     assert pf.load_bus_name == ["d1", "a1", "c1"]        # model-1 loads only
-    orc = BatchedPF(spec=parse_dss(path), system_load_rescale_factor=1.1)
+    orc = BatchedPF(spec=parse_dss(path), system_load_rescale_factor=1.1, semantics=semantics)
     for ts in ["2021-08-12 15:00", "2021-01-01 05:00"]:
         pa = rng.uniform(-100, 300, n)
         pc = rng.uniform(-50, 200, n)
@@ -272,10 +276,13 @@ def test_pf_regcap_feeder_vs_oracle():
         want = orc.calculate(ts, {"a1": pa, "c1": pc}, {}, K=n)
         got = np.stack([N(v[name]) for name in orc.feeder.node_names], 1)
         np.testing.assert_allclose(got, want, rtol=1e-8, atol=0)
+        if semantics == "opendss":
+            np.testing.assert_array_equal(N(pf.iterations), orc.last_iters)
 
 
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
 @pytest.mark.parametrize("loads", [("675c",), ("675c", "671")])
-def test_pf_all_rows_ragged_and_extrema_only(loads):
+def test_pf_all_rows_ragged_and_extrema_only(loads, semantics):
     """All output rows at a ragged batch (the last wave part-empty: the rows'
     DPP broadcasts read every lane, past-n lanes included, and store nothing);
     the epilogue's min/max equal Python's min/max over the rows in order; an
@@ -286,8 +293,8 @@ def test_pf_all_rows_ragged_and_extrema_only(loads):
     n = 1000
     rng = np.random.default_rng(21)
     pf = OpenDSSSolver("ieee_13_dss/IEEE13Nodeckt.dss", "ieee_13_dss/annual_hourly_load_profile.csv",
-                       system_load_rescale_factor=0.65, num_envs=n, device=DEV)
-    orc = BatchedPF(system_load_rescale_factor=0.65)
+                       system_load_rescale_factor=0.65, num_envs=n, device=DEV, convergence=semantics)
+    orc = BatchedPF(system_load_rescale_factor=0.65, semantics=semantics)
     ts = "2020-08-12 13:00"
     p_np = {k: rng.uniform(-400, 300, n) for k in loads}
     pf.calculate_power_flow({k: T(v) for k, v in p_np.items()}, None, current_time=ts)
@@ -304,12 +311,16 @@ def test_pf_all_rows_ragged_and_extrema_only(loads):
     assert np.array_equal(N(lo), vmn) and np.array_equal(N(hi), vmx)
     # the same solve with the extrema only
     p = pf.step_params(ts)
-    t = _lib.PFTables.from_buffer_copy(pf.step_tables(ts))
+    tb = pf.step_tables(ts)
+    t = type(tb).from_buffer_copy(tb)
+    if hasattr(tb, "_od_ref"):
+        t._od_ref = tb._od_ref
     mn = torch.full((n,), -1.0, dtype=torch.float64, device=DEV)
     mx = torch.full((n,), -1.0, dtype=torch.float64, device=DEV)
     t.v_min_out, t.v_max_out = mn.data_ptr(), mx.data_ptr()
     cp = torch.stack([T(p_np[k]) for k in pf._ctrl_names])
-    _lib.check(_lib.lib().pgw_pf_solve(p, t, n, cp.data_ptr(), None, None, None, _lib.stream_ptr(DEV)))
+    fn = _lib.lib().pgw_pf_solve_general if pf.general else _lib.lib().pgw_pf_solve
+    _lib.check(fn(p, t, n, cp.data_ptr(), None, None, None, _lib.stream_ptr(DEV)))
     assert torch.equal(mn, lo) and torch.equal(mx, hi)
 
 
@@ -324,7 +335,7 @@ def test_pf_predictor_vs_oracle_and_cold_start():
     mk = lambda pred: OpenDSSSolver("ieee_13_dss/IEEE13Nodeckt.dss",
                                     "ieee_13_dss/annual_hourly_load_profile.csv",
                                     system_load_rescale_factor=1.2, num_envs=n, device=DEV,
-                                    predictor=pred)
+                                    predictor=pred, convergence="exact")
     warm, cold = mk(True), mk(False)
     orc = BatchedPF(system_load_rescale_factor=1.2)
     for ts in ["2021-08-12 01:00", "2021-08-12 14:00", "2021-08-12 15:00", "2021-08-12 18:00"]:
@@ -344,13 +355,20 @@ def test_pf_predictor_vs_oracle_and_cold_start():
 
 
 # ------------------------------------------------------------------ C4 (coordinated)
+# golden of each power-flow rule: the reference's MultiAgentEnv over the oracle PF
+# with OpenDSS's snap rule (the reference's, the default) or the fixed point
+GOLD_SUFFIX = {"opendss": "_od", "exact": ""}
+
+
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
 @pytest.mark.parametrize("fused", [True, False])
-def test_c4_golden(fused):
+def test_c4_golden(fused, semantics):
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
-    g = load("c4_coordinated")
+    g = load("c4_coordinated" + GOLD_SUFFIX[semantics])
     Tn, NA, K, _ = g["actions"].shape
-    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=K, device=DEV, fused=fused)
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=semantics), num_envs=K, device=DEV,
+                                             fused=fused)
     assert (env._fused is not None) == fused
     env.reset()
     for a, agent in enumerate(env.agents):
@@ -377,14 +395,15 @@ def test_c4_golden(fused):
         assert dones["__all__"] == bool(g["done"][t, 0])
 
 
-def test_c4_fused_equals_generic_full_batch():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_c4_fused_equals_generic_full_batch(semantics):
     """Size-independent property at the BASELINE batch (65,536): the one-kernel
     fused step and the generic per-component path are bit-identical."""
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     n = 65536
-    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=f)
-            for f in (True, False)]
+    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=semantics), num_envs=n, device=DEV,
+                                               fused=f) for f in (True, False)]
     init = torch.rand((5, n), dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(1)) * 50
     for e in envs:
         e.reset()
@@ -410,19 +429,23 @@ def test_c4_fused_equals_generic_full_batch():
 
 
 
-def test_c4_batch_one_and_ragged():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_c4_batch_one_and_ragged(semantics):
     """Batch 1 and a batch that is not a multiple of the 256-thread block."""
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     from oracle.ma_oracle import CoordinatedOracle
+    from oracle.pf_oracle import BatchedPF
     for n in (1, 257):
-        env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV)
+        env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=semantics), num_envs=n,
+                                                 device=DEV)
         rng = np.random.default_rng(n)
         init = rng.uniform(3, 50, (5, n))
         env.reset()
         for a, agent in enumerate(env.agents):
             agent.env_dict["storage"].reset(init_storage=T(init[a]))
         orc = CoordinatedOracle(n)
+        orc.pf = BatchedPF(system_load_rescale_factor=1.2, semantics=semantics)
         orc.reset(init)
         for t in range(5):
             act = rng.uniform(-1, 1, (5, n, 8))
@@ -433,18 +456,20 @@ def test_c4_batch_one_and_ragged():
 
 
 # ------------------------------------------------------------------ heterogeneous
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
 @pytest.mark.parametrize("fused", ["auto", False])
-def test_heterogeneous_scenario_golden(fused):
+def test_heterogeneous_scenario_golden(fused, semantics):
     """The reference's 3-agent heterogeneous scenario (MC building, grid-aware
     PV farm rewarded on min_voltage, EV 25x40) on the fused multi-agent path
     (pgw_ma_step, the default) and the generic path, against the reference run
-    (tests/golden/het_scenario.npz, PF = the oracle behind the reference's
-    PowerFlowSolver ABC), a whole 286-step episode."""
+    (tests/golden/het_scenario{_od}.npz, PF = the oracle behind the reference's
+    PowerFlowSolver ABC with OpenDSS's rule or the fixed point), a whole
+    286-step episode."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
-    g = load("het_scenario")
+    g = load("het_scenario" + GOLD_SUFFIX[semantics])
     Tn, K, _ = g["actions"].shape
-    env = MultiAgentEnv(**make_env_config(), num_envs=K, device=DEV, fused=fused)
+    env = MultiAgentEnv(**make_env_config(pf_convergence=semantics), num_envs=K, device=DEV, fused=fused)
     assert env._fused is None
     assert (env._ma is not None) == (fused == "auto")
     env.reset()
@@ -482,8 +507,10 @@ def _het_act(a):
             "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
 
 
-@pytest.mark.parametrize("record_history,n", [(False, 4096), (True, 4096), (False, 1000), (False, 1)])
-def test_het_multiagent_step_equals_generic(record_history, n):
+@pytest.mark.parametrize("record_history,n,semantics", [(False, 4096, "opendss"), (True, 4096, "opendss"),
+                                                        (False, 1000, "opendss"), (False, 1, "opendss"),
+                                                        (False, 4096, "exact"), (True, 1000, "exact")])
+def test_het_multiagent_step_equals_generic(record_history, n, semantics):
     """pgw_ma_step (the heterogeneous scenario's fused path: every agent's
     components in one launch, the per-bus sums, the power flow with the
     extrema epilogue) against the generic per-agent path, bit for bit, over a
@@ -494,8 +521,8 @@ def test_het_multiagent_step_equals_generic(record_history, n):
     and at batch 1."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
-    envs = [MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=f, record_history=record_history)
-            for f in ("auto", False)]
+    envs = [MultiAgentEnv(**make_env_config(pf_convergence=semantics), num_envs=n, device=DEV, fused=f,
+                          record_history=record_history) for f in ("auto", False)]
     assert envs[0]._ma is not None and envs[1]._ma is None
     rng = np.random.default_rng(11)
     acts = _het_actions(rng, n, 300)
@@ -540,18 +567,19 @@ def test_het_multiagent_step_equals_generic(record_history, n):
         assert torch.equal(h0[0], h1[0]) and torch.equal(h0[1], h1[1]) and h0[2] == h1[2]
 
 
-def test_heterogeneous_golden_full_batch_tiled():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_heterogeneous_golden_full_batch_tiled(semantics):
     """The heterogeneous golden's 2 reference trajectories tiled over 65 536 envs
     on the fused multi-agent path: every env reproduces its trajectory for the
     whole episode (obs incl. the PV farm's min_voltage, all three rewards, the
     done flags, and the node voltages at a few steps), compared on the device."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
-    g = load("het_scenario")
+    g = load("het_scenario" + GOLD_SUFFIX[semantics])
     Tn, K, _ = g["actions"].shape
     n = 65536
     rep = n // K
-    env = MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV)
+    env = MultiAgentEnv(**make_env_config(pf_convergence=semantics), num_envs=n, device=DEV)
     assert env._ma is not None
     env.reset()
     env.agent_dict["building"].env_dict["storage"].reset(init_storage=T(np.tile(g["init_storage"], rep)))
@@ -786,7 +814,8 @@ def test_mc_fused_equals_generic_c3(randomize):
 
 
 # ------------------------------------------------------------------ voltage history
-def test_history_ring_fused_and_generic():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_history_ring_fused_and_generic(semantics):
     """record_history=True: the on-device ring holds every node's voltage and
     every agent's power per step (the reference's self.history,
     multiagent_env.py:129, 191-194).  Fused (kernels write the slot) and generic
@@ -795,7 +824,8 @@ def test_history_ring_fused_and_generic():
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     n, steps = 1000, 12
-    mk = lambda **kw: CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, **kw)
+    mk = lambda **kw: CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=semantics), num_envs=n,
+                                                         device=DEV, **kw)
     envs = [mk(fused=True, record_history=True), mk(fused=False, record_history=True),
             mk(fused=True), mk(fused=True, record_history=True, history_capacity=5)]
     init = torch.rand((5, n), dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(4)) * 50
@@ -835,14 +865,16 @@ def test_history_ring_fused_and_generic():
     assert torch.equal(vg, v) and torch.equal(pg, p)
 
 
-def test_fused_voltages_on_demand_only():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_fused_voltages_on_demand_only(semantics):
     """The fused step writes only the rows it needs; the all-node solve runs
     only when a caller reads another node (never on the step / reset path)."""
     from powergridworld_amd.scenarios.coordinated import (CoordinatedMultiBuildingControlEnv,
                                                           make_c4_config)
     n = 300
-    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
-    ref = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=False)
+    cfg = make_c4_config(pf_convergence=semantics)
+    env = CoordinatedMultiBuildingControlEnv(**cfg, num_envs=n, device=DEV, fused=True)
+    ref = CoordinatedMultiBuildingControlEnv(**cfg, num_envs=n, device=DEV, fused=False)
     init = torch.rand((5, n), dtype=torch.float64, device=DEV, generator=torch.Generator(DEV).manual_seed(8)) * 50
     for e in (env, ref):
         e.reset()
@@ -883,7 +915,7 @@ def test_pf_warm_start_multi_bus():
     n = 4096
     kw = dict(feeder_file="ieee_13_dss/IEEE13Nodeckt.dss",
               loadshape_file="ieee_13_dss/annual_hourly_load_profile.csv",
-              system_load_rescale_factor=0.7, num_envs=n, device=DEV)
+              system_load_rescale_factor=0.7, num_envs=n, device=DEV, convergence="exact")
     cold, warm = OpenDSSSolver(**kw), OpenDSSSolver(**kw, warm_start=True)
     rng = np.random.default_rng(21)
     base = rng.uniform(0, 400, size=(2, n))

@@ -29,7 +29,9 @@ SHAPE = "ieee_13_dss/annual_hourly_load_profile.csv"
 
 
 def _solver(feeder, **kw):
+    """convergence: "exact" unless a test asks for OpenDSS's rule (the solver's default)."""
     from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    kw.setdefault("convergence", "exact")
     return OpenDSSSolver(feeder, SHAPE, device=DEV, **kw)
 
 
@@ -356,7 +358,7 @@ def test_regcontrol_multiagent_generic_path():
                              "control_timedelta": pd.Timedelta(300, "s")},
            "pf_config": {"cls": OpenDSSSolver,
                          "config": {"feeder_file": REGCTL, "loadshape_file": SHAPE,
-                                    "system_load_rescale_factor": 1.0}},
+                                    "system_load_rescale_factor": 1.0, "convergence": "exact"}},
            "agents": [
                {"name": "pv", "bus": "f1", "cls": ThisPVEnv,
                 "config": {"profile_csv": "off-peak.csv", "scaling_factor": 400., "grid_aware": True}},

@@ -148,13 +148,25 @@ def test_mc_c3(exo_frame):
         assert (d == g["done"][t]).all()
 
 
-def test_c4_coordinated_oracle():
+def _c4_oracle(K, NA, semantics):
+    from oracle.ma_oracle import CoordinatedOracle
+    from oracle.pf_oracle import BatchedPF
+    orc = CoordinatedOracle(K, n_agents=NA)
+    orc.pf = BatchedPF(system_load_rescale_factor=1.2, semantics=semantics)
+    return orc
+
+
+# golden of each power-flow rule: OpenDSS's snap solve (the reference's) and the fixed point
+GOLD_SUFFIX = {"opendss": "_od", "exact": ""}
+
+
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_c4_coordinated_oracle(semantics):
     """MultiAgentEnv + CoordinatedMultiBuildingControlEnv (reference, oracle PF behind
     its PowerFlowSolver ABC) vs the oracle's end-to-end C4 restatement."""
-    from oracle.ma_oracle import CoordinatedOracle
-    g = load("c4_coordinated")
+    g = load("c4_coordinated" + GOLD_SUFFIX[semantics])
     T, NA, K, _ = g["actions"].shape
-    orc = CoordinatedOracle(K, n_agents=NA)
+    orc = _c4_oracle(K, NA, semantics)
     obs0 = orc.reset(g["init_storage"])
     np.testing.assert_allclose(obs0, g["obs"][0], 1e-10, 1e-10)
     np.testing.assert_allclose(orc.v, g["v675"][0], 1e-12, 1e-12)
@@ -167,13 +179,13 @@ def test_c4_coordinated_oracle():
         assert orc.done == bool(g["done"][t, 0])
 
 
-def test_c4_two_episodes_oracle():
+@pytest.mark.parametrize("semantics", ["opendss", "exact"])
+def test_c4_two_episodes_oracle(semantics):
     """C4 across the episode boundary (reference run, two episodes per env): the
     SoC the reference drew at each reset is injected; x_k carries over."""
-    from oracle.ma_oracle import CoordinatedOracle
-    g = load("c4_two_episodes")
+    g = load("c4_two_episodes" + GOLD_SUFFIX[semantics])
     E, T, NA, K, _ = g["actions"].shape
-    orc = CoordinatedOracle(K, n_agents=NA)
+    orc = _c4_oracle(K, NA, semantics)
     for e in range(E):
         obs0 = orc.reset(g["init_storage"][e])
         np.testing.assert_allclose(obs0, g["obs"][e, 0], 1e-10, 1e-10)
