@@ -400,8 +400,32 @@ typedef struct pgw_pf_tables {
  * start (device, this step's hour): the first iteration in closed form -- from
  * the direct solution the currents are affine in the env's controllable
  * (P, Q): u_1 = u1b + P u1P + Q u1Q and J_1 = J1b + P J1P + Q J1Q; u1b, u1P,
- * u1Q, J1b, J1P, J1Q (m complex each). */
+ * u1Q, J1b, J1P, J1Q (m complex each).
+ *
+ * resp (device, this step's hour; NULL = every env runs the snap solve): the
+ * RESPONSE TABLE of the hour's snap solve.  With one controllable slot and
+ * Q = 0 the whole stopped solve -- its iteration count k* and the accepted
+ * iteration's compensation currents J' = I'(u_{k*-1}), from which every node
+ * voltage follows as V0 + G J' -- is a function of the env's kW P alone,
+ * smooth between breakpoints where k* changes or an element's |u| crosses its
+ * band limit in one of the iterates.  The table holds it per piece as a
+ * quadratic in P; OpenDSSSolver builds it with pgw_pf_od_probe (the same snap
+ * solve at chosen P: the breakpoints by bisection of its signature, three fit
+ * points per piece, two check points whose error bounds the fit).  Segment j of
+ * the grid resp_x0 + j / resp_inv_h (j < resp_nseg) has its first piece at
+ * record j, further pieces chained by `next`; an env whose P lies in no piece
+ * (a breakpoint's bracket, outside the grid, Q != 0, a piece marked
+ * unfittable) runs the snap solve instead, so the table changes no decision:
+ * results differ from the solve only by the fit error (checked <= the
+ * builder's tolerance at the check points).  Record layout: PGW_OD_REC. */
 #define PGW_PF_OD_MAX_ROWS 28
+/* Response-table record of m elements, doubles: [0] lo, [1] hi (kW; the piece
+ * covers lo <= P <= hi), [2] xc, [3] inv_hw (t = (P - xc) inv_hw), [4] two
+ * int32 (iterations k*, 0 = no fit; next record of the segment, -1 = none),
+ * [5] reserved, then c0, c1, c2 (2 m each, re / im per element):
+ * J'_k(t) = c0_k + t (c1_k + t c2_k). */
+#define PGW_OD_REC_HEAD 6
+#define PGW_OD_REC(m) (PGW_OD_REC_HEAD + 6 * (m))
 typedef struct pgw_pf_od {
   double tol;                        /* 1e-4 (ConvergenceTolerance)            */
   double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M];   /* y0' per element (W, -var) */
@@ -413,6 +437,10 @@ typedef struct pgw_pf_od {
   const double* rows_V0;             /* n_rows complex (device)                */
   const double* rows_G;              /* n_rows x m complex (device)            */
   const double* start;               /* 12 m doubles (device)                  */
+  const double* resp;                /* response table records (device) or NULL */
+  double resp_x0, resp_h;            /* grid origin and step (kW)               */
+  int32_t resp_nseg;                 /* grid segments (primary records)         */
+  int32_t resp_pad;
 } pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)
@@ -424,6 +452,36 @@ typedef struct pgw_pf_od {
 int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out,
                      int32_t* iters, void* stream);
+
+/* Response-table builder (OpenDSSSolver._od_response): the snap solve of
+ * pgw_pf_od at n lanes, lane e at controllable kW P[e] (Q = 0) in hour
+ * e / lanes_per_hour (a multiple of 256): hour h uses p_hours[h] (its base
+ * loads) and the first-iteration table start_h + 12 m h; t->od holds the
+ * hour-independent rest (its start and resp are ignored).  Writes per lane the
+ * accepted iteration's currents J_out[e][k] (m complex, the pgw_pf_od.resp
+ * quantity), the iteration count it_out[e] (as pgw_pf_solve's iters) and
+ * sig_out[e], a 64-bit hash of the count and the band states of every iterate
+ * whose currents the solve formed -- equal signatures: the same piece.
+ * args_buf: device scratch of pgw_pf_od_probe_args_size(n_hours) bytes. */
+int64_t pgw_pf_od_probe_args_size(int32_t n_hours);
+int32_t pgw_pf_od_probe(const pgw_pf_params* p_hours, int32_t n_hours, const pgw_pf_tables* t,
+                        const double* start_h, int32_t lanes_per_hour, int64_t n, const double* P,
+                        double* J_out, uint64_t* sig_out, int32_t* it_out, void* args_buf, void* stream);
+
+/* Pieces -> response records (device).  Piece i: fit points a < mid < b whose
+ * currents are J[ia], J[im], J[ib] (m complex each; idx3[3 i ..]), its
+ * covered range [lo, hi] and xc, inv_hw (meta[4 i ..]), its iteration count
+ * and next record (inext[2 i ..]), written to record rec[i] of `out`:
+ * c0 = J(mid), c1 = (J(b) - J(a)) / 2, c2 = (J(a) + J(b)) / 2 - J(mid) (the
+ * quadratic through the three points when mid is the middle). */
+int32_t pgw_pf_od_resp_fit(int32_t m, int64_t n_pieces, const double* J, const int32_t* idx3,
+                           const double* meta, const int32_t* inext, const int32_t* rec, double* out,
+                           void* stream);
+
+/* Fit check: err[i] = max_k |J'_k(P_i) - J[iq_i][k]| / max_k |J[iq_i][k]| for
+ * the piece in record rec[i] evaluated at P[i] exactly as the step kernels do. */
+int32_t pgw_pf_od_resp_check(int32_t m, int64_t n, const double* recs, const int32_t* rec, const double* P,
+                             const double* J, const int32_t* iq, double* err, void* stream);
 
 /* Predictor records from grid solutions (device): U_grid n_tables x n_points x m
  * complex (U_out of the grid solve) -> rec, n_tables x n_points records of

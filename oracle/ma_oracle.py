@@ -80,9 +80,9 @@ class MultiAgentOracle:
     oracle.  A standalone building returns its lagged reward
     (five_zone_rom_env.py:215); components in an MCOracle the fresh sum."""
 
-    def __init__(self, K, agents, sys_load, start, end, dt=DT, max_episode_steps=None):
+    def __init__(self, K, agents, sys_load, start, end, dt=DT, max_episode_steps=None, semantics="exact"):
         self.K, self.agents = K, agents
-        self.pf = BatchedPF(system_load_rescale_factor=sys_load)
+        self.pf = BatchedPF(system_load_rescale_factor=sys_load, semantics=semantics)
         self.start, self.end, self.dt = pd.Timestamp(start), pd.Timestamp(end), dt
         self.max_episode_steps = np.inf if max_episode_steps is None else max_episode_steps
 

@@ -109,7 +109,16 @@ class PFOD(C.Structure):
     _fields_ = [("tol", f64), ("y0r", f64 * PF_MAX_M), ("y0i", f64 * PF_MAX_M),
                 ("elem_scale", f64 * PF_MAX_M), ("gamma", f64), ("eps", f64), ("gmax", f64),
                 ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("sparse_envs", i32),
-                ("rows_V0", vp), ("rows_G", vp), ("start", vp)]
+                ("rows_V0", vp), ("rows_G", vp), ("start", vp), ("resp", vp), ("resp_x0", f64),
+                ("resp_h", f64), ("resp_nseg", i32), ("resp_pad", i32)]
+
+
+OD_REC_HEAD = 6
+
+
+def od_rec(m):
+    """Doubles per response-table record (PGW_OD_REC)."""
+    return OD_REC_HEAD + 6 * m
 
 
 class PFGElem(C.Structure):
@@ -286,6 +295,10 @@ PGW_ELEM_LINE, PGW_ELEM_XFMR, PGW_ELEM_VSOURCE, PGW_ELEM_SHUNT, PGW_ELEM_XFMR_N 
 _SIGS = {
     "pgw_abi_version": (i32, []),
     "pgw_struct_sizes": (i32, [P(i64), i32]),
+    "pgw_pf_od_probe_args_size": (i64, [i32]),
+    "pgw_pf_od_probe": (i32, [P(PFParams), i32, P(PFTables), vp, i32, i64, vp, vp, vp, vp, vp, vp]),
+    "pgw_pf_od_resp_fit": (i32, [i32, i64, vp, vp, vp, vp, vp, vp, vp]),
+    "pgw_pf_od_resp_check": (i32, [i32, i64, vp, vp, vp, vp, vp, vp, vp]),
     "pgw_last_error": (C.c_char_p, []),
     "pgw_battery_reset": (i32, [P(BatteryParams), i64, vp, vp, Mat, vp]),
     "pgw_battery_step": (i32, [P(BatteryParams), i64, Mat, vp, Mat, vp, vp]),

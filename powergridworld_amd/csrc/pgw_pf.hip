@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cmath>
 #include <type_traits>
+#include <vector>
 
 #include "pgw_common.h"
 
@@ -1042,6 +1043,9 @@ struct ODArgs {
   int32_t min_iter, n_rep, n_rows, max_iter;
   int32_t sparse;                                 // envs a wave's exact test takes one at a time
   int32_t node_mask;                              // bit k: element k is a node (esc[k] > 0)
+  const double* resp;                             // response table of the hour (pgw_pf_od.resp) or null
+  double resp_x0, resp_inv_h;
+  int32_t resp_nseg;
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
 constexpr int kOdChunk = 12;                      // check rows per previous-magnitude pass
@@ -1091,6 +1095,11 @@ static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   o.sparse = d.sparse_envs == 0 ? kOdSparse : d.sparse_envs < 0 ? 0 : min(d.sparse_envs, 64);
   for (int k = 0; k < PGW_PF_MAX_M; ++k)
     if (d.elem_scale[k] > 0.0) o.node_mask |= 1 << k;
+  const bool resp = d.resp && d.resp_nseg > 0 && d.resp_h > 0.0;
+  o.resp = resp ? d.resp : nullptr;
+  o.resp_x0 = d.resp_x0;
+  o.resp_inv_h = resp ? 1.0 / d.resp_h : 0.0;
+  o.resp_nseg = resp ? d.resp_nseg : 0;
   return o;
 }
 
@@ -1128,7 +1137,7 @@ template <int M> struct ODStage {
 };
 
 template <int M>
-__device__ __forceinline__ void od_stage_load(const ODArgs& o, ODStage<M>& g) {
+__device__ __forceinline__ void od_stage_load(const ODArgs& o, const double* start, ODStage<M>& g) {
   constexpr int S = ODRow<M>::kStride;
   const int total = o.n_rows * S;
 #pragma unroll
@@ -1147,7 +1156,7 @@ __device__ __forceinline__ void od_stage_load(const ODArgs& o, ODStage<M>& g) {
 #pragma unroll
   for (int q = 0; q < ODStage<M>::kStQ; ++q) {
     const int i = threadIdx.x + q * kBlock;
-    g.v[ODStage<M>::kRowQ + q] = i < 12 * M ? o.start[i] : 0.0;
+    g.v[ODStage<M>::kRowQ + q] = i < 12 * M ? start[i] : 0.0;
   }
   const int l = threadIdx.x & 15;
   const bool in = l < M;
@@ -1341,9 +1350,14 @@ __device__ __forceinline__ void od_load_J(const ODShared<M>& sh, int it, double 
 //                previous currents and the new ones from this iteration's --
 //                the first n_rep rows, the bounded ones only when some env's
 //                bounds cannot decide (it then takes the exact decision).
-template <int M>
+// SIG (the response-table builder, pgw_pf_od_probe): *sig accumulates, per
+// iteration the env runs, the load band of every element of the iterate whose
+// currents it forms (u_1 .. u_{k*-1}), then the returned count: a 64-bit FNV-1a
+// style hash that tells the smooth pieces of the solve as a function of P apart.
+constexpr uint64_t kFnvBasis = 0xcbf29ce484222325ull, kFnvPrime = 0x100000001b3ull;
+template <int M, bool SIG = false>
 __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, const ODStage<M>& g, bool valid,
-                        ODShared<M>& sh) {
+                        ODShared<M>& sh, uint64_t* sig = nullptr) {
   static_assert(kOdRows <= 2 * M, "od_rows keeps two row magnitudes per current slot");
   const int tid = threadIdx.x;
   // per-element constants resident for DPP: y0' (re, im) and the node scale
@@ -1378,6 +1392,16 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, const ODSt
     ++it;
     double2* const cur = sh.J[it & 1];
     const double2* const prv = sh.J[(it & 1) ^ 1];
+    if constexpr (SIG) {
+      uint64_t bands = 0;
+      static_for<0, M>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        const double m2 = fma(S.ui[k], S.ui[k], S.ur[k] * S.ur[k]);     // (current_od's)
+        const uint64_t b = (uint64_t)(m2 > S.lo2) + (uint64_t)(m2 > S.mn2) + (uint64_t)(m2 > S.mx2);
+        bands |= b << (2 * k);
+      });
+      if (!done) *sig = (*sig ^ bands) * kFnvPrime;
+    }
     // ---- currents of u_{k-1} (into LDS), u_k by the matvec.  (Interleaving
     // element k+1's current law between slices of column k's FMAs measured no
     // faster -- profiles/r04/ab_pipelined_column_loop.txt: the wave is bound by
@@ -1482,7 +1506,91 @@ __device__ int od_solve(PFSolver<M, true, false>& S, const ODArgs& o, const ODSt
     conv_ok = conv_ok || (!done && d > 0);
     done = done || d > 0 || it >= o.max_iter;
   }
-  return conv_ok ? my_it : -my_it;
+  const int ret = conv_ok ? my_it : -my_it;
+  if constexpr (SIG) *sig = (*sig ^ (uint64_t)(uint32_t)ret) * kFnvPrime;
+  return ret;
+}
+
+// ---- the response table (pgw_pf_od.resp) ---------------------------------
+// Record r (PGW_OD_REC doubles, 16-byte aligned): as double2, [0] (lo, hi),
+// [1] (xc, inv_hw), [2] (k* | next << 32, -), then c0, c1, c2 per element.
+constexpr int kOdHops = 8;                         // records tried per env (chain length)
+__device__ __forceinline__ void od_rec_meta(double v, int& it, int& next) {
+  const long long b = __double_as_longlong(v);
+  it = (int)(uint32_t)(b & 0xffffffffll);
+  next = (int)(b >> 32);
+}
+// J'_k at t = (P - xc) inv_hw: c0 + t (c1 + t c2) -- the step kernels and
+// pgw_pf_od_resp_check evaluate it with these operations.
+__device__ __forceinline__ double2 od_rec_j(double2 c0, double2 c1, double2 c2, double t) {
+  return make_double2(fma(t, fma(t, c2.x, c1.x), c0.x), fma(t, fma(t, c2.y, c1.y), c0.y));
+}
+// The env's currents J' and iteration count from the table: false when P
+// (with Q = 0) lies in no piece -- then the env runs the snap solve.
+template <int M>
+__device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double Q, double (&jr)[M],
+                                               double (&ji)[M], int& it) {
+  constexpr int R2 = PGW_OD_REC(M) / 2;
+  const double g = (P - o.resp_x0) * o.resp_inv_h;
+  if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
+  int r = (int)g;
+  for (int hop = 0; hop < kOdHops; ++hop) {
+    const double2* rec = reinterpret_cast<const double2*>(o.resp) + (int64_t)r * R2;
+    double2 c[3 * M];
+    const double2 h0 = rec[0], h1 = rec[1], h2 = rec[2];
+#pragma unroll
+    for (int q = 0; q < 3 * M; ++q) c[q] = rec[3 + q];      // in flight with the header
+    int k_it, next;
+    od_rec_meta(h2.x, k_it, next);
+    if (P >= h0.x && P <= h0.y) {
+      if (k_it == 0) return false;                          // a piece without a fit
+      const double t = (P - h1.x) * h1.y;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        const double2 j = od_rec_j(c[k], c[M + k], c[2 * M + k], t);
+        jr[k] = j.x;
+        ji[k] = j.y;
+      }
+      it = k_it;
+      return true;
+    }
+    if (next < 0) return false;
+    r = next;
+  }
+  return false;
+}
+
+// The envs of the block the table does not cover: stage the check rows (the
+// stage loads already issued unless `late`) and run the snap solve for them;
+// their currents and counts replace (jr, ji, it).  The other lanes park their
+// table currents in their own sh.J[0] slots through the solve (a lane that does
+// not solve never writes its slots there: od_solve stores currents only while
+// the env runs, and currents_1 writes sh.J[1]), so the solve's registers do
+// not add to them.  Block-uniform barriers: every lane of the block calls it.
+template <int M>
+__device__ __forceinline__ void od_fallback(PFSolver<M, true, false>& S, const ODArgs& o, const double* start,
+                                            ODStage<M>& stg, bool late, ODShared<M>& sh, bool need,
+                                            double (&jr)[M], double (&ji)[M], int& it) {
+  if (!__syncthreads_or(need)) return;               // (block-uniform)
+  const int tid = threadIdx.x;
+  if (!need) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) sh.J[0][k * kBlock + tid] = make_double2(jr[k], ji[k]);
+  }
+  if (late) od_stage_load<M>(o, start, stg);
+  od_stage_store<M>(o, stg, sh);
+  __syncthreads();                                   // the staged check rows
+  int its = 0;
+  if (__ballot(need) != 0ull)                        // (wave-uniform) some env of this wave
+    its = od_solve<M>(S, o, stg, need, sh);
+  const double2* J = need ? sh.J[abs(its) & 1] : sh.J[0];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double2 j = J[k * kBlock + tid];
+    jr[k] = j.x;
+    ji[k] = j.y;
+  }
+  it = need ? its : it;
 }
 
 // Fused C4 step, OpenDSS rule: k_coord_pf's prologue (agent powers -> bus
@@ -1496,7 +1604,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   const bool valid = e < n;
   __shared__ ODShared<M> sh;
   ODStage<M> stg;
-  od_stage_load<M>(o, stg);                          // in flight with the loads below
+  // without a response table every env solves: the stage loads go out first,
+  // in flight with the loads below; with one only a block that needs them does
+  const bool early = o.resp == nullptr;
+  if (early) od_stage_load<M>(o, o.start, stg);
   double rp[PGW_MAX_AGENTS];
   const int64_t ec = valid ? e : 0;
 #pragma unroll
@@ -1518,11 +1629,12 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
     for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
   S.powers(a, cp, cq, 1.0);
-  od_stage_store<M>(o, stg, sh);
-  __syncthreads();                                   // the staged check rows
-  const int it = od_solve<M>(S, o, stg, valid, sh);
   double ir[M], ii[M], v0r, v0i;
-  od_load_J<M>(sh, it, ir, ii);
+#pragma unroll
+  for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
+  int it = 0;
+  const bool need = valid && !(o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it));
+  od_fallback<M>(S, o, o.start, stg, !early, sh, need, ir, ii, it);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   // rows 1.. (a history slot holds every node): through the scalar cache, as
@@ -1561,7 +1673,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   const bool valid = e < n;
   __shared__ ODShared<M> sh;
   ODStage<M> stg;
-  od_stage_load<M>(o, stg);                          // in flight with the loads below
+  // the table gives currents, not element voltages: U_out asks for the solve
+  const bool table = o.resp != nullptr && t.U_out == nullptr;
+  if (!table) od_stage_load<M>(o, o.start, stg);     // in flight with the loads below
   PFSolver<M, true, false> S;
   S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
@@ -1571,11 +1685,12 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
   }
   S.powers(a, cp, cq, 1.0);
-  od_stage_store<M>(o, stg, sh);
-  __syncthreads();                                   // the staged check rows
-  const int it = od_solve<M>(S, o, stg, valid, sh);
   double ir[M], ii[M], v0r, v0i;
-  od_load_J<M>(sh, it, ir, ii);
+#pragma unroll
+  for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
+  int it = 0;
+  const bool need = valid && !(table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it));
+  od_fallback<M>(S, o, o.start, stg, table, sh, need, ir, ii, it);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if (valid && t.U_out) {
@@ -1598,6 +1713,97 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     if (t.v_max_out) t.v_max_out[e] = vmx;
   }
   if (iters) iters[e] = it;
+}
+
+// Response-table builder (pgw_pf_od_probe): the snap solve at lane e's kW P[e]
+// (Q = 0) in hour e / lanes_per_hour -- that hour's PFArgs (base loads) and
+// first-iteration table -- with the signature of its pieces.
+template <int M>
+__global__ void __launch_bounds__(kBlock) k_pf_od_probe(const PFArgs* __restrict__ args_h, ODArgs o,
+                                                        pgw_pf_tables t, const double* __restrict__ start_h,
+                                                        int32_t lanes_per_hour, int64_t n,
+                                                        const double* __restrict__ P,
+                                                        double2* __restrict__ J_out, uint64_t* __restrict__ sig_out,
+                                                        int32_t* __restrict__ it_out) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = e < n;
+  const int hour = (int)(((int64_t)blockIdx.x * kBlock) / lanes_per_hour);   // (block-uniform)
+  const PFArgs& a = args_h[hour];
+  const double* start = start_h + (int64_t)hour * 12 * M;
+  __shared__ ODShared<M> sh;
+  ODStage<M> stg;
+  od_stage_load<M>(o, start, stg);
+  PFSolver<M, true, false> S;
+  S.load(a, t.block);
+  double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
+#pragma unroll
+  for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
+    cp[c] = (valid && c == 0) ? P[e] : 0.0;
+    cq[c] = 0.0;
+  }
+  S.powers(a, cp, cq, 1.0);
+  od_stage_store<M>(o, stg, sh);
+  __syncthreads();
+  uint64_t sig = kFnvBasis;
+  const int it = od_solve<M, true>(S, o, stg, valid, sh, &sig);
+  double ir[M], ii[M];
+  od_load_J<M>(sh, it, ir, ii);
+  if (!valid) return;
+#pragma unroll
+  for (int k = 0; k < M; ++k) J_out[e * M + k] = make_double2(ir[k], ii[k]);
+  sig_out[e] = sig;
+  it_out[e] = it;
+}
+
+// Pieces -> records (pgw_pf_od_resp_fit), one thread per piece.
+__global__ void __launch_bounds__(kBlock) k_pf_od_resp_fit(int32_t m, int64_t np, const double2* __restrict__ J,
+                                                           const int32_t* __restrict__ idx3,
+                                                           const double* __restrict__ meta,
+                                                           const int32_t* __restrict__ inext,
+                                                           const int32_t* __restrict__ rec, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= np) return;
+  double* o = out + (int64_t)rec[i] * PGW_OD_REC(m);
+  for (int q = 0; q < 4; ++q) o[q] = meta[4 * i + q];
+  const unsigned long long packed =
+      (unsigned long long)(uint32_t)inext[2 * i] | ((unsigned long long)(uint32_t)inext[2 * i + 1] << 32);
+  o[4] = __longlong_as_double((long long)packed);
+  o[5] = 0.0;
+  const double2* ja = J + (int64_t)idx3[3 * i] * m;
+  const double2* jm = J + (int64_t)idx3[3 * i + 1] * m;
+  const double2* jb = J + (int64_t)idx3[3 * i + 2] * m;
+  double* c = o + PGW_OD_REC_HEAD;
+  for (int k = 0; k < m; ++k) {
+    const double2 a = ja[k], md = jm[k], b = jb[k];
+    c[2 * k] = md.x;
+    c[2 * k + 1] = md.y;
+    c[2 * m + 2 * k] = 0.5 * (b.x - a.x);
+    c[2 * m + 2 * k + 1] = 0.5 * (b.y - a.y);
+    c[4 * m + 2 * k] = 0.5 * (a.x + b.x) - md.x;
+    c[4 * m + 2 * k + 1] = 0.5 * (a.y + b.y) - md.y;
+  }
+}
+
+// Fit check (pgw_pf_od_resp_check), one thread per check point.
+__global__ void __launch_bounds__(kBlock) k_pf_od_resp_check(int32_t m, int64_t n, const double* __restrict__ recs,
+                                                             const int32_t* __restrict__ rec,
+                                                             const double* __restrict__ P,
+                                                             const double2* __restrict__ J,
+                                                             const int32_t* __restrict__ iq,
+                                                             double* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double2* r = reinterpret_cast<const double2*>(recs + (int64_t)rec[i] * PGW_OD_REC(m));
+  const double t = (P[i] - r[1].x) * r[1].y;
+  const double2* jt = J + (int64_t)iq[i] * m;
+  double num = 0.0, den = 0.0;
+  for (int k = 0; k < m; ++k) {
+    const double2 f = od_rec_j(r[3 + k], r[3 + m + k], r[3 + 2 * m + k], t);
+    const double2 w = jt[k];
+    num = fmax(num, hypot(f.x - w.x, f.y - w.y));
+    den = fmax(den, hypot(w.x, w.y));
+  }
+  err[i] = den > 0.0 ? num / den : num;
 }
 
 // Stencil metadata of the predictor grid (one thread per segment): in a
@@ -1959,6 +2165,60 @@ int32_t pgw_voltage_band_penalty(int64_t n, const double* v, double lo, double h
   hipLaunchKernelGGL(k_band_penalty, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, v, lo,
                      hi, scale, out);
   return check_launch("k_band_penalty");
+}
+
+int64_t pgw_pf_od_probe_args_size(int32_t n_hours) {
+  return n_hours <= 0 ? 0 : (int64_t)n_hours * (int64_t)sizeof(PFArgs);
+}
+
+int32_t pgw_pf_od_probe(const pgw_pf_params* p_hours, int32_t n_hours, const pgw_pf_tables* t,
+                        const double* start_h, int32_t lanes_per_hour, int64_t n, const double* P,
+                        double* J_out, uint64_t* sig_out, int32_t* it_out, void* args_buf, void* stream) {
+  PGW_REQUIRE(p_hours && t && t->block && t->od && start_h && P && J_out && sig_out && it_out && args_buf,
+              "pgw_pf_od_probe: null argument");
+  PGW_REQUIRE(n_hours >= 1 && n >= 0 && lanes_per_hour > 0 && lanes_per_hour % kBlock == 0 &&
+              n <= (int64_t)n_hours * lanes_per_hour,
+              "pgw_pf_od_probe: n %lld lanes over %d hours of %d (a multiple of %d)", (long long)n, n_hours,
+              lanes_per_hour, kBlock);
+  std::vector<PFArgs> args(n_hours);
+  for (int h = 0; h < n_hours; ++h) {
+    const int32_t rc = check_od(p_hours[h], *t, "pgw_pf_od_probe");
+    if (rc) return rc;
+    PGW_REQUIRE(p_hours[h].m == p_hours[0].m && p_hours[h].n_ctrl == p_hours[0].n_ctrl &&
+                p_hours[h].max_iter == p_hours[0].max_iter, "pgw_pf_od_probe: hours differ in shape");
+    args[h] = make_pf_args(p_hours[h], *t);
+  }
+  if (n == 0) return PGW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  // (the host array is released on return: wait for the copy)
+  PGW_REQUIRE(hipMemcpyAsync(args_buf, args.data(), sizeof(PFArgs) * n_hours, hipMemcpyHostToDevice, st) ==
+                  hipSuccess && hipStreamSynchronize(st) == hipSuccess,
+              "pgw_pf_od_probe: argument upload failed");
+  hipLaunchKernelGGL(k_pf_od_probe<14>, dim3(grid_for(n)), dim3(kBlock), 0, st,
+                     reinterpret_cast<const PFArgs*>(args_buf), make_od_args(*t->od, p_hours[0].max_iter), *t,
+                     start_h, lanes_per_hour, n, P, reinterpret_cast<double2*>(J_out), sig_out, it_out);
+  return check_launch("k_pf_od_probe");
+}
+
+int32_t pgw_pf_od_resp_fit(int32_t m, int64_t n_pieces, const double* J, const int32_t* idx3,
+                           const double* meta, const int32_t* inext, const int32_t* rec, double* out,
+                           void* stream) {
+  PGW_REQUIRE(m >= 1 && m <= PGW_PF_MAX_M && n_pieces >= 0, "pgw_pf_od_resp_fit: bad m / n_pieces");
+  if (n_pieces == 0) return PGW_OK;
+  PGW_REQUIRE(J && idx3 && meta && inext && rec && out, "pgw_pf_od_resp_fit: null argument");
+  hipLaunchKernelGGL(k_pf_od_resp_fit, dim3(grid_for(n_pieces)), dim3(kBlock), 0, (hipStream_t)stream, m,
+                     n_pieces, reinterpret_cast<const double2*>(J), idx3, meta, inext, rec, out);
+  return check_launch("k_pf_od_resp_fit");
+}
+
+int32_t pgw_pf_od_resp_check(int32_t m, int64_t n, const double* recs, const int32_t* rec, const double* P,
+                             const double* J, const int32_t* iq, double* err, void* stream) {
+  PGW_REQUIRE(m >= 1 && m <= PGW_PF_MAX_M && n >= 0, "pgw_pf_od_resp_check: bad m / n");
+  if (n == 0) return PGW_OK;
+  PGW_REQUIRE(recs && rec && P && J && iq && err, "pgw_pf_od_resp_check: null argument");
+  hipLaunchKernelGGL(k_pf_od_resp_check, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, m, n, recs,
+                     rec, P, reinterpret_cast<const double2*>(J), iq, err);
+  return check_launch("k_pf_od_resp_check");
 }
 
 int32_t pgw_pf_pred_meta(const pgw_pf_params* p, int32_t n_tables, int32_t n_points,

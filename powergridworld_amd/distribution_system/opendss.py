@@ -66,7 +66,7 @@ class OpenDSSSolver(PowerFlowSolver):
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = None, max_iter: int = None,
                  output_nodes=None, predictor: bool = True, warm_start: bool = False,
-                 convergence: str = "opendss", general: bool = None, **kwargs):
+                 convergence: str = "opendss", general: bool = None, od_table: bool = True, **kwargs):
         """convergence: "opendss" (the default) -- OpenDSS's own snap solve as
         the reference runs it (opendss.py:134):
         loads' nominal admittances in Y, start from the direct solution, stop at
@@ -76,11 +76,14 @@ class OpenDSSSolver(PowerFlowSolver):
         and reproducible (DESIGN.md section 2 measures the difference).
         Feeders with more than 16 load phase elements, other load models or
         RegControls run the general kernel (pgw_pf_solve_general); general=True
-        forces it (tests, measurements)."""
+        forces it (tests, measurements).  od_table: the fast OpenDSS-rule
+        kernels read the hour's response table (pgw_pf_od.resp) and solve only
+        the envs it does not cover; False solves every env."""
         super().__init__(**kwargs)
         if convergence not in ("exact", "opendss"):
             raise ValueError("convergence must be 'exact' or 'opendss', got %r" % (convergence,))
         self.convergence = convergence
+        self.od_table = bool(od_table)
         self.num_envs = int(num_envs)
         self.device = _lib.require_device(device)
         spec = load_feeder_spec(feeder_file)
@@ -271,6 +274,8 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_W2 = W / (vb_elem[:, None] * vb_elem[None, :])
         self._od_u0 = U0 / vb_elem
         self._od_start = torch.zeros((self.OD_MAX_TABLES, 12 * M), dtype=torch.float64, device=dev)
+        self._od_resp = None                 # response tables (allocated on the first build)
+        self.od_resp_stats, self.od_resp_brackets = {}, {}
         self._od_index = {}
         self._od_keep = {}
 
@@ -311,8 +316,244 @@ class OpenDSSSolver(PowerFlowSolver):
             self._od_index[k] = idx0 + j
         if hours:
             self._od_start[idx0:idx0 + len(hours)].copy_(torch.from_numpy(recs), non_blocking=False)
+            if self.od_table:
+                self._od_response(hours, idx0)
 
-    def _od_tables(self, hour):
+    # ------------------------------------------------------------ OpenDSS rule: response tables
+    # pgw_pf_od.resp (include/pgw.h): per hour, the snap solve's accepted
+    # currents J' and iteration count as piecewise quadratics of the env's kW
+    # (one controllable slot, Q = 0), built with pgw_pf_od_probe -- the same snap
+    # solve -- on the predictor grid: every segment's ends and midpoint; segments
+    # whose three signatures (iteration count + every iterate's load bands) differ
+    # sampled at OD_RESP_SUB points and every signature change bisected to a
+    # bracket of ~1e-10 kW; three fit points per piece; two check points per
+    # piece bound the fit error (OD_RESP_TOL, relative, else the piece is left to
+    # the solve).  Envs in a bracket, outside the grid or with Q != 0 run the solve.
+    OD_RESP_EXTRA = 1024          # records per hour beyond the grid's (further pieces of a segment)
+    OD_RESP_SUB = 64              # sample points across a segment with a breakpoint
+    OD_RESP_BISECT = 26           # rounds per bracket: h / 64 / 2^26 ~ 1.5e-10 kW
+    OD_RESP_PASSES = 6            # bracket passes (a further breakpoint inside a bracket)
+    OD_RESP_MIN_WIDTH = 1e-9      # kW: narrower pieces are left to the solve
+    OD_RESP_TOL = 2e-11           # fit error bound at the check points (max |dJ| / max |J|)
+
+    @staticmethod
+    def _od_meta_word(it, nxt):
+        """Record word [4] (PGW_OD_REC): int32 k* in the low half, int32 next in
+        the high half, as an int64."""
+        return int(np.array([(it & 0xffffffff) | ((nxt & 0xffffffff) << 32)], np.uint64).view(np.int64)[0])
+
+    def _od_probe(self, hours, idx0, pts):
+        """pgw_pf_od_probe over the batch's hours (rows idx0.. of the start
+        tables): pts[q] = the kW points of hour q.  Returns (J [n, M, 2] device,
+        signatures [n] uint64, iterations [n] int32, per-hour lane offsets)."""
+        M, H, dev = self.M, len(hours), self.device
+        lph = max(256, -(-max(len(p) for p in pts) // 256) * 256)
+        n = H * lph
+        P = np.full(n, self.PREDICTOR_X0)
+        for q, p in enumerate(pts):
+            P[q * lph:q * lph + len(p)] = p
+        Pd = torch.from_numpy(P).to(dev)
+        J = torch.empty((n, M, 2), dtype=torch.float64, device=dev)
+        sig = torch.empty(n, dtype=torch.int64, device=dev)
+        it = torch.empty(n, dtype=torch.int32, device=dev)
+        lib = _lib.lib()
+        args = torch.empty(int(lib.pgw_pf_od_probe_args_size(H)), dtype=torch.uint8, device=dev)
+        ph = (_lib.PFParams * H)(*[self._params_for_hour(hr) for hr in hours])
+        od = _lib.PFOD.from_buffer_copy(self._od_proto)
+        od.start = self._od_start[idx0].data_ptr()
+        t = _lib.PFTables.from_buffer_copy(self.tables)
+        t.od = _lib.C.addressof(od)
+        _lib.check(lib.pgw_pf_od_probe(ph, H, t, self._od_start[idx0].data_ptr(), lph, n, Pd.data_ptr(),
+                                       J.data_ptr(), sig.data_ptr(), it.data_ptr(), args.data_ptr(),
+                                       _lib.stream_ptr(dev)))
+        return J, sig.cpu().numpy().view(np.uint64), it.cpu().numpy(), np.arange(H) * lph
+
+    def _od_response(self, hours, idx0):
+        """Build and upload the response tables of `hours` (rows idx0.. of the
+        start tables).  Control flow and bookkeeping here; every solve, fit and
+        fit check runs on the device."""
+        import time as _time
+        t_start = _time.perf_counter()
+        M, H, dev = self.M, len(hours), self.device
+        x0, h, nseg = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N - 1
+        R = _lib.od_rec(M)
+        rec_n = nseg + self.OD_RESP_EXTRA
+        if self._od_resp is None:
+            self._od_resp = torch.empty((self.OD_MAX_TABLES, rec_n, R), dtype=torch.float64, device=dev)
+        lib, st = _lib.lib(), _lib.stream_ptr(dev)
+        blk = self._od_resp[idx0:idx0 + H]
+        blk[:, :, 0] = float("inf")                        # lo > hi: no piece
+        blk[:, :, 1] = -float("inf")
+        # (k*, next) as two int32 in one double: written through an int64 view
+        # (the pattern of next = -1 is a NaN, which float paths may canonicalise)
+        blk.view(torch.int64)[:, :, 4] = self._od_meta_word(0, -1)
+        x = x0 + h * np.arange(nseg + 1)
+        # ---- 1. every segment's ends and midpoint
+        pts = x0 + 0.5 * h * np.arange(2 * nseg + 1)
+        Jg, sg, itg, og = self._od_probe(hours, idx0, [pts] * H)
+        lanes = og[:, None] + np.arange(2 * nseg + 1)[None, :]
+        S_ = sg[lanes]                                      # [H, 2 nseg + 1]
+        clean = (S_[:, 0:-1:2] == S_[:, 1::2]) & (S_[:, 1::2] == S_[:, 2::2])
+        # ---- 2. segments with a breakpoint: sample, then bracket every change
+        dq, dj = np.nonzero(~clean)
+        sub = np.arange(self.OD_RESP_SUB + 1) / self.OD_RESP_SUB
+        per = [[] for _ in range(H)]
+        for i, (q, j) in enumerate(zip(dq, dj)):
+            per[q].append(i)
+        brk = []                                            # (i = dirty index, lo, hi, s_lo, s_hi)
+        if len(dq):
+            Jd, sd, _, od_ = self._od_probe(hours, idx0, [np.concatenate([x[dj[i]] + h * sub for i in per[q]])
+                                                           if per[q] else np.zeros(0) for q in range(H)])
+            ns = len(sub)
+            for q in range(H):
+                for r, i in enumerate(per[q]):
+                    s = sd[od_[q] + r * ns: od_[q] + (r + 1) * ns]
+                    for k in np.nonzero(s[1:] != s[:-1])[0]:
+                        brk.append((i, x[dj[i]] + h * sub[k], x[dj[i]] + h * sub[k + 1], s[k], s[k + 1]))
+            del Jd
+        done, gaps, passes = [], [], 0
+        work = brk
+        while work and passes < self.OD_RESP_PASSES:
+            passes += 1
+            I = np.array([w[0] for w in work])
+            lo = np.array([w[1] for w in work])
+            hi = np.array([w[2] for w in work])
+            slo = np.array([w[3] for w in work], np.uint64)
+            shi = np.array([w[4] for w in work], np.uint64)
+            hi0, tgt = hi.copy(), shi.copy()
+            qs = dq[I]
+            for _ in range(self.OD_RESP_BISECT):
+                mid = 0.5 * (lo + hi)
+                order = [np.nonzero(qs == q)[0] for q in range(H)]
+                _, sm, _, om = self._od_probe(hours, idx0, [mid[o] for o in order])
+                smid = np.empty(len(mid), np.uint64)
+                for q, o in enumerate(order):
+                    smid[o] = sm[om[q]: om[q] + len(o)]
+                left = smid == slo
+                lo = np.where(left, mid, lo)
+                hi = np.where(left, hi, mid)
+                shi = np.where(left, shi, smid)
+            nxt = []
+            for k in range(len(work)):
+                done.append((I[k], lo[k], hi[k], slo[k], shi[k]))
+                if shi[k] != tgt[k]:                        # a further breakpoint in (hi, hi0]
+                    nxt.append((I[k], hi[k], hi0[k], shi[k], tgt[k]))
+            work = nxt
+        for w in work:                                      # unresolved: left to the solve
+            gaps.append(w)
+        # ---- 3. pieces: clean segments one each, the others between brackets
+        pieces = []          # (q, j, a, b, sig, it, lane triple or None)
+        cq, cj = np.nonzero(clean)
+        n_clean = len(cq)
+        by_seg = {}
+        for (i, lo_, hi_, s0, s1) in done:
+            by_seg.setdefault(i, []).append((lo_, hi_, s0, s1))
+        for (i, lo_, hi_, s0, s1) in gaps:
+            by_seg.setdefault(i, []).append((lo_, hi_, None, None))
+        dirty_pieces = []    # (q, j, a, b, sig)
+        for i, (q, j) in enumerate(zip(dq, dj)):
+            a, sa = x[j], S_[q, 2 * j]
+            for lo_, hi_, s0, s1 in sorted(by_seg.get(i, []), key=lambda z: z[0]):
+                if s0 is not None and lo_ - a >= self.OD_RESP_MIN_WIDTH and s0 == sa:
+                    dirty_pieces.append((q, j, a, lo_, sa))
+                a, sa = hi_, s1
+            if sa is not None and x[j + 1] - a >= self.OD_RESP_MIN_WIDTH and sa == S_[q, 2 * j + 2]:
+                dirty_pieces.append((q, j, a, x[j + 1], sa))
+        # fit points of the pieces between brackets
+        nd = len(dirty_pieces)
+        if nd:
+            fq = np.array([p[0] for p in dirty_pieces])
+            fa = np.array([p[2] for p in dirty_pieces])
+            fb = np.array([p[3] for p in dirty_pieces])
+            fs = np.array([p[4] for p in dirty_pieces], np.uint64)
+            order = [np.nonzero(fq == q)[0] for q in range(H)]
+            Jf, sf, itf, of_ = self._od_probe(hours, idx0, [np.stack([fa[o], 0.5 * (fa[o] + fb[o]), fb[o]], 1).ravel()
+                                                             for o in order])
+            f_lanes = np.empty((nd, 3), np.int64)
+            for q, o in enumerate(order):
+                f_lanes[o] = of_[q] + np.arange(3 * len(o)).reshape(-1, 3)
+            f_ok = (sf[f_lanes] == fs[:, None]).all(1)
+            f_it = itf[f_lanes[:, 1]]
+        # ---- 4. records: segment j's first piece at record j, more in the extra slots
+        extra = np.zeros(H, np.int64)
+        rec_first = {}
+        d_rec = np.empty(nd, np.int64)
+        d_next = np.full(nd, -1, np.int64)
+        prev = {}
+        for k, (q, j, a, b, sg_) in enumerate(dirty_pieces):
+            if (q, j) not in rec_first:
+                rec_first[(q, j)] = k
+                d_rec[k] = j
+            elif extra[q] < self.OD_RESP_EXTRA:
+                d_rec[k] = nseg + extra[q]
+                extra[q] += 1
+                d_next[prev[(q, j)]] = d_rec[k]
+            else:
+                d_rec[k] = -1                              # no room: left to the solve
+                continue
+            prev[(q, j)] = k
+        row = (idx0 + np.arange(H)).astype(np.int64)
+
+        def fit(Jbuf, lanes3, a, b, it_, nxt, recs_global):
+            n_ = len(a)
+            if n_ == 0:
+                return
+            meta = np.stack([a, b, 0.5 * (a + b), 2.0 / (b - a)], 1)
+            inext = np.stack([it_, nxt], 1).astype(np.int32)
+            T = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dtype=dt)).to(dev)
+            _lib.check(lib.pgw_pf_od_resp_fit(M, n_, Jbuf.data_ptr(), T(lanes3, np.int32).data_ptr(),
+                                              T(meta, np.float64).data_ptr(), T(inext, np.int32).data_ptr(),
+                                              T(recs_global, np.int32).data_ptr(), self._od_resp.data_ptr(), st))
+            torch.cuda.synchronize(dev)
+
+        c_lanes = og[cq][:, None] + 2 * cj[:, None] + np.arange(3)[None, :]
+        c_rec = row[cq] * rec_n + cj
+        fit(Jg, c_lanes, x[cj], x[cj + 1], itg[c_lanes[:, 0]], np.full(n_clean, -1), c_rec)
+        if nd:
+            keep = d_rec >= 0
+            d_it = np.where(f_ok, f_it, 0)
+            fit(Jf, f_lanes[keep], fa[keep], fb[keep], d_it[keep], d_next[keep], row[fq[keep]] * rec_n + d_rec[keep])
+        # ---- 5. check points t = +-1/2 of every fitted piece
+        pa = np.concatenate([x[cj], fa[keep] if nd else np.zeros(0)])
+        pb = np.concatenate([x[cj + 1], fb[keep] if nd else np.zeros(0)])
+        pq_ = np.concatenate([cq, fq[keep] if nd else np.zeros(0, np.int64)])
+        psig = np.concatenate([S_[cq, 2 * cj], fs[keep] if nd else np.zeros(0, np.uint64)])
+        prec = np.concatenate([c_rec, (row[fq[keep]] * rec_n + d_rec[keep]) if nd else np.zeros(0, np.int64)])
+        pit = np.concatenate([itg[c_lanes[:, 0]], d_it[keep] if nd else np.zeros(0, np.int32)])
+        pnext = np.concatenate([np.full(n_clean, -1), d_next[keep] if nd else np.zeros(0, np.int64)])
+        w = pb - pa
+        chk = np.stack([pa + 0.25 * w, pa + 0.75 * w], 1)
+        order = [np.nonzero(pq_ == q)[0] for q in range(H)]
+        Jc, sc, _, oc = self._od_probe(hours, idx0, [chk[o].ravel() for o in order])
+        c_l = np.empty((len(pa), 2), np.int64)
+        for q, o in enumerate(order):
+            c_l[o] = oc[q] + np.arange(2 * len(o)).reshape(-1, 2)
+        err = torch.empty(2 * len(pa), dtype=torch.float64, device=dev)
+        T = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dtype=dt)).to(dev)
+        _lib.check(lib.pgw_pf_od_resp_check(M, 2 * len(pa), self._od_resp.data_ptr(),
+                                            T(np.repeat(prec, 2), np.int32).data_ptr(), T(chk.ravel(), np.float64).data_ptr(),
+                                            Jc.data_ptr(), T(c_l.ravel(), np.int32).data_ptr(), err.data_ptr(), st))
+        e_ = err.cpu().numpy().reshape(-1, 2).max(1)
+        bad = (pit != 0) & ((e_ > self.OD_RESP_TOL) | (sc[c_l] != psig[:, None]).any(1) | ~np.isfinite(e_))
+        if bad.any():                                       # left to the solve
+            words = np.array([self._od_meta_word(0, int(nx)) for nx in pnext[bad]], np.int64)
+            self._od_resp.view(-1, R).view(torch.int64)[torch.from_numpy(prec[bad]).to(dev), 4] = \
+                torch.from_numpy(words).to(dev)
+        ok = (pit != 0) & ~bad
+        # the brackets per hour (kW intervals the tables leave to the solve), for tests and diagnostics
+        for q, hr in enumerate(hours):
+            self.od_resp_brackets[hr] = np.array(sorted((lo_, hi_) for (i, lo_, hi_, _, _) in done + gaps
+                                                        if dq[i] == q)).reshape(-1, 2)
+        st_ = self.od_resp_stats
+        st_["hours"] = st_.get("hours", 0) + H
+        st_["segments_with_breakpoints"] = st_.get("segments_with_breakpoints", 0) + len(dq)
+        st_["brackets"] = st_.get("brackets", 0) + len(done)
+        st_["unresolved_brackets"] = st_.get("unresolved_brackets", 0) + len(gaps)
+        st_["pieces"] = st_.get("pieces", 0) + int(ok.sum())
+        st_["pieces_left_to_solve"] = st_.get("pieces_left_to_solve", 0) + int((~ok).sum())
+        st_["max_fit_err"] = max(st_.get("max_fit_err", 0.0), float(e_[ok].max()) if ok.any() else 0.0)
+        st_["build_s"] = st_.get("build_s", 0.0) + (_time.perf_counter() - t_start)
+
         key = (hour, self._cfg_version)
         t = self._tables_cache.get(key)
         if t is not None:
@@ -323,6 +564,9 @@ class OpenDSSSolver(PowerFlowSolver):
             idx = self._od_index[self._hour_key(hour)]
         od = _lib.PFOD.from_buffer_copy(self._od_proto)
         od.start = self._od_start[idx].data_ptr()
+        if self.od_table and self._od_resp is not None:
+            od.resp = self._od_resp[idx].data_ptr()
+            od.resp_x0, od.resp_h, od.resp_nseg = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N - 1
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.od = _lib.C.addressof(od)
         t._od_ref = od                     # the struct lives as long as these tables

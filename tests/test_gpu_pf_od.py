@@ -208,3 +208,110 @@ def test_od_c4_two_episodes_tiled_full_batch():
         err = err.cpu().numpy()
         assert err[0] <= 1 and err[1] < 1e-11 and err[2] < 1e-10 and err[3] == 0, (e, err)
     assert hist[3] + hist[4] > 0, hist
+
+
+# ------------------------------------------------------------------ response table (pgw_pf_od.resp)
+def _served(s, hour, P):
+    """The envs whose (P, Q = 0) the hour's response table serves: the kernels'
+    lookup (od_resp_lookup) restated on the host from the downloaded records."""
+    from powergridworld_amd import _lib
+    idx = s._od_index[s._hour_key(hour)]
+    recs = s._od_resp[idx].cpu().numpy()
+    words = recs[:, 4].copy().view(np.int64)
+    its, nxt = (words & 0xffffffff).astype(np.int64), words >> 32
+    nseg = s.PREDICTOR_N - 1
+    out = np.zeros(len(P), bool)
+    g = (P - s.PREDICTOR_X0) * (1.0 / s.PREDICTOR_H)
+    for e, (p, gg) in enumerate(zip(P, g)):
+        if not (0.0 <= gg < nseg):
+            continue
+        r = int(gg)
+        for _ in range(8):
+            if recs[r, 0] <= p <= recs[r, 1]:
+                out[e] = its[r] != 0
+                break
+            if nxt[r] < 0:
+                break
+            r = int(nxt[r])
+    assert recs.shape[1] == _lib.od_rec(s.M)
+    return out
+
+
+def test_od_response_table_equals_solve():
+    """The response table against every env solved (od_table=False) at the
+    BASELINE batch, over the whole kW grid and right beside every breakpoint
+    bracket (1e-9 .. 1e-3 kW off either end): the same iteration count for
+    every env, every node within 1e-11 rel (the fit is checked at 2e-11 on the
+    currents); the table serves all but the brackets' envs; the build's
+    statistics are sane (no unresolved bracket, fit error within tolerance)."""
+    K = 65536
+    tab, sol = _solver(num_envs=K), _solver(num_envs=K, od_table=False)
+    rng = np.random.default_rng(7)
+    zero = torch.zeros(K, dtype=torch.float64, device=DEV)
+    for t in TIMES:
+        # builds the hour's tables (24 hours ahead) for the controllable slot
+        tab.calculate_power_flow({"675c": zero}, None, current_time=t)
+        hour = tab.hour_of(t)
+        br = tab.od_resp_brackets[hour]
+        assert len(br) > 0
+        near = np.concatenate([br[:, 0] - d for d in (1e-9, 1e-6, 1e-3)] + [br[:, 1] + d for d in (1e-9, 1e-6, 1e-3)]
+                              + [0.5 * (br[:, 0] + br[:, 1])])
+        P = np.concatenate([rng.uniform(-520.0, 1520.0, K - len(near)), near])
+        v = []
+        for s_ in (tab, sol):
+            s_.calculate_power_flow({"675c": torch.tensor(P, device=DEV)}, None, current_time=t)
+            bv = s_.get_bus_voltages()
+            v.append((torch.stack([bv[nm] for nm in s_.feeder.node_names]).clone(), s_.iterations.clone()))
+        torch.cuda.synchronize()
+        (vt, it_t), (vs, it_s) = v
+        assert torch.equal(it_t, it_s), int((it_t != it_s).sum())
+        rel = ((vt - vs).abs() / vs.abs()).max().item()
+        assert rel < 1e-11, rel
+        served = _served(tab, hour, P)
+        inside = (P >= tab.PREDICTOR_X0) & (P < tab.PREDICTOR_X0 + (tab.PREDICTOR_N - 1) * tab.PREDICTOR_H)
+        assert served[: K - len(near)][inside[: K - len(near)]].mean() > 0.999
+        assert not served[-len(br):].any()                # bracket midpoints: the solve
+    st = tab.od_resp_stats
+    assert st["unresolved_brackets"] == 0 and st["max_fit_err"] <= tab.OD_RESP_TOL, st
+    assert st["pieces_left_to_solve"] <= 0.01 * st["pieces"], st
+
+
+def test_od_response_table_bit_identical_paths():
+    """The fused C4 step, the generic path and the all-node solve read the same
+    table records with the same operations: fused == generic bit for bit over a
+    stretch of an episode with the table serving, and the fused step with the
+    table off (every env solved) equals the oracle as the table does."""
+    from oracle.ma_oracle import CoordinatedOracle
+    from oracle.pf_oracle import BatchedPF
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    n = 1024
+    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=f)
+            for f in (True, False, True)]
+    envs[2].pf_solver.od_table = False
+    rng = np.random.default_rng(13)
+    init = rng.uniform(5.0, 45.0, size=(5, n))
+    for env in envs:
+        env.reset()
+        for ai, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=torch.tensor(init[ai], device=DEV))
+    ora = CoordinatedOracle(n)
+    ora.pf = BatchedPF(system_load_rescale_factor=1.2, semantics="opendss")
+    ora.reset(init)
+    for t in range(60):
+        act = rng.uniform(-1, 1, size=(5, n, 8))
+        a_t = torch.tensor(act, device=DEV)
+        outs = [envs[0].step(a_t),
+                envs[1].step({a.name: {"building": a_t[i, :, :6], "pv": a_t[i, :, 6:7], "storage": a_t[i, :, 7:8]}
+                              for i, a in enumerate(envs[1].agents)}),
+                envs[2].step(a_t)]
+        _, o_rew, o_vv = ora.step(act)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][3]["voltage_violation"], outs[1][3]["voltage_violation"])
+        for a in envs[0].agents:
+            assert torch.equal(outs[0][1][a.name], outs[1][1][a.name])
+        for env in envs:
+            np.testing.assert_array_equal(env.pf_solver.iterations.cpu().numpy(), ora.pf.last_iters)
+            np.testing.assert_allclose(env.pf_solver.get_bus_voltage_by_name("675c").cpu().numpy(), ora.v,
+                                       rtol=1e-10, atol=0)
+    for nm in ("632.1", "671.2", "652.1", "675.3"):
+        assert torch.equal(envs[0].voltages[nm], envs[1].voltages[nm])

@@ -72,7 +72,9 @@ def _oracle(case, exo):
     else:
         agents = [("building", "675c", mc()), ("ev-charging", "675c", EVOracle(K, **EV_CFG)),
                   ("pv", "675c", PVOracle(K, "pv_profile.csv", 400.))]
-    return MultiAgentOracle(K, agents, 0.7, COMMON["start_time"], COMMON["end_time"])
+    # the engine's pf_config names no stopping rule: OpenDSS's snap solve, the
+    # reference's (opendss.py:131-135) and the solver's default
+    return MultiAgentOracle(K, agents, 0.7, COMMON["start_time"], COMMON["end_time"], semantics="opendss")
 
 
 def _policy(space, kind, rng):

@@ -1,6 +1,7 @@
-"""C4 at 65,536 envs: exact fixed point vs OpenDSS rule (fast kernels) vs
-OpenDSS rule (general kernel) -- us/step over a driver-shaped region and the
-PF kernel's event-timed mean.  Usage: python tools/gpu/od_probe.py [--steps 200]"""
+"""C4 at 65,536 envs: exact fixed point vs OpenDSS rule (fast kernels, with
+the response table or -- opendss_notable -- every env solved) vs OpenDSS rule
+(general kernel) -- us/step over a driver-shaped region and the PF kernel's
+event-timed mean.  Usage: python tools/gpu/od_probe.py [--steps 200]"""
 import argparse
 import os
 import sys
@@ -15,7 +16,7 @@ from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingCon
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--n", type=int, default=65536)
-ap.add_argument("--modes", default="exact,opendss,opendss_general")
+ap.add_argument("--modes", default="exact,opendss,opendss_notable,opendss_general")
 ap.add_argument("--max-iter", type=int, default=0, help="opendss only: cap the iterations (results "
                                                           "change), for the per-iteration cost")
 ap.add_argument("--nobound", action="store_true", help="opendss only: zero bound constants (timing only)")
@@ -33,6 +34,8 @@ for mode in a.modes.split(","):
     conv = "exact" if mode == "exact" else "opendss"
     env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv, pf_general=mode.endswith("general")),
                                              num_envs=n, device=dev, fused=True)
+    if mode == "opendss_notable":
+        env.pf_solver.od_table = False
     if a.rows and mode == "opendss":
         od = env.pf_solver._od_proto
         od.n_rep = 0 if a.rows == "none" else od.n_rows
@@ -98,5 +101,7 @@ for mode in a.modes.split(","):
         ("/nobound" if a.nobound and mode == "opendss" else "")
     print("%-16s %7.2f us/step  kernels %s  iters mean %.3f max %d  kernel=%s" %
           (tag, us, ks, it.double().mean().item(), it.max().item(), env._fused["kernel"]), flush=True)
+    if getattr(env.pf_solver, "od_resp_stats", None):
+        print("  response tables: %s" % env.pf_solver.od_resp_stats, flush=True)
     del env
     torch.cuda.synchronize()
