@@ -494,17 +494,21 @@ class OpenDSSSolver(PowerFlowSolver):
             prev[(q, j)] = k
         row = (idx0 + np.arange(H)).astype(np.int64)
 
+        T = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dtype=dt)).to(dev)
+
         def fit(Jbuf, lanes3, a, b, it_, nxt, recs_global):
             n_ = len(a)
             if n_ == 0:
                 return
             meta = np.stack([a, b, 0.5 * (a + b), 2.0 / (b - a)], 1)
             inext = np.stack([it_, nxt], 1).astype(np.int32)
-            T = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dtype=dt)).to(dev)
-            _lib.check(lib.pgw_pf_od_resp_fit(M, n_, Jbuf.data_ptr(), T(lanes3, np.int32).data_ptr(),
-                                              T(meta, np.float64).data_ptr(), T(inext, np.int32).data_ptr(),
-                                              T(recs_global, np.int32).data_ptr(), self._od_resp.data_ptr(), st))
-            torch.cuda.synchronize(dev)
+            # (held by name until the kernel has run: a temporary's block could be
+            # handed to the next allocation before the launch reads it)
+            d3, dm, dn, dr = T(lanes3, np.int32), T(meta, np.float64), T(inext, np.int32), T(recs_global, np.int32)
+            _lib.check(lib.pgw_pf_od_resp_fit(M, n_, Jbuf.data_ptr(), d3.data_ptr(), dm.data_ptr(), dn.data_ptr(),
+                                              dr.data_ptr(), self._od_resp.data_ptr(), st))
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
 
         c_lanes = og[cq][:, None] + 2 * cj[:, None] + np.arange(3)[None, :]
         c_rec = row[cq] * rec_n + cj
@@ -529,11 +533,11 @@ class OpenDSSSolver(PowerFlowSolver):
         for q, o in enumerate(order):
             c_l[o] = oc[q] + np.arange(2 * len(o)).reshape(-1, 2)
         err = torch.empty(2 * len(pa), dtype=torch.float64, device=dev)
-        T = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dtype=dt)).to(dev)
-        _lib.check(lib.pgw_pf_od_resp_check(M, 2 * len(pa), self._od_resp.data_ptr(),
-                                            T(np.repeat(prec, 2), np.int32).data_ptr(), T(chk.ravel(), np.float64).data_ptr(),
-                                            Jc.data_ptr(), T(c_l.ravel(), np.int32).data_ptr(), err.data_ptr(), st))
+        dr, dp, dq_ = T(np.repeat(prec, 2), np.int32), T(chk.ravel(), np.float64), T(c_l.ravel(), np.int32)
+        _lib.check(lib.pgw_pf_od_resp_check(M, 2 * len(pa), self._od_resp.data_ptr(), dr.data_ptr(), dp.data_ptr(),
+                                            Jc.data_ptr(), dq_.data_ptr(), err.data_ptr(), st))
         e_ = err.cpu().numpy().reshape(-1, 2).max(1)
+        del dr, dp, dq_
         bad = (pit != 0) & ((e_ > self.OD_RESP_TOL) | (sc[c_l] != psig[:, None]).any(1) | ~np.isfinite(e_))
         if bad.any():                                       # left to the solve
             words = np.array([self._od_meta_word(0, int(nx)) for nx in pnext[bad]], np.int64)
@@ -554,6 +558,7 @@ class OpenDSSSolver(PowerFlowSolver):
         st_["max_fit_err"] = max(st_.get("max_fit_err", 0.0), float(e_[ok].max()) if ok.any() else 0.0)
         st_["build_s"] = st_.get("build_s", 0.0) + (_time.perf_counter() - t_start)
 
+    def _od_tables(self, hour):
         key = (hour, self._cfg_version)
         t = self._tables_cache.get(key)
         if t is not None:

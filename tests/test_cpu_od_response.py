@@ -1,0 +1,199 @@
+"""The response-table builder's host logic (OpenDSSSolver._od_response,
+pgw_pf_od.resp) on the CPU: the device probe, fit and fit check are replaced
+by NumPy restatements (the oracle's snap solve, oracle/pf_oracle.py
+Feeder.snap_opendss's iteration, for the probe), so the bookkeeping -- the
+grid, the signature brackets and their bisection, the pieces, the record
+chains, the check-point rejection -- is checked without a GPU: every kW the
+table serves must give the probe's currents and iteration count; the table
+must serve everything but the brackets.  (The GPU tests in
+tests/test_gpu_pf_od.py check the device path against the solve itself.)"""
+import ctypes
+import datetime
+
+import numpy as np
+import pytest
+import torch
+
+IEEE13 = "ieee_13_dss/IEEE13Nodeckt.dss"
+SHAPE = "ieee_13_dss/annual_hourly_load_profile.csv"
+HOURS = (5403, 5411)             # 08-12 03:00 and 11:00 (a C4 episode's day)
+
+
+def _arr(ptr, n, ct):
+    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), shape=(n,))
+
+
+class _Oracle:
+    """Snap solve of the oracle's feeder at the solver's hourly loads: the
+    accepted iteration's compensation currents in the kernels' units
+    (I' = (I_load - Yeq U) vb per element), the iteration count and a hash of
+    the count and every iterate's load bands -- the probe's outputs."""
+
+    def __init__(self, solver):
+        from oracle.pf_oracle import BatchedPF, _accurate_inverse
+        self.pf = BatchedPF(system_load_rescale_factor=solver.system_load_rescale_factor, semantics="opendss")
+        f = self.f = self.pf.feeder
+        C = f.Cinc
+        self.yeq = (f.base_kw[f.elem_load] * 1000.0 / f.elem_nph -
+                    1j * f.base_kvar[f.elem_load] * 1000.0 / f.elem_nph) / f.elem_vbase ** 2
+        self.Z1 = _accurate_inverse(f.Y + C.T @ np.diag(self.yeq) @ C)
+        self.vmin = np.array(f.load_vmin)[f.elem_load]
+        self.vmax = np.array(f.load_vmax)[f.elem_load]
+        self.vlow = np.array(f.load_vlow)[f.elem_load]
+
+    def __call__(self, hour, P):
+        f, C = self.f, self.f.Cinc
+        ts = datetime.datetime(2021, 1, 1) + datetime.timedelta(hours=hour)
+        kw, kvar = self.pf.loads(ts, {"675c": P}, None, K=len(P))
+        W_ph = kw[:, f.elem_load] * 1000.0 / f.elem_nph
+        var_ph = kvar[:, f.elem_load] * 1000.0 / f.elem_nph
+        K = len(P)
+        V = np.tile(self.Z1 @ f.I_src, (K, 1))
+        vbn = f.kv_ln * 1000.0
+        active = np.ones(K, bool)
+        iters = np.zeros(K, np.int64)
+        sig = np.full(K, 0xcbf29ce484222325, np.uint64)
+        Jacc = np.zeros((K, C.shape[0]), complex)
+        prime = np.uint64(0x100000001b3)
+        for it in range(1, 16):
+            U = V @ C.T
+            if it >= 2:
+                m = np.abs(U) / f.elem_vbase
+                b = ((m > self.vlow).astype(np.uint64) + (m > self.vmin) + (m > self.vmax)).astype(np.uint64)
+                bands = (b << (2 * np.arange(C.shape[0], dtype=np.uint64))).sum(1).astype(np.uint64)
+                sig = np.where(active, (sig ^ bands) * prime, sig)
+            Jl = self.yeq * U - f.load_currents(U, W_ph, var_ph)
+            Vn = (f.I_src + Jl @ C) @ self.Z1.T
+            err = np.max(np.abs(np.abs(Vn) - np.abs(V)) / vbn, axis=1)
+            Jacc = np.where(active[:, None], Jl, Jacc)
+            V = np.where(active[:, None], Vn, V)
+            iters[active] = it
+            active &= ~((err <= 1e-4) & (it >= 2))
+            if not active.any():
+                break
+        conv = ~active
+        ret = np.where(conv, iters, -iters)
+        sig = (sig ^ ret.astype(np.int64).astype(np.uint32).astype(np.uint64)) * prime
+        return -Jacc * f.elem_vbase, sig, ret.astype(np.int32)
+
+
+@pytest.fixture()
+def cpu_solver(monkeypatch):
+    from powergridworld_amd import _lib
+    from powergridworld_amd.distribution_system import opendss
+    monkeypatch.setattr(_lib, "require_device", lambda device=None: torch.device("cpu"))
+    monkeypatch.setattr(_lib, "stream_ptr", lambda device=None: None)
+    s = opendss.OpenDSSSolver(IEEE13, SHAPE, system_load_rescale_factor=1.2, num_envs=4)
+    assert s._od_fast and s.M == s.feeder.m == 14
+    s.PREDICTOR_LOOKAHEAD = 2                      # two hours per build (the NumPy probe is slow)
+    s.set_controllable_loads(["675c"])
+    orc = _Oracle(s)
+    bufs = {}
+
+    def probe(hours, idx0, pts):
+        M, H = s.M, len(hours)
+        lph = max(256, -(-max(len(p) for p in pts) // 256) * 256)
+        J = np.zeros((H * lph, M), complex)
+        sig = np.zeros(H * lph, np.uint64)
+        it = np.zeros(H * lph, np.int32)
+        for q, (hr, p) in enumerate(zip(hours, pts)):
+            if len(p):
+                j_, s_, i_ = orc(hr, np.asarray(p, float))
+                J[q * lph:q * lph + len(p)], sig[q * lph:q * lph + len(p)], it[q * lph:q * lph + len(p)] = j_, s_, i_
+        Jt = torch.from_numpy(np.ascontiguousarray(np.stack([J.real, J.imag], -1)))
+        bufs[Jt.data_ptr()] = Jt
+        return Jt, sig, it, np.arange(H) * lph
+
+    real = _lib.lib()
+
+    class Lib:
+        def __getattr__(self, name):
+            return getattr(real, name)
+
+        @staticmethod
+        def pgw_pf_od_resp_fit(m, n, J, idx3, meta, inext, rec, out, stream):
+            Jb = bufs[J].numpy().reshape(-1, m, 2)
+            i3 = _arr(idx3, 3 * n, ctypes.c_int32).reshape(n, 3)
+            mt = _arr(meta, 4 * n, ctypes.c_double).reshape(n, 4)
+            nx = _arr(inext, 2 * n, ctypes.c_int32).reshape(n, 2)
+            rc = _arr(rec, n, ctypes.c_int32)
+            R = _lib.od_rec(m)
+            o = s._od_resp.numpy().reshape(-1, R)
+            o[rc, :4] = mt
+            o.view(np.int64)[rc, 4] = (nx[:, 0].astype(np.int64) & 0xffffffff) | (nx[:, 1].astype(np.int64) << 32)
+            a, md, b = Jb[i3[:, 0]], Jb[i3[:, 1]], Jb[i3[:, 2]]
+            c = o[rc, 6:].reshape(n, 3, m, 2)
+            c[:, 0], c[:, 1], c[:, 2] = md, 0.5 * (b - a), 0.5 * (a + b) - md
+            o[rc, 6:] = c.reshape(n, -1)
+            return 0
+
+        @staticmethod
+        def pgw_pf_od_resp_check(m, n, recs, rec, P, J, iq, err, stream):
+            R = _lib.od_rec(m)
+            o = s._od_resp.numpy().reshape(-1, R)
+            rc = _arr(rec, n, ctypes.c_int32)
+            p = _arr(P, n, ctypes.c_double)
+            Jb = bufs[J].numpy().reshape(-1, m, 2)[_arr(iq, n, ctypes.c_int32)]
+            t = (p - o[rc, 2]) * o[rc, 3]
+            c = o[rc, 6:].reshape(n, 3, m, 2)
+            f = c[:, 0] + t[:, None, None] * (c[:, 1] + t[:, None, None] * c[:, 2])
+            num = np.abs((f - Jb)[..., 0] + 1j * (f - Jb)[..., 1]).max(1)
+            den = np.abs(Jb[..., 0] + 1j * Jb[..., 1]).max(1)
+            _arr(err, n, ctypes.c_double)[:] = num / den
+            return 0
+
+    monkeypatch.setattr(_lib, "lib", lambda: Lib())
+    monkeypatch.setattr(s, "_od_probe", probe)
+    return s, orc
+
+
+def _lookup(s, hour, P):
+    """The kernels' lookup restated: (served, J', iterations) per kW."""
+    from powergridworld_amd import _lib
+    R = _lib.od_rec(s.M)
+    recs = s._od_resp[s._od_index[s._hour_key(hour)]].numpy()
+    words = recs[:, 4].copy().view(np.int64)
+    its, nxt = (words & 0xffffffff).astype(np.int32), words >> 32
+    nseg = s.PREDICTOR_N - 1
+    g = (P - s.PREDICTOR_X0) * (1.0 / s.PREDICTOR_H)
+    served = np.zeros(len(P), bool)
+    J = np.zeros((len(P), s.M), complex)
+    it = np.zeros(len(P), np.int32)
+    for e, (p, gg) in enumerate(zip(P, g)):
+        if not 0.0 <= gg < nseg:
+            continue
+        r = int(gg)
+        for _ in range(8):
+            if recs[r, 0] <= p <= recs[r, 1]:
+                if its[r] != 0:
+                    t = (p - recs[r, 2]) * recs[r, 3]
+                    c = recs[r, 6:R].reshape(3, s.M, 2)
+                    v = c[0] + t * (c[1] + t * c[2])
+                    served[e], J[e], it[e] = True, v[:, 0] + 1j * v[:, 1], its[r]
+                break
+            if nxt[r] < 0:
+                break
+            r = int(nxt[r])
+    return served, J, it
+
+
+def test_response_table_builder_against_the_solve(cpu_solver):
+    s, orc = cpu_solver
+    s._od_tables(HOURS[0])                         # builds HOURS[0] and the next hour
+    st = s.od_resp_stats
+    print("response-table build (NumPy probe):", st)
+    assert st["hours"] == 2 and st["unresolved_brackets"] == 0, st
+    assert st["max_fit_err"] <= s.OD_RESP_TOL and st["pieces_left_to_solve"] <= 0.01 * st["pieces"], st
+    rng = np.random.default_rng(3)
+    for hour in (HOURS[0], HOURS[0] + 1):
+        br = s.od_resp_brackets[hour]
+        assert len(br) > 5 and (br[:, 1] - br[:, 0] < 1e-8).all()
+        near = np.concatenate([br[:, 0] - 1e-7, br[:, 1] + 1e-7, 0.5 * (br[:, 0] + br[:, 1])])
+        P = np.concatenate([rng.uniform(-500.0, 1499.9, 4000), near])
+        served, J, it = _lookup(s, hour, P)
+        Jo, _, ito = orc(hour, P)
+        assert served[:4000].mean() > 0.995 and served[4000:4000 + 2 * len(br)].all()
+        assert not served[-len(br):].any()             # inside a bracket: the solve
+        np.testing.assert_array_equal(it[served], ito[served])
+        rel = np.abs(J[served] - Jo[served]).max(1) / np.abs(Jo[served]).max(1)
+        assert rel.max() < 1e-10, rel.max()
