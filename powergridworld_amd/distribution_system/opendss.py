@@ -544,9 +544,10 @@ class OpenDSSSolver(PowerFlowSolver):
             self._od_resp.view(-1, R).view(torch.int64)[torch.from_numpy(prec[bad]).to(dev), 4] = \
                 torch.from_numpy(words).to(dev)
         ok = (pit != 0) & ~bad
-        # the brackets per hour (kW intervals the tables leave to the solve), for tests and diagnostics
+        # the brackets per table row (kW intervals the tables leave to the solve;
+        # an hour's row: _od_index[_hour_key(hour)]), for tests and diagnostics
         for q, hr in enumerate(hours):
-            self.od_resp_brackets[hr] = np.array(sorted((lo_, hi_) for (i, lo_, hi_, _, _) in done + gaps
+            self.od_resp_brackets[idx0 + q] = np.array(sorted((lo_, hi_) for (i, lo_, hi_, _, _) in done + gaps
                                                         if dq[i] == q)).reshape(-1, 2)
         st_ = self.od_resp_stats
         st_["hours"] = st_.get("hours", 0) + H

@@ -186,7 +186,7 @@ def test_response_table_builder_against_the_solve(cpu_solver):
     assert st["max_fit_err"] <= s.OD_RESP_TOL and st["pieces_left_to_solve"] <= 0.01 * st["pieces"], st
     rng = np.random.default_rng(3)
     for hour in (HOURS[0], HOURS[0] + 1):
-        br = s.od_resp_brackets[hour]
+        br = s.od_resp_brackets[s._od_index[s._hour_key(hour)]]
         assert len(br) > 5 and (br[:, 1] - br[:, 0] < 1e-8).all()
         near = np.concatenate([br[:, 0] - 1e-7, br[:, 1] + 1e-7, 0.5 * (br[:, 0] + br[:, 1])])
         P = np.concatenate([rng.uniform(-500.0, 1499.9, 4000), near])

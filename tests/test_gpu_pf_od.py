@@ -252,7 +252,7 @@ def test_od_response_table_equals_solve():
         # builds the hour's tables (24 hours ahead) for the controllable slot
         tab.calculate_power_flow({"675c": zero}, None, current_time=t)
         hour = tab.hour_of(t)
-        br = tab.od_resp_brackets[hour]
+        br = tab.od_resp_brackets[tab._od_index[tab._hour_key(hour)]]
         assert len(br) > 0
         near = np.concatenate([br[:, 0] - d for d in (1e-9, 1e-6, 1e-3)] + [br[:, 1] + d for d in (1e-9, 1e-6, 1e-3)]
                               + [0.5 * (br[:, 0] + br[:, 1])])
