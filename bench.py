@@ -66,19 +66,36 @@ PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 OD_REP_ROWS = 11
 OD_FLOPS_ITER = 8 * M_ELEM ** 2 + 14 * M_ELEM + 6 * M_ELEM
 OD_FLOPS_ENV = 16 * M_ELEM + 2 * OD_REP_ROWS * (8 * M_ELEM + 4) + 18 * M_ELEM + 8 * M_ELEM + 4 + 10
+# k_coord_pf_od with the hour's response table (pgw_pf_od.resp): per env one
+# record (PGW_OD_REC(14) = 90 doubles, 720 B, L2-resident: 2.3 MB per hour), the
+# quadratic of 2 m currents (2 FMAs each), the output row (8 m + 4) and the reward
+OD_TABLE_REC_BYTES = 8 * (6 + 6 * M_ELEM)
+OD_TABLE_FLOPS_ENV = 4 * 2 * M_ELEM + 8 * M_ELEM + 4 + 10
 PF_KERNEL_NAME = {"exact": "k_coord_pf<14,true,false,false>", "opendss": "k_coord_pf_od<14>"}
+# (k_coord_pf_od<14>: with the hour's response table, pgw_pf_od.resp, the default)
 PF_KERNEL = "k_coord_pf"              # PGW_T_COORD_PF: whichever PF kernel the step's mode runs
 
 
-def pf_roofline(conv, avg_us, mean_it, n):
-    """Achieved fp64 TF/s of the step's PF kernel from its algorithmic flops."""
+def pf_roofline(conv, avg_us, mean_it, n, table=False):
+    """The step's PF kernel against its bound.  Exact fixed point: fp64 VALU, on
+    its algorithmic flops.  OpenDSS rule with the response table: a latency
+    chain (agent powers from HBM -> the env's record from L2 -> the reward
+    atomics), reported as HBM GB/s of its algorithmic bytes with the record bytes
+    and flops beside; without the table (od_table=False): fp64 VALU."""
+    if conv == "opendss" and table:
+        gbs = PF_BYTES * n / (avg_us * 1e-6) / 1e9
+        return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                "note": "latency-bound: HBM agent powers -> one %d-byte response-table record per env "
+                        "(L2, %.1f GB/s of record gather) -> output row, reward atomics"
+                        % (OD_TABLE_REC_BYTES, OD_TABLE_REC_BYTES * n / (avg_us * 1e-6) / 1e9),
+                "flops_per_env": OD_TABLE_FLOPS_ENV, "l2_bytes_per_env": OD_TABLE_REC_BYTES}
     if conv == "exact":
         flops = PF_FLOPS_ITER * mean_it + PF_FLOPS_ENV
     else:
         flops = OD_FLOPS_ITER * max(mean_it - 1.0, 0.0) + OD_FLOPS_ENV
     tfs = flops * n / (avg_us * 1e-6) / 1e12
-    return {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
-            "flops_per_env": flops}
+    return {"bound": "fp64 valu", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tfs / FP64_PEAK_TFS, "flops_per_env": flops}
 
 
 KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "(unused)", "k_ma_step", "k_pf_general")
@@ -204,14 +221,15 @@ def pf_variant(conv, n, steps, warmup, pool, dev):
     tot, cnt = timed_pass(run, 64)
     it = env.pf_solver.iterations.abs().double()
     p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
+    table = conv == "opendss" and env.pf_solver.od_table
     out = {"pf_convergence": conv, "value": N_AGENTS * n * steps / dt, "unit": "agent-env-steps/s",
            "ms_per_step": dt / steps * 1e3, "steps": steps, "pf_iterations_mean": float(it.mean()),
            "pf_iterations_max": int(it.max()),
            "k_coord_agents_std_avg_us": tot[0] / cnt[0] * 1e3 if cnt[0] else None,
            "pf_kernel": {"name": PF_KERNEL_NAME[conv] if env.pf_solver._od_fast or conv == "exact"
-                         else "k_pf_general", "avg_us": p_us, "bound": "fp64 valu"}}
+                         else "k_pf_general", "avg_us": p_us}}
     if p_us:
-        out["pf_kernel"].update(pf_roofline(conv, p_us, float(it.mean()), n))
+        out["pf_kernel"].update(pf_roofline(conv, p_us, float(it.mean()), n, table))
     del env
     return out
 
@@ -459,12 +477,24 @@ def main():
                                    "traffic": traffic.get(KERNELS[0])}
         if p_us:
             pk = PF_KERNEL_NAME[conv]
-            kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1], "bound": "fp64 valu",
-                           "note": "fp64 VALU DPP FMAs, no MFMA (MI355X fp64 vector peak = matrix "
-                                   "peak); issue-bound, one wave per SIMD at 65,536 envs",
+            table = conv == "opendss" and env.pf_solver.od_table
+            kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1],
+                           "note": ("the hour's response table serves every env whose kW lies in a fitted "
+                                    "piece, the snap solve (fp64 VALU DPP FMAs) the rest" if table else
+                                    "fp64 VALU DPP FMAs, no MFMA (MI355X fp64 vector peak = matrix peak); "
+                                    "issue-bound, one wave per SIMD at 65,536 envs"),
                            "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
                            "traffic": traffic.get(pk)}
-            kernels[pk].update(pf_roofline(conv, p_us, mean_it, n))
+            kernels[pk].update(pf_roofline(conv, p_us, mean_it, n, table))
+            if table:
+                st = dict(env.pf_solver.od_resp_stats)
+                kernels[pk]["response_table"] = {
+                    k: st.get(k) for k in ("hours", "segments_with_breakpoints", "brackets", "unresolved_brackets",
+                                           "pieces", "pieces_left_to_solve", "max_fit_err", "build_s")}
+                kernels[pk]["response_table"]["note"] = (
+                    "built on the device by the snap solve itself (pgw_pf_od_probe) about once per 24 "
+                    "simulated hours, cached across episodes (every episode repeats the hours); build_s "
+                    "is the whole build time of this run, outside the timed region")
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "

@@ -7,7 +7,9 @@ with actions resident in HBM (a pool of pre-generated batches); episodes reset
 inside the timed region.  One JSON line per config.
 
 Usage: python tools/bench_configs.py [--configs C2,C3,HET,HETG,HS,...] [--steps K] [--warmup W]
-(HETG: the heterogeneous scenario on the generic path, fused=False; C3F / C3G8F:
+(HET: OpenDSS's snap-solve rule, the default, with its response table; HETS:
+every env solved; HETX: the exact fixed point; HETG: the heterogeneous scenario
+on the generic path, fused=False; C3F / C3G8F:
 C3 with fp32 storage (pgw_mc_agent_step_f32); C3L: C3 at
 65 536 envs; C2Gk / C3Gk: the step replayed from captured hipGraphs of k steps,
 C3 through the device clocks; C3Pk / HSPk: captured once per episode position,
@@ -142,10 +144,11 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True, dtype=
                 batch=n, agents=1, steps=steps, seconds=dt)
 
 
-def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto"):
+def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss", table=True):
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     from powergridworld_amd.multiagent_env import MultiAgentEnv
-    env = MultiAgentEnv(**make_env_config(), num_envs=n, device=dev, fused=fused)
+    env = MultiAgentEnv(**make_env_config(pf_convergence=conv), num_envs=n, device=dev, fused=fused)
+    env.pf_solver.od_table = table
     gen = torch.Generator(dev).manual_seed(0)
     acts = []
     for _ in range(pool):
@@ -163,9 +166,10 @@ def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto"):
         return dones["__all__"]
 
     dt = timed_loop(env, step, env.reset, steps, warmup)
-    return dict(config="HET" if fused else "HETG",
+    return dict(config=("HET" if fused else "HETG") + ("X" if conv == "exact" else "") + ("" if table else "S"),
                 workload="3-agent heterogeneous (MC building, grid-aware PV farm, EV 25x40) + IEEE-13 PF, "
                          + ("fused multi-agent step (pgw_ma_step)" if env._ma is not None else "generic path"),
+                pf_convergence=conv, pf_response_table=bool(table and conv == "opendss"),
                 batch=n, agents=3, steps=steps, seconds=dt)
 
 
@@ -212,6 +216,8 @@ def main():
     torch.cuda.set_device(dev)
     fns = {"C2": bench_c2, "C3": bench_c3, "HET": bench_het, "HS": bench_hs,
            "HETG": lambda *a: bench_het(*a, fused=False),
+           "HETX": lambda *a: bench_het(*a, conv="exact"),
+           "HETS": lambda *a: bench_het(*a, table=False),
            "C2G1": lambda *a: bench_c2(*a, graph=1), "C2G8": lambda *a: bench_c2(*a, graph=8),
            "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8),
            "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),
