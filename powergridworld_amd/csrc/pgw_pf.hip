@@ -1593,6 +1593,48 @@ __device__ __forceinline__ void od_fallback(PFSolver<M, true, false>& S, const O
   it = need ? its : it;
 }
 
+// Output rows 1.. of the OpenDSS-rule kernels, staged in the LDS the solve
+// leaves idle once the block is past it: od_rows_issue loads a row entry per
+// lane and slot (a fixed count, clamped in-bounds addresses, all in flight
+// with the prologue's loads), od_rows_put stores them in pf_rows_out's resident
+// row layout, whose DPP row groups then evaluate the rows (the exact kernels'
+// path; per row pf_node_pu's operations, so every node is bit-identical
+// whichever kernel and row computes it).
+constexpr int kOdRowQ = kRowsLds / kBlock;
+template <int M>
+__device__ __forceinline__ bool od_rows_lds(int n_out) {
+  return n_out > 1 && n_out * 16 * PFRow<M>::kPairs <= kRowsLds;
+}
+template <int M>
+__device__ __forceinline__ void od_rows_issue(const pgw_pf_tables& t, int n_out, double (&v)[kOdRowQ]) {
+  constexpr int S = 16 * PFRow<M>::kPairs;
+  const int total = n_out * S;
+#pragma unroll
+  for (int q = 0; q < kOdRowQ; ++q) {
+    const int i = threadIdx.x + q * kBlock;
+    const int o = i / S, j = i - o * S;
+    const bool has = i < total && j < 2 + 2 * M;
+    const int oc = min(o, max(n_out - 1, 0)), jc = min(j, 1 + 2 * M);
+    const double* p = jc < 2 ? t.V0 + (2 * oc + jc)
+                             : t.G + (2 * M * oc + (jc < 2 + M ? 2 * (jc - 2) : 2 * (jc - 2 - M) + 1));
+    v[q] = has ? *p : 0.0;
+  }
+}
+template <int M>
+__device__ __forceinline__ double* od_rows_put(ODShared<M>& sh, int n_out, const double (&v)[kOdRowQ]) {
+  static_assert(sizeof(ODShared<M>) >= kRowsLds * sizeof(double), "the rows fit the solve's LDS");
+  constexpr int S = 16 * PFRow<M>::kPairs;
+  double* s = reinterpret_cast<double*>(&sh);
+  __syncthreads();                                   // every lane past the solve (and its sh.J reads)
+#pragma unroll
+  for (int q = 0; q < kOdRowQ; ++q) {
+    const int i = threadIdx.x + q * kBlock;
+    if (i < n_out * S) s[i] = v[q];
+  }
+  __syncthreads();
+  return s;
+}
+
 // Fused C4 step, OpenDSS rule: k_coord_pf's prologue (agent powers -> bus
 // load) and epilogue (output row 0 = the coordinated bus, violation, reward),
 // the snap solve in between.
@@ -1608,6 +1650,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   // in flight with the loads below; with one only a block that needs them does
   const bool early = o.resp == nullptr;
   if (early) od_stage_load<M>(o, o.start, stg);
+  const bool rows_lds = od_rows_lds<M>(a.n_out);     // (uniform) a history slot: every node
+  double rv[kOdRowQ];
+  if (rows_lds) od_rows_issue<M>(t, a.n_out, rv);
   double rp[PGW_MAX_AGENTS];
   const int64_t ec = valid ? e : 0;
 #pragma unroll
@@ -1637,10 +1682,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   od_fallback<M>(S, o, o.start, stg, !early, sh, need, ir, ii, it);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
-  // rows 1.. (a history slot holds every node): through the scalar cache, as
-  // k_pf_solve_od, in pf_node_pu's operation order (bit-identical per node)
+  // rows 1.. (a history slot holds every node)
   double vsel = v0;
-  pf_rows_out<M>(t, false, nullptr, a.n_out, ir, ii, [&](int ro, double v) {
+  const double* srow = rows_lds ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
+  pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
     if (valid && b.v_out) b.v_out[(int64_t)ro * n + e] = (Sto)v;
     vsel = (ro == c.vv_row) ? v : vsel;
   });
@@ -1661,8 +1706,8 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
 
 // pgw_pf_solve, OpenDSS rule: k_pf_solve's prologue (the env's controllable
 // powers) and outputs (every output row from the accepted iteration's currents
-// -- through the scalar cache: the solve's LDS leaves no room to stage them --,
-// extrema, element voltages), the snap solve in between.
+// -- staged in the solve's LDS after it, od_rows_put --, extrema, element
+// voltages), the response table / snap solve in between.
 template <int M>
 __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_pf_tables t, int64_t n,
                                                         const double* __restrict__ ctrl_p,
@@ -1676,6 +1721,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   // the table gives currents, not element voltages: U_out asks for the solve
   const bool table = o.resp != nullptr && t.U_out == nullptr;
   if (!table) od_stage_load<M>(o, o.start, stg);     // in flight with the loads below
+  const bool rows_lds = od_rows_lds<M>(a.n_out);     // (uniform)
+  double rv[kOdRowQ];
+  if (rows_lds) od_rows_issue<M>(t, a.n_out, rv);
   PFSolver<M, true, false> S;
   S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
@@ -1700,12 +1748,25 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
       t.U_out[2 * (e * M + k) + 1] = S.ui[k];
     }
   }
-  double vmn = v0, vmx = v0;
-  pf_rows_out<M>(t, false, nullptr, a.n_out, ir, ii, [&](int ro, double v) {
-    if (valid && v_out) v_out[(int64_t)ro * n + e] = v;
-    vmn = (v < vmn) ? v : vmn;
-    vmx = (v > vmx) ? v : vmx;
-  });
+  double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
+  const double* srow = rows_lds ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
+  if (v_out || !rows_lds) {
+    pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
+      if (valid && v_out) v_out[(int64_t)ro * n + e] = v;
+      vmn = (v < vmn) ? v : vmn;
+      vmx = (v > vmx) ? v : vmx;
+    });
+  } else {
+    // extrema only: min / max of |V|^2 over the rows, one sqrt each at the end
+    // (as k_pf_solve: sqrt is monotone and correctly rounded)
+    double mn2 = fma(v0i, v0i, v0r * v0r), mx2 = mn2;
+    pf_rows_out<M, false>(t, rows_lds, srow, a.n_out, ir, ii, [&](int, double m2) {
+      mn2 = (m2 < mn2) ? m2 : mn2;
+      mx2 = (m2 > mx2) ? m2 : mx2;
+    });
+    vmn = sqrt(mn2);
+    vmx = sqrt(mx2);
+  }
   if (!valid) return;
   if (a.n_out > 0) {
     if (v_out) v_out[e] = v0;
