@@ -331,6 +331,7 @@ _SIGS = {
     "pgw_pf_pack_size": (i64, [i32]),
     "pgw_timing_start": (i32, [i32]),
     "pgw_debug_pf_trace": (i32, [vp]),
+    "pgw_debug_mc_trace": (i32, [vp]),
     "pgw_pf_pred_meta": (i32, [P(PFParams), i32, i32, vp, vp, vp, vp]),
     "pgw_pf_pred_pack": (i32, [P(PFParams), i32, i32, vp, vp, vp]),
     "pgw_timing_stop": (i32, [vp, vp]),

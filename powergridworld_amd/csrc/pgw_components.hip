@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <type_traits>
 
 #include "pgw_common.h"
 
@@ -507,6 +508,24 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
 }
 
 // ====================================================================== fused MC step
+// Debug phase trace (pgw_debug_mc_trace): the TR instantiations of k_mc_step
+// and k_ma_step have lane 0 of every wave record wall_clock64() (100 MHz) at
+// its phase boundaries into g_mc_trace[(block * 8 + wave) * 8 + slot]; the
+// product launches the TR = false kernels, which hold no trace code at all.
+// Slots: 0 entry, 1 after the block's staging barrier, 2 the wave's component
+// (or walk group) done, 3 after the split barrier, 4 the EV fold and finish
+// done, 5 after the final barrier, 6 the sums written (wave 0).
+__device__ long long* g_mc_trace = nullptr;
+template <bool TR>
+__device__ __forceinline__ void mc_trace(long long* tr, int slot) {
+  if constexpr (TR) {
+    if ((threadIdx.x & 63) == 0) {
+      typedef __attribute__((address_space(1))) long long* gptr;
+      ((gptr)tr)[((int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + slot] = wall_clock64();
+    }
+  }
+}
+
 // One component of an MC agent for env e; writes its real power (and its
 // reward where it has one) to the component's own buffers.
 // `V`: the step's shared values -- the launch's own fields (pgw_mc_step_args)
@@ -576,10 +595,12 @@ __device__ __forceinline__ void mc_component(const Args& a, const V& v, const Co
 // block barrier the EV slot's wave folds the partial sums in group order and
 // finishes the EV step.  C3 runs one wave per SIMD and the EV wave's walk --
 // one memory round trip per chunk -- was the block's critical path.
-template <class Args, bool STD, bool CLK>
+template <class Args, bool STD, bool CLK, bool TR = false>
 __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, BldDerived d, int64_t n) {
   using S = typename McStore<Args>::S;
   const Args& a = PGW_KERNARG0(Args);
+  long long* const tr = TR ? g_mc_trace : nullptr;
+  mc_trace<TR>(tr, 0);
   __shared__ double s_rp[4][64], s_rew[4][64];
   __shared__ uint64_t s_bits[PGW_EV_MAX_WORDS * 64];
   __shared__ double s_evs[kEvGroups][4][64];
@@ -605,6 +626,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
       reinterpret_cast<double*>(&s_dyn)[i] = reinterpret_cast<const double*>(a.dyn + r)[i];
   }
   if (CLK || split) __syncthreads();
+  mc_trace<TR>(tr, 1);
   const pgw_ev_step_info& evs = CLK ? s_dyn.ev_step : a.ev_step;
   const bool ev_wave = split && (w >= a.n_comp || w == ev_slot);
   if (e < n) {
@@ -630,8 +652,10 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
                        : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
     }
   }
+  mc_trace<TR>(tr, 2);
   if (split) {
     __syncthreads();
+    mc_trace<TR>(tr, 3);
     if (w == ev_slot && e < n) {
       EvSums t{0.0, 0.0, 0.0, 0.0, 0, 0};
 #pragma unroll
@@ -649,8 +673,10 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
       s_rp[w][lane] = C.real_power[e];
       s_rew[w][lane] = a.ev_reward[e];
     }
+    mc_trace<TR>(tr, 4);
   }
   __syncthreads();
+  mc_trace<TR>(tr, 5);
   if (CLK && threadIdx.x == 0) a.clock[blockIdx.x] = k + 1;    // (every wave read k before the barrier)
   if (w != 0 || e >= n) return;
   double rp_sum = 0.0, rew_sum = 0.0;
@@ -660,6 +686,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   }
   a.real_power[e] = (S)rp_sum;
   a.reward[e] = (S)rew_sum;
+  mc_trace<TR>(tr, 6);
 }
 
 // ====================================================================== fused multi-agent step
@@ -677,10 +704,12 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
 // the light PV / storage slots share one (pgw_ma_step_args.wave_*): a wave per
 // slot made the heterogeneous scenario's blocks 5 waves, which at the kernel's
 // register count did not all fit at once.
-template <bool STD>
+template <bool STD, bool TR = false>
 __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_args a_, BldDerived d,
                                                                    int64_t n) {
   const pgw_ma_step_args& a = PGW_KERNARG0(pgw_ma_step_args);
+  long long* const tr = TR ? g_mc_trace : nullptr;
+  mc_trace<TR>(tr, 0);
   __shared__ double s_rp[PGW_MA_MAX_SLOTS][64], s_rew[PGW_MA_MAX_SLOTS][64];
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
@@ -729,7 +758,9 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_a
       }
     }
   }
+  mc_trace<TR>(tr, 2);
   __syncthreads();
+  mc_trace<TR>(tr, 5);
   if (wv != 0 || e >= n) return;
   double ap[PGW_MAX_AGENTS];
 #pragma unroll
@@ -757,6 +788,7 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_a
       acc = (g < a.n_agents && a.agent_bus[g] == b) ? acc + ap[g] : acc;
     a.bus_p[(int64_t)b * n + e] = acc;
   }
+  mc_trace<TR>(tr, 6);
 }
 
 // ====================================================================== MC reduce
@@ -786,6 +818,8 @@ static int initial_ev_split_mode() {
   return (v && (v[0] == '0' || v[0] == '1')) ? v[0] - '0' : -1;
 }
 static std::atomic<int> g_mc_ev_split{initial_ev_split_mode()};
+// pgw_debug_mc_trace: set -> the MC / multi-agent steps launch their TR kernels
+static std::atomic<bool> g_mc_trace_on{false};
 
 #define PGW_LAUNCH(kernel, n, stream, ...)                                         \
   do {                                                                                 \
@@ -966,6 +1000,13 @@ int32_t pgw_ev_step_f32(const pgw_ev_params* p, const pgw_ev_step_info* s, int64
              reward);
 }
 
+int32_t pgw_debug_mc_trace(long long* buf) {
+  PGW_REQUIRE(hipMemcpyToSymbol(HIP_SYMBOL(g_mc_trace), &buf, sizeof(buf)) == hipSuccess,
+              "pgw_debug_mc_trace: hipMemcpyToSymbol failed");
+  g_mc_trace_on.store(buf != nullptr);
+  return PGW_OK;
+}
+
 int32_t pgw_mc_ev_split_mode(int32_t mode, int32_t* previous) {
   PGW_REQUIRE(mode >= -1 && mode <= 1, "pgw_mc_ev_split_mode: mode must be -1, 0 or 1");
   const int old = g_mc_ev_split.exchange(mode);
@@ -1023,7 +1064,9 @@ static int32_t mc_agent_step(const Args* a, int64_t n, void* stream) {
   const bool split = has_ev && (force >= 0 ? force == 1 : blocks <= 256 && chunks >= 2);
   const dim3 grid((unsigned)blocks), block(64u * (unsigned)(a->n_comp + (split ? kEvGroups - 1 : 0)));
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, *a, d, n); };
-  if (std_bld)
+  if (g_mc_trace_on.load() && !a->clock && std::is_same<Args, pgw_mc_step_args>::value)
+    std_bld ? go(k_mc_step<Args, true, false, true>) : go(k_mc_step<Args, false, false, true>);
+  else if (std_bld)
     a->clock ? go(k_mc_step<Args, true, true>) : go(k_mc_step<Args, true, false>);
   else
     a->clock ? go(k_mc_step<Args, false, true>) : go(k_mc_step<Args, false, false>);
@@ -1112,7 +1155,10 @@ int32_t pgw_ma_step(const pgw_ma_step_args* a, const pgw_pf_params* pf, const pg
   const BldDerived d = make_bld_derived(a->bld);
   const dim3 grid((unsigned)((n + 63) / 64)), block(64u * (unsigned)a->n_waves);
   hipStream_t st = (hipStream_t)stream;
-  if (std_bld)
+  if (g_mc_trace_on.load())
+    std_bld ? launch_timed(PGW_T_MA_STEP, k_ma_step<true, true>, grid, block, st, *a, d, n)
+            : launch_timed(PGW_T_MA_STEP, k_ma_step<false, true>, grid, block, st, *a, d, n);
+  else if (std_bld)
     launch_timed(PGW_T_MA_STEP, k_ma_step<true>, grid, block, st, *a, d, n);
   else
     launch_timed(PGW_T_MA_STEP, k_ma_step<false>, grid, block, st, *a, d, n);

@@ -64,7 +64,8 @@ def _step_ma(env, a):
     return o, r, d["__all__"], m.get("voltage_violation") if isinstance(m, dict) else None
 
 
-def test_checkpoint_c4_fused_across_reset():
+@pytest.mark.parametrize("conv", ["opendss", "exact"])
+def test_checkpoint_c4_fused_across_reset(conv):
     from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
     n = 2048
     g = torch.Generator(DEV).manual_seed(5)
@@ -75,11 +76,12 @@ def test_checkpoint_c4_fused_across_reset():
         if d["__all__"]:
             env.reset()
         return env.packed_obs(), r, d["__all__"], m["voltage_violation"], env.pf_solver.get_bus_voltage_by_name("675c")
-    make = lambda: CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV)
+    make = lambda: CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n, device=DEV)
     _check(make, acts[:280], acts[280:], step)
 
 
-def test_checkpoint_heterogeneous_fused():
+@pytest.mark.parametrize("conv", ["opendss", "exact"])
+def test_checkpoint_heterogeneous_fused(conv):
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     n = 1024
@@ -91,7 +93,7 @@ def test_checkpoint_heterogeneous_fused():
                "pv": a[:, 8:9], "ev-charging": a[:, 9:10]}
         o, r, d, m = env.step(act)
         return o, r, d["__all__"], env.pf_solver.voltage_extrema()
-    make = lambda: MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV)
+    make = lambda: MultiAgentEnv(**make_env_config(pf_convergence=conv), num_envs=n, device=DEV)
     _check(make, acts[:25], acts[25:], step)
 
 

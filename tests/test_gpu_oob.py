@@ -87,13 +87,15 @@ def test_oob_mc_c3_fused_and_generic(randomize):
     assert want > 0 and count(fused) == want and count(generic) == want
 
 
+@pytest.mark.parametrize("conv", ["opendss", "exact"])
 @pytest.mark.parametrize("fused", [True, False])
-def test_oob_c4_meta(fused):
+def test_oob_c4_meta(fused, conv):
     """C4 (5 agents x [building, PV, storage]): the fused kernels and the generic
     path count the same warnings; meta["oob_actions"] is the running total."""
     from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
     n, steps = 1024, 10
-    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=fused)
+    env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n, device=DEV,
+                                             fused=fused)
     assert (env._fused is not None) == fused
     env.reset()
     rng = np.random.default_rng(3)
@@ -140,7 +142,8 @@ def test_oob_warning_logged_at_a_later_reset(caplog):
     assert any("8 action(s)" in r.getMessage() for r in caplog.records)
 
 
-def test_oob_heterogeneous_fused_and_generic():
+@pytest.mark.parametrize("conv", ["opendss", "exact"])
+def test_oob_heterogeneous_fused_and_generic(conv):
     """The heterogeneous scenario on the fused multi-agent step (pgw_ma_step) and
     on the generic path: one warning per (env, component, step) whose rescaled
     action is out of the box -- the building's six actions count once."""
@@ -155,7 +158,7 @@ def test_oob_heterogeneous_fused_and_generic():
         want += sum(int(bad(A[t, :, j]).sum()) for j in range(6, 10))   # pv, storage, pv farm, EV
     got = []
     for fused in ("auto", False):
-        env = MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=fused)
+        env = MultiAgentEnv(**make_env_config(pf_convergence=conv), num_envs=n, device=DEV, fused=fused)
         assert (env._ma is not None) == (fused == "auto")
         env.reset()
         for t in range(steps):
