@@ -135,7 +135,8 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
                                                     const Mt& act, S* __restrict__ x,
                                                     S* __restrict__ pcons, S* __restrict__ rout,
                                                     S* __restrict__ rstate, int32_t lagged,
-                                                    const pgw_building_ext& ext, const Mt& obs) {
+                                                    const pgw_building_ext& ext, const Mt& obs,
+                                                    double* fresh_out = nullptr) {
   if constexpr (STD) {
     double av[6], xs[5], fresh;
 #pragma unroll
@@ -148,6 +149,7 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
     pcons[e] = (S)pc;
     if (rout) rout[e] = lagged ? rstate[e] : (S)fresh;
     if (rstate) rstate[e] = (S)fresh;
+    if (fresh_out) *fresh_out = (double)(S)fresh;
     return pc;
   }
   double a[6], xs[5], T[5];
@@ -175,6 +177,7 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
   double fresh = building_reward(p, T, exn.comfort_lb, exn.comfort_ub, pc);
   if (rout) rout[e] = lagged ? rstate[e] : (S)fresh;
   if (rstate) rstate[e] = (S)fresh;
+  if (fresh_out) *fresh_out = (double)(S)fresh;
   BuildingExt xv = building_ext(ext, e);
   building_write_obs(p, T, exn, pc, xv, [&](int j, double v) { st(obs, e, j, v); });
   return pc;
@@ -242,7 +245,7 @@ enum { kEvTable = 0, kEvPerEnv = 1, kEvDivide = 2 };
 // ((p0 + p1) + p2) + p3 instead, a rounding difference of an ulp or so: the
 // goldens compare at rtol 1e-12, the north star allows 1e-6.)
 constexpr int kEvChunk = 8;
-constexpr int kEvGroups = 4;
+constexpr int kEvGroups = 8;
 struct EvSums {
   double demand, consumed, dsum, unserved;
   int dcnt, nact;
@@ -258,9 +261,10 @@ __device__ __forceinline__ int ev_group_len(int chunks) { return max(1, (chunks 
 // took the EV kernels from 3 to 2 waves per SIMD.
 constexpr int kEvFoldThreads = 512;
 // every block that runs the one-lane walk must fit: k_ev_step (kBlock), k_mc_step
-// (64 x (4 components + kEvGroups - 1 split waves)), k_ma_step (64 x slots)
+// unsplit (64 x 4 components; its split blocks walk with SPLIT = true, no fold
+// buffer), k_ma_step (64 x slots)
 static_assert(kBlock <= kEvFoldThreads, "s_ev_fold: k_ev_step block");
-static_assert(64 * (4 + kEvGroups - 1) <= kEvFoldThreads, "s_ev_fold: k_mc_step block");
+static_assert(64 * 4 <= kEvFoldThreads, "s_ev_fold: k_mc_step block");
 static_assert(64 * PGW_MA_MAX_SLOTS <= kEvFoldThreads, "s_ev_fold: k_ma_step block");
 __shared__ double s_ev_fold[4][kEvFoldThreads];
 
@@ -435,9 +439,16 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
   return t;
 }
 
+// A component's real power and reward as stored (S-rounded), handed to the
+// block's sums in registers: reading the component's own stores back cost a
+// store-to-load round trip at the end of every component wave.
+struct RpRew {
+  double rp, rew;
+};
+
 // The step's state, reward and obs from the walk's totals (:253-262, :135-142).
 template <class S, class Mt>
-__device__ __forceinline__ void ev_finish(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t e,
+__device__ __forceinline__ RpRew ev_finish(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t e,
                                           const EvSums& t, const Mt& obs, S* __restrict__ rp,
                                           S* __restrict__ rew) {
   double st_[6];
@@ -447,19 +458,22 @@ __device__ __forceinline__ void ev_finish(const pgw_ev_params& p, const pgw_ev_s
   st_[3] = p.mult * t.demand;
   st_[4] = t.dcnt ? t.dsum / (double)t.dcnt : 0.0;
   st_[5] = t.unserved;
-  rp[e] = (S)(p.mult * t.consumed);                  // :255
+  const S rp_e = (S)(p.mult * t.consumed);           // :255
+  rp[e] = rp_e;
   // step_reward :135-142
   double ur = -p.u_pen * (st_[5] * st_[5]);
   double pk = pymax(0.0, st_[2] - p.thr);
   double pr = -p.p_pen * (pk * pk);
-  rew[e] = (S)((ur + pr) / p.reward_scale);
+  const S rew_e = (S)((ur + pr) / p.reward_scale);
+  rew[e] = rew_e;
 #pragma unroll
   for (int j = 0; j < 6; ++j)
     st(obs, e, j, p.rescale ? to_scaled(st_[j], p.obs_low[j], p.obs_high[j]) : st_[j]);
+  return {(double)rp_e, (double)rew_e};
 }
 
 template <int MODE, class S, class Mt>
-__device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+__device__ __forceinline__ RpRew ev_step_mode(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
                                              int64_t e, const Mt& act, const double* __restrict__ endp,
                                              S* __restrict__ req, uint64_t* __restrict__ chg,
                                              const Mt& obs, S* __restrict__ rp,
@@ -467,18 +481,18 @@ __device__ __forceinline__ void ev_step_mode(const pgw_ev_params& p, const pgw_e
   const double kwh = ev_kwh(p, s, e, act, true);
   const int nc = ev_chunks(s);
   const EvSums t = ev_walk<MODE, false>(p, s, n, e, kwh, endp, req, chg, 0, nc, ev_group_len(nc), nullptr, 0);
-  ev_finish(p, s, e, t, obs, rp, rew);
+  return ev_finish(p, s, e, t, obs, rp, rew);
 }
 
 template <class S, class Mt>
-__device__ __forceinline__ void ev_step_env(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
+__device__ __forceinline__ RpRew ev_step_env(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
                                             int64_t e, const Mt& act, const double* __restrict__ endp,
                                             S* __restrict__ req, uint64_t* __restrict__ chg,
                                             const Mt& obs, S* __restrict__ rp,
                                             S* __restrict__ rew) {
-  if (s.env_start) ev_step_mode<kEvPerEnv>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
-  else if (s.tl_rcp) ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
-  else ev_step_mode<kEvDivide>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  if (s.env_start) return ev_step_mode<kEvPerEnv>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  if (s.tl_rcp) return ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  return ev_step_mode<kEvDivide>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
 }
 
 // Group g's part of the walk (k_mc_step's split EV waves).
@@ -504,7 +518,7 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
                                                     S* __restrict__ rew) {
   int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
-  ev_step_env(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  (void)ev_step_env(p, s, n, e, act, endp, req, chg, obs, rp, rew);
 }
 
 // ====================================================================== fused MC step
@@ -542,25 +556,31 @@ template <> struct McStore<pgw_mc_step_args_f32> {
 static_assert(sizeof(pgw_mc_step_args_f32) == sizeof(pgw_mc_step_args), "pgw_mc_step_args_f32 layout");
 
 template <bool STD, class Args, class V, class Comp>
-__device__ __forceinline__ void mc_component(const Args& a, const V& v, const Comp& C,
-                                             const BldDerived& d, int64_t n, int64_t e) {
+__device__ __forceinline__ RpRew mc_component(const Args& a, const V& v, const Comp& C,
+                                              const BldDerived& d, int64_t n, int64_t e) {
   using S = typename McStore<Args>::S;
   using Mt = typename McStore<Args>::Mt;
   switch (C.kind) {
-    case PGW_MC_BUILDING:
-      (void)building_step_env<STD, S, Mt>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action, a.bld_x,
-                                          C.real_power, (S*)nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
-      break;
-    case PGW_MC_PV:
-      C.real_power[e] = (S)pv_step_env(a.pv, e, v.pv_pmax, C.action, a.pv_min_voltage, C.obs);
-      break;
-    case PGW_MC_STORAGE:
-      C.real_power[e] = (S)battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
-      break;
+    case PGW_MC_BUILDING: {
+      double fresh = 0.0;
+      const S pc = (S)building_step_env<STD, S, Mt>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action,
+                                                    a.bld_x, C.real_power, (S*)nullptr, a.bld_reward_state,
+                                                    0, a.bld_ext, C.obs, &fresh);
+      return {(double)pc, fresh};
+    }
+    case PGW_MC_PV: {
+      const S r = (S)pv_step_env(a.pv, e, v.pv_pmax, C.action, a.pv_min_voltage, C.obs);
+      C.real_power[e] = r;
+      return {(double)r, 0.0};
+    }
+    case PGW_MC_STORAGE: {
+      const S r = (S)battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
+      C.real_power[e] = r;
+      return {(double)r, 0.0};
+    }
     default:
-      ev_step_env(a.ev, v.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
-                  C.real_power, a.ev_reward);
-      break;
+      return ev_step_env(a.ev, v.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
+                         C.real_power, a.ev_reward);
   }
 }
 
@@ -591,10 +611,13 @@ __device__ __forceinline__ void mc_component(const Args& a, const V& v, const Co
 //
 // Split EV (blockDim.x > 64 n_comp: the launch added kEvGroups - 1 waves): the
 // EV slot's vehicle walk is shared by kEvGroups waves of the block, each over
-// one group of chunks (ev_walk), with the charging bits ORed in LDS; after a
-// block barrier the EV slot's wave folds the partial sums in group order and
-// finishes the EV step.  C3 runs one wave per SIMD and the EV wave's walk --
-// one memory round trip per chunk -- was the block's critical path.
+// one group of chunks (ev_walk), with the charging bits ORed in LDS; the last
+// group wave to finish its walk (an LDS arrival count, acquire-release at
+// workgroup scope) folds the partial sums in group order and finishes the EV
+// step -- without waiting for the building wave, as a block barrier would.
+// C3 runs one block per CU; the phase trace (tools/gpu/mc_trace.py) showed the
+// walk groups (about 2 us per chunk each) as the critical path at midday and
+// the building wave plus the fold behind a barrier at night.
 template <class Args, bool STD, bool CLK, bool TR = false>
 __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, BldDerived d, int64_t n) {
   using S = typename McStore<Args>::S;
@@ -605,14 +628,17 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   __shared__ uint64_t s_bits[PGW_EV_MAX_WORDS * 64];
   __shared__ double s_evs[kEvGroups][4][64];
   __shared__ int s_evc[kEvGroups][2][64];
+  __shared__ int s_arrive;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
   const bool split = (int)(blockDim.x >> 6) > a.n_comp;                   // (uniform)
   int ev_slot = 0;
   for (int c = 0; c < a.n_comp; ++c) ev_slot = a.comp[c].kind == PGW_MC_EV ? c : ev_slot;
-  if (split)
+  if (split) {
     for (int i = threadIdx.x; i < PGW_EV_MAX_WORDS * 64; i += blockDim.x) s_bits[i] = 0ull;
+    if (threadIdx.x == 0) s_arrive = 0;
+  }
   // CLK: the step's record staged in LDS by the block (80 doubles): its
   // fields are then read at fixed LDS addresses, with no pointer to keep live
   // (a pointer into the table costs SGPRs the step does not have)
@@ -629,9 +655,9 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   mc_trace<TR>(tr, 1);
   const pgw_ev_step_info& evs = CLK ? s_dyn.ev_step : a.ev_step;
   const bool ev_wave = split && (w >= a.n_comp || w == ev_slot);
-  if (e < n) {
-    if (ev_wave) {
-      const int g = w >= a.n_comp ? w - a.n_comp + 1 : 0;
+  if (ev_wave) {
+    const int g = w >= a.n_comp ? w - a.n_comp + 1 : 0;
+    if (e < n) {
       const EvSums t = ev_step_group(a.ev, evs, n, e, a.comp[ev_slot].action, a.ev_endp, a.ev_req,
                                      a.ev_charging, g, s_bits, lane);
       s_evs[g][0][lane] = t.demand;
@@ -640,40 +666,47 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
       s_evs[g][3][lane] = t.unserved;
       s_evc[g][0][lane] = t.dcnt;
       s_evc[g][1][lane] = t.nact;
-    } else {
-      const auto& C = a.comp[w];
-      if constexpr (CLK)
-        mc_component<STD>(a, s_dyn, C, d, n, e);
-      else
-        mc_component<STD>(a, a, C, d, n, e);
-      const int kind = C.kind;
-      s_rp[w][lane] = C.real_power[e];               // this thread's own writes
-      s_rew[w][lane] = kind == PGW_MC_BUILDING ? a.bld_reward_state[e]
-                       : kind == PGW_MC_EV ? a.ev_reward[e] : 0.0;
     }
-  }
-  mc_trace<TR>(tr, 2);
-  if (split) {
-    __syncthreads();
-    mc_trace<TR>(tr, 3);
-    if (w == ev_slot && e < n) {
-      EvSums t{0.0, 0.0, 0.0, 0.0, 0, 0};
+    mc_trace<TR>(tr, 2);
+    // arrival: this wave's partials and charging bits (LDS) are released to
+    // the wave that arrives last, which acquires them and finishes the step
+    int prior = 0;
+    if (lane == 0)
+      prior = __hip_atomic_fetch_add(&s_arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prior = __builtin_amdgcn_readfirstlane(prior);
+    if (prior == kEvGroups - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (e < n) {
+        EvSums t{0.0, 0.0, 0.0, 0.0, 0, 0};
 #pragma unroll
-      for (int g = 0; g < kEvGroups; ++g) {
-        t.demand = t.demand + s_evs[g][0][lane];
-        t.consumed = t.consumed + s_evs[g][1][lane];
-        t.dsum = t.dsum + s_evs[g][2][lane];
-        t.unserved = t.unserved + s_evs[g][3][lane];
-        t.dcnt += s_evc[g][0][lane];
-        t.nact += s_evc[g][1][lane];
+        for (int q = 0; q < kEvGroups; ++q) {
+          t.demand = t.demand + s_evs[q][0][lane];
+          t.consumed = t.consumed + s_evs[q][1][lane];
+          t.dsum = t.dsum + s_evs[q][2][lane];
+          t.unserved = t.unserved + s_evs[q][3][lane];
+          t.dcnt += s_evc[q][0][lane];
+          t.nact += s_evc[q][1][lane];
+        }
+        for (int j = 0; j < evs.n_words; ++j) a.ev_charging[(int64_t)j * n + e] = s_bits[j * 64 + lane];
+        const auto& C = a.comp[ev_slot];
+        const RpRew r = ev_finish(a.ev, evs, e, t, C.obs, C.real_power, a.ev_reward);
+        s_rp[ev_slot][lane] = r.rp;
+        s_rew[ev_slot][lane] = r.rew;
       }
-      for (int j = 0; j < evs.n_words; ++j) a.ev_charging[(int64_t)j * n + e] = s_bits[j * 64 + lane];
-      const auto& C = a.comp[ev_slot];
-      ev_finish(a.ev, evs, e, t, C.obs, C.real_power, a.ev_reward);
-      s_rp[w][lane] = C.real_power[e];
-      s_rew[w][lane] = a.ev_reward[e];
+      mc_trace<TR>(tr, 4);
     }
-    mc_trace<TR>(tr, 4);
+  } else {
+    if (e < n) {
+      const auto& C = a.comp[w];
+      RpRew r;
+      if constexpr (CLK)
+        r = mc_component<STD>(a, s_dyn, C, d, n, e);
+      else
+        r = mc_component<STD>(a, a, C, d, n, e);
+      s_rp[w][lane] = r.rp;
+      s_rew[w][lane] = r.rew;
+    }
+    mc_trace<TR>(tr, 2);
   }
   __syncthreads();
   mc_trace<TR>(tr, 5);
@@ -704,8 +737,10 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
 // the light PV / storage slots share one (pgw_ma_step_args.wave_*): a wave per
 // slot made the heterogeneous scenario's blocks 5 waves, which at the kernel's
 // register count did not all fit at once.
+// (3 waves per SIMD at least: the heterogeneous scenario's 1 024 three-wave
+// blocks then all fit at once, 4 per CU; at 2 they ran in two rounds)
 template <bool STD, bool TR = false>
-__global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_args a_, BldDerived d,
+__global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_waves_per_eu(3))) k_ma_step(pgw_ma_step_args a_, BldDerived d,
                                                                    int64_t n) {
   const pgw_ma_step_args& a = PGW_KERNARG0(pgw_ma_step_args);
   long long* const tr = TR ? g_mc_trace : nullptr;
@@ -723,15 +758,17 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) k_ma_step(pgw_ma_step_a
   if (e < n) {
     if (kind0 == PGW_MC_BUILDING) {
       const pgw_mc_component& C = a.comp[c0];
-      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e, C.action, a.bld_x,
-                                              C.real_power, nullptr, a.bld_reward_state, 0, a.bld_ext, C.obs);
-      s_rew[c0][lane] = a.bld_reward_state[e];        // the fresh reward (MC semantics)
+      double fresh = 0.0;                             // the fresh reward (MC semantics)
+      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e,
+                                                               C.action, a.bld_x, C.real_power, nullptr,
+                                                               a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh);
+      s_rew[c0][lane] = fresh;
     } else if (kind0 == PGW_MC_EV) {
       const pgw_mc_component& C = a.comp[c0];
-      ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs, C.real_power,
-                  a.ev_reward);
-      s_rp[c0][lane] = C.real_power[e];               // this thread's own writes
-      s_rew[c0][lane] = a.ev_reward[e];
+      const RpRew r = ev_step_env(a.ev, a.ev_step, n, e, C.action, a.ev_endp, a.ev_req, a.ev_charging, C.obs,
+                                  C.real_power, a.ev_reward);
+      s_rp[c0][lane] = r.rp;
+      s_rew[c0][lane] = r.rew;
     } else {
       for (int i = 0; i < a.wave_count[wv]; ++i) {
         const int w = a.wave_slot[a.wave_first[wv] + i];
@@ -1046,8 +1083,8 @@ static int32_t mc_agent_step(const Args* a, int64_t n, void* stream) {
     if (a->comp[c].kind == PGW_MC_BUILDING) std_bld = bld_is_std(a->bld);
   if (n == 0) return PGW_OK;
   // the EV walk split over kEvGroups waves (k_mc_step) where the blocks are at
-  // most one per CU anyway: a 7-wave block of ~165 VGPRs fits once per CU, where
-  // 4-wave blocks fit 3 times
+  // most one per CU anyway: an 11-wave block of 168 VGPRs fits once per CU,
+  // where 4-wave blocks fit 3 times
   bool has_ev = false;
   for (int c = 0; c < a->n_comp; ++c) has_ev = has_ev || a->comp[c].kind == PGW_MC_EV;
   const int64_t blocks = (n + 63) / 64;
