@@ -770,24 +770,53 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
       s_rp[c0][lane] = r.rp;
       s_rew[c0][lane] = r.rew;
     } else {
-      for (int i = 0; i < a.wave_count[wv]; ++i) {
-        const int w = a.wave_slot[a.wave_first[wv] + i];
+      // the light slots in two passes: every slot's loads (action, SoC or the
+      // min voltage) go out before any slot's stores -- one slot after another
+      // each waited for the previous slot's stores too (vmcnt is in order):
+      // three round trips where one does (HET's PV farm, building PV, storage)
+      const int cnt = a.wave_count[wv], first = a.wave_first[wv];
+      double act_v[PGW_MA_MAX_SLOTS], st_v[PGW_MA_MAX_SLOTS];
+#pragma unroll
+      for (int i = 0; i < PGW_MA_MAX_SLOTS; ++i) {
+        if (i >= cnt) break;
+        const int w = a.wave_slot[first + i];
         const pgw_mc_component& C = a.comp[w];
-        double rp, rew = 0.0;
+        act_v[i] = C.action.ptr ? ld(C.action, e, 0) : 0.0;
         if (C.kind == PGW_MC_PV) {
           const bool two = a.slot_pv2[w] != 0;
           const double* vmin = two ? a.pv2_min_voltage : a.pv_min_voltage;
-          rp = pv_step_env(two ? a.pv2 : a.pv, e, two ? a.pv2_pmax : a.pv_pmax, C.action, vmin, C.obs);
+          st_v[i] = ((two ? a.pv2 : a.pv).grid_aware || a.slot_reward[w]) ? vmin[e] : 0.0;
+        } else {
+          st_v[i] = a.bat_soc[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PGW_MA_MAX_SLOTS; ++i) {
+        if (i >= cnt) break;
+        const int w = a.wave_slot[first + i];
+        const pgw_mc_component& C = a.comp[w];
+        double rp, rew = 0.0;
+        if (C.kind == PGW_MC_PV) {                    // pv_step_env on the loaded values
+          const bool two = a.slot_pv2[w] != 0;
+          const pgw_pv_params& pp = two ? a.pv2 : a.pv;
+          const double pmax = two ? a.pv2_pmax : a.pv_pmax;
+          const double x = st_v[i];
+          st(C.obs, e, 0, pv_obs(pp, pmax));
+          if (pp.grid_aware) st(C.obs, e, 1, pp.rescale ? to_scaled(x, pp.vmin_low, pp.vmin_high) : x);
+          rp = C.action.ptr ? pv_real_power(pp, act_v[i], pmax) : 0.0;
           if (a.slot_reward[w]) {                     // ThisPVEnv.step_reward: k_band_penalty's ops
-            const double x = vmin[e];
             const double l = x - a.band_lo, u = a.band_hi - x;
             const double viol = ((l < 0.0) ? l : 0.0) + ((u < 0.0) ? u : 0.0);
             const double y = a.band_scale * viol;
             rew = -(y * y);
             a.slot_reward[w][e] = rew;
           }
-        } else {
-          rp = battery_step_env(a.bat, e, C.action, a.bat_soc, C.obs);
+        } else {                                      // battery_step_env on the loaded values
+          double soc = st_v[i];
+          const double power = battery_step(a.bat, act_v[i], soc);
+          a.bat_soc[e] = soc;
+          st(C.obs, e, 0, battery_obs(a.bat, soc));
+          rp = -power;
         }
         C.real_power[e] = rp;
         s_rp[w][lane] = rp;
