@@ -1,13 +1,15 @@
-# PMC passes (each its own rocprofv3 run, --pmc only) over the C3 config bench:
-# where k_mc_step's waves spend their cycles.
+# PMC passes (each its own rocprofv3 run, --pmc only) over the C3 config bench
+# (or the configs named second, e.g. C3,HET): where k_mc_step's (k_ma_step's)
+# waves spend their cycles.  Usage: bash tools/gpu/pmc_c3.sh TAG [configs]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 TAG=${1:-c3}
+CFGS=${2:-C3}
 run_pass() {
   name=$1; shift
-  cd /tmp && timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/$TAG/$name" -o run -- python3 "$GRAFT_REPO_ROOT/tools/bench_configs.py" --configs C3 --steps 100 --warmup 5 > "$GRAFT_REPO_ROOT/gpurun_out/pmc/${TAG}_$name.log" 2>&1
+  cd /tmp && timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc/$TAG/$name" -o run -- python3 "$GRAFT_REPO_ROOT/tools/bench_configs.py" --configs "$CFGS" --steps 100 --warmup 5 > "$GRAFT_REPO_ROOT/gpurun_out/pmc/${TAG}_$name.log" 2>&1
   rc=$?; cd "$GRAFT_REPO_ROOT"; return $rc
 }
 run_pass p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA || exit $?
