@@ -61,7 +61,7 @@ def c3(every):
             t = buf.view(-1, 8, 8).cpu().numpy()
             nw = int((t[0, :, 0] != 0).sum())
             if k % every == 0:
-                roles = ["bld", "pv", "sto", "ev0", "ev1", "ev2", "ev3"][:nw]
+                roles = (["bld", "pv", "sto", "ev0"] + ["ev%d" % g for g in range(1, 8)])[:nw]
                 spans.append(summarize("C3 step %3d" % k, buf, nw, roles, "waves %d" % nw))
     finally:
         _lib.check(_lib.lib().pgw_debug_mc_trace(None))
