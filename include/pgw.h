@@ -680,7 +680,7 @@ enum { PGW_T_COORD_AGENTS = 0, PGW_T_COORD_PF = 1, PGW_T_PF_SOLVE = 2, PGW_T_RES
 /* Debug: device buffer of 8 int64 per k_coord_pf / k_pf_solve wave (NULL = off); lane 0 of
  * each wave writes wall_clock64() (100 MHz) at its phase boundaries. */
 int32_t pgw_debug_pf_trace(long long* buf);
-/* Debug: device buffer of 64 int64 per block (8 waves x 8 slots) of k_mc_step /
+/* Debug: device buffer of 128 int64 per block (16 waves x 8 slots) of k_mc_step /
  * k_ma_step (NULL = off); while set, pgw_mc_agent_step (fp64, unclocked) and
  * pgw_ma_step launch trace instantiations whose lane 0 of each wave writes
  * wall_clock64() (100 MHz) at its phase boundaries (pgw_components.hip). */

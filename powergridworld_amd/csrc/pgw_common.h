@@ -392,11 +392,14 @@ inline bool bld_is_std(const pgw_building_params& p) {
 // reward :315-335): av = the 6 actions as given (rescaled if p.rescale), xs =
 // x_k in/out.  Returns p_consumed; `reward` = the fresh reward; obs slot j goes
 // to store(j, value).
-template <class Store>
+struct NoStamp {
+  __device__ void operator()(int) const {}
+};
+template <class Store, class Stamp = NoStamp>
 __device__ __forceinline__ double bld_std_step(const pgw_building_params& B, const BldDerived& d,
                                                const pgw_building_exo& ex, const pgw_building_exo& exn,
                                                double (&av)[6], double (&xs)[5], double& reward,
-                                               Store&& store) {
+                                               Store&& store, Stamp&& stamp = Stamp()) {
   double T[5];
   bool bad = false;
 #pragma unroll
@@ -407,6 +410,7 @@ __device__ __forceinline__ double bld_std_step(const pgw_building_params& B, con
   if (B.rescale) oob_note(B.oob, bad);
 #pragma unroll
   for (int z = 0; z < 5; ++z) T[z] = B.C[z] * xs[z] + B.mean[z];
+  stamp(3);                        // (debug trace: the loads have arrived)
 #pragma unroll
   for (int z = 0; z < 5; ++z) {
     const int nz = z < 2 ? 4 : (z == 2 ? 3 : 2);
@@ -424,6 +428,7 @@ __device__ __forceinline__ double bld_std_step(const pgw_building_params& B, con
   for (int z = 0; z < 5; ++z) T[z] = B.C[z] * xs[z] + B.mean[z];
   const double pc = building_p_consumed(av, ex.T_oa);
   reward = building_reward(B, T, exn.comfort_lb, exn.comfort_ub, pc, exact_div(-pc, 12.0, 1.0 / 12.0));
+  stamp(7);                        // (debug trace: state, power and reward done)
   const double lb = exn.comfort_lb, ub = exn.comfort_ub;
 #pragma unroll
   for (int j = 0; j < 15; ++j) {

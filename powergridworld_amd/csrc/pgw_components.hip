@@ -90,6 +90,25 @@ __global__ void __launch_bounds__(kBlock) k_pv(pgw_pv_params p, int64_t n, doubl
   if (rp) rp[e] = (S)r;
 }
 
+// Debug phase trace (pgw_debug_mc_trace): the TR instantiations of k_mc_step
+// and k_ma_step have lane 0 of every wave record wall_clock64() (100 MHz) at
+// its phase boundaries into g_mc_trace[(block * 8 + wave) * 8 + slot]; the
+// product launches the TR = false kernels, which hold no trace code at all.
+// Slots: 0 entry, 1 after the block's staging barrier, 2 the wave's component
+// (or walk group) done, 3 the building's loads arrived, 4 the EV fold and
+// finish done, 5 after the final barrier, 6 the sums written, 7 the building's
+// state update and reward done (its obs next).  16 waves per block.
+__device__ long long* g_mc_trace = nullptr;
+template <bool TR>
+__device__ __forceinline__ void mc_trace(long long* tr, int slot) {
+  if constexpr (TR) {
+    if ((threadIdx.x & 63) == 0) {
+      typedef __attribute__((address_space(1))) long long* gptr;
+      ((gptr)tr)[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + slot] = wall_clock64();
+    }
+  }
+}
+
 // ====================================================================== building
 template <class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p, pgw_building_exo ex0,
@@ -128,7 +147,7 @@ __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p
 
 // One env's FiveZoneROMEnv.step_ (:183-225); returns p_consumed (its real power).
 // STD: the reference's default model/obs layout (bld_is_std), via bld_std_step.
-template <bool STD, class S = double, class Mt = pgw_mat>
+template <bool STD, class S = double, class Mt = pgw_mat, bool TR = false>
 __device__ __forceinline__ double building_step_env(const pgw_building_params& p, const BldDerived& d,
                                                     const pgw_building_exo& ex,
                                                     const pgw_building_exo& exn, int64_t n, int64_t e,
@@ -143,7 +162,9 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
     for (int j = 0; j < 6; ++j) av[j] = ld(act, e, j);
 #pragma unroll
     for (int z = 0; z < 5; ++z) xs[z] = x[z * n + e];
-    const double pc = bld_std_step(p, d, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); });
+    long long* const tr = TR ? g_mc_trace : nullptr;
+    const double pc = bld_std_step(p, d, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); },
+                                   [&](int slot) { mc_trace<TR>(tr, slot); });
 #pragma unroll
     for (int z = 0; z < 5; ++z) x[z * n + e] = (S)xs[z];
     pcons[e] = (S)pc;
@@ -522,24 +543,6 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
 }
 
 // ====================================================================== fused MC step
-// Debug phase trace (pgw_debug_mc_trace): the TR instantiations of k_mc_step
-// and k_ma_step have lane 0 of every wave record wall_clock64() (100 MHz) at
-// its phase boundaries into g_mc_trace[(block * 8 + wave) * 8 + slot]; the
-// product launches the TR = false kernels, which hold no trace code at all.
-// Slots: 0 entry, 1 after the block's staging barrier, 2 the wave's component
-// (or walk group) done, 3 after the split barrier, 4 the EV fold and finish
-// done, 5 after the final barrier, 6 the sums written (wave 0).
-__device__ long long* g_mc_trace = nullptr;
-template <bool TR>
-__device__ __forceinline__ void mc_trace(long long* tr, int slot) {
-  if constexpr (TR) {
-    if ((threadIdx.x & 63) == 0) {
-      typedef __attribute__((address_space(1))) long long* gptr;
-      ((gptr)tr)[((int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + slot] = wall_clock64();
-    }
-  }
-}
-
 // One component of an MC agent for env e; writes its real power (and its
 // reward where it has one) to the component's own buffers.
 // `V`: the step's shared values -- the launch's own fields (pgw_mc_step_args)
@@ -555,7 +558,7 @@ template <> struct McStore<pgw_mc_step_args_f32> {
 };
 static_assert(sizeof(pgw_mc_step_args_f32) == sizeof(pgw_mc_step_args), "pgw_mc_step_args_f32 layout");
 
-template <bool STD, class Args, class V, class Comp>
+template <bool STD, bool TR, class Args, class V, class Comp>
 __device__ __forceinline__ RpRew mc_component(const Args& a, const V& v, const Comp& C,
                                               const BldDerived& d, int64_t n, int64_t e) {
   using S = typename McStore<Args>::S;
@@ -563,7 +566,7 @@ __device__ __forceinline__ RpRew mc_component(const Args& a, const V& v, const C
   switch (C.kind) {
     case PGW_MC_BUILDING: {
       double fresh = 0.0;
-      const S pc = (S)building_step_env<STD, S, Mt>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action,
+      const S pc = (S)building_step_env<STD, S, Mt, TR>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action,
                                                     a.bld_x, C.real_power, (S*)nullptr, a.bld_reward_state,
                                                     0, a.bld_ext, C.obs, &fresh);
       return {(double)pc, fresh};
@@ -700,9 +703,9 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
       const auto& C = a.comp[w];
       RpRew r;
       if constexpr (CLK)
-        r = mc_component<STD>(a, s_dyn, C, d, n, e);
+        r = mc_component<STD, TR>(a, s_dyn, C, d, n, e);
       else
-        r = mc_component<STD>(a, a, C, d, n, e);
+        r = mc_component<STD, TR>(a, a, C, d, n, e);
       s_rp[w][lane] = r.rp;
       s_rew[w][lane] = r.rew;
     }
@@ -759,7 +762,7 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
     if (kind0 == PGW_MC_BUILDING) {
       const pgw_mc_component& C = a.comp[c0];
       double fresh = 0.0;                             // the fresh reward (MC semantics)
-      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e,
+      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat, TR>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e,
                                                                C.action, a.bld_x, C.real_power, nullptr,
                                                                a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh);
       s_rew[c0][lane] = fresh;

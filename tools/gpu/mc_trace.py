@@ -26,7 +26,7 @@ dev = torch.device("cuda:0")
 
 
 def summarize(tag, buf, n_waves, roles, extra=""):
-    t = buf.view(-1, 8, 8)[:, :n_waves].cpu().numpy().astype(np.float64) / 100.0   # us
+    t = buf.view(-1, 16, 8)[:, :n_waves].cpu().numpy().astype(np.float64) / 100.0   # us
     t0 = t[:, :, 0].min()
     start = t[:, :, 0].min(1) - t0                     # block start
     end = t[:, 0, 6] - t0                              # wave 0's sums written
@@ -36,9 +36,16 @@ def summarize(tag, buf, n_waves, roles, extra=""):
         tag, extra, end.max(), np.median(start), start.max(), np.median(end - start), (end - start).max())
     for w in range(n_waves):
         line += " %s %.2f/%.2f" % (roles[w], np.median(comp[:, w]), comp[:, w].max())
-    if t.shape[1] > 0 and np.isfinite(t[:, :, 4]).all() and (t[:, :, 4] > 0).any():
-        fold = t[:, :, 4].max(1) - t[:, :, 3].max(1)
+    raw = buf.view(-1, 16, 8)[:, :n_waves].cpu().numpy()
+    if (raw[:, :, 4] != 0).any():                     # the EV finisher: fold + finish after its own walk
+        fin = raw[:, :, 4] != 0
+        fold = (np.where(fin, t[:, :, 4], 0).max(1) - np.where(fin, t[:, :, 2], 0).max(1))
         line += " | fold+finish %.2f" % np.median(fold)
+    bw = [w for w in range(n_waves) if (raw[:, w, 3] != 0).all()]
+    if bw:                                            # the building wave's phases
+        w = bw[0]
+        line += " | bld loads %.2f state+reward %.2f obs %.2f" % (
+            np.median(t[:, w, 3] - t[:, w, 0]), np.median(t[:, w, 7] - t[:, w, 3]), np.median(t[:, w, 2] - t[:, w, 7]))
     crit = np.bincount(np.argmax(t[:, :, 2], 1), minlength=n_waves)
     line += " | last-to-finish wave counts %s" % crit.tolist()
     print(line, flush=True)
@@ -50,7 +57,7 @@ def c3(every):
     n = 16384
     env, acts = c3_env(dev, n)
     env.reset()
-    buf = torch.zeros((n // 64) * 64, dtype=torch.int64, device=dev)
+    buf = torch.zeros((n // 64) * 128, dtype=torch.int64, device=dev)
     spans = []
     _lib.check(_lib.lib().pgw_debug_mc_trace(_lib.dptr(buf)))
     try:
@@ -58,7 +65,7 @@ def c3(every):
             buf.zero_()
             env.step(acts[k % len(acts)])
             torch.cuda.synchronize()
-            t = buf.view(-1, 8, 8).cpu().numpy()
+            t = buf.view(-1, 16, 8).cpu().numpy()
             nw = int((t[0, :, 0] != 0).sum())
             if k % every == 0:
                 roles = (["bld", "pv", "sto", "ev0"] + ["ev%d" % g for g in range(1, 8)])[:nw]
@@ -87,7 +94,7 @@ def het(every):
     kind_name = {0: "bld", 1: "pv", 2: "sto", 3: "ev"}
     roles = ["+".join(kind_name[args.comp[args.wave_slot[args.wave_first[w] + i]].kind]
                       for i in range(args.wave_count[w])) for w in range(args.n_waves)]
-    buf = torch.zeros((n // 64) * 64, dtype=torch.int64, device=dev)
+    buf = torch.zeros((n // 64) * 128, dtype=torch.int64, device=dev)
     spans = []
     _lib.check(_lib.lib().pgw_debug_mc_trace(_lib.dptr(buf)))
     try:
@@ -95,7 +102,7 @@ def het(every):
             buf.zero_()
             env.step(acts[k % len(acts)])
             torch.cuda.synchronize()
-            t = buf.view(-1, 8, 8).cpu().numpy()
+            t = buf.view(-1, 16, 8).cpu().numpy()
             nw = int((t[0, :, 0] != 0).sum())
             if k % every == 0:
                 spans.append(summarize("HET step %3d" % k, buf, nw, roles, "waves %d" % nw))
