@@ -428,13 +428,27 @@ template <int M>
 __device__ __forceinline__ bool pf_rows_stage(const pgw_pf_tables& t, int n_out, double* s) {
   constexpr int S = 16 * PFRow<M>::kPairs;
   if (n_out * S > kRowsLds || n_out <= 1) return false;   // uniform
-  for (int i = threadIdx.x; i < n_out * S; i += kBlock) {
-    const int o = i / S, j = i - o * S;
-    double v = 0.0;
-    if (j < 2) v = t.V0[2 * o + j];
-    else if (j < 2 + M) v = t.G[2 * M * o + 2 * (j - 2)];
-    else if (j < 2 + 2 * M) v = t.G[2 * M * o + 2 * (j - 2 - M) + 1];
-    s[i] = v;
+  // four entries per lane in flight per pass (branch-free sources), then
+  // their LDS stores: one L2 round trip per 4 kBlock entries instead of one
+  // per kBlock (the rolled loop waited for each load before the next)
+  constexpr int kQ = 4;
+  const int total = n_out * S;
+  for (int base = 0; base < total; base += kQ * kBlock) {   // uniform
+    double v[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const int i = base + q * kBlock + threadIdx.x;
+      const int o = i / S, j = i - o * S;
+      const bool has = i < total && j < 2 + 2 * M;
+      const double* p = j < 2 ? t.V0 + (2 * o + j)
+                              : t.G + (2 * M * o + (j < 2 + M ? 2 * (j - 2) : 2 * (j - 2 - M) + 1));
+      v[q] = has ? *p : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const int i = base + q * kBlock + threadIdx.x;
+      if (i < total) s[i] = v[q];
+    }
   }
   return true;
 }
