@@ -145,9 +145,39 @@ __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p
   if (rstate) rstate[e] = (S)building_reward(p, T, ex0.comfort_lb, ex0.comfort_ub, 0.0);
 }
 
+// The fused kernels' building wave reads its parameters (pgw_building_params,
+// BldDerived: ~1.6 KB) from LDS: from the kernel-argument segment they are ~30
+// dependent scalar loads, each waited for before its use (the SGPRs cannot hold
+// them all), and the phase trace put the step at 8.6 us, 4.5 of them the obs
+// loop (tools/gpu/mc_trace.py).  The wave copies them itself -- its 64 lanes
+// issue the copy together with the step's own HBM loads, one round trip for
+// both -- so no block barrier is involved.
+__device__ __forceinline__ void bld_stage_wave(const pgw_building_params& p, const BldDerived& d,
+                                               pgw_building_params& sp, BldDerived& sd, int lane) {
+  constexpr int kP = (int)(sizeof(pgw_building_params) / 8), kD = (int)(sizeof(BldDerived) / 8);
+  static_assert(sizeof(pgw_building_params) % 8 == 0 && sizeof(BldDerived) % 8 == 0, "staged as doubles");
+  double v[(kP + kD + 63) / 64];
+#pragma unroll
+  for (int k = 0; k < (kP + kD + 63) / 64; ++k) {
+    const int i = lane + 64 * k;
+    v[k] = i < kP ? reinterpret_cast<const double*>(&p)[i]
+                  : i < kP + kD ? reinterpret_cast<const double*>(&d)[i - kP] : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < (kP + kD + 63) / 64; ++k) {
+    const int i = lane + 64 * k;
+    if (i < kP) reinterpret_cast<double*>(&sp)[i] = v[k];
+    else if (i < kP + kD) reinterpret_cast<double*>(&sd)[i - kP] = v[k];
+  }
+  // (one wave: its LDS operations complete in order; the fence keeps the
+  // compiler from moving the other lanes' reads above these writes)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 // One env's FiveZoneROMEnv.step_ (:183-225); returns p_consumed (its real power).
 // STD: the reference's default model/obs layout (bld_is_std), via bld_std_step.
-template <bool STD, class S = double, class Mt = pgw_mat, bool TR = false>
+// SP: the parameters are staged into LDS (sp, sd) by the calling wave first.
+template <bool STD, class S = double, class Mt = pgw_mat, bool TR = false, bool SP = false>
 __device__ __forceinline__ double building_step_env(const pgw_building_params& p, const BldDerived& d,
                                                     const pgw_building_exo& ex,
                                                     const pgw_building_exo& exn, int64_t n, int64_t e,
@@ -155,15 +185,19 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
                                                     S* __restrict__ pcons, S* __restrict__ rout,
                                                     S* __restrict__ rstate, int32_t lagged,
                                                     const pgw_building_ext& ext, const Mt& obs,
-                                                    double* fresh_out = nullptr) {
+                                                    double* fresh_out = nullptr,
+                                                    pgw_building_params* sp = nullptr, BldDerived* sd = nullptr) {
   if constexpr (STD) {
     double av[6], xs[5], fresh;
 #pragma unroll
     for (int j = 0; j < 6; ++j) av[j] = ld(act, e, j);
 #pragma unroll
     for (int z = 0; z < 5; ++z) xs[z] = x[z * n + e];
+    if constexpr (SP) bld_stage_wave(p, d, *sp, *sd, (int)(threadIdx.x & 63));
+    const pgw_building_params& P = SP ? *sp : p;
+    const BldDerived& D = SP ? *sd : d;
     long long* const tr = TR ? g_mc_trace : nullptr;
-    const double pc = bld_std_step(p, d, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); },
+    const double pc = bld_std_step(P, D, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); },
                                    [&](int slot) { mc_trace<TR>(tr, slot); });
 #pragma unroll
     for (int z = 0; z < 5; ++z) x[z * n + e] = (S)xs[z];
@@ -560,15 +594,16 @@ static_assert(sizeof(pgw_mc_step_args_f32) == sizeof(pgw_mc_step_args), "pgw_mc_
 
 template <bool STD, bool TR, class Args, class V, class Comp>
 __device__ __forceinline__ RpRew mc_component(const Args& a, const V& v, const Comp& C,
-                                              const BldDerived& d, int64_t n, int64_t e) {
+                                              const BldDerived& d, int64_t n, int64_t e,
+                                              pgw_building_params* sp, BldDerived* sd) {
   using S = typename McStore<Args>::S;
   using Mt = typename McStore<Args>::Mt;
   switch (C.kind) {
     case PGW_MC_BUILDING: {
       double fresh = 0.0;
-      const S pc = (S)building_step_env<STD, S, Mt, TR>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action,
-                                                    a.bld_x, C.real_power, (S*)nullptr, a.bld_reward_state,
-                                                    0, a.bld_ext, C.obs, &fresh);
+      const S pc = (S)building_step_env<STD, S, Mt, TR, true>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e,
+                                                          C.action, a.bld_x, C.real_power, (S*)nullptr,
+                                                          a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh, sp, sd);
       return {(double)pc, fresh};
     }
     case PGW_MC_PV: {
@@ -632,6 +667,8 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   __shared__ double s_evs[kEvGroups][4][64];
   __shared__ int s_evc[kEvGroups][2][64];
   __shared__ int s_arrive;
+  __shared__ pgw_building_params s_bp;                // the building wave's parameters (bld_stage_wave)
+  __shared__ BldDerived s_bd;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
@@ -703,9 +740,9 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
       const auto& C = a.comp[w];
       RpRew r;
       if constexpr (CLK)
-        r = mc_component<STD, TR>(a, s_dyn, C, d, n, e);
+        r = mc_component<STD, TR>(a, s_dyn, C, d, n, e, &s_bp, &s_bd);
       else
-        r = mc_component<STD, TR>(a, a, C, d, n, e);
+        r = mc_component<STD, TR>(a, a, C, d, n, e, &s_bp, &s_bd);
       s_rp[w][lane] = r.rp;
       s_rew[w][lane] = r.rew;
     }
@@ -749,6 +786,8 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
   long long* const tr = TR ? g_mc_trace : nullptr;
   mc_trace<TR>(tr, 0);
   __shared__ double s_rp[PGW_MA_MAX_SLOTS][64], s_rew[PGW_MA_MAX_SLOTS][64];
+  __shared__ pgw_building_params s_bp;                // the building wave's parameters (bld_stage_wave)
+  __shared__ BldDerived s_bd;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
@@ -762,9 +801,10 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
     if (kind0 == PGW_MC_BUILDING) {
       const pgw_mc_component& C = a.comp[c0];
       double fresh = 0.0;                             // the fresh reward (MC semantics)
-      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat, TR>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e,
-                                                               C.action, a.bld_x, C.real_power, nullptr,
-                                                               a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh);
+      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat, TR, true>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n,
+                                                                     e, C.action, a.bld_x, C.real_power, nullptr,
+                                                                     a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh,
+                                                                     &s_bp, &s_bd);
       s_rew[c0][lane] = fresh;
     } else if (kind0 == PGW_MC_EV) {
       const pgw_mc_component& C = a.comp[c0];
