@@ -109,6 +109,13 @@ __device__ __forceinline__ void mc_trace(long long* tr, int slot) {
   }
 }
 
+// A component's real power and reward as stored (S-rounded), handed to the
+// block's sums in registers: reading the component's own stores back cost a
+// store-to-load round trip at the end of every component wave.
+struct RpRew {
+  double rp, rew;
+};
+
 // ====================================================================== building
 template <class S, class Mt>
 __global__ void __launch_bounds__(kBlock) k_building_reset(pgw_building_params p, pgw_building_exo ex0,
@@ -174,10 +181,65 @@ __device__ __forceinline__ void bld_stage_wave(const pgw_building_params& p, con
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// The std building step in two parts: its per-env inputs (the 6 actions, x_k)
+// and the step from them, so that the fused kernels' building wave can issue
+// the inputs' HBM loads together with its parameter staging (bld_stage_wave).
+struct BldIn {
+  double av[6], xs[5];
+};
+template <class S, class Mt>
+__device__ __forceinline__ void bld_std_load(int64_t n, int64_t e, const Mt& act, const S* __restrict__ x,
+                                             BldIn& in) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) in.av[j] = ld(act, e, j);
+#pragma unroll
+  for (int z = 0; z < 5; ++z) in.xs[z] = x[z * n + e];
+}
+template <class S, class Mt, bool TR = false>
+__device__ __forceinline__ double bld_std_from(const pgw_building_params& p, const BldDerived& d,
+                                               const pgw_building_exo& ex, const pgw_building_exo& exn,
+                                               int64_t n, int64_t e, BldIn& in, S* __restrict__ x,
+                                               S* __restrict__ pcons, S* __restrict__ rout,
+                                               S* __restrict__ rstate, int32_t lagged, const Mt& obs,
+                                               double* fresh_out) {
+  double fresh;
+  long long* const tr = TR ? g_mc_trace : nullptr;
+  const double pc = bld_std_step(p, d, ex, exn, in.av, in.xs, fresh, [&](int j, double v) { st(obs, e, j, v); },
+                                 [&](int slot) { mc_trace<TR>(tr, slot); });
+#pragma unroll
+  for (int z = 0; z < 5; ++z) x[z * n + e] = (S)in.xs[z];
+  pcons[e] = (S)pc;
+  if (rout) rout[e] = lagged ? rstate[e] : (S)fresh;
+  if (rstate) rstate[e] = (S)fresh;
+  if (fresh_out) *fresh_out = (double)(S)fresh;
+  return pc;
+}
+
+// The fused kernels' std building wave (all its lanes, e < n or not: every
+// lane copies its share of the parameters): inputs and parameter copy in one
+// round trip, then the step from LDS.  Returns the stored (p_consumed, reward).
+template <class S, class Mt, bool TR>
+__device__ __forceinline__ RpRew bld_wave_std(const pgw_building_params& p, const BldDerived& d,
+                                              pgw_building_params& sp, BldDerived& sd,
+                                              const pgw_building_exo& ex, const pgw_building_exo& exn,
+                                              int64_t n, int64_t e, const Mt& act, S* __restrict__ x,
+                                              S* __restrict__ pcons, S* __restrict__ rstate, const Mt& obs) {
+  BldIn in;
+  if (e < n) bld_std_load(n, e, act, x, in);
+  bld_stage_wave(p, d, sp, sd, (int)(threadIdx.x & 63));
+  RpRew r{0.0, 0.0};
+  if (e < n) {
+    double fresh = 0.0;
+    const S pc = (S)bld_std_from<S, Mt, TR>(sp, sd, ex, exn, n, e, in, x, pcons, (S*)nullptr, rstate, 0, obs,
+                                            &fresh);
+    r = {(double)pc, fresh};
+  }
+  return r;
+}
+
 // One env's FiveZoneROMEnv.step_ (:183-225); returns p_consumed (its real power).
 // STD: the reference's default model/obs layout (bld_is_std), via bld_std_step.
-// SP: the parameters are staged into LDS (sp, sd) by the calling wave first.
-template <bool STD, class S = double, class Mt = pgw_mat, bool TR = false, bool SP = false>
+template <bool STD, class S = double, class Mt = pgw_mat, bool TR = false>
 __device__ __forceinline__ double building_step_env(const pgw_building_params& p, const BldDerived& d,
                                                     const pgw_building_exo& ex,
                                                     const pgw_building_exo& exn, int64_t n, int64_t e,
@@ -185,27 +247,11 @@ __device__ __forceinline__ double building_step_env(const pgw_building_params& p
                                                     S* __restrict__ pcons, S* __restrict__ rout,
                                                     S* __restrict__ rstate, int32_t lagged,
                                                     const pgw_building_ext& ext, const Mt& obs,
-                                                    double* fresh_out = nullptr,
-                                                    pgw_building_params* sp = nullptr, BldDerived* sd = nullptr) {
+                                                    double* fresh_out = nullptr) {
   if constexpr (STD) {
-    double av[6], xs[5], fresh;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) av[j] = ld(act, e, j);
-#pragma unroll
-    for (int z = 0; z < 5; ++z) xs[z] = x[z * n + e];
-    if constexpr (SP) bld_stage_wave(p, d, *sp, *sd, (int)(threadIdx.x & 63));
-    const pgw_building_params& P = SP ? *sp : p;
-    const BldDerived& D = SP ? *sd : d;
-    long long* const tr = TR ? g_mc_trace : nullptr;
-    const double pc = bld_std_step(P, D, ex, exn, av, xs, fresh, [&](int j, double v) { st(obs, e, j, v); },
-                                   [&](int slot) { mc_trace<TR>(tr, slot); });
-#pragma unroll
-    for (int z = 0; z < 5; ++z) x[z * n + e] = (S)xs[z];
-    pcons[e] = (S)pc;
-    if (rout) rout[e] = lagged ? rstate[e] : (S)fresh;
-    if (rstate) rstate[e] = (S)fresh;
-    if (fresh_out) *fresh_out = (double)(S)fresh;
-    return pc;
+    BldIn in;
+    bld_std_load(n, e, act, x, in);
+    return bld_std_from<S, Mt, TR>(p, d, ex, exn, n, e, in, x, pcons, rout, rstate, lagged, obs, fresh_out);
   }
   double a[6], xs[5], T[5];
   bool bad = false;
@@ -494,13 +540,6 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
   return t;
 }
 
-// A component's real power and reward as stored (S-rounded), handed to the
-// block's sums in registers: reading the component's own stores back cost a
-// store-to-load round trip at the end of every component wave.
-struct RpRew {
-  double rp, rew;
-};
-
 // The step's state, reward and obs from the walk's totals (:253-262, :135-142).
 template <class S, class Mt>
 __device__ __forceinline__ RpRew ev_finish(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t e,
@@ -594,16 +633,15 @@ static_assert(sizeof(pgw_mc_step_args_f32) == sizeof(pgw_mc_step_args), "pgw_mc_
 
 template <bool STD, bool TR, class Args, class V, class Comp>
 __device__ __forceinline__ RpRew mc_component(const Args& a, const V& v, const Comp& C,
-                                              const BldDerived& d, int64_t n, int64_t e,
-                                              pgw_building_params* sp, BldDerived* sd) {
+                                              const BldDerived& d, int64_t n, int64_t e) {
   using S = typename McStore<Args>::S;
   using Mt = typename McStore<Args>::Mt;
   switch (C.kind) {
     case PGW_MC_BUILDING: {
       double fresh = 0.0;
-      const S pc = (S)building_step_env<STD, S, Mt, TR, true>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e,
-                                                          C.action, a.bld_x, C.real_power, (S*)nullptr,
-                                                          a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh, sp, sd);
+      const S pc = (S)building_step_env<STD, S, Mt, TR>(a.bld, d, v.bld_ex_t, v.bld_ex_next, n, e, C.action,
+                                                    a.bld_x, C.real_power, (S*)nullptr, a.bld_reward_state,
+                                                    0, a.bld_ext, C.obs, &fresh);
       return {(double)pc, fresh};
     }
     case PGW_MC_PV: {
@@ -735,14 +773,26 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
       }
       mc_trace<TR>(tr, 4);
     }
+  } else if (STD && a.comp[w].kind == PGW_MC_BUILDING) {   // (uniform) the std building: bld_wave_std
+    using Mt = typename McStore<Args>::Mt;
+    const auto& C = a.comp[w];
+    const pgw_building_exo& ex = CLK ? s_dyn.bld_ex_t : a.bld_ex_t;
+    const pgw_building_exo& exn = CLK ? s_dyn.bld_ex_next : a.bld_ex_next;
+    const RpRew r = bld_wave_std<S, Mt, TR>(a.bld, d, s_bp, s_bd, ex, exn, n, e, C.action, a.bld_x,
+                                            C.real_power, a.bld_reward_state, C.obs);
+    if (e < n) {
+      s_rp[w][lane] = r.rp;
+      s_rew[w][lane] = r.rew;
+    }
+    mc_trace<TR>(tr, 2);
   } else {
     if (e < n) {
       const auto& C = a.comp[w];
       RpRew r;
       if constexpr (CLK)
-        r = mc_component<STD, TR>(a, s_dyn, C, d, n, e, &s_bp, &s_bd);
+        r = mc_component<STD, TR>(a, s_dyn, C, d, n, e);
       else
-        r = mc_component<STD, TR>(a, a, C, d, n, e, &s_bp, &s_bd);
+        r = mc_component<STD, TR>(a, a, C, d, n, e);
       s_rp[w][lane] = r.rp;
       s_rew[w][lane] = r.rew;
     }
@@ -797,14 +847,22 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
   // spilling SGPRs: 10 us for a PV-only step)
   const int c0 = a.wave_slot[a.wave_first[wv]];
   const int kind0 = a.comp[c0].kind;
-  if (e < n) {
+  if (STD && kind0 == PGW_MC_BUILDING) {           // (uniform) every lane stages: bld_wave_std
+    const pgw_mc_component& C = a.comp[c0];
+    const RpRew r = bld_wave_std<double, pgw_mat, TR>(a.bld, d, s_bp, s_bd, a.bld_ex_t, a.bld_ex_next, n, e,
+                                                      C.action, a.bld_x, C.real_power, a.bld_reward_state, C.obs);
+    if (e < n) {
+      s_rp[c0][lane] = r.rp;
+      s_rew[c0][lane] = r.rew;                      // the fresh reward (MC semantics)
+    }
+  } else if (e < n) {
     if (kind0 == PGW_MC_BUILDING) {
       const pgw_mc_component& C = a.comp[c0];
       double fresh = 0.0;                             // the fresh reward (MC semantics)
-      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat, TR, true>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n,
-                                                                     e, C.action, a.bld_x, C.real_power, nullptr,
-                                                                     a.bld_reward_state, 0, a.bld_ext, C.obs, &fresh,
-                                                                     &s_bp, &s_bd);
+      s_rp[c0][lane] = building_step_env<STD, double, pgw_mat, TR>(a.bld, d, a.bld_ex_t, a.bld_ex_next, n, e,
+                                                                   C.action, a.bld_x, C.real_power, nullptr,
+                                                                   a.bld_reward_state, 0, a.bld_ext, C.obs,
+                                                                   &fresh);
       s_rew[c0][lane] = fresh;
     } else if (kind0 == PGW_MC_EV) {
       const pgw_mc_component& C = a.comp[c0];
