@@ -345,6 +345,14 @@ enum { kEvTable = 0, kEvPerEnv = 1, kEvDivide = 2 };
 // pairwise from 8 elements on.  With more than one group the totals here are
 // ((p0 + p1) + p2) + p3 instead, a rounding difference of an ulp or so: the
 // goldens compare at rtol 1e-12, the north star allows 1e-6.)
+// A lane's double, read by the whole wave from lane l (uniform): two
+// v_readlane_b32 into SGPRs.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 constexpr int kEvChunk = 8;
 constexpr int kEvGroups = 8;
 struct EvSums {
@@ -428,6 +436,20 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
     const uint64_t win = s.window[w];
     const uint64_t prev = chg[(int64_t)w * n + e];
     uint64_t now_bits = 0ull;
+    // kEvTable: the word's 64 table entries, one per lane (a coalesced 1 KB
+    // load with the first chunks' requirements); vehicle b's pair is then
+    // read from lane b (readlane, no memory operation), where a 16-byte
+    // broadcast load per vehicle doubled the chunk's memory instructions and
+    // held 4 VGPRs per vehicle in flight
+    double lane_tl = 0.0, lane_rc = 0.0;
+    if constexpr (MODE == kEvTable) {
+      const int vl = w * 64 + (int)(threadIdx.x & 63);
+      if (vl < p.n_vehicles) {
+        const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[vl];
+        lane_tl = q.x;
+        lane_rc = q.y;
+      }
+    }
     // the chunk's loads all go out before any is used: the requirements
     // (vector) and the vehicles' time left (uniform: scalar loads)
     auto load = [&](Chunk& C) {
@@ -442,15 +464,9 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
           C.tls[i] = (en - s.time) / 60.0;
           C.rcs[i] = 0.0;
           C.wins[i] = (s.time >= s.env_start[(int64_t)v * n + e]) && (s.time <= floor(en));
-        } else if constexpr (MODE == kEvTable) { // host table: the same IEEE quotient, and its reciprocal
-          // a VECTOR load of the (uniform) entry: it returns in order with the
-          // chunk's requirement loads (vmcnt), where scalar loads return out of
-          // order and made every chunk wait for all of them (lgkmcnt(0))
-          int vv = v;
-          asm volatile("" : "+v"(vv));
-          const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[vv];
-          C.tls[i] = q.x;
-          C.rcs[i] = q.y;
+        } else if constexpr (MODE == kEvTable) { // host table: read at use (process), from its lane
+          C.tls[i] = 0.0;
+          C.rcs[i] = 0.0;
         } else {
           C.tls[i] = (endp[v] - s.time) / 60.0;
           C.rcs[i] = 0.0;
@@ -480,7 +496,9 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         const int b = in ? __builtin_ctzll(m) : 0;
         m &= m - 1;
         const int v = w * 64 + b;
-        const double r = C.rs[i], tl = C.tls[i], rc = C.rcs[i];
+        const double r = C.rs[i];
+        const double tl = MODE == kEvTable ? readlane_f64(lane_tl, b) : C.tls[i];
+        const double rc = MODE == kEvTable ? readlane_f64(lane_rc, b) : C.rcs[i];
         act[i] = in && C.wins[i] && (r > 0.0);
         chg_now[i] = act[i] && (tl > 0.0);
         dep[i] = in && !act[i] && ((prev >> b) & 1ull);   // departed: not charging now (:239-243)
@@ -507,19 +525,25 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         unserved = dep[i] ? unserved + C.rs[i] : unserved;
       }
     };
-    // two chunk buffers in turn: the next chunk's loads go out before the
-    // current chunk's stores (a copy `cur = next` would wait for them)
-    Chunk A, B;
-    A.bits = take_mine();
-    if (A.bits) load(A);
-    while (A.bits) {
-      B.bits = take_mine();
-      if (B.bits) load(B);
-      process(A);
-      if (!B.bits) break;
+    // chunks in pairs: both chunks' loads go out before either is processed
+    // (unconditionally: an empty second chunk reloads vehicle w*64, harmless),
+    // then the two are processed in order -- one memory round trip per pair.
+    // (A rotating two-buffer pipeline, the next pair's loads before this
+    // pair's processing, compiled to one round trip per chunk: the
+    // per-wave phase trace showed each chunk costing a full round trip.)
+    // (randomize's per-env tables load two more values per vehicle: one chunk
+    // at a time there, pairs spilled)
+    while (budget > 0) {                             // (uniform)
+      Chunk A, B;
       A.bits = take_mine();
-      if (A.bits) load(A);
-      process(B);
+      load(A);
+      if constexpr (MODE != kEvPerEnv) {
+        B.bits = take_mine();
+        load(B);
+      }
+      process(A);
+      if constexpr (MODE != kEvPerEnv)
+        if (B.bits) process(B);
     }
     if constexpr (SPLIT) {
       if (now_bits) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[w * 64 + lane]),
