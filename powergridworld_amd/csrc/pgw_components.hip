@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   __shared__ uint64_t s_bits[PGW_EV_MAX_WORDS * 64];
   __shared__ double s_evs[kEvGroups][4][64];
   __shared__ int s_evc[kEvGroups][2][64];
-  __shared__ int s_arrive;
+  __shared__ int s_arrive, s_done;
   __shared__ pgw_building_params s_bp;                // the building wave's parameters (bld_stage_wave)
   __shared__ BldDerived s_bd;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // component slot
@@ -739,7 +739,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   for (int c = 0; c < a.n_comp; ++c) ev_slot = a.comp[c].kind == PGW_MC_EV ? c : ev_slot;
   if (split) {
     for (int i = threadIdx.x; i < PGW_EV_MAX_WORDS * 64; i += blockDim.x) s_bits[i] = 0ull;
-    if (threadIdx.x == 0) s_arrive = 0;
+    if (threadIdx.x == 0) s_arrive = s_done = 0;
   }
   // CLK: the step's record staged in LDS by the block (80 doubles): its
   // fields are then read at fixed LDS addresses, with no pointer to keep live
@@ -822,10 +822,22 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
     }
     mc_trace<TR>(tr, 2);
   }
-  __syncthreads();
+  // the sums: split blocks let the wave that finishes last form them (an
+  // arrival count as for the EV fold), so the light waves leave at once
+  // instead of waiting at a barrier for the walk; unsplit ones use wave 0
+  if (split) {
+    int prior = 0;
+    if (lane == 0) prior = __hip_atomic_fetch_add(&s_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prior = __builtin_amdgcn_readfirstlane(prior);
+    if (prior != (int)(blockDim.x >> 6) - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    __syncthreads();
+  }
   mc_trace<TR>(tr, 5);
-  if (CLK && threadIdx.x == 0) a.clock[blockIdx.x] = k + 1;    // (every wave read k before the barrier)
-  if (w != 0 || e >= n) return;
+  // (every wave read k before the staging barrier)
+  if (CLK && lane == 0 && (split || w == 0)) a.clock[blockIdx.x] = k + 1;
+  if ((!split && w != 0) || e >= n) return;
   double rp_sum = 0.0, rew_sum = 0.0;
   for (int c = 0; c < a.n_comp; ++c) {
     rp_sum = rp_sum + s_rp[c][lane];

@@ -29,7 +29,8 @@ def summarize(tag, buf, n_waves, roles, extra=""):
     t = buf.view(-1, 16, 8)[:, :n_waves].cpu().numpy().astype(np.float64) / 100.0   # us
     t0 = t[:, :, 0].min()
     start = t[:, :, 0].min(1) - t0                     # block start
-    end = t[:, 0, 6] - t0                              # wave 0's sums written
+    raw6 = buf.view(-1, 16, 8)[:, :n_waves, 6].cpu().numpy()
+    end = np.where(raw6 != 0, t[:, :, 6], -np.inf).max(1) - t0   # the sums written (by whichever wave)
     comp = t[:, :, 2] - t[:, :, 0]                     # each wave's own work
     wait = t[:, :, 5] - t[:, :, 2]                     # each wave's wait at the barriers
     line = "%s %s span %.2f  block start p50 %.2f max %.2f  block life p50 %.2f max %.2f |" % (
