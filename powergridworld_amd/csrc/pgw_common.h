@@ -430,13 +430,22 @@ __device__ __forceinline__ double bld_std_step(const pgw_building_params& B, con
   reward = building_reward(B, T, exn.comfort_lb, exn.comfort_ub, pc, exact_div(-pc, 12.0, 1.0 / 12.0));
   stamp(7);                        // (debug trace: state, power and reward done)
   const double lb = exn.comfort_lb, ub = exn.comfort_ub;
+  // (the rescale test hoisted out of the loop: a branch per slot kept the
+  // compiler from reading the next slots' bounds ahead -- two waited LDS
+  // round trips per slot when the parameters are staged in LDS)
+  auto obs_value = [&](int j) {
+    return j < 5 ? T[j] - ub : j < 10 ? lb - T[j - 5] : j == 10 ? lb
+         : j == 11 ? ub : j == 12 ? exn.T_oa : j == 13 ? pc : exn.time_of_day;
+  };
+  if (B.rescale) {
 #pragma unroll
-  for (int j = 0; j < 15; ++j) {
-    const double o = j < 5 ? T[j] - ub : j < 10 ? lb - T[j - 5] : j == 10 ? lb
-                   : j == 11 ? ub : j == 12 ? exn.T_oa : j == 13 ? pc : exn.time_of_day;
-    double c = clip_fast(o, B.obs_low[j], B.obs_high[j]);
-    if (B.rescale) c = exact_div(2.0 * c - d.obs_sum[j], d.obs_rng[j], d.obs_rcp[j]);
-    store(j, c);
+    for (int j = 0; j < 15; ++j) {
+      const double c = clip_fast(obs_value(j), B.obs_low[j], B.obs_high[j]);
+      store(j, exact_div(2.0 * c - d.obs_sum[j], d.obs_rng[j], d.obs_rcp[j]));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 15; ++j) store(j, clip_fast(obs_value(j), B.obs_low[j], B.obs_high[j]));
   }
   return pc;
 }
