@@ -2,6 +2,7 @@
 // One thread per env; env-minor SoA state, so every per-env load/store of a
 // field is a contiguous, fully coalesced 512-B wave access.
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -863,6 +864,25 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
 // the light PV / storage slots share one (pgw_ma_step_args.wave_*): a wave per
 // slot made the heterogeneous scenario's blocks 5 waves, which at the kernel's
 // register count did not all fit at once.
+// The agents' and buses' part of pgw_ma_step_args (n_agents .. bus_p), as laid
+// out there: copied whole into LDS for the sums.
+struct MaSums {
+  int32_t n_agents, n_bus;
+  int32_t first[PGW_MAX_AGENTS], count[PGW_MAX_AGENTS];
+  int32_t bus[PGW_MAX_AGENTS], sum[PGW_MAX_AGENTS];
+  double* rp[PGW_MAX_AGENTS];
+  double* rew[PGW_MAX_AGENTS];
+  double* bus_p;
+};
+static_assert(offsetof(pgw_ma_step_args, n_waves) - offsetof(pgw_ma_step_args, n_agents) == sizeof(MaSums) &&
+              offsetof(pgw_ma_step_args, n_agents) % 8 == 0 && sizeof(MaSums) % 8 == 0 && sizeof(MaSums) / 8 <= 64,
+              "MaSums mirrors pgw_ma_step_args");
+static_assert(offsetof(pgw_ma_step_args, agent_first) - offsetof(pgw_ma_step_args, n_agents) == offsetof(MaSums, first) &&
+              offsetof(pgw_ma_step_args, agent_sum) - offsetof(pgw_ma_step_args, n_agents) == offsetof(MaSums, sum) &&
+              offsetof(pgw_ma_step_args, agent_real_power) - offsetof(pgw_ma_step_args, n_agents) == offsetof(MaSums, rp) &&
+              offsetof(pgw_ma_step_args, bus_p) - offsetof(pgw_ma_step_args, n_agents) == offsetof(MaSums, bus_p),
+              "MaSums field offsets");
+
 // (3 waves per SIMD at least: the heterogeneous scenario's 1 024 three-wave
 // blocks then all fit at once, 4 per CU; at 2 they ran in two rounds)
 template <bool STD, bool TR = false>
@@ -874,7 +894,16 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
   __shared__ double s_rp[PGW_MA_MAX_SLOTS][64], s_rew[PGW_MA_MAX_SLOTS][64];
   __shared__ pgw_building_params s_bp;                // the building wave's parameters (bld_stage_wave)
   __shared__ BldDerived s_bd;
+  __shared__ MaSums s_sums;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // the sums' plan (agents' slots, buses, output pointers), read by wave 0
+  // after the barrier: staged here by the block's last wave (not the
+  // building's), so the tail is LDS reads, not ~40 waited scalar loads
+  if (wv == (int)(blockDim.x >> 6) - 1) {
+    constexpr int kW = (int)(sizeof(MaSums) / 8);
+    const int l = (int)(threadIdx.x & 63);
+    if (l < kW) reinterpret_cast<uint64_t*>(&s_sums)[l] = reinterpret_cast<const uint64_t*>(&a.n_agents)[l];
+  }
   const int lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
   // the wave's role, uniform: a building or an EV slot runs alone in its wave,
@@ -965,31 +994,32 @@ __global__ void __launch_bounds__(64 * PGW_MA_MAX_SLOTS) __attribute__((amdgpu_w
   __syncthreads();
   mc_trace<TR>(tr, 5);
   if (wv != 0 || e >= n) return;
+  const MaSums& m = s_sums;
   double ap[PGW_MAX_AGENTS];
 #pragma unroll
   for (int g = 0; g < PGW_MAX_AGENTS; ++g) {     // (constant indices: ap stays in registers)
     ap[g] = 0.0;
-    if (g >= a.n_agents) continue;
-    const int c0 = a.agent_first[g];
-    if (a.agent_sum[g]) {
+    if (g >= m.n_agents) continue;
+    const int c0 = m.first[g];
+    if (m.sum[g]) {
       double rp_sum = 0.0, rew_sum = 0.0;
-      for (int c = c0; c < c0 + a.agent_count[g]; ++c) {
+      for (int c = c0; c < c0 + m.count[g]; ++c) {
         rp_sum = rp_sum + s_rp[c][lane];
         rew_sum = rew_sum + s_rew[c][lane];
       }
-      a.agent_real_power[g][e] = rp_sum;
-      a.agent_reward[g][e] = rew_sum;
+      m.rp[g][e] = rp_sum;
+      m.rew[g][e] = rew_sum;
       ap[g] = rp_sum;
     } else {
       ap[g] = s_rp[c0][lane];
     }
   }
-  for (int b = 0; b < a.n_bus; ++b) {
+  for (int b = 0; b < m.n_bus; ++b) {
     double acc = 0.0;
 #pragma unroll
     for (int g = 0; g < PGW_MAX_AGENTS; ++g)
-      acc = (g < a.n_agents && a.agent_bus[g] == b) ? acc + ap[g] : acc;
-    a.bus_p[(int64_t)b * n + e] = acc;
+      acc = (g < m.n_agents && m.bus[g] == b) ? acc + ap[g] : acc;
+    m.bus_p[(int64_t)b * n + e] = acc;
   }
   mc_trace<TR>(tr, 6);
 }
