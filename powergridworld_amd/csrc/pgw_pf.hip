@@ -30,9 +30,13 @@
 #include <algorithm>
 #include <cmath>
 #include <type_traits>
+#include <atomic>
 #include <vector>
 
 #include "pgw_common.h"
+
+// pgw_debug_pf_trace set: k_coord_pf_od launches its trace instantiation
+static std::atomic<bool> g_pf_trace_on{false};
 
 namespace pgw {
 
@@ -1652,12 +1656,17 @@ __device__ __forceinline__ double* od_rows_put(ODShared<M>& sh, int n_out, const
 // Fused C4 step, OpenDSS rule: k_coord_pf's prologue (agent powers -> bus
 // load) and epilogue (output row 0 = the coordinated bus, violation, reward),
 // the snap solve in between.
-template <int M, class Bufs>
+// TR: the trace instantiation (pgw_debug_pf_trace set): phase stamps 0 entry,
+// 1 powers summed, 2 table lookup done, 3 past the fallback, 4 node 0, 5 rows,
+// 6 reward atomics issued.
+template <int M, class Bufs, bool TR = false>
 __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
                                                         int64_t n, Bufs b) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
+  long long* const tr = TR ? g_pf_trace : nullptr;
+  if constexpr (TR) pf_trace(tr, 0);
   __shared__ ODShared<M> sh;
   ODStage<M> stg;
   // without a response table every env solves: the stage loads go out first,
@@ -1688,14 +1697,18 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
     for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) cp[s] = (s == slot) ? cp[s] + rp[ag] : cp[s];
   }
   S.powers(a, cp, cq, 1.0);
+  if constexpr (TR) { if (S.pc != -1e300) pf_trace(tr, 1); }
   double ir[M], ii[M], v0r, v0i;
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
   int it = 0;
   const bool need = valid && !(o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it));
+  if constexpr (TR) { if (ir[0] != -1e300) pf_trace(tr, 2); }
   od_fallback<M>(S, o, o.start, stg, !early, sh, need, ir, ii, it);
+  if constexpr (TR) pf_trace(tr, 3);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  if constexpr (TR) { if (v0 != -1.0) pf_trace(tr, 4); }
   // rows 1.. (a history slot holds every node)
   double vsel = v0;
   const double* srow = rows_lds ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
@@ -1703,6 +1716,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
     if (valid && b.v_out) b.v_out[(int64_t)ro * n + e] = (Sto)v;
     vsel = (ro == c.vv_row) ? v : vsel;
   });
+  if constexpr (TR) { if (vsel != -1.0) pf_trace(tr, 5); }
   if (!valid) return;
   if (b.v_out) b.v_out[e] = (Sto)v0;
   if (b.iters) b.iters[e] = it;
@@ -1716,6 +1730,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
         (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
   }
+  if constexpr (TR) pf_trace(tr, 6);
 }
 
 // pgw_pf_solve, OpenDSS rule: k_pf_solve's prologue (the env's controllable
@@ -2177,8 +2192,12 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   if (rc) return rc;
   hipStream_t pst = st;
   if (pft->od) {
-    launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs>, dim3(grid_for(n)), dim3(kBlock), pst, c, a,
-                 make_od_args(*pft->od, pf->max_iter), *pft, n, b);
+    if (g_pf_trace_on.load())
+      launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs, true>, dim3(grid_for(n)), dim3(kBlock), pst, c, a,
+                   make_od_args(*pft->od, pf->max_iter), *pft, n, b);
+    else
+      launch_timed(PGW_T_COORD_PF, k_coord_pf_od<14, Bufs>, dim3(grid_for(n)), dim3(kBlock), pst, c, a,
+                   make_od_args(*pft->od, pf->max_iter), *pft, n, b);
     return check_launch("k_coord_pf_od");
   }
   PGW_PF_DISPATCH(*pf, *pft, launch_coord_pf, c, a, *pft, n, b, pst);
@@ -2330,6 +2349,7 @@ int32_t pgw_pf_pred_pack(const pgw_pf_params* p, int32_t n_tables, int32_t n_poi
 int32_t pgw_debug_pf_trace(long long* buf) {
   PGW_REQUIRE(hipMemcpyToSymbol(HIP_SYMBOL(g_pf_trace), &buf, sizeof(buf)) == hipSuccess,
               "pgw_debug_pf_trace: hipMemcpyToSymbol failed");
+  g_pf_trace_on.store(buf != nullptr);
   return PGW_OK;
 }
 
