@@ -354,6 +354,13 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(x >> 32), l);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// The host's time-left table is read by readlane (ev_walk), which needs every
+// lane of the wave walking; the grid's last, partial wave divides in the
+// kernel instead (kEvDivide: (end_park - t) / 60 and r / tl with the same IEEE
+// operations as the host table and exact_div -- the same values).
+__device__ __forceinline__ bool ev_table_ok(const pgw_ev_step_info& s) {
+  return s.tl_rcp != nullptr && __builtin_amdgcn_read_exec() == ~0ull;
+}
 constexpr int kEvChunk = 8;
 constexpr int kEvGroups = 8;
 struct EvSums {
@@ -441,7 +448,9 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
     // load with the first chunks' requirements); vehicle b's pair is then
     // read from lane b (readlane, no memory operation), where a 16-byte
     // broadcast load per vehicle doubled the chunk's memory instructions and
-    // held 4 VGPRs per vehicle in flight
+    // held 4 VGPRs per vehicle in flight.  Only in a whole wave (ev_table_ok):
+    // the callers run the walk for their e < n lanes, and a lane that is off
+    // never loads its entry.
     double lane_tl = 0.0, lane_rc = 0.0;
     if constexpr (MODE == kEvTable) {
       const int vl = w * 64 + (int)(threadIdx.x & 63);
@@ -498,8 +507,11 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         m &= m - 1;
         const int v = w * 64 + b;
         const double r = C.rs[i];
-        const double tl = MODE == kEvTable ? readlane_f64(lane_tl, b) : C.tls[i];
-        const double rc = MODE == kEvTable ? readlane_f64(lane_rc, b) : C.rcs[i];
+        double tl = C.tls[i], rc = C.rcs[i];
+        if constexpr (MODE == kEvTable) {
+          tl = readlane_f64(lane_tl, b);
+          rc = readlane_f64(lane_rc, b);
+        }
         act[i] = in && C.wins[i] && (r > 0.0);
         chg_now[i] = act[i] && (tl > 0.0);
         dep[i] = in && !act[i] && ((prev >> b) & 1ull);   // departed: not charging now (:239-243)
@@ -610,7 +622,7 @@ __device__ __forceinline__ RpRew ev_step_env(const pgw_ev_params& p, const pgw_e
                                             const Mt& obs, S* __restrict__ rp,
                                             S* __restrict__ rew) {
   if (s.env_start) return ev_step_mode<kEvPerEnv>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
-  if (s.tl_rcp) return ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
+  if (ev_table_ok(s)) return ev_step_mode<kEvTable>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
   return ev_step_mode<kEvDivide>(p, s, n, e, act, endp, req, chg, obs, rp, rew);
 }
 
@@ -624,7 +636,7 @@ __device__ __forceinline__ EvSums ev_step_group(const pgw_ev_params& p, const pg
   const int nc = ev_chunks(s), K = ev_group_len(nc);
   const int lo = min(g * K, nc), hi = min(lo + K, nc);
   if (s.env_start) return ev_walk<kEvPerEnv, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
-  if (s.tl_rcp) return ev_walk<kEvTable, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
+  if (ev_table_ok(s)) return ev_walk<kEvTable, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
   return ev_walk<kEvDivide, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
 }
 
