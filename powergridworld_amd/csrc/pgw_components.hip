@@ -485,7 +485,20 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         m &= m - 1;
       }
     };
-    auto process = [&](const Chunk& C) {
+    // the chunk's new requirements go out after the pair is processed
+    // (store_nr): a store between the pair's two chunks made the second one
+    // wait for it (vmcnt counts loads and stores in order)
+    auto store_nr = [&](const Chunk& C, const S (&val)[kEvChunk]) {
+      uint64_t m = C.bits;
+#pragma unroll
+      for (int i = 0; i < kEvChunk; ++i) {
+        const bool in = m != 0;
+        const int b = in ? __builtin_ctzll(m) : 0;
+        m &= m - 1;
+        if (in) req[(int64_t)(w * 64 + b) * n + e] = val[i];
+      }
+    };
+    auto process = [&](const Chunk& C, S (&val)[kEvChunk]) {
       if (!SPLIT && at == next_fold) {               // (uniform) a group boundary
         // (the first total is the first group's sum: 0.0 + p0 == p0, a sum from
         // +0.0 being never -0.0)
@@ -505,7 +518,6 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         const bool in = m != 0;                      // uniform: the chunk's tail is not
         const int b = in ? __builtin_ctzll(m) : 0;
         m &= m - 1;
-        const int v = w * 64 + b;
         const double r = C.rs[i];
         double tl = C.tls[i], rc = C.rcs[i];
         if constexpr (MODE == kEvTable) {
@@ -522,7 +534,7 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         // under a branch leaves the compiler no static count of outstanding
         // memory operations, and it then waits for all of them (vmcnt(0)),
         // stores included, before every later load's use
-        if (in) req[(int64_t)v * n + e] = (S)(chg_now[i] ? r - cv[i] : r);
+        val[i] = (S)(chg_now[i] ? r - cv[i] : r);
       }
       m = C.bits;
 #pragma unroll
@@ -548,15 +560,19 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
     // at a time there, pairs spilled)
     while (budget > 0) {                             // (uniform)
       Chunk A, B;
+      S va[kEvChunk], vb[kEvChunk];
       A.bits = take_mine();
       load(A);
       if constexpr (MODE != kEvPerEnv) {
         B.bits = take_mine();
         load(B);
       }
-      process(A);
+      process(A, va);
       if constexpr (MODE != kEvPerEnv)
-        if (B.bits) process(B);
+        if (B.bits) process(B, vb);
+      store_nr(A, va);
+      if constexpr (MODE != kEvPerEnv)
+        if (B.bits) store_nr(B, vb);
     }
     if constexpr (SPLIT) {
       if (now_bits) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[w * 64 + lane]),
