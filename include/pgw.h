@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 27
+#define PGW_ABI_VERSION 28
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -426,6 +426,14 @@ typedef struct pgw_pf_tables {
  * J'_k(t) = c0_k + t (c1_k + t c2_k). */
 #define PGW_OD_REC_HEAD 6
 #define PGW_OD_REC(m) (PGW_OD_REC_HEAD + 6 * (m))
+/* Node records (resp_v, optional): one per response record, same index, 12
+ * doubles: the record's header [0..5] copied, then the fitted complex voltage
+ * (pu) of one node, V(t) = v0 + t (v1 + t v2), [6..11] = v0, v1, v2 (re, im):
+ * V0_node + G_node J'(t) composed on the host.  Output row resp_v_row (the
+ * controllable load's node) is then read from it for every env the table
+ * serves, and a solve whose only output is that row reads 96 bytes per env
+ * instead of the 720-byte record. */
+#define PGW_OD_VREC 12
 typedef struct pgw_pf_od {
   double tol;                        /* 1e-4 (ConvergenceTolerance)            */
   double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M];   /* y0' per element (W, -var) */
@@ -440,7 +448,8 @@ typedef struct pgw_pf_od {
   const double* resp;                /* response table records (device) or NULL */
   double resp_x0, resp_h;            /* grid origin and step (kW)               */
   int32_t resp_nseg;                 /* grid segments (primary records)         */
-  int32_t resp_pad;
+  int32_t resp_v_row;                /* output row of the node records; < 0 none */
+  const double* resp_v;              /* node records (PGW_OD_VREC each) or NULL */
 } pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 27
+ABI_VERSION = 28
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -110,10 +110,11 @@ class PFOD(C.Structure):
                 ("elem_scale", f64 * PF_MAX_M), ("gamma", f64), ("eps", f64), ("gmax", f64),
                 ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("sparse_envs", i32),
                 ("rows_V0", vp), ("rows_G", vp), ("start", vp), ("resp", vp), ("resp_x0", f64),
-                ("resp_h", f64), ("resp_nseg", i32), ("resp_pad", i32)]
+                ("resp_h", f64), ("resp_nseg", i32), ("resp_v_row", i32), ("resp_v", vp)]
 
 
 OD_REC_HEAD = 6
+OD_VREC = 12                     # doubles per node record (PGW_OD_VREC)
 
 
 def od_rec(m):

@@ -1064,6 +1064,8 @@ struct ODArgs {
   const double* resp;                             // response table of the hour (pgw_pf_od.resp) or null
   double resp_x0, resp_inv_h;
   int32_t resp_nseg;
+  int32_t resp_v_row;                             // output row of the node records (-1: none)
+  const double* resp_v;                           // node records (pgw_pf_od.resp_v) or null
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
 constexpr int kOdChunk = 12;                      // check rows per previous-magnitude pass
@@ -1118,6 +1120,8 @@ static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   o.resp_x0 = d.resp_x0;
   o.resp_inv_h = resp ? 1.0 / d.resp_h : 0.0;
   o.resp_nseg = resp ? d.resp_nseg : 0;
+  o.resp_v = (resp && d.resp_v && d.resp_v_row >= 0) ? d.resp_v : nullptr;
+  o.resp_v_row = o.resp_v ? d.resp_v_row : -1;
   return o;
 }
 
@@ -1547,7 +1551,7 @@ __device__ __forceinline__ double2 od_rec_j(double2 c0, double2 c1, double2 c2, 
 // (with Q = 0) lies in no piece -- then the env runs the snap solve.
 template <int M>
 __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double Q, double (&jr)[M],
-                                               double (&ji)[M], int& it) {
+                                               double (&ji)[M], int& it, int& rec_out) {
   constexpr int R2 = PGW_OD_REC(M) / 2;
   const double g = (P - o.resp_x0) * o.resp_inv_h;
   if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
@@ -1569,6 +1573,40 @@ __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double
         jr[k] = j.x;
         ji[k] = j.y;
       }
+      it = k_it;
+      rec_out = r;
+      return true;
+    }
+    if (next < 0) return false;
+    r = next;
+  }
+  return false;
+}
+
+// The node record's voltage (pu, complex) at P: record r of pgw_pf_od.resp_v,
+// the same t as its response record's (the header is a copy).
+__device__ __forceinline__ double2 od_vrec_eval(const ODArgs& o, int r, double P) {
+  const double2* rec = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)r * (PGW_OD_VREC / 2);
+  const double2 h1 = rec[1], c0 = rec[3], c1 = rec[4], c2 = rec[5];
+  return od_rec_j(c0, c1, c2, (P - h1.x) * h1.y);
+}
+
+// od_resp_lookup for a solve whose only output is the node records' row: the
+// 96-byte node records alone (their headers decide exactly as the response
+// records', so the same envs are served, with the same counts).
+__device__ __forceinline__ bool od_resp_lookup_v(const ODArgs& o, double P, double Q, double2& v, int& it) {
+  constexpr int R2 = PGW_OD_VREC / 2;
+  const double g = (P - o.resp_x0) * o.resp_inv_h;
+  if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
+  int r = (int)g;
+  for (int hop = 0; hop < kOdHops; ++hop) {
+    const double2* rec = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)r * R2;
+    const double2 h0 = rec[0], h1 = rec[1], h2 = rec[2], c0 = rec[3], c1 = rec[4], c2 = rec[5];
+    int k_it, next;
+    od_rec_meta(h2.x, k_it, next);
+    if (P >= h0.x && P <= h0.y) {
+      if (k_it == 0) return false;
+      v = od_rec_j(c0, c1, c2, (P - h1.x) * h1.y);
       it = k_it;
       return true;
     }
@@ -1701,18 +1739,35 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   double ir[M], ii[M], v0r, v0i;
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
-  int it = 0;
-  const bool need = valid && !(o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it));
-  if constexpr (TR) { if (ir[0] != -1e300) pf_trace(tr, 2); }
+  int it = 0, rec = 0;
+  // with node records for output row 0 and no other row (the fused C4 step),
+  // the 96-byte node record is all a served env reads
+  const bool vonly = o.resp_v != nullptr && o.resp_v_row == 0 && a.n_out == 1;   // (uniform)
+  double2 vf = make_double2(0.0, 0.0);
+  bool served;
+  if (vonly) {
+    served = valid && od_resp_lookup_v(o, S.pc, S.qc, vf, it);
+  } else {
+    served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, rec);
+    if (served && o.resp_v) vf = od_vrec_eval(o, rec, S.pc);
+  }
+  const bool need = valid && !served;
+  if constexpr (TR) { if (ir[0] != -1e300 && vf.x != -1e300) pf_trace(tr, 2); }
   od_fallback<M>(S, o, o.start, stg, !early, sh, need, ir, ii, it);
   if constexpr (TR) pf_trace(tr, 3);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
+  if (served && o.resp_v_row == 0) {                 // the node record's row
+    v0r = vf.x;
+    v0i = vf.y;
+  }
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
   if constexpr (TR) { if (v0 != -1.0) pf_trace(tr, 4); }
   // rows 1.. (a history slot holds every node)
   double vsel = v0;
   const double* srow = rows_lds ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
+  const double vfm = sqrt(fma(vf.y, vf.y, vf.x * vf.x));
   pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
+    v = (served && ro == o.resp_v_row) ? vfm : v;
     if (valid && b.v_out) b.v_out[(int64_t)ro * n + e] = (Sto)v;
     vsel = (ro == c.vv_row) ? v : vsel;
   });
@@ -1765,11 +1820,18 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   double ir[M], ii[M], v0r, v0i;
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
-  int it = 0;
-  const bool need = valid && !(table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it));
+  int it = 0, rec = 0;
+  const bool served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, rec);
+  const double2 vf = (served && o.resp_v) ? od_vrec_eval(o, rec, S.pc) : make_double2(0.0, 0.0);
+  const bool need = valid && !served;
   od_fallback<M>(S, o, o.start, stg, table, sh, need, ir, ii, it);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);
+  if (served && o.resp_v_row == 0) {                 // the node record's row
+    v0r = vf.x;
+    v0i = vf.y;
+  }
   const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  const double vf2 = fma(vf.y, vf.y, vf.x * vf.x);
   if (valid && t.U_out) {
 #pragma unroll
     for (int k = 0; k < M; ++k) {
@@ -1780,7 +1842,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
   const double* srow = rows_lds ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
   if (v_out || !rows_lds) {
+    const double vfm = sqrt(vf2);
     pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
+      v = (served && ro == o.resp_v_row) ? vfm : v;
       if (valid && v_out) v_out[(int64_t)ro * n + e] = v;
       vmn = (v < vmn) ? v : vmn;
       vmx = (v > vmx) ? v : vmx;
@@ -1789,7 +1853,8 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     // extrema only: min / max of |V|^2 over the rows, one sqrt each at the end
     // (as k_pf_solve: sqrt is monotone and correctly rounded)
     double mn2 = fma(v0i, v0i, v0r * v0r), mx2 = mn2;
-    pf_rows_out<M, false>(t, rows_lds, srow, a.n_out, ir, ii, [&](int, double m2) {
+    pf_rows_out<M, false>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double m2) {
+      m2 = (served && ro == o.resp_v_row) ? vf2 : m2;
       mn2 = (m2 < mn2) ? m2 : mn2;
       mx2 = (m2 > mx2) ? m2 : mx2;
     });

@@ -266,6 +266,7 @@ class OpenDSSSolver(PowerFlowSolver):
         dev = self.device
         cdev = lambda a: torch.tensor(np.ascontiguousarray(a).view(np.float64).ravel(), dtype=torch.float64,
                                       device=dev)
+        self._od_Gall, self._od_V0all = Gs, V0s          # every node's row (the node records)
         self._od_rows_V0 = cdev(V0s[rows] if rows else np.zeros(1, complex))
         self._od_rows_G = cdev(Gs[rows] if rows else np.zeros((1, M), complex))
         od.rows_V0, od.rows_G = self._od_rows_V0.data_ptr(), self._od_rows_G.data_ptr()
@@ -275,6 +276,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_u0 = U0 / vb_elem
         self._od_start = torch.zeros((self.OD_MAX_TABLES, 12 * M), dtype=torch.float64, device=dev)
         self._od_resp = None                 # response tables (allocated on the first build)
+        self._od_vresp = None                # their node records (pgw_pf_od.resp_v)
         self.od_resp_stats, self.od_resp_brackets = {}, {}
         self._od_index = {}
         self._od_keep = {}
@@ -367,6 +369,29 @@ class OpenDSSSolver(PowerFlowSolver):
                                        J.data_ptr(), sig.data_ptr(), it.data_ptr(), args.data_ptr(),
                                        _lib.stream_ptr(dev)))
         return J, sig.cpu().numpy().view(np.uint64), it.cpu().numpy(), np.arange(H) * lph
+
+    def _od_vnode(self):
+        """The node whose voltage the node records carry: the controllable
+        load's, when it is one phase-to-ground element (C4, HET: 675c ->
+        675.3); None otherwise (no node records)."""
+        f = self.feeder
+        if len(self._ctrl_names) != 1:
+            return None
+        li = f.load_names.index(self._ctrl_names[0])
+        ks = [k for k in range(f.m) if f.elem_load[k] == li]
+        if len(ks) != 1 or f.elem_q[ks[0]] >= 0:
+            return None
+        return int(f.elem_p[ks[0]])
+
+    def _od_vcoef(self, recs):
+        """Node-record coefficients [.., 3] complex (v0, v1, v2) of response
+        records recs [.., R]: V_node = V0 + G J'(t), composed."""
+        node, M = self._od_vnode(), self.M
+        c = torch.view_as_complex(recs[..., 6:6 + 6 * M].reshape(*recs.shape[:-1], 3, M, 2).contiguous())
+        G = torch.from_numpy(np.ascontiguousarray(self._od_Gall[node, :M])).to(recs.device)
+        v = (c * G).sum(-1)
+        v[..., 0] = v[..., 0] + complex(self._od_V0all[node])
+        return v
 
     def _od_response(self, hours, idx0):
         """Build and upload the response tables of `hours` (rows idx0.. of the
@@ -538,12 +563,32 @@ class OpenDSSSolver(PowerFlowSolver):
                                             Jc.data_ptr(), dq_.data_ptr(), err.data_ptr(), st))
         e_ = err.cpu().numpy().reshape(-1, 2).max(1)
         del dr, dp, dq_
+        vnode = self._od_vnode()
+        if vnode is not None and len(pa):
+            # the node records' voltage at the same check points against the
+            # probed currents composed exactly (relative error, as the currents')
+            rr = self._od_resp.view(-1, R)[torch.from_numpy(prec).to(dev)]          # [P, R]
+            vc = self._od_vcoef(rr)                                                 # [P, 3]
+            tt = (torch.from_numpy(chk).to(dev) - rr[:, 2:3]) * rr[:, 3:4]          # [P, 2]
+            vfit = vc[:, :1] + tt * (vc[:, 1:2] + tt * vc[:, 2:3])
+            Jl = torch.view_as_complex(Jc.reshape(-1, M, 2)[torch.from_numpy(c_l.ravel()).to(dev)].contiguous())
+            G = torch.from_numpy(np.ascontiguousarray(self._od_Gall[vnode, :M])).to(dev)
+            vtrue = ((Jl * G).sum(-1) + complex(self._od_V0all[vnode])).reshape(-1, 2)
+            ev = ((vfit - vtrue).abs() / vtrue.abs()).max(1).values.cpu().numpy()
+            e_ = np.maximum(e_, np.where(np.isfinite(ev), ev, np.inf))
         bad = (pit != 0) & ((e_ > self.OD_RESP_TOL) | (sc[c_l] != psig[:, None]).any(1) | ~np.isfinite(e_))
         if bad.any():                                       # left to the solve
             words = np.array([self._od_meta_word(0, int(nx)) for nx in pnext[bad]], np.int64)
             self._od_resp.view(-1, R).view(torch.int64)[torch.from_numpy(prec[bad]).to(dev), 4] = \
                 torch.from_numpy(words).to(dev)
         ok = (pit != 0) & ~bad
+        if vnode is not None:                               # node records: headers copied bitwise
+            if self._od_vresp is None:
+                self._od_vresp = torch.zeros((self.OD_MAX_TABLES, rec_n, _lib.OD_VREC), dtype=torch.float64,
+                                             device=dev)
+            vb = self._od_vresp[idx0:idx0 + H]
+            vb.view(torch.int64)[:, :, :6] = blk.view(torch.int64)[:, :, :6]
+            vb[:, :, 6:12] = torch.view_as_real(self._od_vcoef(blk)).reshape(H, rec_n, 6)
         # the brackets per table row (kW intervals the tables leave to the solve;
         # an hour's row: _od_index[_hour_key(hour)]), for tests and diagnostics
         for q, hr in enumerate(hours):
@@ -570,9 +615,16 @@ class OpenDSSSolver(PowerFlowSolver):
             idx = self._od_index[self._hour_key(hour)]
         od = _lib.PFOD.from_buffer_copy(self._od_proto)
         od.start = self._od_start[idx].data_ptr()
+        od.resp_v_row = -1
         if self.od_table and self._od_resp is not None:
             od.resp = self._od_resp[idx].data_ptr()
             od.resp_x0, od.resp_h, od.resp_nseg = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N - 1
+            vnode = self._od_vnode()
+            if self._od_vresp is not None and vnode is not None:
+                name = self.feeder.node_names[vnode]
+                if name in self.output_names:
+                    od.resp_v = self._od_vresp[idx].data_ptr()
+                    od.resp_v_row = self.output_names.index(name)
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.od = _lib.C.addressof(od)
         t._od_ref = od                     # the struct lives as long as these tables

@@ -197,3 +197,38 @@ def test_response_table_builder_against_the_solve(cpu_solver):
         np.testing.assert_array_equal(it[served], ito[served])
         rel = np.abs(J[served] - Jo[served]).max(1) / np.abs(Jo[served]).max(1)
         assert rel.max() < 1e-10, rel.max()
+
+
+def test_node_records_compose_the_response(cpu_solver):
+    """The node records (pgw_pf_od.resp_v): headers bit-copies of the response
+    records', coefficients V0 + G J' composed, so a served env's node voltage
+    from them equals the one from its currents, and both equal the solve's."""
+    s, orc = cpu_solver
+    s._od_tables(HOURS[0])
+    node = s._od_vnode()
+    assert node is not None and s.feeder.node_names[node] == "675.3"
+    idx = s._od_index[s._hour_key(HOURS[0])]
+    recs, vrec = s._od_resp[idx].numpy(), s._od_vresp[idx].numpy()
+    np.testing.assert_array_equal(recs[:, :6].view(np.int64), vrec[:, :6].view(np.int64))
+    od = s._od_tables(HOURS[0]).od
+    from powergridworld_amd import _lib
+    o = _lib.PFOD.from_address(od)
+    assert o.resp_v == s._od_vresp[idx].data_ptr() and s.output_names[o.resp_v_row] == "675.3"
+    G, V0 = s._od_Gall[node, :s.M], s._od_V0all[node]
+    P = np.random.default_rng(5).uniform(-500.0, 1499.9, 2000)
+    served, J, _ = _lookup(s, HOURS[0], P)
+    Jo, _, _ = orc(HOURS[0], P)
+    g = (P - s.PREDICTOR_X0) / s.PREDICTOR_H
+    n_checked = 0
+    for e in np.nonzero(served)[0][:300]:
+        r = int(g[e])                      # (the first record; chained pieces skipped here)
+        if not (recs[r, 0] <= P[e] <= recs[r, 1]):
+            continue
+        t = (P[e] - vrec[r, 2]) * vrec[r, 3]
+        c = vrec[r, 6:12].reshape(3, 2)
+        v = c[0] + t * (c[1] + t * c[2])
+        vfit = v[0] + 1j * v[1]
+        np.testing.assert_allclose(vfit, V0 + (G * J[e]).sum(), rtol=1e-13)
+        np.testing.assert_allclose(abs(vfit), abs(V0 + (G * Jo[e]).sum()), rtol=1e-11)
+        n_checked += 1
+    assert n_checked > 200
