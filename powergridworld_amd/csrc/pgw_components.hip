@@ -402,7 +402,7 @@ __device__ __forceinline__ double ev_kwh(const pgw_ev_params& p, const pgw_ev_st
 // scan in one lane, folding at the group boundaries, the charging bits stored
 // per word.  SPLIT = true: one group's chunks; the bits are ORed into the
 // block's s_bits[word][lane] and the group's partial sums returned unfolded.
-template <int MODE, bool SPLIT, class S>
+template <int MODE, bool SPLIT, class S, bool TR = false>
 __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
                                           int64_t e, double kwh, const double* __restrict__ endp,
                                           S* __restrict__ req, uint64_t* __restrict__ chg, int c_lo,
@@ -558,6 +558,7 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
     // per-wave phase trace showed each chunk costing a full round trip.)
     // (randomize's per-env tables load two more values per vehicle: one chunk
     // at a time there, pairs spilled)
+    bool first_pair = true;                          // (debug trace only)
     while (budget > 0) {                             // (uniform)
       Chunk A, B;
       S va[kEvChunk], vb[kEvChunk];
@@ -568,8 +569,11 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         load(B);
       }
       process(A, va);
+      if constexpr (TR) { if (demand != -1.0 && first_pair) mc_trace<TR>(g_mc_trace, 3); }
       if constexpr (MODE != kEvPerEnv)
         if (B.bits) process(B, vb);
+      if constexpr (TR) { if (demand != -1.0 && first_pair) mc_trace<TR>(g_mc_trace, 7); }
+      first_pair = false;
       store_nr(A, va);
       if constexpr (MODE != kEvPerEnv)
         if (B.bits) store_nr(B, vb);
@@ -643,7 +647,7 @@ __device__ __forceinline__ RpRew ev_step_env(const pgw_ev_params& p, const pgw_e
 }
 
 // Group g's part of the walk (k_mc_step's split EV waves).
-template <class S, class Mt>
+template <class S, class Mt, bool TR = false>
 __device__ __forceinline__ EvSums ev_step_group(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
                                                 int64_t e, const Mt& act, const double* __restrict__ endp,
                                                 S* __restrict__ req, uint64_t* __restrict__ chg, int g,
@@ -652,7 +656,7 @@ __device__ __forceinline__ EvSums ev_step_group(const pgw_ev_params& p, const pg
   const int nc = ev_chunks(s), K = ev_group_len(nc);
   const int lo = min(g * K, nc), hi = min(lo + K, nc);
   if (s.env_start) return ev_walk<kEvPerEnv, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
-  if (ev_table_ok(s)) return ev_walk<kEvTable, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
+  if (ev_table_ok(s)) return ev_walk<kEvTable, true, S, TR>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
   return ev_walk<kEvDivide, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
 }
 
@@ -789,8 +793,9 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   if (ev_wave) {
     const int g = w >= a.n_comp ? w - a.n_comp + 1 : 0;
     if (e < n) {
-      const EvSums t = ev_step_group(a.ev, evs, n, e, a.comp[ev_slot].action, a.ev_endp, a.ev_req,
-                                     a.ev_charging, g, s_bits, lane);
+      const EvSums t = ev_step_group<S, typename McStore<Args>::Mt, TR>(a.ev, evs, n, e, a.comp[ev_slot].action,
+                                                                        a.ev_endp, a.ev_req, a.ev_charging, g,
+                                                                        s_bits, lane);
       s_evs[g][0][lane] = t.demand;
       s_evs[g][1][lane] = t.consumed;
       s_evs[g][2][lane] = t.dsum;

@@ -1551,7 +1551,7 @@ __device__ __forceinline__ double2 od_rec_j(double2 c0, double2 c1, double2 c2, 
 // (with Q = 0) lies in no piece -- then the env runs the snap solve.
 template <int M>
 __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double Q, double (&jr)[M],
-                                               double (&ji)[M], int& it, int& rec_out) {
+                                               double (&ji)[M], int& it, double2& vf) {
   constexpr int R2 = PGW_OD_REC(M) / 2;
   const double g = (P - o.resp_x0) * o.resp_inv_h;
   if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
@@ -1562,6 +1562,15 @@ __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double
     const double2 h0 = rec[0], h1 = rec[1], h2 = rec[2];
 #pragma unroll
     for (int q = 0; q < 3 * M; ++q) c[q] = rec[3 + q];      // in flight with the header
+    // the node record's coefficients in the same round trip (its header is a
+    // copy of this one); zero without node records
+    double2 v0 = make_double2(0.0, 0.0), v1 = v0, v2 = v0;
+    if (o.resp_v) {
+      const double2* vr = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)r * (PGW_OD_VREC / 2);
+      v0 = vr[3];
+      v1 = vr[4];
+      v2 = vr[5];
+    }
     int k_it, next;
     od_rec_meta(h2.x, k_it, next);
     if (P >= h0.x && P <= h0.y) {
@@ -1574,21 +1583,13 @@ __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double
         ji[k] = j.y;
       }
       it = k_it;
-      rec_out = r;
+      vf = od_rec_j(v0, v1, v2, t);
       return true;
     }
     if (next < 0) return false;
     r = next;
   }
   return false;
-}
-
-// The node record's voltage (pu, complex) at P: record r of pgw_pf_od.resp_v,
-// the same t as its response record's (the header is a copy).
-__device__ __forceinline__ double2 od_vrec_eval(const ODArgs& o, int r, double P) {
-  const double2* rec = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)r * (PGW_OD_VREC / 2);
-  const double2 h1 = rec[1], c0 = rec[3], c1 = rec[4], c2 = rec[5];
-  return od_rec_j(c0, c1, c2, (P - h1.x) * h1.y);
 }
 
 // od_resp_lookup for a solve whose only output is the node records' row: the
@@ -1739,7 +1740,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   double ir[M], ii[M], v0r, v0i;
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
-  int it = 0, rec = 0;
+  int it = 0;
   // with node records for output row 0 and no other row (the fused C4 step),
   // the 96-byte node record is all a served env reads
   const bool vonly = o.resp_v != nullptr && o.resp_v_row == 0 && a.n_out == 1;   // (uniform)
@@ -1748,8 +1749,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   if (vonly) {
     served = valid && od_resp_lookup_v(o, S.pc, S.qc, vf, it);
   } else {
-    served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, rec);
-    if (served && o.resp_v) vf = od_vrec_eval(o, rec, S.pc);
+    served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf);
   }
   const bool need = valid && !served;
   if constexpr (TR) { if (ir[0] != -1e300 && vf.x != -1e300) pf_trace(tr, 2); }
@@ -1820,9 +1820,9 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   double ir[M], ii[M], v0r, v0i;
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
-  int it = 0, rec = 0;
-  const bool served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, rec);
-  const double2 vf = (served && o.resp_v) ? od_vrec_eval(o, rec, S.pc) : make_double2(0.0, 0.0);
+  int it = 0;
+  double2 vf = make_double2(0.0, 0.0);
+  const bool served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf);
   const bool need = valid && !served;
   od_fallback<M>(S, o, o.start, stg, table, sh, need, ir, ii, it);
   pf_node0<M>(v0r, v0i, S.w, ir, ii);

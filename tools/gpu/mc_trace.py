@@ -42,7 +42,11 @@ def summarize(tag, buf, n_waves, roles, extra=""):
         fin = raw[:, :, 4] != 0
         fold = (np.where(fin, t[:, :, 4], 0).max(1) - np.where(fin, t[:, :, 2], 0).max(1))
         line += " | fold+finish %.2f" % np.median(fold)
-    bw = [w for w in range(n_waves) if (raw[:, w, 3] != 0).all()]
+    for w in range(n_waves):                          # EV group waves: the first pair's chunks
+        if roles[w].startswith("ev") and (raw[:, w, 3] != 0).all() and (raw[:, w, 7] != 0).all():
+            line += " | %s to A %.2f B %.2f" % (roles[w], np.median(t[:, w, 3] - t[:, w, 0]),
+                                               np.median(t[:, w, 7] - t[:, w, 3]))
+    bw = [w for w in range(n_waves) if (raw[:, w, 3] != 0).all() and roles[w].startswith("bld")]
     if bw:                                            # the building wave's phases
         w = bw[0]
         line += " | bld loads %.2f state+reward %.2f obs %.2f" % (
