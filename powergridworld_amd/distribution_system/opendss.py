@@ -277,6 +277,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_start = torch.zeros((self.OD_MAX_TABLES, 12 * M), dtype=torch.float64, device=dev)
         self._od_resp = None                 # response tables (allocated on the first build)
         self._od_vresp = None                # their node records (pgw_pf_od.resp_v)
+        self.od_node_records = True          # False: every solve reads the node's row from the currents
         self.od_resp_stats, self.od_resp_brackets = {}, {}
         self._od_index = {}
         self._od_keep = {}
@@ -620,7 +621,7 @@ class OpenDSSSolver(PowerFlowSolver):
             od.resp = self._od_resp[idx].data_ptr()
             od.resp_x0, od.resp_h, od.resp_nseg = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N - 1
             vnode = self._od_vnode()
-            if self._od_vresp is not None and vnode is not None:
+            if self._od_vresp is not None and vnode is not None and self.od_node_records:
                 name = self.feeder.node_names[vnode]
                 if name in self.output_names:
                     od.resp_v = self._od_vresp[idx].data_ptr()
