@@ -791,28 +791,7 @@ __global__ void __launch_bounds__(64 * (4 + kEvGroups - 1)) k_mc_step(Args a_, B
   const pgw_ev_step_info& evs = CLK ? s_dyn.ev_step : a.ev_step;
   const bool ev_wave = split && (w >= a.n_comp || w == ev_slot);
   if (ev_wave) {
-    // group of this wave: the walk's groups are consecutive chunk ranges, the
-    // last ones the lightest (often empty), so they go to the waves that share
-    // a SIMD with the building wave (waves of a block are dealt to the 4 SIMDs
-    // in turn), the heavy ones to the others -- the building's SIMD was the
-    // block's busiest.  Which wave walks which group does not change the sums
-    // (they fold by group).
-    int g = 0;
-    {
-      int bw = -1;
-      for (int c = 0; c < a.n_comp; ++c) bw = a.comp[c].kind == PGW_MC_BUILDING ? c : bw;
-      const int nw = (int)(blockDim.x >> 6);
-      int pos = 0, late = 0, mine_late = 0;        // (uniform) rank of this wave among the EV waves
-      for (int v = 0; v < nw; ++v) {
-        const bool is_ev = v >= a.n_comp || v == ev_slot;
-        if (!is_ev) continue;
-        const bool l = bw >= 0 && (v & 3) == (bw & 3);
-        if (v == w) mine_late = l;
-        if (v < w && l == (bw >= 0 && (w & 3) == (bw & 3))) ++pos;
-        late += l;
-      }
-      g = mine_late ? (kEvGroups - late) + pos : pos;
-    }
+    const int g = w >= a.n_comp ? w - a.n_comp + 1 : 0;
     if (e < n) {
       const EvSums t = ev_step_group<S, typename McStore<Args>::Mt, TR>(a.ev, evs, n, e, a.comp[ev_slot].action,
                                                                         a.ev_endp, a.ev_req, a.ev_charging, g,
