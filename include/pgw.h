@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 28
+#define PGW_ABI_VERSION 29
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -635,6 +635,10 @@ int32_t pgw_pf_solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, i
  * ---------------------------------------------------------------------- */
 #define PGW_REG_MAX_PHASES 12
 #define PGW_REG_MAX_CTRL 12
+#define PGW_REG_MAX_MON 3
+#define PGW_REG_PICK_PHASE 0
+#define PGW_REG_PICK_MAX 1
+#define PGW_REG_PICK_MIN 2
 typedef struct pgw_reg_phase {
   int32_t a, b;              /* R indices of the winding-1 / winding-2 terminal     */
   int32_t ctrl;              /* the RegControl whose tap this phase follows          */
@@ -643,13 +647,26 @@ typedef struct pgw_reg_phase {
   double tap1, tap2;         /* the DSS taps (those of Z0)                           */
 } pgw_reg_phase;
 typedef struct pgw_reg_ctrl {
-  int32_t pt_node;           /* R index of the monitored winding's PT-phase terminal */
-  int32_t pt_phase;          /* the pgw_reg_phase of that terminal (LDC current)     */
+  /* Sampled voltages: n_mon monitored phases, each an R node (the monitored
+   * winding's terminal, or with Bus= the regulated bus's node) and the
+   * pgw_reg_phase whose current is that phase's LDC current.  pick: which one
+   * controls -- PGW_REG_PICK_PHASE the single entry (PTphase=k),
+   * PGW_REG_PICK_MAX / _MIN the phase of largest / smallest |V| (PTphase=max /
+   * min, the first on a tie). */
+  int32_t n_mon, pick;
+  int32_t mon_node[PGW_REG_MAX_MON];
+  int32_t mon_phase[PGW_REG_MAX_MON];
   int32_t winding;           /* the monitored winding (1 or 2)                       */
   int32_t max_tap_change;    /* taps per control action                              */
+  int32_t ldc;               /* 1: subtract (R + jX) I / ctprim (no Bus=)            */
+  int32_t vlim_node;         /* Vlimit with Bus=: R index of the winding's first-phase
+                                terminal; -1: the control voltage before LDC         */
+  int32_t inverse_time;      /* 1: delay / min(10, 2 |vreg - v| / band)              */
+  int32_t pad_;
   double vreg, band, ptratio, ctprim, r_ldc, x_ldc;  /* RegControl properties        */
   double vbase;              /* the winding's rated phase voltage / ptratio (V)      */
   double incr, min_tap, max_tap, delay;
+  double vlimit;             /* Vlimit (V on the PT base; 0 = off)                   */
 } pgw_reg_ctrl;
 typedef struct pgw_reg_params {
   int32_t n_reg, r_reg;      /* as pgw_pfg_params                                    */
@@ -668,12 +685,15 @@ int32_t pgw_reg_factor(const pgw_reg_params* p, int64_t n, const double* taps, c
                        double* Kreg, void* stream);
 /* One control pass (RegControl.Sample + DoPendingAction, STATIC mode) after a
  * solve that wrote reg_x / reg_c: per env and RegControl, the monitored
- * voltage V / ptratio, less the line-drop compensation (R + jX) I / ctprim,
- * against vreg +- band / 2; an out-of-band control moves its tap by the
- * needed change truncated to whole steps (at least one, at most
- * max_tap_change, inside [min_tap, max_tap]); of the controls that act, only
- * those with the smallest delay do so this pass.  active[e] = 1 where any
- * tap moved (else 0); *n_changed (device int32) += that count. */
+ * voltage V / ptratio (PTphase=max / min: the phase of largest / smallest
+ * |V|; Bus=: at the regulated bus), less the line-drop compensation
+ * (R + jX) I / ctprim (not with Bus=), against vreg +- band / 2, and with
+ * Vlimit the local voltage against vlimit (above it the boost is vlimit - V);
+ * an acting control moves its tap by the needed change truncated to whole
+ * steps (at least one, at most max_tap_change, inside [min_tap, max_tap]);
+ * of the controls that act, only those with the smallest delay (inverse time:
+ * delay / min(10, 2 |vreg - v| / band)) do so this pass.  active[e] = 1
+ * where any tap moved (else 0); *n_changed (device int32) += that count. */
 int32_t pgw_reg_control(const pgw_reg_params* p, int64_t n, const double* reg_x, const double* reg_c,
                         double* taps, int32_t* active, int32_t* n_changed, void* stream);
 

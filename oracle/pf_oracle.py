@@ -487,7 +487,12 @@ class Feeder:
     # published documentation: Sample() reads the monitored winding's PT-phase
     # voltage on the 120-V base (V / PTratio) less the line-drop compensation
     # (R + jX) * I / CTprim (I = the current the regulator delivers into the
-    # bus); outside Vreg +- band/2 it queues the needed tap change, which
+    # bus) -- PTphase=max / min: the phase of largest / smallest |V| (first on
+    # a tie), whose current is then the LDC current; Bus=: the regulated bus's
+    # node of the phase instead of the winding's (no LDC); Vlimit: above it
+    # the local voltage (the winding's first phase with Bus=, else the control
+    # voltage before LDC) forces a change down to it; InverseTime: the action's
+    # delay is Delay / min(10, 2 |Vreg - V| / band); outside Vreg +- band/2 it queues the needed tap change, which
     # DoPendingAction (STATIC) applies truncated to whole steps (at least one,
     # at most MaxTapChange, inside [MinTap, MaxTap]; step = (MaxTap - MinTap) /
     # NumTaps); SolveSnap solves, samples, executes the queue's nearest-delay
@@ -507,8 +512,12 @@ class Feeder:
             t = xf[pr["transformer"].lower()]
             f = lambda k: float(pr[k])
             step = (float(t.get("maxtap", 1.1)) - float(t.get("mintap", 0.9))) / float(t.get("numtaps", 32))
+            ptp = pr["ptphase"].lower()
             out.append((t, dict(winding=int(f("winding")), vreg=f("vreg"), band=f("band"), ptratio=f("ptratio"),
-                                ctprim=f("ctprim"), R=f("r"), X=f("x"), ptphase=int(f("ptphase")),
+                                ctprim=f("ctprim"), R=f("r"), X=f("x"),
+                                ptphase=ptp if ptp in ("max", "min") else int(ptp),
+                                bus=pr.get("bus", "").lower(), vlimit=float(pr.get("vlimit", "0")),
+                                inverse=pr.get("inversetime", "no").lower() in ("yes", "y", "true", "t", "1"),
                                 maxtapchange=int(f("maxtapchange")), delay=f("delay"), step=step,
                                 mintap=float(t.get("mintap", 0.9)), maxtap=float(t.get("maxtap", 1.1)),
                                 tap0=t["windings"][int(f("winding")) - 1].get("tap", 1.0))))
@@ -556,30 +565,52 @@ class Feeder:
         voltages V (one env): the new taps (only the nearest-delay actions)."""
         want, delays = list(taps), []
         ctrls = self.reg_controls()
+        dl = [math.inf] * len(ctrls)
         for g, (t, c) in enumerate(ctrls):
-            p = c["ptphase"] - 1
+            cand = range(t["phases"]) if c["ptphase"] in ("max", "min") else [c["ptphase"] - 1]
+
+            def sensed(p):                     # the sampled node of phase p
+                a, b = self._reg_nodes(t, p)
+                if not c["bus"]:
+                    return a if c["winding"] == 1 else b
+                bname, nds = _bus(c["bus"], [])
+                if p < len(nds):
+                    return self.node(bname, nds[p])
+                wb, wn = _bus(t["windings"][c["winding"] - 1]["bus"], [1, 2, 3][:t["phases"]])
+                return self.node(bname, wn[p])
+            p = cand[0]
+            for q in cand[1:]:
+                better = abs(V[sensed(q)]) > abs(V[sensed(p)]) if c["ptphase"] == "max" else \
+                    abs(V[sensed(q)]) < abs(V[sensed(p)])
+                p = q if better else p
             a, b = self._reg_nodes(t, p)
-            vc = V[a if c["winding"] == 1 else b] / c["ptratio"]
-            if c["R"] != 0.0 or c["X"] != 0.0:
+            vc = V[sensed(p)] / c["ptratio"]
+            vlocal = 0.0
+            if c["vlimit"] > 0:
+                a0, b0 = self._reg_nodes(t, 0)
+                vlocal = abs(V[a0 if c["winding"] == 1 else b0] / c["ptratio"]) if c["bus"] else abs(vc)
+            if not c["bus"] and (c["R"] != 0.0 or c["X"] != 0.0):
                 tp = [w.get("tap", 1.0) for w in t["windings"]]
                 tp[c["winding"] - 1] = taps[g]
                 i_in = self._reg_yw(t, tp)[c["winding"] - 1] @ np.array([V[a], V[b]])
                 vc = vc - complex(c["R"], c["X"]) * (-i_in / c["ctprim"])
             dv = c["vreg"] - abs(vc)
-            if abs(dv) > c["band"] / 2:
+            over = c["vlimit"] > 0 and vlocal > c["vlimit"]
+            if abs(dv) > c["band"] / 2 or over:
                 w = t["windings"][c["winding"] - 1]
                 vbase = w["kv"] * 1000 / (math.sqrt(3) if t["phases"] == 3 else 1.0) / c["ptratio"]
-                need = dv / vbase
+                need = (c["vlimit"] - vlocal if over else dv) / vbase
                 steps = min(max(math.trunc(abs(need) / c["step"]), 1), c["maxtapchange"])
                 nt = taps[g] + (steps if need > 0 else -steps) * c["step"]
                 nt = min(max(nt, c["mintap"]), c["maxtap"])
                 if nt != taps[g]:
                     want[g] = nt
-                    delays.append(c["delay"])
+                    dl[g] = c["delay"] / min(10.0, 2.0 * abs(dv) / c["band"]) if c["inverse"] else c["delay"]
+                    delays.append(dl[g])
         if not delays:
             return list(taps), False
         dmin = min(delays)
-        out = [want[g] if (want[g] != taps[g] and ctrls[g][1]["delay"] == dmin) else taps[g]
+        out = [want[g] if (want[g] != taps[g] and dl[g] == dmin) else taps[g]
                for g in range(len(ctrls))]
         return out, True
 

@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 28
+ABI_VERSION = 29
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -141,7 +141,8 @@ class PFGTables(C.Structure):
                 ("env_active", vp), ("reg_rho", vp)]
 
 
-PFG_MAX_REG, REG_MAX_PHASES, REG_MAX_CTRL = 24, 12, 12
+PFG_MAX_REG, REG_MAX_PHASES, REG_MAX_CTRL, REG_MAX_MON = 24, 12, 12, 3
+REG_PICK_PHASE, REG_PICK_MAX, REG_PICK_MIN = 0, 1, 2
 
 
 class RegPhase(C.Structure):
@@ -150,10 +151,12 @@ class RegPhase(C.Structure):
 
 
 class RegCtrl(C.Structure):
-    _fields_ = [("pt_node", i32), ("pt_phase", i32), ("winding", i32), ("max_tap_change", i32),
+    _fields_ = [("n_mon", i32), ("pick", i32), ("mon_node", i32 * REG_MAX_MON),
+                ("mon_phase", i32 * REG_MAX_MON), ("winding", i32), ("max_tap_change", i32), ("ldc", i32),
+                ("vlim_node", i32), ("inverse_time", i32), ("pad_", i32),
                 ("vreg", f64), ("band", f64), ("ptratio", f64), ("ctprim", f64), ("r_ldc", f64),
                 ("x_ldc", f64), ("vbase", f64), ("incr", f64), ("min_tap", f64), ("max_tap", f64),
-                ("delay", f64)]
+                ("delay", f64), ("vlimit", f64)]
 
 
 class RegParams(C.Structure):

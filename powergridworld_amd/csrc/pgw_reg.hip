@@ -12,7 +12,9 @@
 // columns; two envs of 32 lanes each when 2r <= 32) in LDS,
 // Gauss-Jordan with partial pivoting, the pivot column read into registers
 // before the wave updates its columns; the control pass is one lane per env
-// (a handful of complex multiply-adds per RegControl).  Both are tiny next to
+// (a handful of complex multiply-adds per RegControl; Sample's options --
+// PTphase=max / min, a remote regulated bus, Vlimit, inverse time -- are
+// per-control branches on uniform settings).  Both are tiny next to
 // the power flow itself: K is rebuilt only for the envs whose taps moved.
 #include <cmath>
 
@@ -173,17 +175,43 @@ __global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64
 #pragma unroll
   for (int l = 0; l < kRegMax; ++l)
     c[l] = l < p.r_reg ? c2{rc[2 * ((int64_t)l * n + e)], rc[2 * ((int64_t)l * n + e) + 1]} : c2{0.0, 0.0};
+  double dl[PGW_REG_MAX_CTRL];                       // each acting control's delay
   for (int g = 0; g < p.n_ctrl; ++g) {
     const pgw_reg_ctrl& C = p.ctrl[g];
     const double tap = taps[(int64_t)g * n + e];
     want[g] = tap;
-    // RegControl.Sample: the PT voltage on the 120-V base, less the line-drop
-    // compensation (R + jX) I / CTprim with I the current the regulator delivers
-    // from the monitored winding into its bus
-    const c2 vpt = reg_node_v(p, C.pt_node, rx, c, n, e);
-    c2 vc = cscale(vpt, 1.0 / C.ptratio);
-    if (C.r_ldc != 0.0 || C.x_ldc != 0.0) {
-      const pgw_reg_phase& ph = p.phase[C.pt_phase];
+    dl[g] = INFINITY;
+    // RegControl.Sample: the monitored voltage -- the PT phase's, or with
+    // PTphase=max / min the phase of largest / smallest |V| (the first on a
+    // tie) -- on the 120-V base (V / PTratio)
+    int k = 0;
+    c2 vk = reg_node_v(p, C.mon_node[0], rx, c, n, e);
+    double mk = sqrt(vk.x * vk.x + vk.y * vk.y);
+    for (int i = 1; i < C.n_mon; ++i) {
+      const c2 v = reg_node_v(p, C.mon_node[i], rx, c, n, e);
+      const double mv = sqrt(v.x * v.x + v.y * v.y);
+      if (C.pick == PGW_REG_PICK_MAX ? mv > mk : mv < mk) {
+        k = i;
+        vk = v;
+        mk = mv;
+      }
+    }
+    c2 vc = {vk.x / C.ptratio, vk.y / C.ptratio};
+    // Vlimit: the local voltage -- the control voltage before LDC, or with a
+    // regulated bus the winding's first phase (V / PTratio)
+    double vlocal = 0.0;
+    if (C.vlimit > 0.0) {
+      if (C.vlim_node >= 0) {
+        const c2 vl = reg_node_v(p, C.vlim_node, rx, c, n, e);
+        vlocal = sqrt((vl.x / C.ptratio) * (vl.x / C.ptratio) + (vl.y / C.ptratio) * (vl.y / C.ptratio));
+      } else {
+        vlocal = sqrt(vc.x * vc.x + vc.y * vc.y);
+      }
+    }
+    // the line-drop compensation (R + jX) I / CTprim, I the current the
+    // controlled phase delivers from the monitored winding into its bus
+    if (C.ldc) {
+      const pgw_reg_phase& ph = p.phase[C.mon_phase[k]];
       double t1, t2;
       reg_taps(ph, tap, t1, t2);
       c2 yaa, yab, ybb;
@@ -195,17 +223,20 @@ __global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64
     }
     const double vact = sqrt(vc.x * vc.x + vc.y * vc.y);
     const double dv = C.vreg - vact;
-    if (fabs(dv) > C.band * 0.5) {
-      // DoPendingAction (STATIC): the needed change, truncated to whole taps,
-      // at least one, at most max_tap_change, inside [min_tap, max_tap]
-      const double need = dv / C.vbase;
+    const bool over = C.vlimit > 0.0 && vlocal > C.vlimit;
+    if (fabs(dv) > C.band * 0.5 || over) {
+      // DoPendingAction (STATIC): the needed change (above Vlimit: down to it),
+      // truncated to whole taps, at least one, at most max_tap_change, inside
+      // [min_tap, max_tap]
+      const double need = (over ? C.vlimit - vlocal : dv) / C.vbase;
       double steps = trunc(fabs(need) / C.incr);
       steps = fmin(fmax(steps, 1.0), (double)C.max_tap_change);
       double nt = tap + (need > 0.0 ? steps : -steps) * C.incr;
       nt = fmin(fmax(nt, C.min_tap), C.max_tap);
       if (nt != tap) {
         want[g] = nt;
-        dmin = fmin(dmin, C.delay);
+        dl[g] = C.inverse_time ? C.delay / fmin(10.0, 2.0 * fabs(dv) / C.band) : C.delay;
+        dmin = fmin(dmin, dl[g]);
       }
     }
   }
@@ -213,7 +244,7 @@ __global__ void __launch_bounds__(kBlock) k_reg_control(pgw_reg_params p_, int64
   bool moved = false;
   for (int g = 0; g < p.n_ctrl; ++g) {
     const double tap = taps[(int64_t)g * n + e];
-    if (want[g] != tap && p.ctrl[g].delay == dmin) {
+    if (want[g] != tap && dl[g] == dmin) {
       taps[(int64_t)g * n + e] = want[g];
       moved = true;
     }
@@ -241,10 +272,16 @@ static int32_t reg_check(const pgw_reg_params* p, const char* who) {
   }
   for (int g = 0; g < p->n_ctrl; ++g) {
     const pgw_reg_ctrl& C = p->ctrl[g];
-    PGW_REQUIRE(C.pt_node >= 0 && C.pt_node < p->r_reg && C.pt_phase >= 0 && C.pt_phase < p->n_phase &&
+    PGW_REQUIRE(C.n_mon >= 1 && C.n_mon <= PGW_REG_MAX_MON && C.pick >= PGW_REG_PICK_PHASE &&
+                    C.pick <= PGW_REG_PICK_MIN && (C.pick != PGW_REG_PICK_PHASE || C.n_mon == 1) &&
                     (C.winding == 1 || C.winding == 2) && C.ptratio > 0.0 && C.ctprim > 0.0 && C.incr > 0.0 &&
-                    C.vbase > 0.0 && C.min_tap <= C.max_tap && C.max_tap_change >= 1,
+                    C.vbase > 0.0 && C.min_tap <= C.max_tap && C.max_tap_change >= 1 && C.band > 0.0 &&
+                    C.vlimit >= 0.0 && C.vlim_node >= -1 && C.vlim_node < p->r_reg,
                 "%s: RegControl %d", who, g);
+    for (int i = 0; i < C.n_mon; ++i)
+      PGW_REQUIRE(C.mon_node[i] >= 0 && C.mon_node[i] < p->r_reg && C.mon_phase[i] >= 0 &&
+                      C.mon_phase[i] < p->n_phase && p->phase[C.mon_phase[i]].ctrl == g,
+                  "%s: RegControl %d monitored phase %d", who, g, i);
   }
   return PGW_OK;
 }

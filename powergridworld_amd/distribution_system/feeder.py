@@ -344,10 +344,14 @@ class Feeder(object):
         (RegControl.pas): transformer, winding, vreg (120), band (3), ptratio
         (60), CTprim (300), R / X (line-drop compensation, V at CT rating),
         PTphase (1), maxtapchange (16), delay (15 s: the STATIC mode's order),
-        tapwinding (= winding); the transformer's NumTaps (32) / MaxTap (1.1) /
-        MinTap (0.9) give the tap step.  Refused: reversible, vlimit, remote bus
-        sensing, inverse time, PTphase=max/min, a tap winding other than the
-        monitored one, delta or centre-tapped regulator windings."""
+        tapwinding (= winding), PTphase=max / min (the phase of largest /
+        smallest |V|), Bus (the regulated bus: its node of each monitored
+        phase -- the listed nodes in phase order, else the winding's node
+        numbers -- sensed instead of the winding, no line-drop compensation),
+        Vlimit (0 = off), InverseTime; the transformer's NumTaps (32) / MaxTap
+        (1.1) / MinTap (0.9) give the tap step.  Refused: reversible,
+        PTphase=avg, a tap winding other than the monitored one, delta or
+        centre-tapped regulator windings."""
         spec = self.spec
         rcs = spec.get("regcontrols") or []
         if not rcs or spec.get("controlmode", "static") == "off":
@@ -369,8 +373,7 @@ class Feeder(object):
             if name in seen:
                 raise NotImplementedError("RegControl %s: a second control on transformer %s" % (rc["name"], name))
             seen.add(name)
-            for bad in ("reversible", "revvreg", "revband", "vlimit", "bus", "inversetime", "revneutral",
-                        "ldc_z", "rev_z", "cogen"):
+            for bad in ("reversible", "revvreg", "revband", "revneutral", "ldc_z", "rev_z", "cogen"):
                 v = str(pr.get(bad, "")).lower()
                 if bad in pr and v not in ("", "no", "n", "false", "0", "0.0"):
                     raise NotImplementedError("RegControl %s: %s=%s is not simulated" % (rc["name"], bad, v))
@@ -390,7 +393,7 @@ class Feeder(object):
                                                                         for _, lo in prs):
                 raise NotImplementedError("RegControl %s: regulator %s needs wye windings to ground" % (rc["name"], name))
             ptp = str(pr["ptphase"]).lower()
-            if not ptp.isdigit() or not 1 <= int(ptp) <= ph:
+            if not (ptp in ("max", "min") and ph > 1) and not (ptp.isdigit() and 1 <= int(ptp) <= ph):
                 raise NotImplementedError("RegControl %s: PTphase=%s" % (rc["name"], ptp))
             w1, w2 = t["windings"]
             s3 = math.sqrt(3.0)
@@ -406,16 +409,30 @@ class Feeder(object):
                 b = rix(self.node(terms[1][0], terms[1][1][p][0]))
                 phases.append(dict(a=a, b=b, ctrl=g, tap_winding=tw, A=A, B=B, C=C,
                                    tap1=w1.get("tap", 1.0), tap2=w2.get("tap", 1.0)))
-            ptph = first + int(ptp) - 1
+            mon = list(range(ph)) if ptp in ("max", "min") else [int(ptp) - 1]
+            wt = terms[w - 1]
+            bus = str(pr.get("bus", "")).strip().lower()
+            if bus:                                      # the regulated bus's node per monitored phase
+                parts = bus.split(".")
+                nds = [int(x) for x in parts[1:]]
+                mon_nodes = [rix(self.node(parts[0], nds[q] if q < len(nds) else wt[1][q][0])) for q in mon]
+            else:
+                mon_nodes = [phases[first + q]["a" if w == 1 else "b"] for q in mon]
+            truthy = lambda k: str(pr.get(k, "no")).lower() in ("yes", "y", "true", "t", "1")
             numtaps = float(t.get("numtaps", 32.0))
             maxtap, mintap = float(t.get("maxtap", 1.10)), float(t.get("mintap", 0.90))
             ptratio = num("ptratio")
             vw = vw1 if w == 1 else vw2
-            ctrls.append(dict(pt_node=phases[ptph]["a" if w == 1 else "b"], pt_phase=ptph, winding=w,
+            ctrls.append(dict(n_mon=len(mon), pick={"max": 1, "min": 2}.get(ptp, 0), mon_node=mon_nodes,
+                              mon_phase=[first + q for q in mon], winding=w,
+                              ldc=int(not bus and (num("r") != 0.0 or num("x") != 0.0)),
+                              vlim_node=phases[first]["a" if w == 1 else "b"] if bus else -1,
+                              inverse_time=int(truthy("inversetime")),
                               max_tap_change=int(num("maxtapchange")), vreg=num("vreg"), band=num("band"),
                               ptratio=ptratio, ctprim=num("ctprim"), r_ldc=num("r"), x_ldc=num("x"),
                               vbase=vw / ptratio, incr=(maxtap - mintap) / numtaps, min_tap=mintap,
-                              max_tap=maxtap, delay=num("delay"), name=rc["name"]))
+                              max_tap=maxtap, delay=num("delay"), vlimit=num("vlimit") if "vlimit" in pr else 0.0,
+                              name=rc["name"]))
             taps0.append(t["windings"][w - 1].get("tap", 1.0))
         if len(phases) > _lib.REG_MAX_PHASES or len(ctrls) > _lib.REG_MAX_CTRL:
             raise NotImplementedError("%d regulated phases / %d RegControls (max %d / %d)"

@@ -1026,9 +1026,12 @@ class OpenDSSSolver(PowerFlowSolver):
             d.tap1, d.tap2 = ph["tap1"], ph["tap2"]
         for g, c in enumerate(reg["ctrls"]):
             d = rp.ctrl[g]
-            for key in ("pt_node", "pt_phase", "winding", "max_tap_change", "vreg", "band", "ptratio",
-                        "ctprim", "r_ldc", "x_ldc", "vbase", "incr", "min_tap", "max_tap", "delay"):
+            for key in ("n_mon", "pick", "winding", "max_tap_change", "ldc", "vlim_node", "inverse_time", "vreg",
+                        "band", "ptratio", "ctprim", "r_ldc", "x_ldc", "vbase", "incr", "min_tap", "max_tap",
+                        "delay", "vlimit"):
                 setattr(d, key, c[key])
+            for i in range(c["n_mon"]):
+                d.mon_node[i], d.mon_phase[i] = c["mon_node"][i], c["mon_phase"][i]
         rp.S, rp.rho = self._reg_S.data_ptr(), self._reg_rho.data_ptr()
         self._reg_params = rp
         self.control_iterations = 0

@@ -468,6 +468,72 @@ def test_regcontrol_model_woodbury_matches_rebuilt_network():
     assert not moved
 
 
+REGCTL2 = os.path.join(REPO, "tests", "data", "regctl2_feeder.dss")
+
+
+def test_regcontrol_sample_options_model():
+    """RegControl's Sample options (tests/data/regctl2_feeder.dss): Bus= puts
+    the regulated bus's nodes into R as sensed nodes (no line-drop
+    compensation; Vlimit then reads the winding's first phase), PTphase=max /
+    min monitor every phase of a gang-operated unit, Vlimit and InverseTime
+    reach the control records; the Woodbury model with the extra sensed nodes
+    still gives the rebuilt network's voltages; the oracle's loop ends in band
+    (or at Vlimit) at light load.  Parity unpinned (no OpenDSS)."""
+    from powergridworld_amd import _lib
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    spec = load_feeder_spec(REGCTL2)
+    f, o = Feeder(spec), OracleFeeder(spec)
+    reg = f.regulators()
+    R = reg["nodes"]
+    name = lambda j: f.node_names[R[j]]
+    c = {d["name"]: d for d in reg["ctrls"]}
+    assert len(reg["phases"]) == 9 and len(R) == 21
+    assert [name(j) for j in c["reg1"]["mon_node"]] == ["b3.1"] and c["reg1"]["ldc"] == 0
+    assert name(c["reg1"]["vlim_node"]) == "rg60.1"
+    assert c["reg2"]["ldc"] == 1 and c["reg2"]["vlimit"] == 126.5 and c["reg2"]["vlim_node"] == -1
+    assert c["reg3"]["inverse_time"] == 1 and c["reg3"]["n_mon"] == 1
+    assert c["regg"]["pick"] == _lib.REG_PICK_MAX and c["regg"]["n_mon"] == 3 and c["regg"]["ldc"] == 1
+    assert [name(j) for j in c["regg"]["mon_node"]] == ["b5.1", "b5.2", "b5.3"]
+    assert c["regh"]["pick"] == _lib.REG_PICK_MIN and c["regh"]["inverse_time"] == 1
+    assert [name(j) for j in c["regh"]["mon_node"]] == ["b8.1", "b8.2", "b8.3"]
+    assert c["regh"]["mon_phase"] == [6, 7, 8] and name(c["regh"]["vlim_node"]) == "b7.1"
+    r = len(R)
+    rng = np.random.default_rng(1)
+    for _ in range(3):
+        taps = reg["taps0"] + 0.00625 * rng.integers(-8, 9, size=len(reg["ctrls"]))
+        D = np.zeros((r, r), complex)
+        for ph in reg["phases"]:
+            t = taps[ph["ctrl"]]
+            t1 = t if ph["tap_winding"] == 1 else ph["tap1"]
+            t2 = t if ph["tap_winding"] == 2 else ph["tap2"]
+            Y = lambda a, b: np.array([[ph["A"] / a ** 2, ph["B"] / (a * b)], [ph["B"] / (a * b), ph["C"] / b ** 2]])
+            D[np.ix_([ph["a"], ph["b"]], [ph["a"], ph["b"]])] += Y(t1, t2) - Y(ph["tap1"], ph["tap2"])
+        K = np.linalg.solve(np.eye(r) + D @ reg["S"], D)
+        V = f.V0 - f.Z[:, R] @ (K @ f.V0[R])
+        ot = o.with_taps(list(taps))
+        np.testing.assert_allclose(V, ot.V0, rtol=1e-9, atol=1e-9 * np.abs(ot.V0).max())
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float)
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float)
+    V, it, tp, cp = o.solve_regulated(0.5 * kw[None], 0.5 * kvar[None], reg["taps0"][None])
+    assert 2 <= cp[0] < 15 and (tp[0] != reg["taps0"]).any()
+    _, moved = o.reg_control_pass(V[0], list(tp[0]))
+    assert not moved
+
+
+def test_regcontrol_refuses_unsimulated_options(tmp_path):
+    """Reversible regulators and PTphase=avg stay refused, loudly."""
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    txt = open(REGCTL2).read()
+    for old, bad in (("maxtapchange=4 inversetime=yes", "maxtapchange=4 inversetime=yes reversible=yes"),
+                     ("ptphase=max", "ptphase=avg")):
+        assert old in txt
+        fn = tmp_path / "bad.dss"
+        fn.write_text(txt.replace(old, bad, 1))
+        with pytest.raises(NotImplementedError):
+            Feeder(load_feeder_spec(str(fn))).regulators()
+
+
 def test_checkpoint_walk_restores_in_place():
     """checkpoint.state_dict / load_state_dict on a stand-in object tree (CPU
     tensors): tensors restored in place (identity kept), a view restored

@@ -24,6 +24,7 @@ FEEDER48 = os.path.join(HERE, "data", "feeder48.dss")
 MODELS = os.path.join(HERE, "data", "models_feeder.dss")
 XFMR3 = os.path.join(HERE, "data", "xfmr3_feeder.dss")
 REGCTL = os.path.join(HERE, "data", "regctl_feeder.dss")
+REGCTL2 = os.path.join(HERE, "data", "regctl2_feeder.dss")
 IEEE13 = "ieee_13_dss/IEEE13Nodeckt.dss"
 SHAPE = "ieee_13_dss/annual_hourly_load_profile.csv"
 
@@ -173,10 +174,13 @@ def test_three_winding_and_centre_tap_transformers_vs_oracle():
     np.testing.assert_allclose(g2, o2, rtol=1e-9, atol=0)
 
 
+@pytest.mark.parametrize("feeder", ["regctl", "regctl2"])
 @pytest.mark.parametrize("semantics", ["exact", "opendss"])
-def test_regcontrol_vs_oracle(semantics):
+def test_regcontrol_vs_oracle(semantics, feeder):
     """RegControl (tests/data/regctl_feeder.dss: three single-phase regulators,
-    one with line-drop compensation, and a gang-operated 3-phase one): per-env
+    one with line-drop compensation, and a gang-operated 3-phase one;
+    regctl2_feeder.dss: Sample's options -- a remote regulated bus, Vlimit
+    over line-drop compensation, inverse time, PTphase=max / min): per-env
     taps through the Woodbury-corrected general kernel and the device control
     pass (pgw_reg_control / pgw_reg_factor) against the oracle's SolveSnap
     restatement that rebuilds and re-inverts Y at every tap set -- the same
@@ -184,13 +188,15 @@ def test_regcontrol_vs_oracle(semantics):
     consecutive steps (taps persist) from random per-env starting taps.
     Parity unpinned (no OpenDSS)."""
     K = 192
-    o = _oracle(REGCTL, 1.0)
-    s = _solver(REGCTL, num_envs=K, convergence=semantics)
+    path = {"regctl": REGCTL, "regctl2": REGCTL2}[feeder]
+    o = _oracle(path, 1.0)
+    s = _solver(path, num_envs=K, convergence=semantics)
     f = o.feeder
     reg = s.regulators
-    assert s.general and reg is not None and len(reg["ctrls"]) == 4
+    nc = len(reg["ctrls"])
+    assert s.general and reg is not None and nc == {"regctl": 4, "regctl2": 5}[feeder]
     rng = np.random.default_rng(11)
-    taps = reg["taps0"][None, :] + 0.00625 * rng.integers(-6, 7, size=(K, 4))
+    taps = reg["taps0"][None, :] + 0.00625 * rng.integers(-6, 7, size=(K, nc))
     s.set_regulator_taps(torch.tensor(taps.T.copy(), device=DEV))
     moved = 0
     for t in TIMES[1:3]:
