@@ -461,6 +461,13 @@ typedef struct pgw_pf_od {
 int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
                      const double* ctrl_p, const double* ctrl_q, double* v_out,
                      int32_t* iters, void* stream);
+/* fp32-storage variant: ctrl_p / ctrl_q / v_out float, widened
+ * on load and rounded once on store; the solve itself is the fp64 one (same
+ * kernels, same iteration counts), and the pgw_pf_tables outputs (extrema,
+ * element voltages) stay double. */
+int32_t pgw_pf_solve_f32(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
+                         const float* ctrl_p, const float* ctrl_q, float* v_out,
+                         int32_t* iters, void* stream);
 
 /* Response-table builder (OpenDSSSolver._od_response): the snap solve of
  * pgw_pf_od at n lanes, lane e at controllable kW P[e] (Q = 0) in hour

@@ -327,6 +327,7 @@ _SIGS = {
     "pgw_ev_step": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
+    "pgw_pf_solve_f32": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_solve_general": (i32, [P(PFGParams), P(PFGTables), i64, vp, vp, vp, vp, vp]),
     "pgw_reg_factor": (i32, [P(RegParams), i64, vp, vp, vp, vp]),
     "pgw_reg_control": (i32, [P(RegParams), i64, vp, vp, vp, vp, vp, vp]),

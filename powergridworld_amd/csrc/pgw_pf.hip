@@ -537,11 +537,14 @@ __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_ld
   }
 }
 
-template <int M, bool UB, bool GC, bool KEEP>
+// IO: the storage type of ctrl_p / ctrl_q / v_out (double, or float for
+// pgw_pf_solve_f32: inputs widened, every output rounded once; the arithmetic
+// is the fp64 solve's).
+template <int M, bool UB, bool GC, bool KEEP, class IO = double>
 __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, int64_t n,
-                                                     const double* __restrict__ ctrl_p,
-                                                     const double* __restrict__ ctrl_q,
-                                                     double* __restrict__ v_out,
+                                                     const IO* __restrict__ ctrl_p,
+                                                     const IO* __restrict__ ctrl_q,
+                                                     IO* __restrict__ v_out,
                                                      int32_t* __restrict__ iters) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
@@ -557,8 +560,8 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
-    cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
-    cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
+    cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? (double)ctrl_p[(int64_t)c * n + e] : 0.0;
+    cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? (double)ctrl_q[(int64_t)c * n + e] : 0.0;
   }
   S.powers(a, cp, cq, (t.load_scale && valid) ? t.load_scale[e] : 1.0);
   pf_trace(trace, 1);
@@ -585,7 +588,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   if constexpr (kKeep) {
     if (v_out || !rows_lds) {
       pf_rows_out<M>(t, rows_lds, s_rows, a.n_out, ir, ii, [&](int o, double v) {
-        if (valid && v_out) v_out[(int64_t)o * n + e] = v;
+        if (valid && v_out) v_out[(int64_t)o * n + e] = (IO)v;
         vmn = (v < vmn) ? v : vmn;
         vmx = (v > vmx) ? v : vmx;
       });
@@ -606,7 +609,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve(PFArgs a, pgw_pf_tables t, 
   if (!valid) return;
   if (t.sig_out) t.sig_out[e] = sig;
   if (a.n_out > 0) {
-    if (v_out) v_out[e] = v0;
+    if (v_out) v_out[e] = (IO)v0;
     if (t.v_min_out) t.v_min_out[e] = vmn;
     if (t.v_max_out) t.v_max_out[e] = vmx;
   }
@@ -1792,11 +1795,11 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
 // powers) and outputs (every output row from the accepted iteration's currents
 // -- staged in the solve's LDS after it, od_rows_put --, extrema, element
 // voltages), the response table / snap solve in between.
-template <int M>
+template <int M, class IO = double>
 __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_pf_tables t, int64_t n,
-                                                        const double* __restrict__ ctrl_p,
-                                                        const double* __restrict__ ctrl_q,
-                                                        double* __restrict__ v_out,
+                                                        const IO* __restrict__ ctrl_p,
+                                                        const IO* __restrict__ ctrl_q,
+                                                        IO* __restrict__ v_out,
                                                         int32_t* __restrict__ iters) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool valid = e < n;
@@ -1813,8 +1816,8 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
-    cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? ctrl_p[(int64_t)c * n + e] : 0.0;
-    cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? ctrl_q[(int64_t)c * n + e] : 0.0;
+    cp[c] = (valid && c < a.n_ctrl && ctrl_p) ? (double)ctrl_p[(int64_t)c * n + e] : 0.0;
+    cq[c] = (valid && c < a.n_ctrl && ctrl_q) ? (double)ctrl_q[(int64_t)c * n + e] : 0.0;
   }
   S.powers(a, cp, cq, 1.0);
   double ir[M], ii[M], v0r, v0i;
@@ -1845,7 +1848,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     const double vfm = sqrt(vf2);
     pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
       v = (served && ro == o.resp_v_row) ? vfm : v;
-      if (valid && v_out) v_out[(int64_t)ro * n + e] = v;
+      if (valid && v_out) v_out[(int64_t)ro * n + e] = (IO)v;
       vmn = (v < vmn) ? v : vmn;
       vmx = (v > vmx) ? v : vmx;
     });
@@ -1863,7 +1866,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   }
   if (!valid) return;
   if (a.n_out > 0) {
-    if (v_out) v_out[e] = v0;
+    if (v_out) v_out[e] = (IO)v0;
     if (t.v_min_out) t.v_min_out[e] = vmn;
     if (t.v_max_out) t.v_max_out[e] = vmx;
   }
@@ -2105,10 +2108,10 @@ static PFArgs make_pf_args(const pgw_pf_params& p, const pgw_pf_tables& t) {
   return a;
 }
 
-template <int M, bool UB, bool GC, bool KEEP>
-static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t n, const double* cp,
-                               const double* cq, double* v_out, int32_t* iters, hipStream_t st) {
-  launch_timed(PGW_T_PF_SOLVE, k_pf_solve<M, UB, GC, KEEP>, dim3(grid_for(n)), dim3(kBlock), st, a, t, n,
+template <int M, bool UB, bool GC, bool KEEP, class IO>
+static int32_t launch_pf_solve(const PFArgs& a, const pgw_pf_tables& t, int64_t n, const IO* cp,
+                               const IO* cq, IO* v_out, int32_t* iters, hipStream_t st) {
+  launch_timed(PGW_T_PF_SOLVE, k_pf_solve<M, UB, GC, KEEP, IO>, dim3(grid_for(n)), dim3(kBlock), st, a, t, n,
                cp, cq, v_out, iters);
   return check_launch("k_pf_solve");
 }
@@ -2467,9 +2470,12 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
   return PGW_OK;
 }
 
-int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
-                     const double* ctrl_p, const double* ctrl_q, double* v_out, int32_t* iters,
-                     void* stream) {
+}  // extern "C"
+
+// pgw_pf_solve / pgw_pf_solve_f32 (IO: the per-env buffers' storage type)
+template <class IO>
+static int32_t pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n, const IO* ctrl_p,
+                        const IO* ctrl_q, IO* v_out, int32_t* iters, void* stream) {
   PGW_REQUIRE(p && t && t->block && n >= 0, "pgw_pf_solve: null argument");
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PF_MAX_M && p->m == padded_m(p->m),
               "pgw_pf_solve: m=%d not padded (pgw_pf_padded_m)", p->m);
@@ -2485,11 +2491,25 @@ int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
   if (n == 0) return PGW_OK;
   const PFArgs a = make_pf_args(*p, *t);
   if (t->od) {
-    launch_timed(PGW_T_PF_SOLVE, k_pf_solve_od<14>, dim3(grid_for(n)), dim3(kBlock), (hipStream_t)stream, a,
+    launch_timed(PGW_T_PF_SOLVE, k_pf_solve_od<14, IO>, dim3(grid_for(n)), dim3(kBlock), (hipStream_t)stream, a,
                  make_od_args(*t->od, p->max_iter), *t, n, ctrl_p, ctrl_q, v_out, iters);
     return check_launch("k_pf_solve_od");
   }
   PGW_PF_DISPATCH(*p, *t, launch_pf_solve, a, *t, n, ctrl_p, ctrl_q, v_out, iters, (hipStream_t)stream);
+}
+
+extern "C" {
+
+int32_t pgw_pf_solve(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
+                     const double* ctrl_p, const double* ctrl_q, double* v_out, int32_t* iters,
+                     void* stream) {
+  return pf_solve(p, t, n, ctrl_p, ctrl_q, v_out, iters, stream);
+}
+
+int32_t pgw_pf_solve_f32(const pgw_pf_params* p, const pgw_pf_tables* t, int64_t n,
+                         const float* ctrl_p, const float* ctrl_q, float* v_out, int32_t* iters,
+                         void* stream) {
+  return pf_solve(p, t, n, ctrl_p, ctrl_q, v_out, iters, stream);
 }
 
 int32_t pgw_coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, const pgw_pf_tables* pft,

@@ -315,3 +315,39 @@ def test_od_response_table_bit_identical_paths():
                                        rtol=1e-10, atol=0)
     for nm in ("632.1", "671.2", "652.1", "675.3"):
         assert torch.equal(envs[0].voltages[nm], envs[1].voltages[nm])
+
+
+# ------------------------------------------------------------------ fp32 storage (pgw_pf_solve_f32)
+@pytest.mark.parametrize("conv", ["opendss", "opendss_no_table", "exact"])
+def test_pf_solve_f32_equals_fp64_solve(conv):
+    """pgw_pf_solve_f32 (SURVEY 8(b)'s fp32 entry): float controllable powers
+    in, float node voltages out, the fp64 solve in between -- every output the
+    fp64 entry's value on the same (widened) inputs rounded once, every
+    iteration count equal, at 4 096 envs over four hours, under the OpenDSS
+    rule (with and without the response table) and the exact fixed point."""
+    from powergridworld_amd import _lib
+    K = 4096
+    kw = dict(convergence="exact") if conv == "exact" else {}
+    if conv == "opendss_no_table":
+        kw["od_table"] = False
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    s = OpenDSSSolver(IEEE13, SHAPE, device=DEV, system_load_rescale_factor=1.2, num_envs=K,
+                      **dict({"convergence": "opendss"}, **kw))
+    lib = _lib.lib()
+    st = _lib.stream_ptr(torch.device(DEV))
+    for t, (p, q) in zip(TIMES, _loads(K, 7)):
+        s.calculate_power_flow({"675c": torch.tensor(p, device=DEV)}, None, current_time=t)   # tables built
+        prm, tb = s.step_params(t), s.solve_tables(t, True)
+        n_out = prm.n_out
+        p32 = torch.tensor(p, dtype=torch.float32, device=DEV)[None].contiguous()
+        p64 = p32.double()
+        v64 = torch.empty((n_out, K), dtype=torch.float64, device=DEV)
+        v32 = torch.empty((n_out, K), dtype=torch.float32, device=DEV)
+        i64 = torch.empty(K, dtype=torch.int32, device=DEV)
+        i32 = torch.empty(K, dtype=torch.int32, device=DEV)
+        _lib.check(lib.pgw_pf_solve(prm, tb, K, _lib.dptr(p64), None, _lib.dptr(v64), _lib.dptr(i64), st))
+        _lib.check(lib.pgw_pf_solve_f32(prm, tb, K, _lib.dptr(p32), None, _lib.dptr(v32), _lib.dptr(i32), st))
+        torch.cuda.synchronize()
+        assert torch.equal(i64, i32), t
+        assert torch.equal(v64.float(), v32), t
+        assert (i64 != 0).all() and torch.isfinite(v64).all()
