@@ -1030,7 +1030,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf(CoordPFArgs c, PFArgs a, pg
     // reward -= share as a no-return atomic add of -share: one IEEE add per
     // address (bit-identical to the subtraction, deterministic), no load
     // round trip at the end of the kernel.  fp32 storage: the share is rounded
-    // to fp32 first, so the add is RN32(r - RN32(share)).
+    // to fp32 first, so the add is RN32(r - RN32(share)).  (Reading the
+    // rewards with the powers instead, k_coord_pf_od's form, measured no
+    // faster here: profiles/r05/ab_rewx.txt.)
 #pragma unroll
     for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
       if (ag < c.n_agents)
@@ -1724,6 +1726,13 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
     rp[ag] = (double)b.agent_power[(int64_t)min(ag, c.n_agents - 1) * n + ec] *
              ((valid && ag < c.n_agents) ? 1.0 : 0.0);
+  // the agents' rewards, read with their powers (one round trip): the
+  // epilogue stores reward + (-share) -- the read-modify-write's value --
+  // instead of 5 device-scope atomics at the end
+  Sto rw[PGW_MAX_AGENTS];
+#pragma unroll
+  for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
+    rw[ag] = (c.coordinated && ag < c.n_agents) ? b.reward[(int64_t)ag * n + ec] : (Sto)0;
   PFSolver<M, true, false> S;
   S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
@@ -1784,9 +1793,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
     const double share = (vv * c.vv_penalty) / (double)c.n_agents;
 #pragma unroll
     for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
-      if (ag < c.n_agents)
-        (void)__hip_atomic_fetch_add(b.reward + (int64_t)ag * n + e, (Sto)(-share), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+      if (ag < c.n_agents) b.reward[(int64_t)ag * n + e] = (Sto)(rw[ag] + (Sto)(-share));
   }
   if constexpr (TR) pf_trace(tr, 6);
 }
