@@ -434,6 +434,14 @@ typedef struct pgw_pf_tables {
  * serves, and a solve whose only output is that row reads 96 bytes per env
  * instead of the 720-byte record. */
 #define PGW_OD_VREC 12
+/* Extrema rows (resp_rows, ABI 29; 0 = every row): with v_out NULL and the
+ * extrema wanted (pgw_pf_tables.v_min_out / v_max_out), bit r set for output
+ * row r (1 <= r < 64) that can be the minimum or the maximum |V| of an env
+ * the hour's table serves -- proved on the host from the records' quadratics
+ * (interval bounds of every row's |V|^2 over every served piece, with a
+ * margin far above rounding): a wave whose envs are all served evaluates
+ * only those rows (and row 0), which leaves every extremum's value unchanged;
+ * a wave with an env solved in full evaluates every row. */
 typedef struct pgw_pf_od {
   double tol;                        /* 1e-4 (ConvergenceTolerance)            */
   double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M];   /* y0' per element (W, -var) */
@@ -450,6 +458,7 @@ typedef struct pgw_pf_od {
   int32_t resp_nseg;                 /* grid segments (primary records)         */
   int32_t resp_v_row;                /* output row of the node records; < 0 none */
   const double* resp_v;              /* node records (PGW_OD_VREC each) or NULL */
+  uint64_t resp_rows;                /* extrema rows of served envs; 0 = all    */
 } pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

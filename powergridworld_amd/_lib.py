@@ -110,7 +110,7 @@ class PFOD(C.Structure):
                 ("elem_scale", f64 * PF_MAX_M), ("gamma", f64), ("eps", f64), ("gmax", f64),
                 ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("sparse_envs", i32),
                 ("rows_V0", vp), ("rows_G", vp), ("start", vp), ("resp", vp), ("resp_x0", f64),
-                ("resp_h", f64), ("resp_nseg", i32), ("resp_v_row", i32), ("resp_v", vp)]
+                ("resp_h", f64), ("resp_nseg", i32), ("resp_v_row", i32), ("resp_v", vp), ("resp_rows", u64)]
 
 
 OD_REC_HEAD = 6

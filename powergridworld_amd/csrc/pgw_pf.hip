@@ -537,6 +537,37 @@ __device__ __forceinline__ void pf_rows_out(const pgw_pf_tables& t, bool rows_ld
   }
 }
 
+// pf_rows_out's squared magnitudes for the rows of `mask` only (bit r: row r,
+// 1 <= r < n_out; wave-uniform), four at a time from the staged rows -- each
+// row with pf_row4_dpp's operations, so a row's value is the one pf_rows_out
+// gives it.
+template <int M, class F>
+__device__ __forceinline__ void pf_rows_mask2(const double* s, int n_out, uint64_t mask, const double (&ir)[M],
+                                              const double (&ii)[M], F&& f) {
+  constexpr int P = PFRow<M>::kPairs;
+  if (n_out < 64) mask &= (1ull << n_out) - 1;
+  mask &= ~1ull;
+  while (mask) {                                     // (uniform)
+    int r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      r[q] = mask ? __builtin_ctzll(mask) : -1;
+      mask &= mask - 1;
+    }
+    double wa[P], wb[P], wc[P], wd[P];
+    pf_row_load<M>(s, r[0], wa);
+    pf_row_load<M>(s, r[1] < 0 ? r[0] : r[1], wb);
+    pf_row_load<M>(s, r[2] < 0 ? r[0] : r[2], wc);
+    pf_row_load<M>(s, r[3] < 0 ? r[0] : r[3], wd);
+    double ar, ai, br, bi, cr, ci, dr, di;
+    pf_row4_dpp<M>(ar, ai, br, bi, cr, ci, dr, di, wa, wb, wc, wd, ir, ii);
+    f(r[0], pf_mag<M, false>(ar, ai));
+    if (r[1] >= 0) f(r[1], pf_mag<M, false>(br, bi));
+    if (r[2] >= 0) f(r[2], pf_mag<M, false>(cr, ci));
+    if (r[3] >= 0) f(r[3], pf_mag<M, false>(dr, di));
+  }
+}
+
 // IO: the storage type of ctrl_p / ctrl_q / v_out (double, or float for
 // pgw_pf_solve_f32: inputs widened, every output rounded once; the arithmetic
 // is the fp64 solve's).
@@ -1071,6 +1102,7 @@ struct ODArgs {
   int32_t resp_nseg;
   int32_t resp_v_row;                             // output row of the node records (-1: none)
   const double* resp_v;                           // node records (pgw_pf_od.resp_v) or null
+  uint64_t resp_rows;                             // extrema rows of served envs (0: all)
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
 constexpr int kOdChunk = 12;                      // check rows per previous-magnitude pass
@@ -1127,6 +1159,7 @@ static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   o.resp_nseg = resp ? d.resp_nseg : 0;
   o.resp_v = (resp && d.resp_v && d.resp_v_row >= 0) ? d.resp_v : nullptr;
   o.resp_v_row = o.resp_v ? d.resp_v_row : -1;
+  o.resp_rows = resp ? d.resp_rows : 0;
   return o;
 }
 
@@ -1863,11 +1896,17 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     // extrema only: min / max of |V|^2 over the rows, one sqrt each at the end
     // (as k_pf_solve: sqrt is monotone and correctly rounded)
     double mn2 = fma(v0i, v0i, v0r * v0r), mx2 = mn2;
-    pf_rows_out<M, false>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double m2) {
+    auto ext = [&](int ro, double m2) {
       m2 = (served && ro == o.resp_v_row) ? vf2 : m2;
       mn2 = (m2 < mn2) ? m2 : mn2;
       mx2 = (m2 > mx2) ? m2 : mx2;
-    });
+    };
+    // only the rows that can hold a served env's extremum (pgw_pf_od.resp_rows),
+    // unless an env of this wave was solved in full
+    if (rows_lds && o.resp_rows != 0 && __ballot(valid && !served) == 0ull)
+      pf_rows_mask2<M>(srow, a.n_out, o.resp_rows | (o.resp_v_row > 0 ? 1ull << o.resp_v_row : 0ull), ir, ii, ext);
+    else
+      pf_rows_out<M, false>(t, rows_lds, srow, a.n_out, ir, ii, ext);
     vmn = sqrt(mn2);
     vmx = sqrt(mx2);
   }

@@ -277,7 +277,9 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_start = torch.zeros((self.OD_MAX_TABLES, 12 * M), dtype=torch.float64, device=dev)
         self._od_resp = None                 # response tables (allocated on the first build)
         self._od_vresp = None                # their node records (pgw_pf_od.resp_v)
+        self._od_rowmask = {}                # pgw_pf_od.resp_rows per (table row, configuration)
         self.od_node_records = True          # False: every solve reads the node's row from the currents
+        self.od_row_masks = True             # pgw_pf_od.resp_rows (False: every row, for A/Bs and tests)
         self.od_resp_stats, self.od_resp_brackets = {}, {}
         self._od_index = {}
         self._od_keep = {}
@@ -393,6 +395,50 @@ class OpenDSSSolver(PowerFlowSolver):
         v = (c * G).sum(-1)
         v[..., 0] = v[..., 0] + complex(self._od_V0all[node])
         return v
+
+    def _od_row_mask(self, idx):
+        """pgw_pf_od.resp_rows of table row idx for the present output rows (0 =
+        every row): the rows r >= 1 that can hold the minimum or the maximum
+        |V| of an env the table serves.  Every served record's rows are
+        V_r(t) = A_r + t (B_r + t C_r) (V0 + G J'(t) composed); |V_r|^2 over the
+        piece's t range is bounded by 9 samples plus a Lipschitz margin plus
+        1e-9 (far above the kernels' rounding and the node records' fit), and a
+        row is kept when its lower bound reaches every row's upper bound (a
+        minimum candidate) or its upper bound every row's lower bound (a maximum
+        candidate) in some piece.  Cached per (row, configuration)."""
+        key = (idx, self._cfg_version)
+        if key in self._od_rowmask:
+            return self._od_rowmask[key]
+        names = list(self.output_names)
+        mask = 0
+        if self._od_resp is not None and 2 <= len(names) <= 64:
+            f, M, dev = self.feeder, self.M, self.device
+            recs = self._od_resp[idx]
+            meta = recs.view(torch.int64)[:, 4]
+            rr = recs[((meta & 0xffffffff) != 0) & (recs[:, 0] <= recs[:, 1])]
+            if rr.shape[0]:
+                rows = [f.node_index[nm] for nm in names]
+                G = torch.from_numpy(np.ascontiguousarray(self._od_Gall[rows][:, :M])).to(dev)
+                V0 = torch.from_numpy(np.ascontiguousarray(self._od_V0all[rows])).to(dev)
+                c = torch.view_as_complex(rr[:, 6:6 + 6 * M].reshape(-1, 3, M, 2).contiguous())
+                abc = torch.einsum("pqm,rm->pqr", c, G)                          # [P, 3, rows]
+                A, B, C = abc[:, 0] + V0, abc[:, 1], abc[:, 2]
+                tl, th = (rr[:, 0] - rr[:, 2]) * rr[:, 3], (rr[:, 1] - rr[:, 2]) * rr[:, 3]
+                S = 9
+                ts = (tl[:, None] + (th - tl)[:, None] * torch.linspace(0.0, 1.0, S, dtype=torch.float64,
+                                                                          device=dev)[None, :])[:, :, None]
+                V = A[:, None, :] + ts * (B[:, None, :] + ts * C[:, None, :])    # [P, S, rows]
+                m2 = V.real * V.real + V.imag * V.imag
+                T = torch.maximum(tl.abs(), th.abs())[:, None]
+                L = 2.0 * (A.abs() + B.abs() * T + C.abs() * T * T) * (B.abs() + 2.0 * C.abs() * T)
+                marg = L * ((th - tl)[:, None] / (S - 1)) * 0.5 + 1e-9
+                lo, hi = m2.min(1).values - marg, m2.max(1).values + marg
+                cand = ((lo <= hi.min(1, keepdim=True).values) | (hi >= lo.max(1, keepdim=True).values)).any(0)
+                cand = cand.cpu().numpy()
+                ok = bool(torch.isfinite(lo).all() and torch.isfinite(hi).all())
+                mask = sum(1 << r for r in range(1, len(names)) if cand[r]) if ok else 0
+        self._od_rowmask[key] = mask
+        return mask
 
     def _od_response(self, hours, idx0):
         """Build and upload the response tables of `hours` (rows idx0.. of the
@@ -590,6 +636,12 @@ class OpenDSSSolver(PowerFlowSolver):
             vb = self._od_vresp[idx0:idx0 + H]
             vb.view(torch.int64)[:, :, :6] = blk.view(torch.int64)[:, :, :6]
             vb[:, :, 6:12] = torch.view_as_real(self._od_vcoef(blk)).reshape(H, rec_n, 6)
+        # the extrema rows of the rebuilt table rows (computed here, with the
+        # build, not at the first step of each hour)
+        for q in range(H):
+            for k in [k for k in self._od_rowmask if k[0] == idx0 + q]:
+                del self._od_rowmask[k]
+            self._od_row_mask(idx0 + q)
         # the brackets per table row (kW intervals the tables leave to the solve;
         # an hour's row: _od_index[_hour_key(hour)]), for tests and diagnostics
         for q, hr in enumerate(hours):
@@ -620,6 +672,7 @@ class OpenDSSSolver(PowerFlowSolver):
         if self.od_table and self._od_resp is not None:
             od.resp = self._od_resp[idx].data_ptr()
             od.resp_x0, od.resp_h, od.resp_nseg = self.PREDICTOR_X0, self.PREDICTOR_H, self.PREDICTOR_N - 1
+            od.resp_rows = self._od_row_mask(idx) if self.od_row_masks else 0
             vnode = self._od_vnode()
             if self._od_vresp is not None and vnode is not None and self.od_node_records:
                 name = self.feeder.node_names[vnode]

@@ -348,6 +348,46 @@ def test_het_opendss_fused_equals_generic():
         assert torch.equal(envs[0].pf_solver.iterations, envs[1].pf_solver.iterations)
 
 
+def test_het_extrema_rows_mask_changes_nothing():
+    """pgw_pf_od.resp_rows (OpenDSSSolver._od_row_mask): the heterogeneous
+    scenario's extrema evaluated on the rows the host proved can hold a served
+    env's minimum or maximum |V| are bit-identical to every row's -- the
+    rewards, the PV farm's min-voltage observation, the iteration counts and
+    both extrema, over 60 steps at 8 192 envs -- and the masks are non-trivial
+    (fewer rows than the outputs)."""
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    n = 8192
+    envs = [MultiAgentEnv(**make_env_config(pf_convergence="opendss"), num_envs=n, device=DEV) for _ in range(2)]
+    envs[1].pf_solver.od_row_masks = False
+    rng = np.random.default_rng(13)
+    for e in envs:
+        for k, a in enumerate(e.agents):
+            for c in (a.envs if hasattr(a, "envs") else [a]):
+                if hasattr(c, "seed"):
+                    c.seed(60 + k)
+        e.reset()
+    s0 = envs[0].pf_solver
+    masks = [m for (idx, cfg), m in s0._od_rowmask.items()]
+    n_out = len(s0.output_names)
+    assert masks and all(0 < bin(m).count("1") < n_out - 1 for m in masks), (n_out, [bin(m).count("1") for m in masks])
+    for t in range(60):
+        act = {"building": {"building": torch.tensor(rng.uniform(-1, 1, (n, 6)), device=DEV),
+                            "pv": torch.tensor(rng.uniform(-1, 1, (n, 1)), device=DEV),
+                            "storage": torch.tensor(rng.uniform(-1, 1, (n, 1)), device=DEV)},
+               "pv": torch.tensor(rng.uniform(-1, 1, (n, 1)), device=DEV),
+               "ev-charging": torch.tensor(rng.uniform(-1, 1, (n, 1)), device=DEV)}
+        res = [e.step(act) for e in envs]
+        torch.cuda.synchronize()
+        (o0, r0, _, _), (o1, r1, _, _) = res
+        for name in r0:
+            assert torch.equal(r0[name], r1[name]), (t, name)
+        assert torch.equal(o0["pv"], o1["pv"]), t
+        assert torch.equal(envs[0].pf_solver.iterations, envs[1].pf_solver.iterations)
+        for x, y in zip(envs[0].pf_solver.voltage_extrema(), envs[1].pf_solver.voltage_extrema()):
+            assert torch.equal(x, y), t
+
+
 def test_regcontrol_multiagent_generic_path():
     """A MultiAgentEnv on the RegControl feeder (PV farm, EV station and battery
     agents on its loads f1 / a1 / f2): the fused paths step aside (the control
