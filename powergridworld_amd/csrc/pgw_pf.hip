@@ -1782,7 +1782,7 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   }
   S.powers(a, cp, cq, 1.0);
   if constexpr (TR) { if (S.pc != -1e300) pf_trace(tr, 1); }
-  double ir[M], ii[M], v0r, v0i;
+  double ir[M], ii[M], v0r = 0.0, v0i = 0.0;
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
   int it = 0;
@@ -1800,7 +1800,10 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   if constexpr (TR) { if (ir[0] != -1e300 && vf.x != -1e300) pf_trace(tr, 2); }
   od_fallback<M>(S, o, o.start, stg, !early, sh, need, ir, ii, it);
   if constexpr (TR) pf_trace(tr, 3);
-  pf_node0<M>(v0r, v0i, S.w, ir, ii);
+  // node 0 from the currents -- unless every env of the wave takes it from its
+  // node record anyway (the fused C4 step's usual case; pf_node0's DPP sums
+  // need the whole wave, so the test is wave-uniform)
+  if (!(vonly && __ballot(valid && !served) == 0ull)) pf_node0<M>(v0r, v0i, S.w, ir, ii);
   if (served && o.resp_v_row == 0) {                 // the node record's row
     v0r = vf.x;
     v0i = vf.y;
