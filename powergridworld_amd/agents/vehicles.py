@@ -283,7 +283,25 @@ class EVChargingEnv(ComponentEnv):
                                                     _lib.dptr(self.req), _lib.dptr(self.charging),
                                                     self._stream()))
         self._advance(None)
+        self._warm_step_infos()
         return self._obs, {}
+
+    def _warm_step_infos(self):
+        """Build the whole episode's step infos at the first reset: they depend
+        only on the time index and the previous step's window (the shared
+        schedule), so every episode reuses them -- and the first episode's steps
+        then cost what later ones do (each built on first use cost ~10 us of
+        host time per step)."""
+        if self.randomize or len(self._info_cache) > 2:
+            return
+        prev = self._prev_window
+        last = min(int(self.max_episode_steps) - 1, len(self.simulation_times) - 1)
+        for ti in range(self.time_index, last):
+            key = (ti, False)
+            c = self._info_cache.get(key)
+            if c is None:
+                c = self._info_cache[key] = self._step_info_at(ti, prev)
+            prev = c[1]
 
     def step(self, action=None, **kwargs):
         """(:171-264)"""
