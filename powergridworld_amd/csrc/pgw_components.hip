@@ -385,17 +385,22 @@ static_assert(64 * 4 <= kEvFoldThreads, "s_ev_fold: k_mc_step block");
 static_assert(64 * PGW_MA_MAX_SLOTS <= kEvFoldThreads, "s_ev_fold: k_ma_step block");
 __shared__ double s_ev_fold[4][kEvFoldThreads];
 
-// The env's charge energy this step (:215-223); `note` counts an out-of-bounds
-// action (once per env: only one of the split waves notes it).
+// The env's EV action (:176-181): loaded at the top, used only once the walk's
+// first loads are out -- the charge energy in each chunk's processing
+// (ev_kwh_of), the out-of-bounds note after the walk (ev_note, once per env:
+// only one of the split waves notes it).  A branch on the action before the
+// walk (the note's atomic) made the vehicle loads wait for its round trip.
 template <class Mt>
-__device__ __forceinline__ double ev_kwh(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t e,
-                                         const Mt& act, bool note) {
-  double a = act.ptr ? ld(act, e, 0) : s.action_default;
-  if (p.rescale) {
-    if (note) oob_note(p.oob, oob_bad(a));
-    a = to_raw(a, 0.0, 1.0);
-  }
+__device__ __forceinline__ double ev_act(const pgw_ev_step_info& s, int64_t e, const Mt& act) {
+  return act.ptr ? ld(act, e, 0) : s.action_default;
+}
+// The env's charge energy this step (:215-223)
+__device__ __forceinline__ double ev_kwh_of(const pgw_ev_params& p, double a) {
+  if (p.rescale) a = to_raw(a, 0.0, 1.0);
   return a * p.rate * p.hours_per_step;
+}
+__device__ __forceinline__ void ev_note(const pgw_ev_params& p, double a) {
+  if (p.rescale) oob_note(p.oob, oob_bad(a));
 }
 
 // Walks chunks [c_lo, c_hi) of the scan (:224-252).  SPLIT = false: the whole
@@ -404,7 +409,7 @@ __device__ __forceinline__ double ev_kwh(const pgw_ev_params& p, const pgw_ev_st
 // block's s_bits[word][lane] and the group's partial sums returned unfolded.
 template <int MODE, bool SPLIT, class S, bool TR = false>
 __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_step_info& s, int64_t n,
-                                          int64_t e, double kwh, const double* __restrict__ endp,
+                                          int64_t e, double act_raw, const double* __restrict__ endp,
                                           S* __restrict__ req, uint64_t* __restrict__ chg, int c_lo,
                                           int c_hi, int K, uint64_t* s_bits, int lane) {
   double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;   // the current group's
@@ -510,6 +515,7 @@ __device__ __forceinline__ EvSums ev_walk(const pgw_ev_params& p, const pgw_ev_s
         next_fold += K;
       }
       ++at;
+      const double kwh = ev_kwh_of(p, act_raw);      // (after the chunk's loads issued)
       double df[kEvChunk], cv[kEvChunk];
       bool act[kEvChunk], chg_now[kEvChunk], dep[kEvChunk];
       uint64_t m = C.bits;
@@ -629,9 +635,10 @@ __device__ __forceinline__ RpRew ev_step_mode(const pgw_ev_params& p, const pgw_
                                              S* __restrict__ req, uint64_t* __restrict__ chg,
                                              const Mt& obs, S* __restrict__ rp,
                                              S* __restrict__ rew) {
-  const double kwh = ev_kwh(p, s, e, act, true);
+  const double a = ev_act(s, e, act);
   const int nc = ev_chunks(s);
-  const EvSums t = ev_walk<MODE, false>(p, s, n, e, kwh, endp, req, chg, 0, nc, ev_group_len(nc), nullptr, 0);
+  const EvSums t = ev_walk<MODE, false>(p, s, n, e, a, endp, req, chg, 0, nc, ev_group_len(nc), nullptr, 0);
+  ev_note(p, a);
   return ev_finish(p, s, e, t, obs, rp, rew);
 }
 
@@ -652,12 +659,15 @@ __device__ __forceinline__ EvSums ev_step_group(const pgw_ev_params& p, const pg
                                                 int64_t e, const Mt& act, const double* __restrict__ endp,
                                                 S* __restrict__ req, uint64_t* __restrict__ chg, int g,
                                                 uint64_t* s_bits, int lane) {
-  const double kwh = ev_kwh(p, s, e, act, g == 0);
+  const double a = ev_act(s, e, act);
   const int nc = ev_chunks(s), K = ev_group_len(nc);
   const int lo = min(g * K, nc), hi = min(lo + K, nc);
-  if (s.env_start) return ev_walk<kEvPerEnv, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
-  if (ev_table_ok(s)) return ev_walk<kEvTable, true, S, TR>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
-  return ev_walk<kEvDivide, true>(p, s, n, e, kwh, endp, req, chg, lo, hi, K, s_bits, lane);
+  EvSums t;
+  if (s.env_start) t = ev_walk<kEvPerEnv, true>(p, s, n, e, a, endp, req, chg, lo, hi, K, s_bits, lane);
+  else if (ev_table_ok(s)) t = ev_walk<kEvTable, true, S, TR>(p, s, n, e, a, endp, req, chg, lo, hi, K, s_bits, lane);
+  else t = ev_walk<kEvDivide, true>(p, s, n, e, a, endp, req, chg, lo, hi, K, s_bits, lane);
+  if (g == 0) ev_note(p, a);
+  return t;
 }
 
 template <class S, class Mt>
