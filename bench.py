@@ -66,11 +66,12 @@ PF_FLOPS_ENV = 12 * M_ELEM + 8 * M_ELEM + 4 + 10
 OD_REP_ROWS = 11
 OD_FLOPS_ITER = 8 * M_ELEM ** 2 + 14 * M_ELEM + 6 * M_ELEM
 OD_FLOPS_ENV = 16 * M_ELEM + 2 * OD_REP_ROWS * (8 * M_ELEM + 4) + 18 * M_ELEM + 8 * M_ELEM + 4 + 10
-# k_coord_pf_od with the hour's response table (pgw_pf_od.resp): per env one
-# record (PGW_OD_REC(14) = 90 doubles, 720 B, L2-resident: 2.3 MB per hour), the
-# quadratic of 2 m currents (2 FMAs each), the output row (8 m + 4) and the reward
-OD_TABLE_REC_BYTES = 8 * (6 + 6 * M_ELEM)
-OD_TABLE_FLOPS_ENV = 4 * 2 * M_ELEM + 8 * M_ELEM + 4 + 10
+# k_coord_pf_od with the hour's response table and its node records
+# (pgw_pf_od.resp / resp_v): per env one node record (PGW_OD_VREC = 12 doubles,
+# 96 B, L2-resident), the complex quadratic of V675.3 (2 x 2 FMAs), |V| and the
+# reward (the response record's 720 B are read only where an env is solved)
+OD_TABLE_REC_BYTES = 8 * 12
+OD_TABLE_FLOPS_ENV = 8 + 4 + 10
 PF_KERNEL_NAME = {"exact": "k_coord_pf<14,true,false,false>", "opendss": "k_coord_pf_od<14>"}
 # (k_coord_pf_od<14>: with the hour's response table, pgw_pf_od.resp, the default)
 PF_KERNEL = "k_coord_pf"              # PGW_T_COORD_PF: whichever PF kernel the step's mode runs
@@ -79,14 +80,15 @@ PF_KERNEL = "k_coord_pf"              # PGW_T_COORD_PF: whichever PF kernel the 
 def pf_roofline(conv, avg_us, mean_it, n, table=False):
     """The step's PF kernel against its bound.  Exact fixed point: fp64 VALU, on
     its algorithmic flops.  OpenDSS rule with the response table: a latency
-    chain (agent powers from HBM -> the env's record from L2 -> the reward
-    atomics), reported as HBM GB/s of its algorithmic bytes with the record bytes
-    and flops beside; without the table (od_table=False): fp64 VALU."""
+    chain (agent powers and rewards from HBM -> the env's node record from L2 ->
+    the outputs and final rewards), reported as HBM GB/s of its algorithmic bytes
+    with the record bytes and flops beside; without the table (od_table=False):
+    fp64 VALU."""
     if conv == "opendss" and table:
         gbs = PF_BYTES * n / (avg_us * 1e-6) / 1e9
         return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                "note": "latency-bound: HBM agent powers -> one %d-byte response-table record per env "
-                        "(L2, %.1f GB/s of record gather) -> output row, reward atomics"
+                "note": "latency-bound: HBM agent powers and rewards -> one %d-byte node record per env "
+                        "(L2, %.1f GB/s of record gather) -> V675.3, violation, final rewards"
                         % (OD_TABLE_REC_BYTES, OD_TABLE_REC_BYTES * n / (avg_us * 1e-6) / 1e9),
                 "flops_per_env": OD_TABLE_FLOPS_ENV, "l2_bytes_per_env": OD_TABLE_REC_BYTES}
     if conv == "exact":
