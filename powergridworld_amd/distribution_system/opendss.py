@@ -48,6 +48,29 @@ def get_hour_of_year(dt):
     return int((dt - beginning_of_year).total_seconds() // 3600)
 
 
+def extrema_candidates(A, B, C, tl, th, samples=9, delta=1e-9):
+    """Rows that can hold the minimum or the maximum |V| over t in [tl, th] of
+    some piece: A, B, C [pieces, rows] complex (V_r(t) = A + t (B + t C)), tl /
+    th [pieces].  Per piece, |V_r|^2 is bounded by `samples` equally spaced
+    values plus a Lipschitz margin (|d|V|^2/dt| <= 2 |V| |V'|) plus `delta`; a
+    row is a candidate when its lower bound reaches every row's upper bound or
+    its upper bound every row's lower bound.  Returns a bool array [rows], or
+    None when a bound is not finite (then every row is kept)."""
+    S = samples
+    ts = (tl[:, None] + (th - tl)[:, None] * torch.linspace(0.0, 1.0, S, dtype=torch.float64,
+                                                              device=A.device)[None, :])[:, :, None]
+    V = A[:, None, :] + ts * (B[:, None, :] + ts * C[:, None, :])            # [P, S, rows]
+    m2 = V.real * V.real + V.imag * V.imag
+    T = torch.maximum(tl.abs(), th.abs())[:, None]
+    L = 2.0 * (A.abs() + B.abs() * T + C.abs() * T * T) * (B.abs() + 2.0 * C.abs() * T)
+    marg = L * ((th - tl)[:, None] / (S - 1)) * 0.5 + delta
+    lo, hi = m2.min(1).values - marg, m2.max(1).values + marg
+    if not (torch.isfinite(lo).all() and torch.isfinite(hi).all()):
+        return None
+    cand = ((lo <= hi.min(1, keepdim=True).values) | (hi >= lo.max(1, keepdim=True).values)).any(0)
+    return cand.cpu().numpy()
+
+
 class OpenDSSSolver(PowerFlowSolver):
 
     # Per-hour predictor grid (single controllable load): the batched solve
@@ -422,21 +445,9 @@ class OpenDSSSolver(PowerFlowSolver):
                 V0 = torch.from_numpy(np.ascontiguousarray(self._od_V0all[rows])).to(dev)
                 c = torch.view_as_complex(rr[:, 6:6 + 6 * M].reshape(-1, 3, M, 2).contiguous())
                 abc = torch.einsum("pqm,rm->pqr", c, G)                          # [P, 3, rows]
-                A, B, C = abc[:, 0] + V0, abc[:, 1], abc[:, 2]
                 tl, th = (rr[:, 0] - rr[:, 2]) * rr[:, 3], (rr[:, 1] - rr[:, 2]) * rr[:, 3]
-                S = 9
-                ts = (tl[:, None] + (th - tl)[:, None] * torch.linspace(0.0, 1.0, S, dtype=torch.float64,
-                                                                          device=dev)[None, :])[:, :, None]
-                V = A[:, None, :] + ts * (B[:, None, :] + ts * C[:, None, :])    # [P, S, rows]
-                m2 = V.real * V.real + V.imag * V.imag
-                T = torch.maximum(tl.abs(), th.abs())[:, None]
-                L = 2.0 * (A.abs() + B.abs() * T + C.abs() * T * T) * (B.abs() + 2.0 * C.abs() * T)
-                marg = L * ((th - tl)[:, None] / (S - 1)) * 0.5 + 1e-9
-                lo, hi = m2.min(1).values - marg, m2.max(1).values + marg
-                cand = ((lo <= hi.min(1, keepdim=True).values) | (hi >= lo.max(1, keepdim=True).values)).any(0)
-                cand = cand.cpu().numpy()
-                ok = bool(torch.isfinite(lo).all() and torch.isfinite(hi).all())
-                mask = sum(1 << r for r in range(1, len(names)) if cand[r]) if ok else 0
+                cand = extrema_candidates(abc[:, 0] + V0, abc[:, 1], abc[:, 2], tl, th)
+                mask = sum(1 << r for r in range(1, len(names)) if cand[r]) if cand is not None else 0
         self._od_rowmask[key] = mask
         return mask
 
