@@ -521,6 +521,42 @@ def test_regcontrol_sample_options_model():
     assert not moved
 
 
+def test_regcontrol_options_oracle_semantics():
+    """The oracle's Sample options on regctl2_feeder.dss, from chosen taps:
+    Vlimit forces Reg2 down while its local voltage is above the limit
+    (whatever its compensated voltage asks) and the control loop ends at or
+    below it; the options reach the oracle's control records."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import load_feeder_spec
+    spec = load_feeder_spec(REGCTL2)
+    o = OracleFeeder(spec)
+    ctrls = o.reg_controls()
+    names = [t["name"] for t, _ in ctrls]
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float) * 0.5
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float) * 0.5
+    taps = [1.0, 1.1, 0.99375, 1.0, 1.0]                 # Reg2 at its top tap: local voltage above Vlimit
+    f = o.with_taps(taps)
+    V, _ = f.solve(kw[None], kvar[None], tol=1e-12)
+    V = V[0]
+    t2, c2 = ctrls[names.index("reg2")]
+    a, b = o._reg_nodes(t2, 0)
+    assert abs(V[b]) / c2["ptratio"] > c2["vlimit"]
+    # Reg2 acts (down, toward the limit) unless an inverse-time control's
+    # shorter delay claims this pass (only the nearest-delay actions act)
+    out, moved = o.reg_control_pass(V, taps)
+    assert moved
+    g2 = names.index("reg2")
+    if out[g2] != taps[g2]:
+        assert out[g2] < taps[g2]
+    else:
+        assert any(out[g] != taps[g] and ctrls[g][1]["inverse"] for g in range(len(ctrls)))
+    # the loop from there ends with Reg2's local voltage at or below the limit
+    Vl, _, tp, _ = o.solve_regulated(kw[None], kvar[None], np.array(taps)[None])
+    assert abs(Vl[0][b]) / c2["ptratio"] <= c2["vlimit"] + 1e-9
+    assert o.reg_controls()[names.index("regh")][1]["bus"] == "b8"
+    assert ctrls[names.index("reg3")][1]["inverse"] and not ctrls[names.index("reg1")][1]["inverse"]
+
+
 def test_regcontrol_refuses_unsimulated_options(tmp_path):
     """Reversible regulators and PTphase=avg stay refused, loudly."""
     from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
