@@ -605,7 +605,13 @@ class Feeder:
                 nt = min(max(nt, c["mintap"]), c["maxtap"])
                 if nt != taps[g]:
                     want[g] = nt
-                    dl[g] = c["delay"] / min(10.0, 2.0 * abs(dv) / c["band"]) if c["inverse"] else c["delay"]
+                    if c["inverse"]:
+                        # (a Vlimit-only trigger can have dv = 0: delay / 0 = +inf, as the kernel's
+                        # IEEE division -- the action then waits behind every finite one)
+                        f = min(10.0, 2.0 * abs(dv) / c["band"])
+                        dl[g] = c["delay"] / f if f > 0.0 else math.inf
+                    else:
+                        dl[g] = c["delay"]
                     delays.append(dl[g])
         if not delays:
             return list(taps), False

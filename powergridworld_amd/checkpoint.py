@@ -18,9 +18,10 @@ buffers) and records
   timestamps) and small NumPy arrays (e.g. the EV's previous parking window);
   scalars inside dicts and lists are keys and indices, not state,
 
-keyed by attribute path.  Cache-version counters, caches and the tensors a
-solver keeps alive for an in-flight table upload are skipped: they describe
-host-side tables, not the env's state; so are the {node: voltage} mappings,
+keyed by attribute path.  Cache-version counters, caches, the tensors a
+solver keeps alive for an in-flight table upload and the solver's per-hour
+tables (derived from the feeder and the hour, indexed on the host) are
+skipped: they describe host-side tables, not the env's state; so are the {node: voltage} mappings,
 views of the solver's output buffers (saved under the buffers' own names).  ``load_state_dict``
 requires the same env configuration (same paths, shapes and dtypes) and
 raises otherwise.
@@ -42,6 +43,12 @@ import torch
 # under their own names; MultiAgentEnv.load_state_dict re-arms them)
 _SKIP_NAMES = ("version", "_ver", "cache", "_lib", "_memo", "keepalive", "voltages")
 _SKIP_EXACT = ("history", "_hist", "_bv")  # the history lists and their device ring (emptied on load)
+# the power-flow solver's per-hour tables (first-iteration / response / node
+# records, predictor): derived data whose host-side index (_od_index,
+# _pred_index) is not state -- a restore keeps the live tables and their index
+# consistent (a checkpoint taken before a table rebuild would otherwise copy
+# another hour's rows under the live index)
+_SKIP_TABLES = ("_od_start", "_od_resp", "_od_vresp", "_pred_table", "_pred_sig", "_pred_meta", "_pred_grid")
 _SCALARS = (bool, numbers.Number, str, type(None), datetime.datetime, datetime.date, np.generic)
 
 
@@ -52,7 +59,7 @@ def _ours(obj):
 
 def _skip(name):
     n = str(name).lower()
-    return n in _SKIP_EXACT or any(s in n for s in _SKIP_NAMES)
+    return n in _SKIP_EXACT or n in _SKIP_TABLES or any(s in n for s in _SKIP_NAMES)
 
 
 def _walk(obj, path, out, seen):

@@ -415,6 +415,14 @@ class Feeder(object):
             if bus:                                      # the regulated bus's node per monitored phase
                 parts = bus.split(".")
                 nds = [int(x) for x in parts[1:]]
+                # Bus= without nodes: each monitored phase senses the winding's own
+                # node number.  OpenDSS might instead take the bus's first nodes in
+                # order; the two differ only for a single-phase unit off phase 1,
+                # which is refused rather than guessed (parity unpinned, no OpenDSS)
+                if not nds and ph == 1 and wt[1][0][0] != 1:
+                    raise NotImplementedError("RegControl %s: Bus=%s without node numbers on a single-phase "
+                                              "regulator of phase %d (name the node: Bus=%s.%d)"
+                                              % (rc["name"], bus, wt[1][0][0], parts[0], wt[1][0][0]))
                 mon_nodes = [rix(self.node(parts[0], nds[q] if q < len(nds) else wt[1][q][0])) for q in mon]
             else:
                 mon_nodes = [phases[first + q]["a" if w == 1 else "b"] for q in mon]

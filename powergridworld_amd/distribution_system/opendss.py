@@ -303,6 +303,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_rowmask = {}                # pgw_pf_od.resp_rows per (table row, configuration)
         self.od_node_records = True          # False: every solve reads the node's row from the currents
         self.od_row_masks = True             # pgw_pf_od.resp_rows (False: every row, for A/Bs and tests)
+        self.od_certify = True               # certify every piece (od_certify; False: probes only, for A/Bs)
         self.od_resp_stats, self.od_resp_brackets = {}, {}
         self._od_index = {}
         self._od_keep = {}
@@ -356,7 +357,11 @@ class OpenDSSSolver(PowerFlowSolver):
     # sampled at OD_RESP_SUB points and every signature change bisected to a
     # bracket of ~1e-10 kW; three fit points per piece; two check points per
     # piece bound the fit error (OD_RESP_TOL, relative, else the piece is left to
-    # the solve).  Envs in a bracket, outside the grid or with Q != 0 run the solve.
+    # the solve); then a certificate per piece (od_certify: Taylor models of the
+    # whole iteration over the interval) proves every band and stopping decision
+    # constant over what the record serves, cutting the piece to its longest
+    # certified run.  Envs in a bracket or a cut-off guard zone, outside the grid
+    # or with Q != 0 run the solve.
     OD_RESP_EXTRA = 1024          # records per hour beyond the grid's (further pieces of a segment)
     OD_RESP_SUB = 64              # sample points across a segment with a breakpoint
     OD_RESP_BISECT = 26           # rounds per bracket: h / 64 / 2^26 ~ 1.5e-10 kW
@@ -635,6 +640,25 @@ class OpenDSSSolver(PowerFlowSolver):
             ev = ((vfit - vtrue).abs() / vtrue.abs()).max(1).values.cpu().numpy()
             e_ = np.maximum(e_, np.where(np.isfinite(ev), ev, np.inf))
         bad = (pit != 0) & ((e_ > self.OD_RESP_TOL) | (sc[c_l] != psig[:, None]).any(1) | ~np.isfinite(e_))
+        # ---- 6. certificates (od_certify): every band and stopping decision of
+        # the snap solve proven constant over the served interval; a piece is cut
+        # to its longest certified run, or left to the solve
+        cand = np.nonzero((pit != 0) & ~bad)[0]
+        n_cut, kw_cut, t_cert = 0, 0.0, _time.perf_counter()
+        if self.od_certify and len(cand):
+            from powergridworld_amd.distribution_system.od_certify import SnapModel, certify_pieces
+            model = SnapModel.from_solver(self, list(range(idx0, idx0 + H)), hours)
+            c_lo, c_hi, c_kw = certify_pieces(model, pq_[cand], pa[cand], pb[cand], pit[cand], psig[cand],
+                                              min_width=self.OD_RESP_MIN_WIDTH)
+            none = c_lo > c_hi
+            bad[cand[none]] = True
+            cut = ~none & ((c_lo > pa[cand]) | (c_hi < pb[cand]))
+            n_cut = int(cut.sum())
+            kw_cut = float(((pb - pa)[cand] - np.where(none, 0.0, c_hi - c_lo)).sum())
+            if n_cut:
+                hdr = torch.from_numpy(np.stack([c_lo[cut], c_hi[cut]], 1)).to(dev)
+                self._od_resp.view(-1, R)[torch.from_numpy(prec[cand[cut]]).to(dev), 0:2] = hdr
+        t_cert = _time.perf_counter() - t_cert
         if bad.any():                                       # left to the solve
             words = np.array([self._od_meta_word(0, int(nx)) for nx in pnext[bad]], np.int64)
             self._od_resp.view(-1, R).view(torch.int64)[torch.from_numpy(prec[bad]).to(dev), 4] = \
@@ -666,6 +690,11 @@ class OpenDSSSolver(PowerFlowSolver):
         st_["pieces"] = st_.get("pieces", 0) + int(ok.sum())
         st_["pieces_left_to_solve"] = st_.get("pieces_left_to_solve", 0) + int((~ok).sum())
         st_["max_fit_err"] = max(st_.get("max_fit_err", 0.0), float(e_[ok].max()) if ok.any() else 0.0)
+        st_["certified"] = bool(self.od_certify)
+        st_["certified_pieces"] = st_.get("certified_pieces", 0) + (int(ok.sum()) if self.od_certify else 0)
+        st_["pieces_cut_by_certificate"] = st_.get("pieces_cut_by_certificate", 0) + n_cut
+        st_["uncertified_kw"] = st_.get("uncertified_kw", 0.0) + kw_cut
+        st_["certify_s"] = st_.get("certify_s", 0.0) + t_cert
         st_["build_s"] = st_.get("build_s", 0.0) + (_time.perf_counter() - t_start)
 
     def _od_tables(self, hour):

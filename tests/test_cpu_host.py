@@ -557,6 +557,31 @@ def test_regcontrol_options_oracle_semantics():
     assert ctrls[names.index("reg3")][1]["inverse"] and not ctrls[names.index("reg1")][1]["inverse"]
 
 
+def test_regcontrol_inverse_time_vlimit_only_trigger():
+    """InverseTime with Vlimit the only trigger (|Vreg - V| = 0): the oracle's
+    delay is Delay / 0 = +inf, as k_reg_control's IEEE division gives (ADVICE
+    r05: it raised ZeroDivisionError), and the tap still moves down toward the
+    limit."""
+    from oracle.pf_oracle import Feeder as OracleFeeder
+    from powergridworld_amd.distribution_system.feeder import load_feeder_spec
+    spec = load_feeder_spec(REGCTL2)
+    o = OracleFeeder(spec)
+    ctrls = o.reg_controls()
+    names = [t["name"] for t, _ in ctrls]
+    t, c = ctrls[names.index("reg3")]
+    kw = np.array([ld["kw"] for ld in spec["loads"]], float) * 0.5
+    kvar = np.array([ld["kvar"] for ld in spec["loads"]], float) * 0.5
+    taps = [1.0, 1.0, 1.0, 1.0, 1.0]
+    V = o.with_taps(taps).solve(kw[None], kvar[None], tol=1e-12)[0][0]
+    a, b = o._reg_nodes(t, 0)
+    c2 = dict(c, R=0.0, X=0.0, bus="", ptphase=1, inverse=True)
+    vc = abs(V[a if c2["winding"] == 1 else b] / c2["ptratio"])
+    c2["vreg"], c2["vlimit"] = vc, 0.99 * vc                 # dv = 0 exactly, local voltage above the limit
+    o.reg_controls = lambda: [(t, c2)]
+    out, moved = o.reg_control_pass(V, [taps[names.index("reg3")]])
+    assert moved and out[0] < taps[names.index("reg3")]
+
+
 def test_regcontrol_refuses_unsimulated_options(tmp_path):
     """Reversible regulators and PTphase=avg stay refused, loudly."""
     from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
@@ -568,6 +593,25 @@ def test_regcontrol_refuses_unsimulated_options(tmp_path):
         fn.write_text(txt.replace(old, bad, 1))
         with pytest.raises(NotImplementedError):
             Feeder(load_feeder_spec(str(fn))).regulators()
+
+
+def test_regcontrol_bus_without_nodes_off_phase_1_refused(tmp_path):
+    """Bus= with no node numbers on a single-phase regulator of phase 2: which
+    node OpenDSS senses there is unpinned, so it is refused; the
+    same control with the node named is accepted and senses that node."""
+    from powergridworld_amd.distribution_system.feeder import Feeder, load_feeder_spec
+    txt = open(REGCTL2).read()
+    old = "New RegControl.Reg2 transformer=Reg2 winding=2 vreg=123 band=2 ptratio=20 ctprim=700 R=3 X=6 vlimit=126.5"
+    assert old in txt
+    fn = tmp_path / "bus_nonodes.dss"
+    fn.write_text(txt.replace(old, old + " bus=B3", 1))
+    with pytest.raises(NotImplementedError):
+        Feeder(load_feeder_spec(str(fn))).regulators()
+    fn2 = tmp_path / "bus_node2.dss"
+    fn2.write_text(txt.replace(old, old + " bus=B3.2", 1))
+    f = Feeder(load_feeder_spec(str(fn2)))
+    reg = f.regulators()
+    assert reg is not None and f.node_index["b3.2"] in [int(x) for x in np.asarray(reg["nodes"])]
 
 
 def test_checkpoint_walk_restores_in_place():

@@ -188,12 +188,16 @@ def test_response_table_builder_against_the_solve(cpu_solver):
     for hour in (HOURS[0], HOURS[0] + 1):
         br = s.od_resp_brackets[s._od_index[s._hour_key(hour)]]
         assert len(br) > 5 and (br[:, 1] - br[:, 0] < 1e-8).all()
-        near = np.concatenate([br[:, 0] - 1e-7, br[:, 1] + 1e-7, 0.5 * (br[:, 0] + br[:, 1])])
+        # 1e-7 kW from a bracket: inside the certificate's guard zone or served;
+        # 1e-3 kW: served (the guard zones are ~1e-5 kW, delta / the margins' slope)
+        near = np.concatenate([br[:, 0] - 1e-7, br[:, 1] + 1e-7, br[:, 0] - 1e-3, br[:, 1] + 1e-3,
+                               0.5 * (br[:, 0] + br[:, 1])])
         P = np.concatenate([rng.uniform(-500.0, 1499.9, 4000), near])
         served, J, it = _lookup(s, hour, P)
         Jo, _, ito = orc(hour, P)
-        assert served[:4000].mean() > 0.995 and served[4000:4000 + 2 * len(br)].all()
-        assert not served[-len(br):].any()             # inside a bracket: the solve
+        nb = len(br)
+        assert served[:4000].mean() > 0.995 and served[4000 + 2 * nb:4000 + 4 * nb].all()
+        assert not served[-nb:].any()                  # inside a bracket: the solve
         np.testing.assert_array_equal(it[served], ito[served])
         rel = np.abs(J[served] - Jo[served]).max(1) / np.abs(Jo[served]).max(1)
         assert rel.max() < 1e-10, rel.max()
@@ -232,3 +236,86 @@ def test_node_records_compose_the_response(cpu_solver):
         np.testing.assert_allclose(abs(vfit), abs(V0 + (G * Jo[e]).sum()), rtol=1e-11)
         n_checked += 1
     assert n_checked > 200
+
+
+def _toy_model(vmin2):
+    """Two elements, their own nodes, a weak coupling (every solve stops at
+    iteration 2).  |u_1,0(P)|^2 = 0.96^2 + 1e-6 (P - 0.1)^2: with vmin^2 just
+    above its minimum, element 0 of u_1 drops below vmin only for P within
+    ~0.02 kW of 0.1 -- an excursion between the probes a segment [-0.3125,
+    0.3125] gets (its ends, midpoint and quarter points)."""
+    from powergridworld_amd.distribution_system.od_certify import SnapModel
+    c = lambda *v: torch.tensor(v, dtype=torch.complex128)
+    W = torch.tensor([[1e-9, 2e-10], [2e-10, 1e-9]], dtype=torch.complex128)
+    return SnapModel(u1b=c(0.96 - 1e-4j, 1.0)[None], u1P=c(1e-3j, 0.0), J0=c(-50.0, -40.0)[None],
+                     jP=c(-1.0, 0.0), s0=c(5e4 - 2e4j, 4e4 - 1e4j)[None],
+                     fr=torch.tensor([1000.0, 0.0], dtype=torch.float64), y0=c(5e4 - 2e4j, 4e4 - 1e4j),
+                     u0=c(0.96, 1.0), W=W, G=W.clone(), V0=c(0.96, 1.0),
+                     lo2=0.25, mn2=vmin2, mx2=1.1025, tol=1e-4, min_iter=2, max_iter=15)
+
+
+def test_certificate_rejects_narrow_excursion():
+    """A band flip that the builder's probes step over: the probes' signatures
+    agree, the certificate does not certify the piece as a whole, and the run it
+    keeps holds the probes' decisions at every point (checked densely)."""
+    from powergridworld_amd.distribution_system import od_certify as C
+    a, b = -0.3125, 0.3125
+    excursion = (0.1 - 0.02, 0.1 + 0.02)
+    m = _toy_model(0.96 ** 2 + 1e-6 * 0.02 ** 2)
+    probes = np.array([a, a + 0.25 * (b - a), 0.5 * (a + b), a + 0.75 * (b - a), b])
+    it_p, sig_p = m.solve_points(np.zeros(5, int), probes)
+    assert len(set(sig_p.tolist())) == 1 and (it_p.numpy() == 2).all()      # the probes see one piece
+    dense = np.linspace(a, b, 20001)
+    it_d, sig_d = m.solve_points(np.zeros(len(dense), int), dense)
+    inside = (dense > excursion[0] + 1e-6) & (dense < excursion[1] - 1e-6)
+    assert (sig_d[inside] != sig_p[0]).all() and (sig_d[~inside & (np.abs(dense - 0.1) > 0.021)] == sig_p[0]).all()
+    ok, _, _ = C.certify(m, [0], [a], [b])
+    assert not ok[0]
+    lo, hi, kw = C.certify_pieces(m, [0], [a], [b], [int(it_p[0])], [sig_p[0]])
+    assert lo[0] == a and excursion[0] - 1e-3 < hi[0] <= excursion[0]      # the longer side, up to the flip
+    on = (dense >= lo[0]) & (dense <= hi[0])
+    assert on.sum() > 10000 and (sig_d[on] == sig_p[0]).all() and (it_d.numpy()[on] == 2).all()
+    assert kw[0] > (hi[0] - lo[0]) + 0.18             # the far side certifies too (not served: one run)
+    # without the excursion (vmin below the dip) the piece certifies whole
+    m2 = _toy_model(0.96 ** 2 - 1e-6)
+    it2, sg2 = m2.solve_points([0], [0.0])
+    assert C.certify(m2, [0], [a], [b])[0][0]
+    lo2, hi2, _ = C.certify_pieces(m2, [0], [a], [b], [int(it2[0])], [sg2[0]])
+    assert (lo2[0], hi2[0]) == (a, b)
+
+
+def test_certified_table_matches_the_solve_densely(cpu_solver):
+    """The pieces the certificate cut (next to every breakpoint) and a random
+    sample of the others, probed at 64 points each across what their records
+    serve: the oracle's snap solve gives the table's iteration count at every
+    point and currents within 1e-10.  Also: the certificate's own model of the
+    iteration agrees with the oracle's solve point by point."""
+    from powergridworld_amd import _lib
+    from powergridworld_amd.distribution_system.od_certify import SnapModel
+    s, orc = cpu_solver
+    hour = HOURS[0]
+    s._od_tables(hour)
+    st = s.od_resp_stats
+    assert st["certified"] and st["pieces_cut_by_certificate"] > 0 and st["uncertified_kw"] < 1e-2, st
+    row = s._od_index[s._hour_key(hour)]
+    recs = s._od_resp[row].numpy()
+    words = recs[:, 4].copy().view(np.int64)
+    its = (words & 0xffffffff).astype(np.int32)
+    live = np.nonzero((its != 0) & (recs[:, 0] <= recs[:, 1]))[0]
+    # the fitted piece [xc - 1/inv_hw, xc + 1/inv_hw] against what the record serves
+    a_fit, b_fit = recs[live, 2] - 1.0 / recs[live, 3], recs[live, 2] + 1.0 / recs[live, 3]
+    cut = live[(recs[live, 0] > a_fit + 1e-11) | (recs[live, 1] < b_fit - 1e-11)]
+    rng = np.random.default_rng(11)
+    pick = np.unique(np.concatenate([cut, rng.choice(live, 64, replace=False)]))
+    assert len(cut) >= 5
+    P = (recs[pick, 0][:, None] + (recs[pick, 1] - recs[pick, 0])[:, None] * ((np.arange(64) + 0.5) / 64)[None]).ravel()
+    served, J, it = _lookup(s, hour, P)
+    Jo, sgo, ito = orc(hour, P)
+    assert served.all()
+    np.testing.assert_array_equal(it, ito)
+    rel = np.abs(J - Jo).max(1) / np.abs(Jo).max(1)
+    assert rel.max() < 1e-10, rel.max()
+    model = SnapModel.from_solver(s, [row], [hour])
+    itm, sgm = model.solve_points(np.zeros(len(P), int), P)
+    np.testing.assert_array_equal(itm.numpy(), ito)
+    np.testing.assert_array_equal(sgm, sgo)

@@ -276,6 +276,45 @@ def test_od_response_table_equals_solve():
     assert st["pieces_left_to_solve"] <= 0.01 * st["pieces"], st
 
 
+@pytest.mark.parametrize("scenario", ["c4", "het"])
+def test_od_response_table_dense_every_hour(scenario):
+    """The certified response table against every env solved, densely: all 24
+    hours of the scenario's day, 64 points inside every one of the grid's 3 200
+    segments of 0.625 kW (204 800 envs per hour, 4.9 M probes per scenario):
+    the same iteration count at every point, every node within 1e-11 rel.  C4:
+    rescale 1.2 on 2021-08-12 (make_c4_config); HET: rescale 0.65 on 2020-08-12
+    (heterogeneous.make_env_config)."""
+    rescale, day = {"c4": (1.2, "08-12-2021"), "het": (0.65, "08-12-2020")}[scenario]
+    nseg, per = 3200, 64
+    K = nseg * per
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    tab, sol = [OpenDSSSolver(IEEE13, SHAPE, device=DEV, system_load_rescale_factor=rescale, num_envs=K,
+                              convergence="opendss", od_table=o) for o in (True, False)]
+    x0, h = tab.PREDICTOR_X0, tab.PREDICTOR_H
+    j = np.repeat(np.arange(nseg), per)
+    P = x0 + h * (j + (np.tile(np.arange(per), nseg) + 0.5) / per)
+    Pd = torch.tensor(P, device=DEV)
+    worst, mism, served_n = 0.0, 0, 0
+    for hr in range(24):
+        t = pd.Timestamp("%s %02d:10:00" % (day, hr))
+        res = []
+        for s_ in (tab, sol):
+            s_.calculate_power_flow({"675c": Pd}, None, current_time=t)
+            bv = s_.get_bus_voltages()
+            res.append((torch.stack([bv[nm] for nm in s_.feeder.node_names]), s_.iterations.clone()))
+        (vt, it_t), (vs, it_s) = res
+        mism += int((it_t != it_s).sum())
+        worst = max(worst, ((vt - vs).abs() / vs.abs()).max().item())
+        served_n += int(_served(tab, tab.hour_of(t), P).sum())
+        del res, vt, vs
+    st = tab.od_resp_stats
+    print("dense %s: %d probes, %d iteration mismatches, worst node rel %.3e, served %.6f; table %s"
+          % (scenario, 24 * K, mism, worst, served_n / (24 * K), st))
+    assert mism == 0 and worst < 1e-11, (mism, worst)
+    assert served_n > 0.999 * 24 * K
+    assert st["certified"] and st["unresolved_brackets"] == 0, st
+
+
 def test_od_response_table_bit_identical_paths():
     """The fused C4 step, the generic path and the all-node solve read the same
     table records with the same operations: fused == generic bit for bit over a
