@@ -2,12 +2,14 @@
 with the IEEE-13 power flow (BASELINE.json config C4), batch 65,536 per GPU.
 
 One "step" = one MultiAgentEnv.step of the whole batch through the public API
-(fused path: one pgw_coord_step call = k_coord_agents_std (5 x [building, PV,
-storage] per env) + the power flow with the coordinated reward: by default
-k_coord_pf_od, OpenDSS's snap-solve rule as the reference runs it (about once
-per episode also the first-iteration tables of the next 24 simulated hours);
---pf-convergence exact: k_coord_pf, the exact fixed point with its predictor
-tables), actions already resident in HBM.  Episodes (286 steps) end with done["__all__"]; the following env.reset()
+(fused path: one pgw_coord_step call.  By default, OpenDSS's snap-solve rule
+as the reference runs it with the hour's certified response table:
+k_coord_step_od -- 5 x [building, PV, storage] per env and the power flow's
+table lookup with the coordinated reward, one launch -- then
+k_coord_pf_od_list, the snap solve of the envs the table did not serve;
+--pf-split off: k_coord_agents_std + k_coord_pf_od (bit-identical);
+--pf-convergence exact: k_coord_agents_std + k_coord_pf, the exact fixed point
+with its predictor tables), actions already resident in HBM.  Episodes (286 steps) end with done["__all__"]; the following env.reset()
 is inside the timed region.  Kernel durations come from HIP events the library
 records around every --time-every-th launch, on the launch's stream.
 
@@ -49,6 +51,11 @@ FP64_PEAK_TFS = 78.6         # MI355X spec, FP64 vector (= FP64 matrix); tools/m
 #   writes x_k 5x8 + soc 8 + obs 17x8 + reward 8 + power 8     = 200
 AGENT_BYTES = 112 + 200
 AGENT_BYTES_F32 = AGENT_BYTES // 2       # the same items in fp32 (pgw_coord_step_f32)
+# k_coord_step_od (the agents and the PF's table lookup in one launch) -- per env
+# the 5 agents' bytes above plus the PF's outputs V675.3, violation (8 B each)
+# and the iteration count (4 B); the agent powers stay in LDS, the node record
+# (96 B) is an L2 gather, the rewards are written once (final)
+STEP_OD_ENV_BYTES = 5 * AGENT_BYTES + 8 + 8 + 4
 # k_coord_pf -- per env: reads 5 agent powers + 5 rewards, writes 5 rewards + v + vv + iters
 PF_BYTES = 8 * (5 + 5 + 5 + 1 + 1) + 4
 # k_coord_pf -- algorithmic fp64 FLOPs (m = 14 load phase elements): per fixed-point
@@ -77,16 +84,20 @@ PF_KERNEL_NAME = {"exact": "k_coord_pf<14,true,false,false>", "opendss": "k_coor
 PF_KERNEL = "k_coord_pf"              # PGW_T_COORD_PF: whichever PF kernel the step's mode runs
 
 
-def pf_roofline(conv, avg_us, mean_it, n, table=False):
+def pf_roofline(conv, avg_us, mean_it, n, table=False, split=False):
     """The step's PF kernel against its bound.  Exact fixed point: fp64 VALU, on
     its algorithmic flops.  OpenDSS rule with the response table: a latency
     chain (agent powers and rewards from HBM -> the env's node record from L2 ->
     the outputs and final rewards), reported as HBM GB/s of its algorithmic bytes
     with the record bytes and flops beside; without the table (od_table=False):
     fp64 VALU."""
+    if conv == "opendss" and table and split:
+        return {"bound": "latency", "note": "k_coord_pf_od_list: the snap solve of the envs the fused step listed "
+                                            "(none when the table serves every env): a small fixed grid that reads "
+                                            "the list's count and exits; its time is a dispatch's"}
     if conv == "opendss" and table:
         gbs = PF_BYTES * n / (avg_us * 1e-6) / 1e9
-        return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+        return {"bound": "latency", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                 "note": "latency-bound: HBM agent powers and rewards -> one %d-byte node record per env "
                         "(L2, %.1f GB/s of record gather) -> V675.3, violation, final rewards"
                         % (OD_TABLE_REC_BYTES, OD_TABLE_REC_BYTES * n / (avg_us * 1e-6) / 1e9),
@@ -125,6 +136,9 @@ def parse():
                     help="the headline's power-flow stopping rule: OpenDSS's snap solve (the "
                          "reference's: loads' Yeq in Y, node-magnitude test 1e-4, 2..15 iterations) "
                          "or the exact fixed point; the other runs as variants.*_pf")
+    ap.add_argument("--pf-split", choices=("on", "off"), default="off",
+                    help="OpenDSS rule with node records: agents + table lookup in one launch and the "
+                         "listed envs' snap solve (on), or the two-kernel step (off); bit-identical")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the fp32-storage variant line (N=1 only; never the headline)")
     return ap.parse_args()
@@ -195,7 +209,7 @@ def timed_pass(run, steps):
     return tot, cnt
 
 
-def pf_variant(conv, n, steps, warmup, pool, dev):
+def pf_variant(conv, n, steps, warmup, pool, dev, od_table=True):
     """The same C4 workload (same action pool) with the other power-flow stopping
     rule on the fused step: OpenDSS's snap solve (the reference's,
     opendss.py:131-135; pgw_coord_step + k_coord_pf_od) or the exact fixed point
@@ -204,6 +218,7 @@ def pf_variant(conv, n, steps, warmup, pool, dev):
                                                           make_c4_config)
     env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n,
                                              device=dev, fused=True)
+    env.pf_solver.od_table = bool(od_table)
     P = pool.shape[0]
     env.reset()
     k = [0]
@@ -224,16 +239,60 @@ def pf_variant(conv, n, steps, warmup, pool, dev):
     it = env.pf_solver.iterations.abs().double()
     p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
     table = conv == "opendss" and env.pf_solver.od_table
-    out = {"pf_convergence": conv, "value": N_AGENTS * n * steps / dt, "unit": "agent-env-steps/s",
+    out = {"pf_convergence": conv, "od_table": table, "value": N_AGENTS * n * steps / dt, "unit": "agent-env-steps/s",
            "ms_per_step": dt / steps * 1e3, "steps": steps, "pf_iterations_mean": float(it.mean()),
            "pf_iterations_max": int(it.max()),
            "k_coord_agents_std_avg_us": tot[0] / cnt[0] * 1e3 if cnt[0] else None,
-           "pf_kernel": {"name": PF_KERNEL_NAME[conv] if env.pf_solver._od_fast or conv == "exact"
-                         else "k_pf_general", "avg_us": p_us}}
+           "pf_kernel": {"name": (PF_KERNEL_NAME[conv] if env.pf_solver._od_fast or conv == "exact"
+                                  else "k_pf_general"), "avg_us": p_us}}
+    if conv == "opendss" and not table:
+        out["note"] = ("OpenDSS's rule with every env's snap solve run (od_table=False): the reference's rule "
+                       "without the per-hour response table (k_coord_agents_std + k_coord_pf_od)")
     if p_us:
         out["pf_kernel"].update(pf_roofline(conv, p_us, float(it.mean()), n, table))
     del env
     return out
+
+
+def graph_variant(env, packed, steps, warmup_episodes=1, S=8):
+    """The headline's env and action pool with the fused step captured S steps
+    per hipGraph (MultiAgentEnv.capture_step: one graph per episode position,
+    the pool entry of each step bound at capture); the tail of an episode
+    (fewer than S steps left) and the resets run eagerly.  Bit-identical to the
+    eager step (tests/test_gpu_graph.py::test_c4_graph8_equals_eager_across_
+    episodes).  Reported beside the eager headline, never as it."""
+    P = packed.shape[0]
+    graph = env.capture_step(lambda k: [packed[(k + i) % P] for i in range(S)], steps=S)
+    env.reset()
+
+    def run(m):
+        done_steps, calls = 0, 0
+        while done_steps < m:
+            k, last = env.episode_step, env._episode_last_step()
+            if k + S <= last:
+                _, _, d, _ = graph()
+                done_steps += S
+                calls += 1
+            else:
+                _, _, d, _ = env.step(packed[k % P])
+                done_steps += 1
+            if d["__all__"]:
+                env.reset()
+        return done_steps, calls
+    t0 = time.perf_counter()
+    run(warmup_episodes * 286)                      # every position's graph captured
+    capture_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done_steps, calls = run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": N_AGENTS * env.num_envs * done_steps / dt, "unit": "agent-env-steps/s",
+            "ms_per_step": dt / done_steps * 1e3, "steps": done_steps, "graph_calls": calls,
+            "graphs": len(graph._pos), "warmup_capture_s": capture_s,
+            "note": "S=%d steps per hipGraph launch (one graph per episode position and list parity, captured "
+                    "in a warm-up episode), episode tails and resets eager; same env, state and action pool as "
+                    "the headline, bit-identical outputs" % S}
 
 
 def _oracle_leg(job):
@@ -309,12 +368,14 @@ def stream_copy_gbs(dev, nbytes=1 << 30, reps=20):
 
 
 def load_traffic():
-    """HBM bytes per launch from the committed PMC summary (tools/gpu/pmc_traffic.py)."""
+    """HBM bytes per launch from the committed PMC summary (tools/gpu/pmc_traffic.py)
+    and, per kernel, the PMC run it came from (profiles/<round>/pmc_<run>.txt)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f).get("bytes_per_launch", {})
-    return {}
+            d = json.load(f)
+        return d.get("bytes_per_launch", {}), d.get("runs", {})
+    return {}, {}
 
 
 def _free_port():
@@ -380,6 +441,7 @@ def main():
                                              fused=True)
     if conv == "opendss" and not env.pf_solver._od_fast:
         raise RuntimeError("bench.py: the C4 feeder did not select the fast OpenDSS-rule kernel")
+    env.set_pf_list(args.pf_split == "on")
     for i, agent in enumerate(env.agents):         # per-rank seed offset
         agent.env_dict["storage"].seed(pgd.rank_seed(0, rank, i))
     gen = torch.Generator(dev).manual_seed(pgd.rank_seed(0, rank))     # seed 0 at rank 0
@@ -388,7 +450,6 @@ def main():
     pool.uniform_(-1.0, 1.0, generator=gen)
     packed = pool.transpose(2, 3)                  # [P, agents, N, act_dim] view, env-minor
 
-    env.reset()
     step_count = 0
 
     def run(k):
@@ -403,6 +464,26 @@ def main():
     # the measured HBM ceiling of this box (device copy) -- also brings the GPU
     # out of its idle clocks after the host-only CPU baseline, before warmup
     copy_gbs, torch_copy_gbs = stream_copy_gbs(dev, reps=100)
+    # one cold episode: the env's FIRST reset() -- the
+    # power flow's per-hour tables built on the device (first-iteration tables,
+    # the response table with its certificates, node records) -- and the
+    # episode's steps, the first launches of every kernel included; then the
+    # reset that starts the warm runs (not timed)
+    torch.cuda.synchronize()
+    c0 = time.perf_counter()
+    env.reset()
+    torch.cuda.synchronize()
+    cold_reset = time.perf_counter() - c0
+    cold_steps = 0
+    while True:
+        _, _, dones, _ = env.step(packed[step_count % P])
+        step_count += 1
+        cold_steps += 1
+        if dones["__all__"]:
+            break
+    torch.cuda.synchronize()
+    cold_total = pgd.max_over_ranks(time.perf_counter() - c0, dev)
+    env.reset()
     # no garbage pending in the timed region -- collected BEFORE the warmup: the
     # first env.step after a gc.collect() costs ~120 us more host time (cold
     # caches), +6 us/step on a 20-step region (tools/gpu/short_region.py,
@@ -467,36 +548,47 @@ def main():
         wenv = 64                                                             # envs per PF wave
         wmax = iters_last.abs()[: (n // wenv) * wenv].view(-1, wenv).max(1).values
         wave_hist = {int(k): int(v) for k, v in zip(*torch.unique(wmax, return_counts=True))}
-        traffic = load_traffic()
+        traffic, traffic_runs = load_traffic()
         kernels = {}
         a_us, p_us = avg_us[KERNELS[0]], avg_us[KERNELS[1]]
+        table = conv == "opendss" and env.pf_solver.od_table
+        split = table and bool(env._fused.get("od_on"))
+        ak = "k_coord_step_od" if split else "k_coord_agents_std"
+        a_bytes = STEP_OD_ENV_BYTES * n if split else AGENT_BYTES * N_AGENTS * n
         if a_us:
-            gbs = AGENT_BYTES * N_AGENTS * n / (a_us * 1e-6) / 1e9
-            kernels[KERNELS[0]] = {"avg_us": a_us, "timed_launches": cnt[0], "bound": "hbm",
-                                   "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": gbs / HBM_PEAK_GBS,
-                                   "bytes_per_launch": AGENT_BYTES * N_AGENTS * n,
-                                   "traffic": traffic.get(KERNELS[0])}
+            gbs = a_bytes / (a_us * 1e-6) / 1e9
+            kernels[ak] = {"avg_us": a_us, "timed_launches": cnt[0], "bound": "hbm",
+                           "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": a_bytes,
+                           "traffic": traffic.get(ak), "traffic_run": traffic_runs.get(ak)}
+            if split:
+                kernels[ak]["note"] = ("the 5 agents' steps and the power flow's response-table lookup (node "
+                                       "records) in one launch: %d B per env (agents 5 x %d + V675.3, violation, "
+                                       "iteration count)" % (STEP_OD_ENV_BYTES, AGENT_BYTES))
         if p_us:
-            pk = PF_KERNEL_NAME[conv]
-            table = conv == "opendss" and env.pf_solver.od_table
+            pk = "k_coord_pf_od_list<14>" if split else PF_KERNEL_NAME[conv]
             kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1],
                            "note": ("the hour's response table serves every env whose kW lies in a fitted "
                                     "piece, the snap solve (fp64 VALU DPP FMAs) the rest" if table else
                                     "fp64 VALU DPP FMAs, no MFMA (MI355X fp64 vector peak = matrix peak); "
                                     "issue-bound, one wave per SIMD at 65,536 envs"),
-                           "hbm_gbs": PF_BYTES * n / (p_us * 1e-6) / 1e9,
-                           "traffic": traffic.get(pk)}
-            kernels[pk].update(pf_roofline(conv, p_us, mean_it, n, table))
+                           "traffic": traffic.get(pk), "traffic_run": traffic_runs.get(pk)}
+            if not split:
+                kernels[pk]["hbm_gbs"] = PF_BYTES * n / (p_us * 1e-6) / 1e9
+            kernels[pk].update(pf_roofline(conv, p_us, mean_it, n, table, split))
             if table:
                 st = dict(env.pf_solver.od_resp_stats)
                 kernels[pk]["response_table"] = {
                     k: st.get(k) for k in ("hours", "segments_with_breakpoints", "brackets", "unresolved_brackets",
-                                           "pieces", "pieces_left_to_solve", "max_fit_err", "build_s")}
+                                           "pieces", "pieces_left_to_solve", "max_fit_err", "certified",
+                                           "certified_pieces", "pieces_cut_by_certificate", "uncertified_kw",
+                                           "certify_s", "build_s")}
                 kernels[pk]["response_table"]["note"] = (
                     "built on the device by the snap solve itself (pgw_pf_od_probe) about once per 24 "
-                    "simulated hours, cached across episodes (every episode repeats the hours); build_s "
-                    "is the whole build time of this run, outside the timed region")
+                    "simulated hours, every piece certified (od_certify: Taylor-model bounds prove every band and "
+                    "stopping decision constant over what its record serves; cut pieces leave a guard zone "
+                    "to the solve), cached across episodes (every episode repeats the hours); build_s is the "
+                    "whole build time of this run (in episode_cold), outside the timed region")
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "
@@ -508,6 +600,7 @@ def main():
         d = kernels[dom]
         roof = {"kernel": dom, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": d["traffic"],
+                "traffic_run": d.get("traffic_run"),
                 "avg_launch_us": d["avg_us"], "timed_launches": d["timed_launches"]}
         if d["unit"] == "GB/s":
             roof["peak_measured_copy"] = copy_gbs
@@ -550,6 +643,13 @@ def main():
                                       "`steps` steps right after the timed region (not inside it)"},
             "pf_iterations": {"mean": mean_it, "max": max_it, "wave_max_hist": wave_hist,
                               "unconverged_envs": unconverged},
+            "episode_cold": {"steps": cold_steps, "ms": cold_total * 1e3, "reset_ms": cold_reset * 1e3,
+                             "ms_per_step": cold_total / cold_steps * 1e3,
+                             "value": N_AGENTS * total_envs * cold_steps / cold_total,
+                             "pf_table_build_s": env.pf_solver.od_resp_stats.get("build_s"),
+                             "note": "the env's first reset() (the power flow's per-hour tables built and "
+                                     "certified on the device) plus the whole first episode, first launches "
+                                     "included, no events"},
             "episode": {"steps": ep_steps, "ms_per_step": ep_elapsed / ep_steps * 1e3,
                         "gathered_env_stats": int(ep_stats.shape[0]),
                         "value": N_AGENTS * total_envs * ep_steps / ep_elapsed,
@@ -559,10 +659,14 @@ def main():
         }
         if world == 1 and not args.no_variants:
             other = "exact" if conv == "opendss" else "opendss"
-            out["variants"] = {"f32": f32_variant(conv, n, min(args.steps, 286), args.warmup, P,
+            out["variants"] = {"graph8": graph_variant(env, packed, args.steps),
+                               "f32": f32_variant(conv, n, min(args.steps, 286), args.warmup, P,
                                                   pgd.rank_seed(0, rank), dev),
                                other + "_pf": pf_variant(other, n, min(args.steps, 286), args.warmup, packed,
                                                          dev)}
+            if conv == "opendss":
+                out["variants"]["opendss_no_table"] = pf_variant("opendss", n, min(args.steps, 286), args.warmup,
+                                                                 packed, dev, od_table=False)
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out))

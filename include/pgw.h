@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 29
+#define PGW_ABI_VERSION 30
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -829,6 +829,14 @@ typedef struct pgw_coord_buffers {
   double* v_out;
   double* vv;
   int32_t* iters;
+  /* OpenDSS rule with the hour's node records (pgw_pf_od.resp_v, output row 0
+   * only): scratch for the envs the table does not serve -- od_list [n],
+   * od_count [2] (zero-initialised once), od_parity flipped by the caller
+   * every step (a step appends to od_count[parity] and zeroes the other).
+   * Null: the two-kernel step (agents, then the PF kernel for every env). */
+  int32_t* od_list;
+  int32_t* od_count;
+  int32_t od_parity, pad_;
 } pgw_coord_buffers;
 
 typedef struct pgw_coord_step_info {

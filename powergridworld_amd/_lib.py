@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 29
+ABI_VERSION = 30
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -195,7 +195,8 @@ class CoordParams(C.Structure):
 class CoordBuffers(C.Structure):
     _fields_ = [("action", Mat), ("act_stride_agent", i64), ("obs", Mat), ("obs_stride_agent", i64),
                 ("x", vp), ("soc", vp), ("reward", vp), ("agent_power", vp), ("v_out", vp),
-                ("vv", vp), ("iters", vp)]
+                ("vv", vp), ("iters", vp), ("od_list", vp), ("od_count", vp), ("od_parity", i32),
+                ("pad_", i32)]
 
 
 class CoordBuffersF32(C.Structure):

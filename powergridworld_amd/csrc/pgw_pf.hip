@@ -28,6 +28,7 @@
 //   k_coord_pf      one lane per env: bus loads = sum of agent powers, power
 //                   flow, voltage-violation penalty folded into the rewards.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <type_traits>
 #include <atomic>
@@ -1633,7 +1634,8 @@ __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double
 // od_resp_lookup for a solve whose only output is the node records' row: the
 // 96-byte node records alone (their headers decide exactly as the response
 // records', so the same envs are served, with the same counts).
-__device__ __forceinline__ bool od_resp_lookup_v(const ODArgs& o, double P, double Q, double2& v, int& it) {
+template <class OA>
+__device__ __forceinline__ bool od_resp_lookup_v(const OA& o, double P, double Q, double2& v, int& it) {
   constexpr int R2 = PGW_OD_VREC / 2;
   const double g = (P - o.resp_x0) * o.resp_inv_h;
   if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
@@ -1736,19 +1738,21 @@ __device__ __forceinline__ double* od_rows_put(ODShared<M>& sh, int n_out, const
 // TR: the trace instantiation (pgw_debug_pf_trace set): phase stamps 0 entry,
 // 1 powers summed, 2 table lookup done, 3 past the fallback, 4 node 0, 5 rows,
 // 6 reward atomics issued.
-template <int M, class Bufs, bool TR = false>
-__global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
-                                                        int64_t n, Bufs b) {
+// LIST (k_coord_pf_od_list): env e comes from the fused step's list of envs
+// the table did not serve (k_coord_step_od), so every valid lane solves; the
+// agents' rewards it reads are their raw values, which k_coord_step_od left
+// in place for exactly these envs.
+template <int M, class Bufs, bool TR, bool LIST>
+__device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFArgs& a, const ODArgs& o,
+                                                const pgw_pf_tables& t, int64_t n, const Bufs& b, int64_t e,
+                                                bool valid, ODShared<M>& sh) {
   using Sto = std::remove_pointer_t<decltype(b.reward)>;
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = e < n;
   long long* const tr = TR ? g_pf_trace : nullptr;
   if constexpr (TR) pf_trace(tr, 0);
-  __shared__ ODShared<M> sh;
   ODStage<M> stg;
   // without a response table every env solves: the stage loads go out first,
   // in flight with the loads below; with one only a block that needs them does
-  const bool early = o.resp == nullptr;
+  const bool early = LIST || o.resp == nullptr;
   if (early) od_stage_load<M>(o, o.start, stg);
   const bool rows_lds = od_rows_lds<M>(a.n_out);     // (uniform) a history slot: every node
   double rv[kOdRowQ];
@@ -1791,7 +1795,9 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
   const bool vonly = o.resp_v != nullptr && o.resp_v_row == 0 && a.n_out == 1;   // (uniform)
   double2 vf = make_double2(0.0, 0.0);
   bool served;
-  if (vonly) {
+  if constexpr (LIST) {
+    served = false;
+  } else if (vonly) {
     served = valid && od_resp_lookup_v(o, S.pc, S.qc, vf, it);
   } else {
     served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf);
@@ -1832,6 +1838,152 @@ __global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a,
       if (ag < c.n_agents) b.reward[(int64_t)ag * n + e] = (Sto)(rw[ag] + (Sto)(-share));
   }
   if constexpr (TR) pf_trace(tr, 6);
+}
+
+template <int M, class Bufs, bool TR = false>
+__global__ void __launch_bounds__(kBlock) k_coord_pf_od(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
+                                                        int64_t n, Bufs b) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ ODShared<M> sh;
+  coord_pf_od_env<M, Bufs, TR, false>(c, a, o, t, n, b, e, e < n, sh);
+}
+
+// The node records' lookup of the fused C4 step (od_resp_lookup_v's fields).
+struct ODVLook {
+  const double* resp_v;
+  double resp_x0, resp_inv_h;
+  int32_t resp_nseg;
+  int32_t timing_only;      // PGW_STEP_NOLOOKUP (A/B timing only): no lookup, no list -- results wrong
+};
+
+// Fused C4 step, OpenDSS rule with the hour's node records (pgw_pf_od.resp_v,
+// output row 0 the coordinated bus, no other row): the agents AND the power
+// flow's table lookup in one launch.  A block is n_agents waves over 64 envs;
+// wave a runs agent a's step (std_agent_compute, k_coord_agents_std's
+// operations and stores) and leaves its real power in LDS; after the block
+// barrier wave 0 sums the bus load in agent order (k_coord_pf_od's prologue),
+// looks the env up in the node records and, where the table serves it, writes
+// V675.3, the violation and the iteration count and leaves the reward share in
+// LDS; every wave then stores its agent's final reward (raw + (-share), as
+// k_coord_pf_od's epilogue).  Envs the table does not serve keep their raw
+// rewards and are appended to b.od_list (count b.od_count[parity]) for
+// k_coord_pf_od_list, launched next.  Block 0 zeroes the other parity's count
+// (the next step's list).  Bit-identical to k_coord_agents_std + k_coord_pf_od.
+// WT: every store write-through (st_wt), so the step leaves no dirty L2 lines
+// for the next launch's boundary to write back.
+template <bool WT>
+__global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) k_coord_step_od(pgw_coord_params p_, pgw_coord_step_info s,
+                                                                       int64_t n, pgw_coord_buffers b, double pv_ob,
+                                                                       StdDerived dv, CoordPFArgs c, ODVLook o) {
+  auto put = [](auto* q, auto v) {
+    if constexpr (WT) st_wt(q, v);
+    else *q = v;
+  };
+  const pgw_coord_params& p = PGW_KERNARG0(pgw_coord_params);   // (no private copy)
+  const int a = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const bool valid = e < n;
+  __shared__ double s_pow[PGW_MAX_AGENTS][64];
+  __shared__ double s_share[64];
+  __shared__ int s_served[64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) b.od_count[(b.od_parity & 1) ^ 1] = 0;
+  double rw = 0.0;
+  if (valid) {
+    StdAgentIn in[1];
+    const double* ap = b.action.ptr + a * b.act_stride_agent + e * b.action.s_env;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) in[0].av[j] = ld_act(ap + j * b.action.s_dim);
+    double* xp = b.x + (int64_t)a * 5 * n + e;
+#pragma unroll
+    for (int z = 0; z < 5; ++z) in[0].xs[z] = xp[z * n];
+    double* socp = b.soc + (int64_t)a * n + e;
+    in[0].soc = *socp;
+    double* op = b.obs.ptr + a * b.obs_stride_agent + e * b.obs.s_env;
+    std_agent_compute<1>(p, dv, s, pv_ob, in, [&](int slot, const double (&v)[1]) {
+      if (slot < kSlotSoc) put(xp + slot * n, v[0]);
+      else if (slot == kSlotSoc) put(socp, v[0]);
+      else if (slot < kSlotPower) {
+        if constexpr (WT) st_wt(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
+        else st_obs(op + (slot - kSlotObs) * b.obs.s_dim, v[0]);
+      } else if (slot == kSlotPower) {
+        put(b.agent_power + (int64_t)a * n + e, v[0]);
+        s_pow[a][lane] = v[0];
+      } else {
+        rw = v[0];
+      }
+    });
+  }
+  __syncthreads();
+  if (a == 0) {
+    // the bus load of controllable slot 0 in agent order (k_coord_pf_od: 0 + p0 + p1 ...)
+    double pc = 0.0;
+#pragma unroll
+    for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag) {
+      const int slot = ag < c.n_agents ? c.agent_ctrl[ag] : -1;
+      const double rp = (valid && ag < c.n_agents) ? s_pow[ag][lane] * 1.0 : 0.0;
+      pc = (slot == 0) ? pc + rp : pc;
+    }
+    double2 vf = make_double2(0.0, 0.0);
+    int it = 0;
+    // (a local copy: a reference to the by-value kernel argument would put it
+    // in a private-memory frame)
+    const ODVLook ol = {o.resp_v, o.resp_x0, o.resp_inv_h, o.resp_nseg, 0};
+    const bool served = valid && !o.timing_only && od_resp_lookup_v(ol, pc, 0.0, vf, it);
+    double share = 0.0;
+    if (served) {
+      const double v0 = sqrt(fma(vf.y, vf.y, vf.x * vf.x));
+      if (b.v_out) put(b.v_out + e, v0);
+      if (b.iters) put(b.iters + e, (int32_t)it);
+      if (c.coordinated) {
+        const double vv = pymax(pymax(0.0, c.vv_lo - v0), v0 - c.vv_hi);
+        if (b.vv) put(b.vv + e, vv);
+        share = (vv * c.vv_penalty) / (double)c.n_agents;
+      }
+    }
+    // the envs left to the solve: one list slot each, one atomic per wave
+    const bool need = valid && !served && !o.timing_only;
+    const uint64_t m = __ballot(need);
+    if (m) {
+      const int first = __builtin_ctzll(m);
+      int base = 0;
+      if (lane == first) base = atomicAdd(b.od_count + (b.od_parity & 1), __popcll(m));
+      base = __shfl(base, first);
+      if (need) b.od_list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)e;
+    }
+    s_share[lane] = share;
+    s_served[lane] = served ? 1 : 0;
+  }
+  __syncthreads();
+  if (!valid) return;
+  const bool fin = c.coordinated && s_served[lane];
+  put(b.reward + (int64_t)a * n + e, fin ? rw + (-s_share[lane]) : rw);
+}
+
+// The snap solve of the envs k_coord_step_od appended to its list (the table
+// did not serve them: P in a bracket or a guard zone, off the grid, an unfit
+// piece), grid-stride over the list with a small fixed grid: the list's count
+// is read once, so with nothing to solve (the usual step) every block exits
+// after one load.  Outputs as k_coord_pf_od's for these envs.
+template <int M, bool LOOP>
+__global__ void __launch_bounds__(kBlock) k_coord_pf_od_list(CoordPFArgs c, PFArgs a, ODArgs o, pgw_pf_tables t,
+                                                             int64_t n, pgw_coord_buffers b) {
+  const int32_t cnt = b.od_count[b.od_parity & 1];     // (uniform)
+  if ((int64_t)blockIdx.x * kBlock >= cnt) return;     // (block-uniform)
+  __shared__ ODShared<M> sh;
+  if constexpr (LOOP) {
+    for (int64_t base = (int64_t)blockIdx.x * kBlock; base < cnt; base += (int64_t)gridDim.x * kBlock) {
+      const int64_t i = base + threadIdx.x;
+      const bool valid = i < cnt;
+      const int64_t e = valid ? (int64_t)b.od_list[i] : 0;
+      coord_pf_od_env<M, pgw_coord_buffers, false, true>(c, a, o, t, n, b, e, valid, sh);
+      __syncthreads();                                 // (the next pass re-stages sh)
+    }
+  } else {                                             // one block per 256 list slots
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = i < cnt;
+    const int64_t e = valid ? (int64_t)b.od_list[i] : 0;
+    coord_pf_od_env<M, pgw_coord_buffers, false, true>(c, a, o, t, n, b, e, valid, sh);
+  }
 }
 
 // pgw_pf_solve, OpenDSS rule: k_pf_solve's prologue (the env's controllable
@@ -2223,6 +2375,31 @@ static int32_t check_od(const pgw_pf_params& p, const pgw_pf_tables& t, const ch
 
 using namespace pgw;
 
+// k_coord_pf_od_list's grid (blocks of kBlock lanes): with an empty list (the
+// usual step) its time is the dispatch of that many blocks of a 148-KB-LDS,
+// 512-register kernel; a non-empty list of c envs takes ceil(c / (grid kBlock))
+// grid-stride passes.  PGW_OD_LIST_GRID at load (A/Bs), default kOdListGrid.
+constexpr int kOdListGrid = 1 << 30;   // (no cap: one block per 256 list slots)
+static int initial_od_list_grid() {
+  const char* v = getenv("PGW_OD_LIST_GRID");
+  const int g = v ? atoi(v) : 0;
+  return g > 0 ? g : kOdListGrid;
+}
+static const int g_od_list_grid = initial_od_list_grid();
+// k_coord_step_od's stores: plain / nontemporal (default) or write-through
+// (PGW_STEP_WT=1 at load, A/Bs: measured slower, 21.6 -> 23.2 us)
+static bool initial_step_wt() {
+  const char* v = getenv("PGW_STEP_WT");
+  return v && v[0] == '1';
+}
+static const bool g_step_wt = initial_step_wt();
+static const bool g_step_nolookup = getenv("PGW_STEP_NOLOOKUP") && getenv("PGW_STEP_NOLOOKUP")[0] == '1';
+// PGW_STEP_NOP=1 (diagnostics): an empty one-wave kernel between the step's two launches, to time the boundary
+static const bool g_step_nop = getenv("PGW_STEP_NOP") && getenv("PGW_STEP_NOP")[0] == '1';
+__global__ void k_step_nop(int* p) {
+  if (p && threadIdx.x == 1000) *p = 0;
+}
+
 // pgw_coord_step / pgw_coord_step_f32
 // The agents' half of the coordinated step (k_coord_agents_std or the generic
 // k_coord_agents), fp64 buffers.
@@ -2287,6 +2464,39 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   c.vv_hi = p->vv_hi;
   c.vv_penalty = p->vv_penalty;
   const PFArgs a = make_pf_args(*pf, *pft);
+  if constexpr (!kF32) {
+    // OpenDSS rule with the hour's node records and no output row but the
+    // coordinated bus: the agents and the table lookup in one launch
+    // (k_coord_step_od), then the snap solve of the envs it listed
+    // (k_coord_pf_od_list, a small grid that exits at once on an empty list)
+    if (pft->od && b.od_list && b.od_count && !g_pf_trace_on.load()) {
+      const ODArgs o = make_od_args(*pft->od, pf->max_iter);
+      if (std_layout && o.resp_v && o.resp_v_row == 0 && pf->n_out == 1 && p->vv_row == 0) {
+        const ODVLook lk = {o.resp_v, o.resp_x0, o.resp_inv_h, o.resp_nseg, g_step_nolookup ? 1 : 0};
+        if (g_step_wt)
+          launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<true>, dim3((unsigned)((n + 63) / 64)),
+                       dim3(64 * p->n_agents), st, *p, *s, n, b, pv_ob, make_std_derived(*p), c, lk);
+        else
+          launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<false>, dim3((unsigned)((n + 63) / 64)),
+                       dim3(64 * p->n_agents), st, *p, *s, n, b, pv_ob, make_std_derived(*p), c, lk);
+        int32_t rc = check_launch("k_coord_step_od");
+        if (rc) return rc;
+        if (g_step_nop) hipLaunchKernelGGL(k_step_nop, dim3(1), dim3(64), 0, st, (int*)nullptr);
+        if (g_od_list_grid >= grid_for(n))
+          launch_timed(PGW_T_COORD_PF, k_coord_pf_od_list<14, false>, dim3((unsigned)grid_for(n)),
+                       dim3(kBlock), st, c, a, o, *pft, n, b);
+        else
+          launch_timed(PGW_T_COORD_PF, k_coord_pf_od_list<14, true>, dim3((unsigned)g_od_list_grid),
+                       dim3(kBlock), st, c, a, o, *pft, n, b);
+        return check_launch("k_coord_pf_od_list");
+      }
+    }
+    // any other step with a list: the next step's count (k_coord_step_od's job) zeroed here
+    if (b.od_count) {
+      const hipError_t me = hipMemsetAsync(b.od_count + ((b.od_parity & 1) ^ 1), 0, sizeof(int32_t), st);
+      PGW_REQUIRE(me == hipSuccess, "pgw_coord_step: od_count reset: %s", hipGetErrorString(me));
+    }
+  }
   // fp32: env pairs per lane (float2 accesses).  The pair layout measured for
   // fp64 too (19.5 -> 20.2 us), so it is instantiated for fp32 only.
   bool done = false;
@@ -2307,6 +2517,7 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
   }
   int32_t rc = check_launch("k_coord_agents");
   if (rc) return rc;
+  if (g_step_nop) hipLaunchKernelGGL(k_step_nop, dim3(1), dim3(64), 0, st, (int*)nullptr);
   hipStream_t pst = st;
   if (pft->od) {
     if (g_pf_trace_on.load())
@@ -2343,6 +2554,11 @@ static int32_t coord_step_general(const pgw_coord_params* p, const pgw_pfg_param
   const double pv_ob = p->pv.rescale ? (2.0 * std::min(std::max(-s->pv_pmax, p->pv.obs_low), p->pv.obs_high)
                                         - (p->pv.obs_low + p->pv.obs_high)) / (p->pv.obs_high - p->pv.obs_low)
                                      : -s->pv_pmax;
+  if (b.od_count) {                                // (pgw_coord_buffers.od_count: the next step's list)
+    const hipError_t me = hipMemsetAsync(b.od_count + ((b.od_parity & 1) ^ 1), 0, sizeof(int32_t),
+                                         (hipStream_t)stream);
+    PGW_REQUIRE(me == hipSuccess, "pgw_coord_step_general: od_count reset: %s", hipGetErrorString(me));
+  }
   int32_t rc = launch_coord_agents(*p, *s, n, b, pv_ob, coord_is_std(*p), (hipStream_t)stream);
   if (rc) return rc;
   PFGCoord c = {};

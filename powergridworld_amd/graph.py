@@ -319,6 +319,101 @@ class StepGraph:
         return self._finish()
 
 
+class CoordStepGraph:
+    """Captured steps of the fused multi-agent step (MultiAgentEnv fused path,
+    pgw_coord_step / _f32 / _general): `steps` consecutive steps per graph,
+    captured once per episode position (and step parity of the fused step's
+    list counters) on first use, each step's launches holding that step's
+    constants as the eager step builds them (_step_entry: exogenous rows, PV
+    value, the hour's PF parameters and tables).  The actions are read from the
+    packed [n_agents, N, act_dim] tensors bound at capture: `action` is one
+    tensor (every step of every call), a list of `steps`, or a callable k ->
+    list of `steps` tensors for the graph at episode position k.  Host state
+    (clocks, time, done, the list parity) advances in the call exactly as
+    `steps` eager steps advance it, so captured and eager steps mix freely; the
+    steps of one call must lie inside the episode (IndexError before any launch
+    otherwise).  No history ring (record_history=False)."""
+
+    def __init__(self, env, action, steps):
+        steps = int(steps)
+        if steps < 1:
+            raise ValueError("capture_step: steps >= 1")
+        F = env._fused
+        if F is None:
+            raise NotImplementedError("capture_step: the fused multi-agent step only (fused=True)")
+        if env._hist is not None:
+            raise NotImplementedError("capture_step: record_history=True writes per-step ring slots")
+        self.env, self.steps, self._pos = env, steps, {}
+        if callable(action):
+            self._bind = action
+        else:
+            acts = list(action) if isinstance(action, (list, tuple)) else [action] * steps
+            if len(acts) != steps:
+                raise ValueError("capture_step: %d action sets for %d steps" % (len(acts), steps))
+            self._bind = lambda k: acts
+
+    def _step_bufs(self, act, parity):
+        env = self.env
+        F = env._fused
+        na, n = len(env.agents), env.num_envs
+        if not isinstance(act, torch.Tensor) or tuple(act.shape) != (na, n, F["act_dim"]) or \
+                act.dtype != env.dtype or act.device != torch.device(env.device):
+            raise ValueError("capture_step: packed actions must be [%d, %d, %d] %s tensors on %s"
+                             % (na, n, F["act_dim"], env.dtype, env.device))
+        b = type(F["bufs"]).from_buffer_copy(F["bufs"])
+        b.action = F["Mat"](act.data_ptr(), act.stride(1), act.stride(2))
+        b.act_stride_agent = act.stride(0)
+        if F.get("od_on"):
+            b.od_parity = parity
+        return b
+
+    def _graph_at(self, k, parity):
+        env = self.env
+        F, solver = env._fused, env.pf_solver
+        key = (k, parity, solver.tables_version, F.get("od_on"))
+        g = self._pos.get(key)
+        if g is not None:
+            return g[0]
+        acts = list(self._bind(k))
+        if len(acts) != self.steps:
+            raise ValueError("capture_step: %d action sets for %d steps" % (len(acts), self.steps))
+        bld, pv = F["bld0"], F["pv0"]
+        t0 = bld.time_index if bld is not None else None
+        p0 = pv.index if pv is not None else None
+        launches = []
+        for i in range(self.steps):
+            skey = (t0 + i if bld is not None else -1, p0 + i if pv is not None else -1,
+                    env._time_at(env.episode_step + 1 + i), solver.tables_version)
+            ent = F["step_cache"].get(skey) or env._step_entry(skey)
+            if solver.tables_version != key[2]:
+                raise RuntimeError("capture_step: the power-flow tables changed while capturing")
+            launches.append((ent, self._step_bufs(acts[i], (parity + 1 + i) & 1)))
+        fn = getattr(_lib.lib(), F["kernel"])
+        n = env.num_envs
+
+        def launch():
+            st = _lib.stream_ptr(env.device)
+            for (info, pfp, pft, _), b in launches:
+                _lib.check(fn(F["params"], pfp, pft, info, n, b, st))
+        g = _capture(env.device, launch)
+        self._pos[key] = (g, launches, acts)          # (the launches' structs live as long as the graph)
+        return g
+
+    def __call__(self):
+        env = self.env
+        F = env._fused
+        k = env.episode_step
+        last = env._episode_last_step()
+        if last is not None and k + self.steps > last:
+            raise IndexError("capture_step: steps %d..%d run past the episode's last step %d (step eagerly "
+                             "or reset)" % (k + 1, k + self.steps, last))
+        parity = F["bufs"].od_parity if F.get("od_on") else 0
+        self._graph_at(k, parity).launch(_lib.stream_ptr(env.device))
+        for _ in range(self.steps):
+            out = env._advance_fused()
+        return out
+
+
 def kwargs_given(kwargs):
     return any(v is not None for v in kwargs.values())
 

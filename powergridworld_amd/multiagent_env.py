@@ -179,6 +179,7 @@ class MultiAgentEnv(Env):
     def reset(self) -> Dict[str, any]:
         """multiagent_env.py:125-140"""
         self.episode_step = 0
+        self._resets = self.__dict__.get("_resets", 0) + 1
         oob_poll(self.oob_count)
         self.time = self._time_at(0)
         self.history = {"timestamp": [], "voltage": [], "agent_power_p": []}
@@ -842,6 +843,30 @@ class MultiAgentEnv(Env):
         meta["oob_actions"] = self.oob_count
         return obs, rew, done, meta
 
+    def set_pf_list(self, enabled=True):
+        """Fused C4 step under the OpenDSS rule with node records (fp64): True
+        runs the agents and the table lookup in one launch (k_coord_step_od)
+        plus the snap solve of the envs it lists (k_coord_pf_od_list); False
+        (the default) the two-kernel step (k_coord_agents_std, then
+        k_coord_pf_od over every env).  Bit-identical; the split measured no
+        faster, so it is opt-in."""
+        F = self._fused
+        if F is None or self.dtype != torch.float64:
+            return
+        b = F["bufs"]
+        if enabled:
+            if "od_list" not in F:
+                # the envs the response table does not serve: k_coord_step_od lists
+                # them, k_coord_pf_od_list solves them; od_count is two counters, the
+                # step's and the next one's (od_parity, flipped every step)
+                F["od_list"] = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+                F["od_count"] = torch.zeros(2, dtype=torch.int32, device=self.device)
+                b.od_parity = 0
+            b.od_list, b.od_count = F["od_list"].data_ptr(), F["od_count"].data_ptr()
+        else:
+            b.od_list = b.od_count = None
+        F["od_on"] = bool(enabled)
+
     def action_buffer(self):
         """Packed [n_agents, N, act_dim] action tensor the fused step reads
         zero-copy, plus the {agent: {component: [N, d]}} views into it."""
@@ -897,10 +922,17 @@ class MultiAgentEnv(Env):
         if H is not None:            # outputs straight into this step's history slot
             s_ = H["t"] % H["cap"]
             bufs.v_out, bufs.agent_power = H["v"][s_].data_ptr(), H["p"][s_].data_ptr()
+        if F.get("od_on"):
+            bufs.od_parity ^= 1
         rc = getattr(_lib.lib(), F["kernel"])(F["params"], pfp, pft, info,
                                               self.num_envs, bufs, _lib.stream_ptr(self.device))
         if rc:
             _lib.check(rc)
+        return self._fused_post(H, s_ if H is not None else None)
+
+    def _fused_post(self, H, s_):
+        """The fused step's host bookkeeping after its launch."""
+        F, solver = self._fused, self.pf_solver
         self.pf_solver.iterations = F["iters"]
         self._fused_steps += 1
         if H is None:
@@ -927,6 +959,58 @@ class MultiAgentEnv(Env):
         if H is not None:
             self._record(None)
         return F["obs_dict"], F["rew_dict"], F["done_true"] if d else F["done_false"], F["meta"]
+
+    def capture_step(self, action, steps=1):
+        """A CoordStepGraph (graph.py) of `steps` fused multi-agent steps per
+        call, reading the packed actions bound at capture (a [n_agents, N,
+        act_dim] tensor, a list of `steps` of them, or a callable k -> such a
+        list for the graph at episode position k); returns what the last
+        step's env.step returns."""
+        from powergridworld_amd.graph import CoordStepGraph
+        return CoordStepGraph(self, action, steps)
+
+    def _advance_fused(self):
+        """One captured step's host side: step()'s clocks and the fused step's
+        bookkeeping (_fused_post), as the eager step does them after its launch."""
+        self.episode_step += 1
+        self.time = self._time_at(self.episode_step)
+        self._at_reset = False
+        self.obs_dict = {}
+        F = self._fused
+        if F.get("od_on"):
+            F["bufs"].od_parity ^= 1
+        obs, rew, done, meta = self._fused_post(None, None)
+        any_done = any(done.values())
+        d = bool(any_done or self.episode_step == self.max_episode_steps - 1 or self.episode_step >= self._end_step)
+        dones = {a.name: d for a in self.agents}
+        dones["__all__"] = d
+        return obs, rew, dones, meta
+
+    def _episode_last_step(self):
+        """The episode step at which step() returns done (the component clocks
+        advanced on copies; cached per reset)."""
+        c = self.__dict__.get("_ep_last")
+        if c is not None and c[0] == self.__dict__.get("_resets", 0):
+            return c[1]
+        F = self._fused
+        clocks = [(e, "time_index") for e in F["bld_envs"]] + [(e, "index") for e in F["pv_envs"]] + \
+                 [(e, "simulation_step") for e in F["bat_envs"]]
+        saved = [getattr(e, a) for e, a in clocks]
+        last, s = None, self.episode_step
+        try:
+            for _ in range(1 << 20):
+                s += 1
+                for e, a in clocks:
+                    setattr(e, a, getattr(e, a) + 1)
+                if any(e.is_terminal() for e in F["agent0_envs"]) or s == self.max_episode_steps - 1 or \
+                        s >= self._end_step:
+                    last = s
+                    break
+        finally:
+            for (e, a), v in zip(clocks, saved):
+                setattr(e, a, v)
+        self._ep_last = (self.__dict__.get("_resets", 0), last)
+        return last
 
     def _step_entry(self, skey):
         """The fused step's per-step constants for skey = (building time index,

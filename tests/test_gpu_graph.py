@@ -255,3 +255,48 @@ def test_hs_graph_matches_eager_across_reset(steps):
         for e in (ea, eb):
             e.reset(init_storage=init)
     assert len(g._pos_graphs) > 1
+
+
+@pytest.mark.parametrize("conv", ["opendss", "exact"])
+def test_c4_graph8_equals_eager_across_episodes(conv):
+    """The fused C4 step captured 8 steps per graph (MultiAgentEnv.capture_step,
+    graph.CoordStepGraph; one graph per episode position, actions bound per
+    position from a pool) against the eager step over two whole episodes and
+    the resets between them: every output bit for bit at every call; the
+    episode's tail (fewer than 8 steps left) runs eagerly, a call past the
+    last step is refused before launching."""
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    n, P, S = 2048, 16, 8
+    g = torch.Generator(DEV).manual_seed(21)
+    pool = torch.rand((P, 5, 8, n), dtype=torch.float64, device=DEV, generator=g) * 2.2 - 1.1
+    packed = pool.transpose(2, 3)
+    eager, cap = [CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n,
+                                                     device=DEV, fused=True) for _ in range(2)]
+    graph = cap.capture_step(lambda k: [packed[(k + i) % P] for i in range(S)], steps=S)
+
+    def snap(env, r, d):
+        return [env.packed_obs().clone(), torch.stack([r[a.name] for a in env.agents]).clone(),
+                env.pf_solver.get_bus_voltage_by_name("675c").clone(), env.pf_solver.iterations.clone(),
+                torch.tensor(float(d["__all__"]))]
+    for ep in range(2):
+        eager.reset()
+        cap.reset()
+        last = cap._episode_last_step()
+        assert last is not None and last > S
+        k = 0
+        while k < last:
+            if k + S <= last:
+                _, r2, d2, _ = graph()
+                for i in range(S):
+                    _, r1, d1, _ = eager.step(packed[(k + i) % P])
+                k += S
+            else:
+                with pytest.raises(IndexError):
+                    graph()
+                _, r2, d2, _ = cap.step(packed[k % P])
+                _, r1, d1, _ = eager.step(packed[k % P])
+                k += 1
+            for i, (x, y) in enumerate(zip(snap(eager, r1, d1), snap(cap, r2, d2))):
+                assert torch.equal(x, y), "episode %d step %d output %d" % (ep, k, i)
+        assert d1["__all__"] and d2["__all__"] and eager.episode_step == cap.episode_step == last
+    assert len(graph._pos) >= (last // S)

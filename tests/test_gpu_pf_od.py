@@ -356,6 +356,64 @@ def test_od_response_table_bit_identical_paths():
         assert torch.equal(envs[0].voltages[nm], envs[1].voltages[nm])
 
 
+def _unfit(solver, every):
+    """Mark every `every`-th response record of the solver's tables unfit (k*
+    = 0, the chain kept) in the response records and their node records: the
+    envs in those pieces go to the solve."""
+    from powergridworld_amd import _lib
+    for tab, R in ((solver._od_resp, _lib.od_rec(solver.M)), (solver._od_vresp, _lib.OD_VREC)):
+        w = tab.view(-1, R).view(torch.int64)[:, 4]
+        sel = torch.arange(w.shape[0], device=w.device) % every == 0
+        w[sel] = w[sel] & ~0xffffffff
+
+
+@pytest.mark.parametrize("n,every,steps", [(4133, 0, 40), (4133, 3, 20), (4133, 1, 12), (66000, 1, 3)])
+def test_od_split_step_bit_identical(n, every, steps):
+    """The fused C4 step with the agents and the table lookup in one launch
+    (k_coord_step_od) and the listed envs' snap solve (k_coord_pf_od_list)
+    against the two-kernel step (k_coord_agents_std + k_coord_pf_od): every
+    output bit for bit -- with the table serving (every = 0), with a third of
+    the records forced unfit and with all of them (every env in the list; at
+    66 000 envs the list kernel's grid-stride loop takes two passes) -- and the
+    all-unfit case equal to the step without a table (od_table=False)."""
+    from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
+    envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
+            for _ in range(3)]
+    envs[0].set_pf_list(True)
+    envs[2].pf_solver.od_table = False
+    rng = np.random.default_rng(17)
+    init = torch.tensor(rng.uniform(5.0, 45.0, size=(5, n)), device=DEV)
+    for env in envs:
+        env.reset()
+        for ai, agent in enumerate(env.agents):
+            agent.env_dict["storage"].reset(init_storage=init[ai])
+        env.load_component_state()
+        if every and env.pf_solver.od_table:
+            _unfit(env.pf_solver, every)
+    g = torch.Generator(DEV).manual_seed(3)
+    listed = 0
+    for t in range(steps):
+        a = torch.rand((5, n, 8), dtype=torch.float64, device=DEV, generator=g) * 2.2 - 1.1
+        outs = []
+        for env in envs:
+            o, r, d, m = env.step(a)
+            outs.append([env.packed_obs().clone(), torch.stack([r[x.name] for x in env.agents]).clone(),
+                         m["voltage_violation"].clone(), env.pf_solver.get_bus_voltage_by_name("675c").clone(),
+                         env.pf_solver.iterations.clone(), env._fused["agent_power"].clone()])
+        F = envs[0]._fused
+        listed += int(F["od_count"][F["bufs"].od_parity & 1])
+        for i, (x, y) in enumerate(zip(outs[0], outs[1])):
+            assert torch.equal(x, y), "split vs two-kernel: step %d output %d" % (t, i)
+        if every == 1:
+            for i, (x, y) in enumerate(zip(outs[0], outs[2])):
+                assert torch.equal(x, y), "all unfit vs no table: step %d output %d" % (t, i)
+    if every == 1:
+        assert listed == n * steps, listed
+    elif every == 3:
+        assert 0 < listed < n * steps
+    assert (envs[0].pf_solver.iterations > 0).all()
+
+
 # ------------------------------------------------------------------ fp32 storage (pgw_pf_solve_f32)
 @pytest.mark.parametrize("conv", ["opendss", "opendss_no_table", "exact"])
 def test_pf_solve_f32_equals_fp64_solve(conv):
