@@ -167,6 +167,7 @@ def f32_variant(conv, n, steps, warmup, pool_size, seed, dev):
             if dones["__all__"]:
                 env.reset()
     run(warmup)
+    gc.collect()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(steps)
@@ -230,6 +231,7 @@ def pf_variant(conv, n, steps, warmup, pool, dev, od_table=True):
             if dones["__all__"]:
                 env.reset()
     run(warmup)
+    gc.collect()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(steps)
@@ -282,14 +284,17 @@ def graph_variant(env, packed, steps, warmup_episodes=1, S=8):
     t0 = time.perf_counter()
     run(warmup_episodes * 286)                      # every position's graph captured
     capture_s = time.perf_counter() - t0
+    gc.collect()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     done_steps, calls = run(steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    n_graphs = len(graph._pos)
+    graph.release()                  # (not at a later garbage collection, inside another variant's timing)
     return {"value": N_AGENTS * env.num_envs * done_steps / dt, "unit": "agent-env-steps/s",
             "ms_per_step": dt / done_steps * 1e3, "steps": done_steps, "graph_calls": calls,
-            "graphs": len(graph._pos), "warmup_capture_s": capture_s,
+            "graphs": n_graphs, "warmup_capture_s": capture_s,
             "note": "S=%d steps per hipGraph launch (one graph per episode position and list parity, captured "
                     "in a warm-up episode), episode tails and resets eager; same env, state and action pool as "
                     "the headline, bit-identical outputs" % S}

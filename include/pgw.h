@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PGW_ABI_VERSION 30
+#define PGW_ABI_VERSION 31
 
 #define PGW_OK 0
 #define PGW_ERR_ARG (-1)
@@ -459,6 +459,16 @@ typedef struct pgw_pf_od {
   int32_t resp_v_row;                /* output row of the node records; < 0 none */
   const double* resp_v;              /* node records (PGW_OD_VREC each) or NULL */
   uint64_t resp_rows;                /* extrema rows of served envs; 0 = all    */
+  /* Row records (or NULL): per response record, PGW_OD_REC_HEAD header
+   * doubles (a bitwise copy of the response record's) then, for the k-th set
+   * bit r of resp_q_rows (ascending; output rows < 64), the squared magnitude
+   * of output row r as a quartic in the record's t: a0..a4 at
+   * [PGW_OD_REC_HEAD + 5 k ..], |V_r|^2 = a0 + t (a1 + t (a2 + t (a3 + t a4))).
+   * A served env takes every listed row from them on every path.  resp_q_k =
+   * popcount(resp_q_rows); records resp_q_stride doubles apart. */
+  const double* resp_q;
+  uint64_t resp_q_rows;
+  int32_t resp_q_stride, resp_q_k;
 } pgw_pf_od;
 
 /* Element k draws S_k = ((base_kw[k] + ctrl_p[elem_ctrl[k]]) * 1000 / nph[k]) + j(...kvar)

@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PGW_LIB_PATH: another build of the same ABI (same-box A/B measurements only)
 LIB_PATH = os.environ.get("PGW_LIB_PATH") or os.path.join(_HERE, "libpgw.so")
-ABI_VERSION = 30
+ABI_VERSION = 31
 
 f64, i32, i64, u64, vp = C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
 P = C.POINTER
@@ -110,7 +110,8 @@ class PFOD(C.Structure):
                 ("elem_scale", f64 * PF_MAX_M), ("gamma", f64), ("eps", f64), ("gmax", f64),
                 ("gsrc", f64), ("min_iter", i32), ("n_rep", i32), ("n_rows", i32), ("sparse_envs", i32),
                 ("rows_V0", vp), ("rows_G", vp), ("start", vp), ("resp", vp), ("resp_x0", f64),
-                ("resp_h", f64), ("resp_nseg", i32), ("resp_v_row", i32), ("resp_v", vp), ("resp_rows", u64)]
+                ("resp_h", f64), ("resp_nseg", i32), ("resp_v_row", i32), ("resp_v", vp), ("resp_rows", u64),
+                ("resp_q", vp), ("resp_q_rows", u64), ("resp_q_stride", i32), ("resp_q_k", i32)]
 
 
 OD_REC_HEAD = 6

@@ -48,7 +48,8 @@ _SKIP_EXACT = ("history", "_hist", "_bv")  # the history lists and their device 
 # _pred_index) is not state -- a restore keeps the live tables and their index
 # consistent (a checkpoint taken before a table rebuild would otherwise copy
 # another hour's rows under the live index)
-_SKIP_TABLES = ("_od_start", "_od_resp", "_od_vresp", "_pred_table", "_pred_sig", "_pred_meta", "_pred_grid",
+_SKIP_TABLES = ("_od_start", "_od_resp", "_od_vresp", "_od_qrec", "_pred_table", "_pred_sig", "_pred_meta",
+                "_pred_grid",
                 # the fused step's list of envs left to the solve: per-step scratch whose
                 # counters pair with the live env's step parity (a restored count would not)
                 "od_list", "od_count")

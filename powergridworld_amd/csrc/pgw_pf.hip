@@ -1104,6 +1104,9 @@ struct ODArgs {
   int32_t resp_v_row;                             // output row of the node records (-1: none)
   const double* resp_v;                           // node records (pgw_pf_od.resp_v) or null
   uint64_t resp_rows;                             // extrema rows of served envs (0: all)
+  const double* resp_q;                           // row records (pgw_pf_od.resp_q) or null
+  uint64_t resp_q_rows;                           // output rows with a row-record slot (ascending)
+  int32_t resp_q_stride, resp_q_k;
 };
 constexpr int kOdRows = PGW_PF_OD_MAX_ROWS;
 constexpr int kOdChunk = 12;                      // check rows per previous-magnitude pass
@@ -1161,6 +1164,11 @@ static ODArgs make_od_args(const pgw_pf_od& d, int max_iter) {
   o.resp_v = (resp && d.resp_v && d.resp_v_row >= 0) ? d.resp_v : nullptr;
   o.resp_v_row = o.resp_v ? d.resp_v_row : -1;
   o.resp_rows = resp ? d.resp_rows : 0;
+  const bool q = resp && d.resp_q && d.resp_q_rows != 0 && d.resp_q_stride >= PGW_OD_REC_HEAD + 5 * d.resp_q_k;
+  o.resp_q = q ? d.resp_q : nullptr;
+  o.resp_q_rows = q ? d.resp_q_rows : 0;
+  o.resp_q_stride = q ? d.resp_q_stride : 0;
+  o.resp_q_k = q ? d.resp_q_k : 0;
   return o;
 }
 
@@ -1590,17 +1598,17 @@ __device__ __forceinline__ double2 od_rec_j(double2 c0, double2 c1, double2 c2, 
 // (with Q = 0) lies in no piece -- then the env runs the snap solve.
 template <int M>
 __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double Q, double (&jr)[M],
-                                               double (&ji)[M], int& it, double2& vf) {
+                                               double (&ji)[M], int& it, double2& vf, int& rec, double& tq) {
   constexpr int R2 = PGW_OD_REC(M) / 2;
   const double g = (P - o.resp_x0) * o.resp_inv_h;
   if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
   int r = (int)g;
   for (int hop = 0; hop < kOdHops; ++hop) {
-    const double2* rec = reinterpret_cast<const double2*>(o.resp) + (int64_t)r * R2;
+    const double2* rp = reinterpret_cast<const double2*>(o.resp) + (int64_t)r * R2;
     double2 c[3 * M];
-    const double2 h0 = rec[0], h1 = rec[1], h2 = rec[2];
+    const double2 h0 = rp[0], h1 = rp[1], h2 = rp[2];
 #pragma unroll
-    for (int q = 0; q < 3 * M; ++q) c[q] = rec[3 + q];      // in flight with the header
+    for (int q = 0; q < 3 * M; ++q) c[q] = rp[3 + q];       // in flight with the header
     // the node record's coefficients in the same round trip (its header is a
     // copy of this one); zero without node records
     double2 v0 = make_double2(0.0, 0.0), v1 = v0, v2 = v0;
@@ -1623,12 +1631,70 @@ __device__ __forceinline__ bool od_resp_lookup(const ODArgs& o, double P, double
       }
       it = k_it;
       vf = od_rec_j(v0, v1, v2, t);
+      rec = r;
+      tq = t;
       return true;
     }
     if (next < 0) return false;
     r = next;
   }
   return false;
+}
+
+// ---- row records (pgw_pf_od.resp_q): per response record, the squared
+// magnitude of each listed output row as a quartic in the record's t,
+// |V0 + G J'(t)|^2 = a0 + t (a1 + t (a2 + t (a3 + t a4))), composed on the
+// host from the same pieces.  A served env takes every listed row's value from
+// them on every path (all rows, extrema only, fused), so each row is the same
+// bit for bit whichever kernel and row set computes it; an extrema-only solve
+// whose block the table serves entirely reads only these records.
+__device__ __forceinline__ int od_q_slot(const ODArgs& o, int ro) {
+  if (!o.resp_q || ro < 0 || ro >= 64 || !((o.resp_q_rows >> ro) & 1ull)) return -1;
+  return __popcll(o.resp_q_rows & ((1ull << ro) - 1ull));
+}
+__device__ __forceinline__ double od_q_m2(const ODArgs& o, int rec, int slot, double t) {
+  const double* q = o.resp_q + (int64_t)rec * o.resp_q_stride + PGW_OD_REC_HEAD + 5 * slot;
+  return fma(t, fma(t, fma(t, fma(t, q[4], q[3]), q[2]), q[1]), q[0]);
+}
+// The piece of P (Q = 0) from the row records' headers alone (the chain of
+// od_resp_lookup, same decisions): record index, t and the count.
+__device__ __forceinline__ bool od_q_find(const ODArgs& o, double P, double Q, int& it, int& rec, double& tq) {
+  const double g = (P - o.resp_x0) * o.resp_inv_h;
+  if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
+  int r = (int)g;
+  for (int hop = 0; hop < kOdHops; ++hop) {
+    const double2* h = reinterpret_cast<const double2*>(o.resp_q + (int64_t)r * o.resp_q_stride);
+    const double2 h0 = h[0], h1 = h[1], h2 = h[2];
+    int k_it, next;
+    od_rec_meta(h2.x, k_it, next);
+    if (P >= h0.x && P <= h0.y) {
+      if (k_it == 0) return false;
+      it = k_it;
+      rec = r;
+      tq = (P - h1.x) * h1.y;
+      return true;
+    }
+    if (next < 0) return false;
+    r = next;
+  }
+  return false;
+}
+// Record rec's currents J'(t) (od_resp_lookup's values) and node-record value.
+template <int M>
+__device__ __forceinline__ void od_resp_at(const ODArgs& o, int rec, double t, double (&jr)[M], double (&ji)[M],
+                                           double2& vf) {
+  constexpr int R2 = PGW_OD_REC(M) / 2;
+  const double2* rp = reinterpret_cast<const double2*>(o.resp) + (int64_t)rec * R2;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double2 j = od_rec_j(rp[3 + k], rp[3 + M + k], rp[3 + 2 * M + k], t);
+    jr[k] = j.x;
+    ji[k] = j.y;
+  }
+  if (o.resp_v) {
+    const double2* vr = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)rec * (PGW_OD_VREC / 2);
+    vf = od_rec_j(vr[3], vr[4], vr[5], t);
+  }
 }
 
 // od_resp_lookup for a solve whose only output is the node records' row: the
@@ -1794,13 +1860,15 @@ __device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFAr
   // the 96-byte node record is all a served env reads
   const bool vonly = o.resp_v != nullptr && o.resp_v_row == 0 && a.n_out == 1;   // (uniform)
   double2 vf = make_double2(0.0, 0.0);
+  int rec = 0;
+  double tq = 0.0;
   bool served;
   if constexpr (LIST) {
     served = false;
   } else if (vonly) {
     served = valid && od_resp_lookup_v(o, S.pc, S.qc, vf, it);
   } else {
-    served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf);
+    served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf, rec, tq);
   }
   const bool need = valid && !served;
   if constexpr (TR) { if (ir[0] != -1e300 && vf.x != -1e300) pf_trace(tr, 2); }
@@ -1814,7 +1882,12 @@ __device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFAr
     v0r = vf.x;
     v0i = vf.y;
   }
-  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  double m2_0 = fma(v0i, v0i, v0r * v0r);
+  if (o.resp_q) {                                    // (uniform) the row records' row 0
+    const int q0 = od_q_slot(o, 0);
+    if (served && q0 >= 0) m2_0 = od_q_m2(o, rec, q0, tq);
+  }
+  const double v0 = sqrt(m2_0);
   if constexpr (TR) { if (v0 != -1.0) pf_trace(tr, 4); }
   // rows 1.. (a history slot holds every node)
   double vsel = v0;
@@ -1822,6 +1895,8 @@ __device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFAr
   const double vfm = sqrt(fma(vf.y, vf.y, vf.x * vf.x));
   pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
     v = (served && ro == o.resp_v_row) ? vfm : v;
+    const int qs = od_q_slot(o, ro);
+    if (served && qs >= 0) v = sqrt(od_q_m2(o, rec, qs, tq));
     if (valid && b.v_out) b.v_out[(int64_t)ro * n + e] = (Sto)v;
     vsel = (ro == c.vv_row) ? v : vsel;
   });
@@ -2020,15 +2095,39 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
   int it = 0;
   double2 vf = make_double2(0.0, 0.0);
-  const bool served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf);
+  int rec = 0;
+  double tq = 0.0;
+  // extrema only with row records covering every candidate row (and row 0):
+  // a block the table serves entirely reads the row records' headers and
+  // quartics alone -- no currents, no node-0 or row DPP groups, no row staging
+  const bool qfast = table && v_out == nullptr && o.resp_q && rows_lds && o.resp_rows != 0 &&
+                     (od_q_slot(o, 0) >= 0 || o.resp_v_row == 0);        // (uniform)
+  bool served, blk_fast = false;
+  if (qfast) {
+    served = valid && od_q_find(o, S.pc, S.qc, it, rec, tq);
+    if (served && o.resp_v) {
+      const double2* vr = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)rec * (PGW_OD_VREC / 2);
+      vf = od_rec_j(vr[3], vr[4], vr[5], tq);
+    }
+    blk_fast = !__syncthreads_or(valid && !served);   // (block-uniform)
+    if (!blk_fast && served) od_resp_at<M>(o, rec, tq, ir, ii, vf);
+  } else {
+    served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf, rec, tq);
+  }
   const bool need = valid && !served;
   od_fallback<M>(S, o, o.start, stg, table, sh, need, ir, ii, it);
-  pf_node0<M>(v0r, v0i, S.w, ir, ii);
+  v0r = v0i = 0.0;
+  if (!blk_fast) pf_node0<M>(v0r, v0i, S.w, ir, ii);
   if (served && o.resp_v_row == 0) {                 // the node record's row
     v0r = vf.x;
     v0i = vf.y;
   }
-  const double v0 = sqrt(fma(v0i, v0i, v0r * v0r));
+  double m2_0 = fma(v0i, v0i, v0r * v0r);
+  if (o.resp_q) {                                    // (uniform) the row records' row 0
+    const int q0 = od_q_slot(o, 0);
+    if (served && q0 >= 0) m2_0 = od_q_m2(o, rec, q0, tq);
+  }
+  const double v0 = sqrt(m2_0);
   const double vf2 = fma(vf.y, vf.y, vf.x * vf.x);
   if (valid && t.U_out) {
 #pragma unroll
@@ -2038,11 +2137,13 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     }
   }
   double vmn = v0, vmx = v0;      // Python min()/max() over the rows in order
-  const double* srow = rows_lds ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
+  const double* srow = (rows_lds && !blk_fast) ? od_rows_put<M>(sh, a.n_out, rv) : nullptr;
   if (v_out || !rows_lds) {
     const double vfm = sqrt(vf2);
     pf_rows_out<M>(t, rows_lds, srow, a.n_out, ir, ii, [&](int ro, double v) {
       v = (served && ro == o.resp_v_row) ? vfm : v;
+      const int qs = od_q_slot(o, ro);
+      if (served && qs >= 0) v = sqrt(od_q_m2(o, rec, qs, tq));
       if (valid && v_out) v_out[(int64_t)ro * n + e] = (IO)v;
       vmn = (v < vmn) ? v : vmn;
       vmx = (v > vmx) ? v : vmx;
@@ -2050,18 +2151,31 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   } else {
     // extrema only: min / max of |V|^2 over the rows, one sqrt each at the end
     // (as k_pf_solve: sqrt is monotone and correctly rounded)
-    double mn2 = fma(v0i, v0i, v0r * v0r), mx2 = mn2;
+    double mn2 = m2_0, mx2 = mn2;
     auto ext = [&](int ro, double m2) {
       m2 = (served && ro == o.resp_v_row) ? vf2 : m2;
+      const int qs = od_q_slot(o, ro);
+      if (served && qs >= 0) m2 = od_q_m2(o, rec, qs, tq);
       mn2 = (m2 < mn2) ? m2 : mn2;
       mx2 = (m2 > mx2) ? m2 : mx2;
     };
-    // only the rows that can hold a served env's extremum (pgw_pf_od.resp_rows),
-    // unless an env of this wave was solved in full
-    if (rows_lds && o.resp_rows != 0 && __ballot(valid && !served) == 0ull)
-      pf_rows_mask2<M>(srow, a.n_out, o.resp_rows | (o.resp_v_row > 0 ? 1ull << o.resp_v_row : 0ull), ir, ii, ext);
-    else
+    const uint64_t cand = o.resp_rows | (o.resp_v_row > 0 ? 1ull << o.resp_v_row : 0ull);
+    if (blk_fast) {
+      // the candidate rows in order from the row records (and the node record),
+      // the values the masked DPP path below gives them
+      uint64_t m = a.n_out < 64 ? cand & ((1ull << a.n_out) - 1ull) & ~1ull : cand & ~1ull;
+      while (m) {                                    // (uniform)
+        const int ro = __builtin_ctzll(m);
+        m &= m - 1;
+        ext(ro, 0.0);
+      }
+    } else if (rows_lds && o.resp_rows != 0 && __ballot(valid && !served) == 0ull) {
+      // only the rows that can hold a served env's extremum (pgw_pf_od.resp_rows),
+      // unless an env of this wave was solved in full
+      pf_rows_mask2<M>(srow, a.n_out, cand, ir, ii, ext);
+    } else {
       pf_rows_out<M, false>(t, rows_lds, srow, a.n_out, ir, ii, ext);
+    }
     vmn = sqrt(mn2);
     vmx = sqrt(mx2);
   }

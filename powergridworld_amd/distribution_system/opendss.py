@@ -304,6 +304,9 @@ class OpenDSSSolver(PowerFlowSolver):
         self.od_node_records = True          # False: every solve reads the node's row from the currents
         self.od_row_masks = True             # pgw_pf_od.resp_rows (False: every row, for A/Bs and tests)
         self.od_certify = True               # certify every piece (od_certify; False: probes only, for A/Bs)
+        self.od_row_records = True           # pgw_pf_od.resp_q (False: the rows from the currents, for A/Bs)
+        self._od_qrec = None                 # row records [table row, record, OD_QSTRIDE]
+        self._od_qinfo = {}                  # (table row, configuration) -> (row bits, k) or None
         self.od_resp_stats, self.od_resp_brackets = {}, {}
         self._od_index = {}
         self._od_keep = {}
@@ -455,6 +458,56 @@ class OpenDSSSolver(PowerFlowSolver):
                 mask = sum(1 << r for r in range(1, len(names)) if cand[r]) if cand is not None else 0
         self._od_rowmask[key] = mask
         return mask
+
+    OD_QROWS = 12                 # row records: listed output rows per record at most
+    OD_QSTRIDE = 6 + 5 * 12       # doubles per row record (PGW_OD_REC_HEAD + 5 per row)
+
+    def _od_qrows(self, idx):
+        """pgw_pf_od.resp_q of table row idx for the present output rows: the
+        rows that can hold a served env's extremum (_od_row_mask's candidates)
+        and row 0, the node records' row excepted, each as |V_r(t)|^2 = a0 + t
+        (a1 + t (a2 + t (a3 + t a4))) per record -- V_r(t) = A + t (B + t C),
+        V0 + G J'(t) composed (the node records' composition), expanded in
+        fp64.  Written into the row's slice of the row-record buffer with the
+        response records' headers copied bitwise.  Returns (row bits, k) or None
+        (no mask, more than OD_QROWS rows, no response table).  Cached per
+        (row, configuration)."""
+        key = (idx, self._cfg_version)
+        if key in self._od_qinfo:
+            return self._od_qinfo[key]
+        info = None
+        mask = self._od_row_mask(idx)
+        names = list(self.output_names)
+        if mask and self._od_resp is not None:
+            vnode = self._od_vnode()
+            vrow = -1
+            if self._od_vresp is not None and vnode is not None and self.od_node_records:
+                nm = self.feeder.node_names[vnode]
+                vrow = names.index(nm) if nm in names else -1
+            rows = [r for r in [0] + [r for r in range(1, min(len(names), 64)) if (mask >> r) & 1] if r != vrow]
+            if 0 < len(rows) <= self.OD_QROWS:
+                f, M, dev = self.feeder, self.M, self.device
+                R = _lib.od_rec(M)
+                recs = self._od_resp[idx]                                              # [rec_n, R]
+                if self._od_qrec is None:
+                    self._od_qrec = torch.zeros((self.OD_MAX_TABLES, recs.shape[0], self.OD_QSTRIDE),
+                                                dtype=torch.float64, device=dev)
+                nodes = [f.node_index[names[r]] for r in rows]
+                G = torch.from_numpy(np.ascontiguousarray(self._od_Gall[nodes][:, :M])).to(dev)
+                V0 = torch.from_numpy(np.ascontiguousarray(self._od_V0all[nodes])).to(dev)
+                c = torch.view_as_complex(recs[:, 6:6 + 6 * M].reshape(-1, 3, M, 2).contiguous())
+                abc = torch.einsum("pqm,rm->pqr", c, G)                                 # [rec_n, 3, rows]
+                A, B, C = abc[:, 0] + V0, abc[:, 1], abc[:, 2]
+                re = lambda x, y: x.real * y.real + x.imag * y.imag                    # Re(x conj(y))
+                q = torch.stack([re(A, A), 2.0 * re(A, B), re(B, B) + 2.0 * re(A, C), 2.0 * re(B, C), re(C, C)],
+                                -1)                                                     # [rec_n, rows, 5]
+                out = self._od_qrec[idx]
+                out.zero_()
+                out.view(torch.int64)[:, :6] = recs.view(torch.int64)[:, :6]
+                out[:, 6:6 + 5 * len(rows)] = q.reshape(recs.shape[0], -1)
+                info = (sum(1 << r for r in rows), len(rows))
+        self._od_qinfo[key] = info
+        return info
 
     def _od_response(self, hours, idx0):
         """Build and upload the response tables of `hours` (rows idx0.. of the
@@ -676,7 +729,10 @@ class OpenDSSSolver(PowerFlowSolver):
         for q in range(H):
             for k in [k for k in self._od_rowmask if k[0] == idx0 + q]:
                 del self._od_rowmask[k]
+            for k in [k for k in self._od_qinfo if k[0] == idx0 + q]:
+                del self._od_qinfo[k]
             self._od_row_mask(idx0 + q)
+            self._od_qrows(idx0 + q)
         # the brackets per table row (kW intervals the tables leave to the solve;
         # an hour's row: _od_index[_hour_key(hour)]), for tests and diagnostics
         for q, hr in enumerate(hours):
@@ -719,6 +775,10 @@ class OpenDSSSolver(PowerFlowSolver):
                 if name in self.output_names:
                     od.resp_v = self._od_vresp[idx].data_ptr()
                     od.resp_v_row = self.output_names.index(name)
+            qi = self._od_qrows(idx) if self.od_row_records else None
+            if qi is not None:
+                od.resp_q, od.resp_q_rows, od.resp_q_k = self._od_qrec[idx].data_ptr(), qi[0], qi[1]
+                od.resp_q_stride = self.OD_QSTRIDE
         t = _lib.PFTables.from_buffer_copy(self.tables)
         t.od = _lib.C.addressof(od)
         t._od_ref = od                     # the struct lives as long as these tables

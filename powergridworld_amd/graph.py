@@ -399,6 +399,14 @@ class CoordStepGraph:
         self._pos[key] = (g, launches, acts)          # (the launches' structs live as long as the graph)
         return g
 
+    def release(self):
+        """Destroy the captured graphs now (a graph's destruction can wait for the
+        device: do it here, not inside someone's timed region at garbage
+        collection)."""
+        for g in self._pos.values():
+            g[0]._release()
+        self._pos.clear()
+
     def __call__(self):
         env = self.env
         F = env._fused

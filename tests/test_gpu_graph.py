@@ -278,9 +278,14 @@ def test_c4_graph8_equals_eager_across_episodes(conv):
         return [env.packed_obs().clone(), torch.stack([r[a.name] for a in env.agents]).clone(),
                 env.pf_solver.get_bus_voltage_by_name("675c").clone(), env.pf_solver.iterations.clone(),
                 torch.tensor(float(d["__all__"]))]
+    rng = np.random.default_rng(5)
     for ep in range(2):
-        eager.reset()
-        cap.reset()
+        init = torch.tensor(rng.uniform(5.0, 45.0, size=(5, n)), device=DEV)
+        for env in (eager, cap):                   # the same random initial SoC in both
+            env.reset()
+            for ai, agent in enumerate(env.agents):
+                agent.env_dict["storage"].reset(init_storage=init[ai])
+            env.load_component_state()
         last = cap._episode_last_step()
         assert last is not None and last > S
         k = 0

@@ -144,13 +144,14 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True, dtype=
                 batch=n, agents=1, steps=steps, seconds=dt)
 
 
-def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss", table=True, vrec=True):
+def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss", table=True, vrec=True, qrec=True):
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     env = MultiAgentEnv(**make_env_config(pf_convergence=conv), num_envs=n, device=dev, fused=fused)
     env.pf_solver.od_table = table
     if hasattr(env.pf_solver, "od_node_records"):
         env.pf_solver.od_node_records = vrec
+        env.pf_solver.od_row_records = qrec
     gen = torch.Generator(dev).manual_seed(0)
     acts = []
     for _ in range(pool):
@@ -169,7 +170,7 @@ def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss"
 
     dt = timed_loop(env, step, env.reset, steps, warmup)
     return dict(config=("HET" if fused else "HETG") + ("X" if conv == "exact" else "") + ("" if table else "S")
-                + ("" if vrec else "V"),
+                + ("" if vrec else "V") + ("" if qrec else "Q"),
                 workload="3-agent heterogeneous (MC building, grid-aware PV farm, EV 25x40) + IEEE-13 PF, "
                          + ("fused multi-agent step (pgw_ma_step)" if env._ma is not None else "generic path"),
                 pf_convergence=conv, pf_response_table=bool(table and conv == "opendss"),
@@ -222,6 +223,7 @@ def main():
            "HETX": lambda *a: bench_het(*a, conv="exact"),
            "HETS": lambda *a: bench_het(*a, table=False),
            "HETV": lambda *a: bench_het(*a, vrec=False),
+           "HETQ": lambda *a: bench_het(*a, qrec=False),
            "C2G1": lambda *a: bench_c2(*a, graph=1), "C2G8": lambda *a: bench_c2(*a, graph=8),
            "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8),
            "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),
