@@ -419,7 +419,7 @@ class Feeder:
         return V, iters
 
     def snap_opendss(self, load_kw, load_kvar, yprim_kw=None, yprim_kvar=None,
-                     tol=1e-4, min_iter=2, max_iter=15):
+                     tol=1e-4, min_iter=2, max_iter=15, V_start=None):
         """OpenDSS's own snap solve, restated from its published solution method
         (Solution.pas SolveSnap -> SolveCircuit -> DoPFLOWsolution; the
         reference reaches it through ``Solve mode=snap``, opendss.py:134):
@@ -434,6 +434,12 @@ class Feeder:
         * Converged: max over ALL nodes of | |V_new| - |V_old| | / Vbase_node
           <= tol (default 1e-4), tested after every iteration, accepted only
           from MinIterations (default 2) on; at most MaxIterations (default 15).
+
+        ``V_start`` (K, n) node voltages: start the iteration there instead of
+        at SolveYDirect's solution -- the reading in which a snap solve
+        continues from the circuit's previous solution (OpenDSSSolver
+        snap_start="previous"; the stopping test counts from min_iter either
+        way).
 
         ``yprim_kw/kvar`` are the powers whose Yeq sits in Y.  The Loads.kW /
         Loads.kvar setters (DSS C-API Loads_Set_kW: kWBase, LoadSpecType,
@@ -462,6 +468,8 @@ class Feeder:
             Zf = np.broadcast_to(Z1, (K,) + Z1.shape)
         solve = lambda I: np.einsum("kij,kj->ki", Zf, I)
         V = solve(np.tile(self.I_src, (K, 1)))                                # SolveYDirect
+        if V_start is not None:
+            V = np.array(V_start, dtype=complex).reshape(K, -1)
         vbn = self.kv_ln * 1000.0
         iters = np.zeros(K, int)
         active = np.ones(K, bool)

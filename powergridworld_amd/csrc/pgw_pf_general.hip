@@ -498,8 +498,12 @@ int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t 
                   (p->n_chk >= kGR && p->n_chk <= PGW_PFG_MAX_CHK && p->n_chk % kGR == 0 && t->Gc && t->V0c),
               "pgw_pf_solve_general: OPENDSS needs n_chk check rows (multiple of 8, <= %d) and Gc / V0c",
               PGW_PFG_MAX_CHK);
-  PGW_REQUIRE(p->mode != PGW_PF_OPENDSS || !t->U_init,
-              "pgw_pf_solve_general: OPENDSS starts from the direct solution (no U_init)");
+  // (OPENDSS with U_init: OpenDSSSolver(snap_start="previous") -- each env's snap
+  // solve starts from its previous solution instead of the direct one; the
+  // stopping test counts from min_iter either way, so the check rows' first
+  // magnitudes need no start value)
+  PGW_REQUIRE(p->mode != PGW_PF_OPENDSS || !t->U_init || !p->n_reg,
+              "pgw_pf_solve_general: OPENDSS with U_init and RegControls is not supported");
   PGW_REQUIRE(p->n_out >= 0 && (p->n_out == 0 || (t->G && t->V0)), "pgw_pf_solve_general: missing G / V0");
   PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve_general: bad n_ctrl");
   PGW_REQUIRE(p->max_iter >= 1 && p->min_iter >= 1, "pgw_pf_solve_general: bad iteration limits");

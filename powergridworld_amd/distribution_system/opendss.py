@@ -89,7 +89,8 @@ class OpenDSSSolver(PowerFlowSolver):
     def __init__(self, feeder_file: str, loadshape_file: str, system_load_rescale_factor: float = 1.0,
                  num_envs: int = 1, device=None, tol: float = None, max_iter: int = None,
                  output_nodes=None, predictor: bool = True, warm_start: bool = False,
-                 convergence: str = "opendss", general: bool = None, od_table: bool = True, **kwargs):
+                 convergence: str = "opendss", general: bool = None, od_table: bool = True,
+                 snap_start: str = "direct", **kwargs):
         """convergence: "opendss" (the default) -- OpenDSS's own snap solve as
         the reference runs it (opendss.py:134):
         loads' nominal admittances in Y, start from the direct solution, stop at
@@ -101,10 +102,26 @@ class OpenDSSSolver(PowerFlowSolver):
         RegControls run the general kernel (pgw_pf_solve_general); general=True
         forces it (tests, measurements).  od_table: the fast OpenDSS-rule
         kernels read the hour's response table (pgw_pf_od.resp) and solve only
-        the envs it does not cover; False solves every env."""
+        the envs it does not cover; False solves every env.
+        snap_start (OpenDSS rule): "direct" (the default) -- every snap solve
+        starts from the direct solution, as `Solve mode=snap` re-initialises
+        the solution; "previous" -- each env's solve
+        starts from its previous solution (the other reading of
+        opendss.py:134, which this build cannot confirm without OpenDSS): the
+        general kernel with U_init / U_out over a per-env buffer (the first
+        solve starts from the direct solution); no response table, the
+        generic multi-agent path."""
         super().__init__(**kwargs)
         if convergence not in ("exact", "opendss"):
             raise ValueError("convergence must be 'exact' or 'opendss', got %r" % (convergence,))
+        if snap_start not in ("direct", "previous"):
+            raise ValueError("snap_start must be 'direct' or 'previous', got %r" % (snap_start,))
+        if snap_start == "previous" and convergence != "opendss":
+            raise ValueError("snap_start='previous' is a reading of OpenDSS's snap solve (convergence='opendss'); "
+                             "the exact fixed point has warm_start=True")
+        self.snap_start = snap_start
+        if snap_start == "previous":
+            general, od_table = True, False
         self.convergence = convergence
         self.od_table = bool(od_table)
         self.num_envs = int(num_envs)
@@ -129,9 +146,10 @@ class OpenDSSSolver(PowerFlowSolver):
         if self.feeder.m > _lib.PFG_MAX_M:
             raise ValueError("feeder has %d load phase elements (max %d)" % (self.feeder.m, _lib.PFG_MAX_M))
         if convergence == "opendss":
-            if warm_start:
-                raise ValueError("convergence='opendss' starts every solve from the direct solution "
-                                 "(no warm_start)")
+            if warm_start and snap_start != "previous":
+                raise ValueError("convergence='opendss' starts every solve from the direct solution; "
+                                 "snap_start='previous' starts it from the env's previous solution")
+            warm_start = snap_start == "previous"
             self._fd_iter = Feeder(spec, load_yprim=True)      # OpenDSS's Y (+ loads' Yeq)
             tol = self.OPENDSS_TOL if tol is None else tol
             max_iter = self.OPENDSS_MAX_ITER if max_iter is None else max_iter
@@ -1242,7 +1260,7 @@ class OpenDSSSolver(PowerFlowSolver):
         (one controllable load), else the cold-start tables -- or, with
         warm_start, the ones over each env's previous solution."""
         tables = self.step_tables(current_time) if (controllable or self._od_fast) else self.tables
-        if controllable and self.warm_start and tables is self.tables:
+        if (controllable or self.snap_start == "previous") and self.warm_start and tables is self.tables:
             tables = self._warm_tables()
         return tables
 

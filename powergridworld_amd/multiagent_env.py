@@ -386,6 +386,8 @@ class MultiAgentEnv(Env):
             return "the general power flow (large feeder or convergence='opendss') has no fp32 fused step"
         if getattr(self.pf_solver, "regulators", None) is not None:
             return "RegControl (the control loop runs in OpenDSSSolver.calculate_power_flow)"
+        if getattr(self.pf_solver, "snap_start", "direct") != "direct":
+            return "snap_start='previous' (each env's solve starts from its own previous solution)"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)
@@ -656,6 +658,8 @@ class MultiAgentEnv(Env):
             return "power flow solver is not the batched OpenDSSSolver"
         if getattr(self.pf_solver, "regulators", None) is not None:
             return "RegControl (the control loop runs in OpenDSSSolver.calculate_power_flow)"
+        if getattr(self.pf_solver, "snap_start", "direct") != "direct":
+            return "snap_start='previous' (each env's solve starts from its own previous solution)"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)
