@@ -415,9 +415,15 @@ typedef struct pgw_pf_tables {
  * the grid resp_x0 + j / resp_inv_h (j < resp_nseg) has its first piece at
  * record j, further pieces chained by `next`; an env whose P lies in no piece
  * (a breakpoint's bracket, outside the grid, Q != 0, a piece marked
- * unfittable) runs the snap solve instead, so the table changes no decision:
- * results differ from the solve only by the fit error (checked <= the
- * builder's tolerance at the check points).  Record layout: PGW_OD_REC. */
+ * unfittable) runs the snap solve instead.  Every served interval is
+ * certified (OpenDSSSolver._od_response, od_certify.py): Taylor-model bounds
+ * of the iterates over the whole interval prove each element's band in each
+ * iterate and each stopping test's outcome constant there (margins >= 1e-12,
+ * far above the kernels' rounding), and a piece that cannot be proven whole
+ * serves only its longest certified run ([0] lo / [1] hi narrowed).  So the
+ * table changes no decision: results differ from the solve only by the fit
+ * error (checked <= the builder's tolerance at the check points).  Record
+ * layout: PGW_OD_REC. */
 #define PGW_PF_OD_MAX_ROWS 28
 /* Response-table record of m elements, doubles: [0] lo, [1] hi (kW; the piece
  * covers lo <= P <= hi), [2] xc, [3] inv_hw (t = (P - xc) inv_hw), [4] two

@@ -429,6 +429,12 @@ def test_od_row_records_equal_the_currents_rows():
     envs[1].pf_solver.od_row_records = False
     envs[1].pf_solver._tables_cache.clear()
     for env in envs:
+        # the same vehicles and initial SoCs in every env (unseeded, each
+        # randomize=True component draws its own: the bus loads would differ)
+        for k, ag in enumerate(env.agents):
+            for c in (ag.envs if hasattr(ag, "envs") else [ag]):
+                if hasattr(c, "seed"):
+                    c.seed(70 + k)
         env.reset()
     assert envs[0].pf_solver._od_qinfo and any(v is not None for v in envs[0].pf_solver._od_qinfo.values())
     rng = np.random.default_rng(31)
@@ -446,7 +452,10 @@ def test_od_row_records_equal_the_currents_rows():
         assert torch.equal(i0, i1) and torch.equal(i0, i2)
         assert ((a0 - a1).abs() / a1).max().item() < 1e-12 and ((b0 - b1).abs() / b1).max().item() < 1e-12
         assert ((r0 - r1).abs() / (1e-3 + r1.abs())).max().item() < 1e-9
-        assert torch.equal(a0, a2) and torch.equal(b0, b2) and torch.equal(r0, r2), t
+        for nm, x, y in (("vmin", a0, a2), ("vmax", b0, b2), ("reward", r0, r2)):
+            bad = (x != y).nonzero()
+            assert not len(bad), "step %d %s: %d envs differ, e.g. %s: %r vs %r" % (
+                t, nm, len(bad), bad[:3].tolist(), x[tuple(bad[0])].item(), y[tuple(bad[0])].item())
 
 
 # ------------------------------------------------------------------ fp32 storage (pgw_pf_solve_f32)
