@@ -160,25 +160,40 @@ def f32_variant(conv, n, steps, warmup, pool_size, seed, dev):
     env.reset()
     k = [0]
 
+    host = []
+
     def run(m):
         for _ in range(m):
+            h0 = time.perf_counter()
             _, _, dones, _ = env.step(packed[k[0] % pool_size])
             k[0] += 1
             if dones["__all__"]:
                 env.reset()
+            host.append(time.perf_counter() - h0)
+    # as the headline: one whole episode first (every step's launch state built
+    # once, cached across episodes), then collect, then the warmup steps
     run(warmup)
+    while env.episode_step != 0:
+        run(1)
     gc.collect()
+    gc.freeze()
+    run(warmup)
     torch.cuda.synchronize()
+    del host[:]
     t0 = time.perf_counter()
     run(steps)
+    t_host = time.perf_counter()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    host_us = {"sum": sum(host) * 1e6, "max": max(host) * 1e6, "argmax": host.index(max(host)),
+               "sync_wait": (time.perf_counter() - t_host) * 1e6}
     # kernel durations in a separate pass (every launch event-timed), as the headline's
     tot, cnt = timed_pass(run, 64)
     a_us = tot[0] / cnt[0] * 1e3 if cnt[0] else None
     p_us = tot[1] / cnt[1] * 1e3 if cnt[1] else None
     out = {"dtype": "f32 storage, f64 arithmetic", "value": N_AGENTS * n * steps / dt,
            "unit": "agent-env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+           "host_us": host_us,
            "parity": "tests/test_gpu_f32.py::test_c4_f32_one_step_parity[%s] (one step = fp64 result "
                      "rounded once) and ::test_c4_f32_episode_within_bound[%s] (episode within 1e-3 rel "
                      "of fp64), both on this variant's kernels (pgw_coord_step_f32: %s)"
