@@ -279,6 +279,13 @@ int32_t pgw_ev_reset_tables_f32(const pgw_ev_params* p, int64_t n, const double*
 int32_t pgw_ev_step_f32(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_matf action,
                         const double* endp, float* req, uint64_t* charging, pgw_matf obs,
                         float* real_power, float* reward, void* stream);
+/* Doubles per env row of the env-major requirement layout for n_vehicles. */
+int32_t pgw_ev_row(int32_t n_vehicles);
+/* pgw_ev_step on env-major requirements: req (n x pgw_ev_row(V)), per-env
+ * tables likewise; lanes over vehicles, a wave per 1-4 envs. */
+int32_t pgw_ev_step_lanes(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
+                          const double* endp, double* req, uint64_t* charging, pgw_mat obs,
+                          double* real_power, double* reward, void* stream);
 
 /* ------------------------------------------------------------------------
  * MultiComponentEnv reduction (gridworld/base.py:125-156): real_power and

@@ -327,6 +327,8 @@ _SIGS = {
     "pgw_ev_reset_tables_f32": (i32, [P(EVParams), i64, vp, vp, vp, vp]),
     "pgw_ev_step_f32": (i32, [P(EVParams), P(EVStepInfo), i64, Matf, vp, vp, vp, Matf, vp, vp, vp]),
     "pgw_ev_step": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
+    "pgw_ev_step_lanes": (i32, [P(EVParams), P(EVStepInfo), i64, Mat, vp, vp, vp, Mat, vp, vp, vp]),
+    "pgw_ev_row": (i32, [i32]),
     "pgw_agent_reduce": (i32, [P(ReduceArgs), i64, vp, vp, vp]),
     "pgw_pf_solve": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),
     "pgw_pf_solve_f32": (i32, [P(PFParams), P(PFTables), i64, vp, vp, vp, vp, vp]),

@@ -682,6 +682,131 @@ __global__ void __launch_bounds__(kBlock) k_ev_step(pgw_ev_params p, pgw_ev_step
   (void)ev_step_env(p, s, n, e, act, endp, req, chg, obs, rp, rew);
 }
 
+// ---- lanes over vehicles (env-major requirements) --------------------------
+// req[e * VP + v], VP = LPE * W: an env's vehicles are one contiguous row, and
+// LPE lanes (16, 32 or 64: the smallest power of two >= V up to 64) serve one
+// env, lane j its vehicles j, j + 64, ... (word w: vehicle w * 64 + j).  A
+// wave loads EPW = 64 / LPE env rows per instruction, coalesced, and runs
+// NP env passes with every pass's loads out before any is used: one memory
+// round trip per wave.  Sums: per lane over its words in order from 0, then a
+// butterfly over the env's lanes, partners at distance LPE/2 first (every lane
+// ends with the same value); counts and the charging bits from ballots.
+template <int LPE>
+__device__ __forceinline__ double ev_lanes_sum(double x) {
+#pragma unroll
+  for (int m = LPE / 2; m >= 1; m >>= 1) x = x + __shfl_xor(x, m);
+  return x;
+}
+template <int LPE>
+__device__ __forceinline__ uint64_t ev_lanes_bits(uint64_t ballot, int sub) {
+  if constexpr (LPE == 64) return ballot;
+  else return (ballot >> (sub * LPE)) & ((1ull << LPE) - 1ull);
+}
+constexpr int ev_lanes_passes(int W) { return W >= 8 ? 1 : 8 / W; }
+template <int LPE, int W, int MODE, class S, class Mt>
+__global__ void __launch_bounds__(kBlock) k_ev_lanes(pgw_ev_params p, pgw_ev_step_info s, int64_t n, Mt act,
+                                                     const double* __restrict__ endp, S* __restrict__ req,
+                                                     uint64_t* __restrict__ chg, Mt obs, S* __restrict__ rp,
+                                                     S* __restrict__ rew) {
+  static_assert(LPE == 64 || W == 1, "fewer lanes than a wave per env: one word");
+  constexpr int EPW = 64 / LPE, VP = LPE * W, NP = ev_lanes_passes(W);
+  const int lane = threadIdx.x & 63, sub = lane / LPE, j = lane % LPE;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t e0 = wave * (NP * EPW);
+  // the vehicles' shared data (the same in every pass): time left and its
+  // reciprocal, scanned and parked bits
+  double tl[W], rc[W];
+  bool inw[W], win[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const int v = w * 64 + j, b = v & 63;
+    inw[w] = v < p.n_vehicles && ((s.scan[w] >> b) & 1ull);
+    win[w] = (s.window[w] >> b) & 1ull;
+    tl[w] = rc[w] = 0.0;
+    if constexpr (MODE == kEvTable) {
+      if (inw[w]) {
+        const double2 q = reinterpret_cast<const double2*>(s.tl_rcp)[v];
+        tl[w] = q.x;
+        rc[w] = q.y;
+      }
+    } else if constexpr (MODE == kEvDivide) {
+      if (inw[w]) tl[w] = (endp[v] - s.time) / 60.0;
+    }
+  }
+  // every pass's loads before any use
+  double r[NP][W], a[NP], tlp[NP][W];               // (tlp: kEvPerEnv's time left, per env)
+  uint64_t prev[NP][W];
+  bool pw[NP][W];                                    // (kEvPerEnv: parked, per env)
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int64_t e = e0 + i * EPW + sub;
+    const bool ok = e < n;
+    a[i] = ok ? ev_act(s, e, act) : 0.0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int v = w * 64 + j;
+      const bool in = ok && inw[w];
+      r[i][w] = in ? (double)req[e * VP + v] : 0.0;
+      prev[i][w] = ok ? chg[(int64_t)w * n + e] : 0ull;
+      pw[i][w] = win[w];
+      tlp[i][w] = tl[w];
+      if constexpr (MODE == kEvPerEnv) {
+        if (in) {
+          const double en = s.env_endp[e * VP + v];
+          pw[i][w] = (s.time >= s.env_start[e * VP + v]) && (s.time <= floor(en));
+          tlp[i][w] = (en - s.time) / 60.0;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int64_t e = e0 + i * EPW + sub;
+    const bool ok = e < n;
+    const double kwh = ev_kwh_of(p, a[i]);
+    double demand = 0.0, consumed = 0.0, dsum = 0.0, unserved = 0.0;
+    int nact = 0, dcnt = 0;
+    uint64_t now[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int v = w * 64 + j, b = v & 63;
+      const bool in = ok && inw[w];
+      const double rr = r[i][w];
+      const double tlv = tlp[i][w];
+      const bool act_v = in && pw[i][w] && (rr > 0.0);
+      const bool chg_v = act_v && (tlv > 0.0);
+      const bool dep_v = in && !act_v && ((prev[i][w] >> b) & 1ull);
+      double df;
+      if constexpr (MODE == kEvTable) df = pymax(0.0, p.rate - exact_div(rr, tlv, rc[w]));
+      else df = pymax(0.0, p.rate - rr / tlv);
+      const double cv = pymin(kwh, rr);
+      if (chg_v) req[e * VP + v] = (S)(rr - cv);
+      demand = act_v ? demand + rr : demand;
+      consumed = chg_v ? consumed + cv : consumed;
+      dsum = chg_v ? dsum + df : dsum;
+      unserved = dep_v ? unserved + rr : unserved;
+      const uint64_t ba = ev_lanes_bits<LPE>(__ballot(act_v), sub);
+      const uint64_t bc = ev_lanes_bits<LPE>(__ballot(chg_v), sub);
+      now[w] = ba;
+      nact += __builtin_popcountll(ba);
+      dcnt += __builtin_popcountll(bc);
+    }
+    EvSums t;
+    t.demand = ev_lanes_sum<LPE>(demand);
+    t.consumed = ev_lanes_sum<LPE>(consumed);
+    t.dsum = ev_lanes_sum<LPE>(dsum);
+    t.unserved = ev_lanes_sum<LPE>(unserved);
+    t.nact = nact;
+    t.dcnt = dcnt;
+    if (ok && j == 0) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) chg[(int64_t)w * n + e] = now[w];
+      ev_note(p, a[i]);
+      (void)ev_finish(p, s, e, t, obs, rp, rew);
+    }
+  }
+}
+
 // ====================================================================== fused MC step
 // One component of an MC agent for env e; writes its real power (and its
 // reward where it has one) to the component's own buffers.
@@ -1274,6 +1399,52 @@ int32_t pgw_ev_step_f32(const pgw_ev_params* p, const pgw_ev_step_info* s, int64
               "pgw_ev_step_f32: per-env tables need env_start and env_endp, and no tl_rcp");
   PGW_LAUNCH((k_ev_step<float, pgw_matf>), n, stream, *p, *s, n, action, endp, req, charging, obs, real_power,
              reward);
+}
+
+int32_t pgw_ev_row(int32_t n_vehicles) {
+  if (n_vehicles <= 16) return 16;
+  if (n_vehicles <= 32) return 32;
+  int w = 1;
+  while (64 * w < n_vehicles) w *= 2;
+  return 64 * w;
+}
+
+int32_t pgw_ev_step_lanes(const pgw_ev_params* p, const pgw_ev_step_info* s, int64_t n, pgw_mat action,
+                          const double* endp, double* req, uint64_t* charging, pgw_mat obs,
+                          double* real_power, double* reward, void* stream) {
+  PGW_REQUIRE(p && s && endp && req && charging && obs.ptr && real_power && reward && n >= 0,
+              "pgw_ev_step_lanes: null argument");
+  PGW_REQUIRE(s->n_words == (p->n_vehicles + 63) / 64 && s->n_words <= PGW_EV_MAX_WORDS,
+              "pgw_ev_step_lanes: n_words does not match n_vehicles");
+  PGW_REQUIRE(!s->env_start == !s->env_endp && (!s->env_start || !s->tl_rcp),
+              "pgw_ev_step_lanes: per-env tables need env_start and env_endp, and no tl_rcp");
+  if (n == 0) return PGW_OK;
+  const int row = pgw_ev_row(p->n_vehicles);
+  const int lpe = row < 64 ? row : 64, W = row / 64 > 0 ? row / 64 : 1;
+  const int mode = s->env_start ? kEvPerEnv : s->tl_rcp ? kEvTable : kEvDivide;
+  const int64_t per_wave = (int64_t)ev_lanes_passes(W) * (64 / lpe);
+  const int64_t waves = (n + per_wave - 1) / per_wave;
+  const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
+  hipStream_t st = (hipStream_t)stream;
+#define PGW_EV_LANES(L, WW, M)                                                                             \
+  hipLaunchKernelGGL((k_ev_lanes<L, WW, M, double, pgw_mat>), grid, block, 0, st, *p, *s, n, action, endp, req, \
+                     charging, obs, real_power, reward)
+#define PGW_EV_LANES_M(L, WW)                           \
+  do {                                                  \
+    if (mode == kEvTable) PGW_EV_LANES(L, WW, kEvTable);  \
+    else if (mode == kEvPerEnv) PGW_EV_LANES(L, WW, kEvPerEnv); \
+    else PGW_EV_LANES(L, WW, kEvDivide);                 \
+  } while (0)
+  if (lpe == 16) PGW_EV_LANES_M(16, 1);
+  else if (lpe == 32) PGW_EV_LANES_M(32, 1);
+  else if (W == 1) PGW_EV_LANES_M(64, 1);
+  else if (W == 2) PGW_EV_LANES_M(64, 2);
+  else if (W == 4) PGW_EV_LANES_M(64, 4);
+  else if (W == 8) PGW_EV_LANES_M(64, 8);
+  else PGW_EV_LANES_M(64, 16);
+#undef PGW_EV_LANES_M
+#undef PGW_EV_LANES
+  return check_launch("k_ev_lanes");
 }
 
 int32_t pgw_debug_mc_trace(long long* buf) {
