@@ -1656,9 +1656,18 @@ __device__ __forceinline__ double od_q_m2(const ODArgs& o, int rec, int slot, do
   const double* q = o.resp_q + (int64_t)rec * o.resp_q_stride + PGW_OD_REC_HEAD + 5 * slot;
   return fma(t, fma(t, fma(t, fma(t, q[4], q[3]), q[2]), q[1]), q[0]);
 }
+// A record's candidate slots: header word 5 of its row record, the slots the
+// host proved can hold the extremum of an env the record serves
+// (OpenDSSSolver._od_qrows; 0: every slot).
+__device__ __forceinline__ uint64_t od_q_cand(double h5) {
+  const uint64_t m = (uint64_t)__double_as_longlong(h5);
+  return m ? m : ~0ull;
+}
 // The piece of P (Q = 0) from the row records' headers alone (the chain of
-// od_resp_lookup, same decisions): record index, t and the count.
-__device__ __forceinline__ bool od_q_find(const ODArgs& o, double P, double Q, int& it, int& rec, double& tq) {
+// od_resp_lookup, same decisions): record index, t, the count and the
+// record's candidate slots.
+__device__ __forceinline__ bool od_q_find(const ODArgs& o, double P, double Q, int& it, int& rec, double& tq,
+                                          uint64_t& qm) {
   const double g = (P - o.resp_x0) * o.resp_inv_h;
   if (!(Q == 0.0) || !(g >= 0.0 && g < (double)o.resp_nseg)) return false;
   int r = (int)g;
@@ -1672,6 +1681,7 @@ __device__ __forceinline__ bool od_q_find(const ODArgs& o, double P, double Q, i
       it = k_it;
       rec = r;
       tq = (P - h1.x) * h1.y;
+      qm = od_q_cand(h2.y);
       return true;
     }
     if (next < 0) return false;
@@ -2097,6 +2107,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   double2 vf = make_double2(0.0, 0.0);
   int rec = 0;
   double tq = 0.0;
+  uint64_t qm = ~0ull;                               // the record's candidate slots (od_q_cand)
   // extrema only with row records covering every candidate row (and row 0):
   // a block the table serves entirely reads the row records' headers and
   // quartics alone -- no currents, no node-0 or row DPP groups, no row staging
@@ -2104,7 +2115,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
                      (od_q_slot(o, 0) >= 0 || o.resp_v_row == 0);        // (uniform)
   bool served, blk_fast = false;
   if (qfast) {
-    served = valid && od_q_find(o, S.pc, S.qc, it, rec, tq);
+    served = valid && od_q_find(o, S.pc, S.qc, it, rec, tq, qm);
     if (served && o.resp_v) {
       const double2* vr = reinterpret_cast<const double2*>(o.resp_v) + (int64_t)rec * (PGW_OD_VREC / 2);
       vf = od_rec_j(vr[3], vr[4], vr[5], tq);
@@ -2113,6 +2124,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     if (!blk_fast && served) od_resp_at<M>(o, rec, tq, ir, ii, vf);
   } else {
     served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf, rec, tq);
+    if (served && o.resp_q) qm = od_q_cand(o.resp_q[(int64_t)rec * o.resp_q_stride + 5]);
   }
   const bool need = valid && !served;
   od_fallback<M>(S, o, o.start, stg, table, sh, need, ir, ii, it);
@@ -2155,7 +2167,10 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
     auto ext = [&](int ro, double m2) {
       m2 = (served && ro == o.resp_v_row) ? vf2 : m2;
       const int qs = od_q_slot(o, ro);
-      if (served && qs >= 0) m2 = od_q_m2(o, rec, qs, tq);
+      if (served && qs >= 0) {
+        if (!((qm >> qs) & 1ull)) return;            // not this record's candidate: never its extremum
+        m2 = od_q_m2(o, rec, qs, tq);
+      }
       mn2 = (m2 < mn2) ? m2 : mn2;
       mx2 = (m2 > mx2) ? m2 : mx2;
     };

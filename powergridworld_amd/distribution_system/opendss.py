@@ -48,14 +48,10 @@ def get_hour_of_year(dt):
     return int((dt - beginning_of_year).total_seconds() // 3600)
 
 
-def extrema_candidates(A, B, C, tl, th, samples=9, delta=1e-9):
-    """Rows that can hold the minimum or the maximum |V| over t in [tl, th] of
-    some piece: A, B, C [pieces, rows] complex (V_r(t) = A + t (B + t C)), tl /
-    th [pieces].  Per piece, |V_r|^2 is bounded by `samples` equally spaced
-    values plus a Lipschitz margin (|d|V|^2/dt| <= 2 |V| |V'|) plus `delta`; a
-    row is a candidate when its lower bound reaches every row's upper bound or
-    its upper bound every row's lower bound.  Returns a bool array [rows], or
-    None when a bound is not finite (then every row is kept)."""
+def _extrema_bounds(A, B, C, tl, th, samples=9, delta=1e-9):
+    """Per piece and row, bounds (lo, hi) [pieces, rows] of |V_r(t)|^2 over t
+    in [tl, th] (V_r(t) = A + t (B + t C)): `samples` equally spaced values
+    plus a Lipschitz margin (|d|V|^2/dt| <= 2 |V| |V'|) plus `delta`."""
     S = samples
     ts = (tl[:, None] + (th - tl)[:, None] * torch.linspace(0.0, 1.0, S, dtype=torch.float64,
                                                               device=A.device)[None, :])[:, :, None]
@@ -64,11 +60,34 @@ def extrema_candidates(A, B, C, tl, th, samples=9, delta=1e-9):
     T = torch.maximum(tl.abs(), th.abs())[:, None]
     L = 2.0 * (A.abs() + B.abs() * T + C.abs() * T * T) * (B.abs() + 2.0 * C.abs() * T)
     marg = L * ((th - tl)[:, None] / (S - 1)) * 0.5 + delta
-    lo, hi = m2.min(1).values - marg, m2.max(1).values + marg
+    return m2.min(1).values - marg, m2.max(1).values + marg
+
+
+def extrema_candidates(A, B, C, tl, th, samples=9, delta=1e-9):
+    """Rows that can hold the minimum or the maximum |V| over t in [tl, th] of
+    some piece: A, B, C [pieces, rows] complex (V_r(t) = A + t (B + t C)), tl /
+    th [pieces].  Per piece, |V_r|^2 is bounded as _extrema_bounds does; a
+    row is a candidate when its lower bound reaches every row's upper bound or
+    its upper bound every row's lower bound.  Returns a bool array [rows], or
+    None when a bound is not finite (then every row is kept)."""
+    lo, hi = _extrema_bounds(A, B, C, tl, th, samples, delta)
     if not (torch.isfinite(lo).all() and torch.isfinite(hi).all()):
         return None
     cand = ((lo <= hi.min(1, keepdim=True).values) | (hi >= lo.max(1, keepdim=True).values)).any(0)
     return cand.cpu().numpy()
+
+
+def extrema_candidates_per_piece(A, B, C, tl, th, samples=9, delta=1e-9):
+    """extrema_candidates for each piece on its own: [pieces, rows] bool, the
+    rows that can hold that piece's minimum or maximum |V| (every row of a
+    piece whose bounds are not finite).  Comparing fewer rows only adds
+    candidates, so a row set that holds every row the extremum can come from
+    (the table's candidates) is enough."""
+    lo, hi = _extrema_bounds(A, B, C, tl, th, samples, delta)
+    fin = torch.isfinite(lo).all(1) & torch.isfinite(hi).all(1)
+    cand = (lo <= hi.min(1, keepdim=True).values) | (hi >= lo.max(1, keepdim=True).values)
+    cand[~fin] = True
+    return cand
 
 
 class OpenDSSSolver(PowerFlowSolver):
@@ -321,6 +340,7 @@ class OpenDSSSolver(PowerFlowSolver):
         self._od_rowmask = {}                # pgw_pf_od.resp_rows per (table row, configuration)
         self.od_node_records = True          # False: every solve reads the node's row from the currents
         self.od_row_masks = True             # pgw_pf_od.resp_rows (False: every row, for A/Bs and tests)
+        self.od_record_rows = True           # row records' per-record candidate slots (False: every slot)
         self.od_certify = True               # certify every piece (od_certify; False: probes only, for A/Bs)
         self.od_row_records = True           # pgw_pf_od.resp_q (False: the rows from the currents, for A/Bs)
         self._od_qrec = None                 # row records [table row, record, OD_QSTRIDE]
@@ -523,6 +543,24 @@ class OpenDSSSolver(PowerFlowSolver):
                 out.zero_()
                 out.view(torch.int64)[:, :6] = recs.view(torch.int64)[:, :6]
                 out[:, 6:6 + 5 * len(rows)] = q.reshape(recs.shape[0], -1)
+                # header word 5 (unused by the response records): per record, the
+                # slots that can hold its own served envs' extremum -- the rows
+                # compared are the listed ones and the node records' row
+                if self.od_record_rows:
+                    if vrow > 0:
+                        gv = f.node_index[names[vrow]]
+                        Gv = torch.from_numpy(np.ascontiguousarray(self._od_Gall[[gv]][:, :M])).to(dev)
+                        V0v = torch.from_numpy(np.ascontiguousarray(self._od_V0all[[gv]])).to(dev)
+                        av = torch.einsum("pqm,rm->pqr", c, Gv)
+                        A, B, C = torch.cat([A, av[:, 0] + V0v], 1), torch.cat([B, av[:, 1]], 1), \
+                            torch.cat([C, av[:, 2]], 1)
+                    tl, th = (recs[:, 0] - recs[:, 2]) * recs[:, 3], (recs[:, 1] - recs[:, 2]) * recs[:, 3]
+                    cand = extrema_candidates_per_piece(A, B, C, tl, th)[:, :len(rows)]
+                    bits = (cand.to(torch.int64) << torch.arange(len(rows), device=dev)[None, :]).sum(1)
+                    out.view(torch.int64)[:, 5] = bits
+                    st_ = self.od_resp_stats
+                    st_["record_rows_listed"] = st_.get("record_rows_listed", 0) + int(cand.shape[0]) * len(rows)
+                    st_["record_rows_candidates"] = st_.get("record_rows_candidates", 0) + int(cand.sum())
                 info = (sum(1 << r for r in rows), len(rows))
         self._od_qinfo[key] = info
         return info

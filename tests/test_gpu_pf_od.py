@@ -421,13 +421,19 @@ def test_od_row_records_equal_the_currents_rows():
     (od_row_records=False): the same iteration counts, the voltage extrema and
     the PV farm's min_voltage observation within 1e-12 rel, the rewards within
     1e-9 rel, over 30 steps at 8 192 envs; and the generic path equals the
-    fused one bit for bit with the row records on."""
+    fused one bit for bit with the row records on, as does the fused step
+    without the per-record candidate slots (od_record_rows=False: every listed
+    row of a served env evaluated)."""
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     n = 8192
-    envs = [MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=f) for f in (True, True, False)]
+    envs = [MultiAgentEnv(**make_env_config(), num_envs=n, device=DEV, fused=f)
+            for f in (True, True, False, True)]
     envs[1].pf_solver.od_row_records = False
     envs[1].pf_solver._tables_cache.clear()
+    envs[3].pf_solver.od_record_rows = False
+    envs[3].pf_solver._tables_cache.clear()
+    envs[3].pf_solver._od_qinfo.clear()
     for env in envs:
         # the same vehicles and initial SoCs in every env (unseeded, each
         # randomize=True component draws its own: the bus loads would differ)
@@ -437,6 +443,8 @@ def test_od_row_records_equal_the_currents_rows():
                     c.seed(70 + k)
         env.reset()
     assert envs[0].pf_solver._od_qinfo and any(v is not None for v in envs[0].pf_solver._od_qinfo.values())
+    st0 = envs[0].pf_solver.od_resp_stats
+    assert 0 < st0["record_rows_candidates"] < st0["record_rows_listed"], st0
     rng = np.random.default_rng(31)
     for t in range(30):
         a = torch.tensor(rng.uniform(-1.1, 1.1, (n, 10)), device=DEV)
@@ -448,8 +456,9 @@ def test_od_row_records_equal_the_currents_rows():
             vmin, vmax = env.pf_solver.voltage_extrema()
             outs.append((vmin.clone(), vmax.clone(), env.pf_solver.iterations.clone(),
                          torch.stack([r[k] for k in sorted(r)]).clone()))
-        (a0, b0, i0, r0), (a1, b1, i1, r1), (a2, b2, i2, r2) = outs
-        assert torch.equal(i0, i1) and torch.equal(i0, i2)
+        (a0, b0, i0, r0), (a1, b1, i1, r1), (a2, b2, i2, r2), (a3, b3, i3, r3) = outs
+        assert torch.equal(i0, i1) and torch.equal(i0, i2) and torch.equal(i0, i3)
+        assert torch.equal(a0, a3) and torch.equal(b0, b3) and torch.equal(r0, r3)
         assert ((a0 - a1).abs() / a1).max().item() < 1e-12 and ((b0 - b1).abs() / b1).max().item() < 1e-12
         assert ((r0 - r1).abs() / (1e-3 + r1.abs())).max().item() < 1e-9
         for nm, x, y in (("vmin", a0, a2), ("vmax", b0, b2), ("reward", r0, r2)):

@@ -144,7 +144,8 @@ def bench_c3(dev, steps, warmup, n=16384, pool=16, graph=0, clocked=True, dtype=
                 batch=n, agents=1, steps=steps, seconds=dt)
 
 
-def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss", table=True, vrec=True, qrec=True):
+def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss", table=True, vrec=True, qrec=True,
+              rrows=True):
     from powergridworld_amd.scenarios.heterogeneous import make_env_config
     from powergridworld_amd.multiagent_env import MultiAgentEnv
     env = MultiAgentEnv(**make_env_config(pf_convergence=conv), num_envs=n, device=dev, fused=fused)
@@ -152,6 +153,9 @@ def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss"
     if hasattr(env.pf_solver, "od_node_records"):
         env.pf_solver.od_node_records = vrec
         env.pf_solver.od_row_records = qrec
+        env.pf_solver.od_record_rows = rrows
+        env.pf_solver._tables_cache.clear()
+        env.pf_solver._od_qinfo.clear()
     gen = torch.Generator(dev).manual_seed(0)
     acts = []
     for _ in range(pool):
@@ -170,7 +174,7 @@ def bench_het(dev, steps, warmup, n=65536, pool=16, fused="auto", conv="opendss"
 
     dt = timed_loop(env, step, env.reset, steps, warmup)
     return dict(config=("HET" if fused else "HETG") + ("X" if conv == "exact" else "") + ("" if table else "S")
-                + ("" if vrec else "V") + ("" if qrec else "Q"),
+                + ("" if vrec else "V") + ("" if qrec else "Q") + ("" if rrows else "R"),
                 workload="3-agent heterogeneous (MC building, grid-aware PV farm, EV 25x40) + IEEE-13 PF, "
                          + ("fused multi-agent step (pgw_ma_step)" if env._ma is not None else "generic path"),
                 pf_convergence=conv, pf_response_table=bool(table and conv == "opendss"),
@@ -224,6 +228,7 @@ def main():
            "HETS": lambda *a: bench_het(*a, table=False),
            "HETV": lambda *a: bench_het(*a, vrec=False),
            "HETQ": lambda *a: bench_het(*a, qrec=False),
+           "HETR": lambda *a: bench_het(*a, rrows=False),
            "C2G1": lambda *a: bench_c2(*a, graph=1), "C2G8": lambda *a: bench_c2(*a, graph=8),
            "C3G1": lambda *a: bench_c3(*a, graph=1), "C3G8": lambda *a: bench_c3(*a, graph=8),
            "C3P1": lambda *a: bench_c3(*a, graph=1, clocked=False),

@@ -22,12 +22,14 @@ P = torch.linspace(-900.0, 300.0, n, dtype=torch.float64, device=DEV)
 P[:4096] = -283.422709126 + torch.linspace(-0.05, 0.05, 4096, dtype=torch.float64, device=DEV)
 
 
-def solver(rec, masks):
+def solver(rec, masks, recrows=True):
     s = OpenDSSSolver(**dict(cfg["pf_config"]["config"]), num_envs=n, device=DEV)
     s.set_controllable_loads(ctrl)
     s.od_row_records = rec
     s.od_row_masks = masks
+    s.od_record_rows = recrows
     s._tables_cache.clear()
+    s._od_qinfo.clear()
     return s
 
 
@@ -48,12 +50,17 @@ V = full.v_out[:len(full.output_names)].clone()
 vmin_f, vmax_f = V.min(0).values, V.max(0).values
 rowmin = V.argmin(0)
 print("hour", full.hour_of(TIME), "rows", len(full.output_names))
-for name, (rec, masks) in {"q": (True, True), "noq": (False, True), "nomask": (False, False)}.items():
-    s = solver(rec, masks)
+res = {}
+for name, (rec, masks, rr) in {"q": (True, True, True), "q-all-slots": (True, True, False),
+                               "noq": (False, True, True), "nomask": (False, False, True)}.items():
+    s = solver(rec, masks, rr)
     a, b, it = extrema(s)
+    res[name] = (a, b)
     idx = s._od_index.get(s.hour_of(TIME)) if hasattr(s, "_od_index") else None
     bad = ((a - vmin_f).abs() > 1e-12) | ((b - vmax_f).abs() > 1e-12)
-    print(name, "bad", int(bad.sum()), "of", n)
+    st = s.od_resp_stats
+    print(name, "bad", int(bad.sum()), "of", n, "record slots: candidates %s of %s" % (
+        st.get("record_rows_candidates"), st.get("record_rows_listed")))
     if bad.any():
         for e in bad.nonzero().flatten()[:6].tolist():
             print("  P %.9f vmin %.15f full %.15f (row %s) vmax %.15f full %.15f it %d" % (
@@ -63,3 +70,5 @@ for name, (rec, masks) in {"q": (True, True), "noq": (False, True), "nomask": (F
         for k in keys:
             m = s._od_rowmask[k]
             print("  mask", k, [full.output_names[r] for r in range(64) if (m >> r) & 1])
+print("q == q-all-slots bit for bit:", torch.equal(res["q"][0], res["q-all-slots"][0]) and
+      torch.equal(res["q"][1], res["q-all-slots"][1]))
