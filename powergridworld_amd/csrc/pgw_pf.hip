@@ -1846,8 +1846,14 @@ __device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFAr
 #pragma unroll
   for (int ag = 0; ag < PGW_MAX_AGENTS; ++ag)
     rw[ag] = (c.coordinated && ag < c.n_agents) ? b.reward[(int64_t)ag * n + ec] : (Sto)0;
+  // with node records for output row 0 and no other row (the fused C4 step),
+  // the 96-byte node record is all a served env reads
+  const bool vonly = o.resp_v != nullptr && o.resp_v_row == 0 && a.n_out == 1;   // (uniform)
+  // ... and the solve's operands (the resident block) only a wave with an env
+  // the table left needs: there they go out after the lookup
+  const bool lazy = vonly && !LIST && o.resp != nullptr;                          // (uniform)
   PFSolver<M, true, false> S;
-  S.load(a, t.block);
+  if (!lazy) S.load(a, t.block);
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int s = 0; s < PGW_PF_MAX_CTRL; ++s) {
@@ -1866,9 +1872,6 @@ __device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFAr
 #pragma unroll
   for (int k = 0; k < M; ++k) ir[k] = ii[k] = 0.0;
   int it = 0;
-  // with node records for output row 0 and no other row (the fused C4 step),
-  // the 96-byte node record is all a served env reads
-  const bool vonly = o.resp_v != nullptr && o.resp_v_row == 0 && a.n_out == 1;   // (uniform)
   double2 vf = make_double2(0.0, 0.0);
   int rec = 0;
   double tq = 0.0;
@@ -1881,6 +1884,7 @@ __device__ __forceinline__ void coord_pf_od_env(const CoordPFArgs& c, const PFAr
     served = valid && o.resp && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf, rec, tq);
   }
   const bool need = valid && !served;
+  if (lazy && __ballot(need) != 0ull) S.load(a, t.block);   // (wave-uniform)
   if constexpr (TR) { if (ir[0] != -1e300 && vf.x != -1e300) pf_trace(tr, 2); }
   od_fallback<M>(S, o, o.start, stg, !early, sh, need, ir, ii, it);
   if constexpr (TR) pf_trace(tr, 3);
@@ -2087,12 +2091,23 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   ODStage<M> stg;
   // the table gives currents, not element voltages: U_out asks for the solve
   const bool table = o.resp != nullptr && t.U_out == nullptr;
-  if (!table) od_stage_load<M>(o, o.start, stg);     // in flight with the loads below
   const bool rows_lds = od_rows_lds<M>(a.n_out);     // (uniform)
+  // extrema only with row records covering every candidate row (and row 0):
+  // a block the table serves entirely reads the row records' headers and
+  // quartics alone -- no currents, no node-0 or row DPP groups, no row staging
+  const bool qfast = table && v_out == nullptr && o.resp_q && rows_lds && o.resp_rows != 0 &&
+                     (od_q_slot(o, 0) >= 0 || o.resp_v_row == 0);        // (uniform)
   double rv[kOdRowQ];
-  if (rows_lds) od_rows_issue<M>(t, a.n_out, rv);
   PFSolver<M, true, false> S;
-  S.load(a, t.block);
+  // the solve's operands (the block, the output rows) go out first -- in
+  // flight with the env's powers -- except in qfast launches, where a block
+  // the table serves entirely never uses them: there the env's powers go out
+  // alone and the operands follow only for a block with an env left over
+  if (!qfast) {                                      // (uniform)
+    if (!table) od_stage_load<M>(o, o.start, stg);
+    if (rows_lds) od_rows_issue<M>(t, a.n_out, rv);
+    S.load(a, t.block);
+  }
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
 #pragma unroll
   for (int c = 0; c < PGW_PF_MAX_CTRL; ++c) {
@@ -2108,11 +2123,6 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
   int rec = 0;
   double tq = 0.0;
   uint64_t qm = ~0ull;                               // the record's candidate slots (od_q_cand)
-  // extrema only with row records covering every candidate row (and row 0):
-  // a block the table serves entirely reads the row records' headers and
-  // quartics alone -- no currents, no node-0 or row DPP groups, no row staging
-  const bool qfast = table && v_out == nullptr && o.resp_q && rows_lds && o.resp_rows != 0 &&
-                     (od_q_slot(o, 0) >= 0 || o.resp_v_row == 0);        // (uniform)
   bool served, blk_fast = false;
   if (qfast) {
     served = valid && od_q_find(o, S.pc, S.qc, it, rec, tq, qm);
@@ -2121,7 +2131,14 @@ __global__ void __launch_bounds__(kBlock) k_pf_solve_od(PFArgs a, ODArgs o, pgw_
       vf = od_rec_j(vr[3], vr[4], vr[5], tq);
     }
     blk_fast = !__syncthreads_or(valid && !served);   // (block-uniform)
-    if (!blk_fast && served) od_resp_at<M>(o, rec, tq, ir, ii, vf);
+    if (!blk_fast) {                                 // the operands the solve and the rows need
+      od_rows_issue<M>(t, a.n_out, rv);
+      S.load(a, t.block);
+      if (served) od_resp_at<M>(o, rec, tq, ir, ii, vf);
+    } else {
+#pragma unroll
+      for (int q = 0; q < kOdRowQ; ++q) rv[q] = 0.0;   // (never read)
+    }
   } else {
     served = valid && table && od_resp_lookup<M>(o, S.pc, S.qc, ir, ii, it, vf, rec, tq);
     if (served && o.resp_q) qm = od_q_cand(o.resp_q[(int64_t)rec * o.resp_q_stride + 5]);
