@@ -471,14 +471,18 @@ def main():
     packed = pool.transpose(2, 3)                  # [P, agents, N, act_dim] view, env-minor
 
     step_count = 0
+    host_t = []                                    # per-step host time of the last run() (diagnostics)
 
     def run(k):
         nonlocal step_count
+        del host_t[:]
         for _ in range(k):
+            h0 = time.perf_counter()
             _, _, dones, _ = env.step(packed[step_count % P])
             step_count += 1
             if dones["__all__"]:
                 env.reset()
+            host_t.append(time.perf_counter() - h0)
 
     from powergridworld_amd import _lib
     # the measured HBM ceiling of this box (device copy) -- also brings the GPU
@@ -517,10 +521,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
+    t_issued = time.perf_counter()
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
+    host_region = {"issue_us": (t_issued - t0) * 1e6, "sync_wait_us": (time.perf_counter() - t_issued) * 1e6,
+                   "step_max_us": max(host_t) * 1e6, "step_max_at": host_t.index(max(host_t)),
+                   "step_median_us": sorted(host_t)[len(host_t) // 2] * 1e6,
+                   "note": "host side of the timed region on rank 0: time to issue the steps, then the wait for "
+                           "the GPU; the slowest step's host time and its index"}
     elapsed = pgd.max_over_ranks(elapsed, dev)
     # kernel durations: a second pass right after the timed region, every launch
     # bracketed by HIP events on its own stream.  Kept out of `value`'s region:
@@ -670,6 +680,7 @@ def main():
                              "note": "the env's first reset() (the power flow's per-hour tables built and "
                                      "certified on the device) plus the whole first episode, first launches "
                                      "included, no events"},
+            "host_region": host_region,
             "episode": {"steps": ep_steps, "ms_per_step": ep_elapsed / ep_steps * 1e3,
                         "gathered_env_stats": int(ep_stats.shape[0]),
                         "value": N_AGENTS * total_envs * ep_steps / ep_elapsed,
