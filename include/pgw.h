@@ -591,7 +591,14 @@ int32_t pgw_pf_pack(const pgw_pf_params* p, const double* W, const double* U0, c
  * ---------------------------------------------------------------------- */
 #define PGW_PFG_MAX_M 128     /* load phase elements */
 #define PGW_PFG_MAX_CHK 256   /* OpenDSS check rows (nodes) */
-enum { PGW_PF_EXACT = 0, PGW_PF_OPENDSS = 1 };
+/*   PGW_PF_OPENDSS_STEP  the same snap solve with every load's Yeq in Y at the
+ *                   STEP's powers (the reading in which the Loads.kW setters
+ *                   re-stamp Yprim, H1): y0' = the element's own conj(S); the
+ *                   tables hold the hour's reduction (per-hour Yeq) and the
+ *                   controllable elements' per-env Yeq change enters as the
+ *                   n_reg correction columns (Kreg = (I - D W_cc)^-1 D per env,
+ *                   reg_rho = 1), as RegControl taps do. */
+enum { PGW_PF_EXACT = 0, PGW_PF_OPENDSS = 1, PGW_PF_OPENDSS_STEP = 2 };
 
 typedef struct pgw_pfg_elem {
   double base_kw, base_kvar;   /* the element's LOAD kW / kvar before loadshape and rescale */

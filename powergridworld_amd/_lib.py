@@ -166,7 +166,7 @@ class RegParams(C.Structure):
                 ("rho", vp)]
 
 
-PF_EXACT, PF_OPENDSS = 0, 1
+PF_EXACT, PF_OPENDSS, PF_OPENDSS_STEP = 0, 1, 2
 
 
 class PredMeta(C.Structure):

@@ -162,6 +162,7 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
   const int mtot = REG ? m + p.n_reg : m;     // columns of W / Gc / G
   const ceptr el = (ceptr)t.elem;
   const cdptr W = (cdptr)t.W, U0 = (cdptr)t.U0;
+  const bool step_yeq = p.mode == PGW_PF_OPENDSS_STEP;     // (uniform)
 
   // ---- the env's controllable powers (kW, kvar) per slot
   double cp[PGW_PF_MAX_CTRL], cq[PGW_PF_MAX_CTRL];
@@ -269,8 +270,10 @@ __global__ void __launch_bounds__(kBlock) k_pf_general(pgw_pfg_params p, pgw_pfg
           } else {
             elem_law(el, min(k, m - 1), E, m2, fp, fq);
           }
-          const double cr = OD ? fma(sr[j][r], fp, -E.y0r) : sr[j][r] * fp;
-          const double ci = OD ? fma(si[j][r], fq, -E.y0i) : si[j][r] * fq;
+          // (PGW_PF_OPENDSS_STEP: the Yeq in Y is the step's own power)
+          const double y0r = step_yeq ? sr[j][r] : E.y0r, y0i = step_yeq ? si[j][r] : E.y0i;
+          const double cr = OD ? fma(sr[j][r], fp, -y0r) : sr[j][r] * fp;
+          const double ci = OD ? fma(si[j][r], fq, -y0i) : si[j][r] * fq;
           double jr = fma(cr, ur[j][r], -(ci * ui[j][r]));
           double ji = fma(cr, ui[j][r], ci * ur[j][r]);
           if (REG && first) jr = ji = 0.0;
@@ -479,7 +482,7 @@ static int32_t launch_general(const pgw_pfg_params& p, const pgw_pfg_tables& t, 
 template <int CE>
 static int32_t dispatch_cn(const pgw_pfg_params& p, const pgw_pfg_tables& t, int64_t n, const double* cp,
                            const double* cq, double* v_out, int32_t* iters, const PFGCoord& c, hipStream_t st) {
-  if (p.mode != PGW_PF_OPENDSS) return launch_general<CE, 0>(p, t, n, cp, cq, v_out, iters, c, st);
+  if (p.mode == PGW_PF_EXACT) return launch_general<CE, 0>(p, t, n, cp, cq, v_out, iters, c, st);
   const int cn = (p.n_chk + 32 * 1 - 1) / 32;
   if (cn <= 1) return launch_general<CE, 1>(p, t, n, cp, cq, v_out, iters, c, st);
   if (cn <= 2) return launch_general<CE, 2>(p, t, n, cp, cq, v_out, iters, c, st);
@@ -493,8 +496,9 @@ int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t 
   PGW_REQUIRE(p->m >= 1 && p->m <= PGW_PFG_MAX_M && p->m % kGR == 0,
               "pgw_pf_solve_general: m=%d (need a multiple of 8, <= %d)", p->m, PGW_PFG_MAX_M);
   PGW_REQUIRE(t->elem && t->W && t->U0, "pgw_pf_solve_general: missing elem / W / U0");
-  PGW_REQUIRE(p->mode == PGW_PF_EXACT || p->mode == PGW_PF_OPENDSS, "pgw_pf_solve_general: bad mode");
-  PGW_REQUIRE(p->mode != PGW_PF_OPENDSS ||
+  PGW_REQUIRE(p->mode == PGW_PF_EXACT || p->mode == PGW_PF_OPENDSS || p->mode == PGW_PF_OPENDSS_STEP,
+              "pgw_pf_solve_general: bad mode");
+  PGW_REQUIRE(p->mode == PGW_PF_EXACT ||
                   (p->n_chk >= kGR && p->n_chk <= PGW_PFG_MAX_CHK && p->n_chk % kGR == 0 && t->Gc && t->V0c),
               "pgw_pf_solve_general: OPENDSS needs n_chk check rows (multiple of 8, <= %d) and Gc / V0c",
               PGW_PFG_MAX_CHK);
@@ -502,7 +506,7 @@ int32_t solve_general(const pgw_pfg_params* p, const pgw_pfg_tables* t, int64_t 
   // solve starts from its previous solution instead of the direct one; the
   // stopping test counts from min_iter either way, so the check rows' first
   // magnitudes need no start value)
-  PGW_REQUIRE(p->mode != PGW_PF_OPENDSS || !t->U_init || !p->n_reg,
+  PGW_REQUIRE(p->mode == PGW_PF_EXACT || !t->U_init || !p->n_reg,
               "pgw_pf_solve_general: OPENDSS with U_init and RegControls is not supported");
   PGW_REQUIRE(p->n_out >= 0 && (p->n_out == 0 || (t->G && t->V0)), "pgw_pf_solve_general: missing G / V0");
   PGW_REQUIRE(p->n_ctrl >= 0 && p->n_ctrl <= PGW_PF_MAX_CTRL, "pgw_pf_solve_general: bad n_ctrl");

@@ -109,7 +109,7 @@ class OpenDSSSolver(PowerFlowSolver):
                  num_envs: int = 1, device=None, tol: float = None, max_iter: int = None,
                  output_nodes=None, predictor: bool = True, warm_start: bool = False,
                  convergence: str = "opendss", general: bool = None, od_table: bool = True,
-                 snap_start: str = "direct", **kwargs):
+                 snap_start: str = "direct", yprim: str = "dss_file", **kwargs):
         """convergence: "opendss" (the default) -- OpenDSS's own snap solve as
         the reference runs it (opendss.py:134):
         loads' nominal admittances in Y, start from the direct solution, stop at
@@ -129,7 +129,14 @@ class OpenDSSSolver(PowerFlowSolver):
         opendss.py:134, which this build cannot confirm without OpenDSS): the
         general kernel with U_init / U_out over a per-env buffer (the first
         solve starts from the direct solution); no response table, the
-        generic multi-agent path."""
+        generic multi-agent path.
+        yprim (OpenDSS rule): "dss_file" (the default, H2) -- Y keeps every
+        load's Yeq of the DSS file, as the Loads.kW / kvar setters leave Yprim
+        valid; "step" (H1) -- each solve's Y holds its own
+        loads' Yeq (the hour's base loads and each env's controllable power):
+        the general kernel with the hour's reduction and the controllable
+        elements' per-env Yeq change as correction columns
+        (PGW_PF_OPENDSS_STEP); no response table, the generic multi-agent path."""
         super().__init__(**kwargs)
         if convergence not in ("exact", "opendss"):
             raise ValueError("convergence must be 'exact' or 'opendss', got %r" % (convergence,))
@@ -140,6 +147,14 @@ class OpenDSSSolver(PowerFlowSolver):
                              "the exact fixed point has warm_start=True")
         self.snap_start = snap_start
         if snap_start == "previous":
+            general, od_table = True, False
+        if yprim not in ("dss_file", "step"):
+            raise ValueError("yprim must be 'dss_file' or 'step', got %r" % (yprim,))
+        if yprim == "step" and (convergence != "opendss" or snap_start != "direct"):
+            raise ValueError("yprim='step' is a reading of OpenDSS's snap solve from the direct solution "
+                             "(convergence='opendss', snap_start='direct')")
+        self.yprim = yprim
+        if yprim == "step":
             general, od_table = True, False
         self.convergence = convergence
         self.od_table = bool(od_table)
@@ -179,8 +194,11 @@ class OpenDSSSolver(PowerFlowSolver):
         # RegControl (automatic regulator taps, STATIC control mode): per-env taps,
         # the control loop in calculate_power_flow (pgw_reg_control / pgw_reg_factor)
         self.regulators = self.feeder.regulators(Z=self._fd_iter.Z)
+        if self.regulators is not None and yprim == "step":
+            raise ValueError("yprim='step' with RegControls is not supported")
         if self.regulators is not None:
             self._init_regulators()
+        self._h1, self._h1_cache = None, {}
         self.system_load_rescale_factor = system_load_rescale_factor
         self.annual_hourly_load_profile = load_loadshape(loadshape_file)
         if len(self.annual_hourly_load_profile) != 8760:
@@ -906,6 +924,11 @@ class OpenDSSSolver(PowerFlowSolver):
         else:
             self._g_W = dev_c(emaj(Ws.T, mp))           # column k = W''[:, k]
             self._g_G = dev_c(emaj(Gs, ldo))
+        if self.yprim == "step":
+            # H1: the file model's reduction, kept for the hours' tables
+            # (_h1_hour); the correction columns are the controllable elements'
+            self._h1 = dict(Ws=Ws, u0=U0 / vb, Gs=Gs, V0o=V0o / vbn[idx], ldo=ldo, no=no, m=m, mp=mp,
+                            emaj=emaj, dev_c=dev_c)
         self._g_nreg = nreg
         self._g_U0 = dev_c(u0)
         self._g_V0 = dev_c(V0s)
@@ -920,6 +943,8 @@ class OpenDSSSolver(PowerFlowSolver):
             V0cs = np.zeros(n_chk, complex)
             V0cs[:f.n] = V0c / vbn
             Gcs = (Gc / vb[None, :]) / vbn[:, None]
+            if self._h1 is not None:
+                self._h1.update(Gcs=Gcs, V0c=V0c / vbn, n_chk=n_chk)
             if reg is not None:
                 Gcs = np.hstack([np.pad(Gcs, ((0, 0), (0, mp - m))), pad(-ZR / vbn[:, None])])
                 self._g_Gc = dev_c(emaj_aug(Gcs, n_chk))
@@ -935,6 +960,103 @@ class OpenDSSSolver(PowerFlowSolver):
         self._bv_cache = {}
         self._iters = torch.zeros(self.num_envs, dtype=torch.int32, device=dev)
         self._base_params()
+
+    def _h1_hour(self, hour):
+        """yprim='step': the hour's reduction with every load's Yeq at the hour's
+        powers (the controllable loads' base part included), from the file
+        model's by the Yeq change dD: u = U0 + W J' with J' = (conj(S) g - D) u
+        gives W_h = (I - W dD)^-1 W, U0_h = (I - W dD)^-1 U0, and any row read
+        out as V = V0 + G J' becomes V0 + G dD U0_h + G (I + dD W_h) J'.  The
+        controllable elements' columns (W_h, G_h, Gc_h) follow as the
+        correction columns, their rows of W_h / U0_h as the correction's x.
+        Cached per (hour, configuration) on the device."""
+        key = (hour, self._cfg_version)
+        c = self._h1_cache.get(key)
+        if c is not None:
+            return c
+        H, f = self._h1, self.feeder
+        m, mp, ldo, no, n_chk = H["m"], H["mp"], H["ldo"], H["no"], H["n_chk"]
+        emaj, dev_c = H["emaj"], H["dev_c"]
+        coef, resc = float(self.annual_hourly_load_profile[hour]), float(self.system_load_rescale_factor)
+        dD = np.zeros(m, complex)
+        for k in range(m):
+            if f.elem_model[k] == 1:               # the kernel's (coef * base) * rescale; other models fixed
+                li = f.elem_load[k]
+                dP = (coef * f.base_kw[li]) * resc - f.base_kw[li]
+                dQ = (coef * f.base_kvar[li]) * resc - f.base_kvar[li]
+                dD[k] = complex(dP * 1000.0 / f.elem_nph[k], -(dQ * 1000.0 / f.elem_nph[k]))
+        Ws, u0 = H["Ws"], H["u0"]
+        A = np.eye(m) - Ws * dD[None, :]
+        Wh = np.linalg.solve(A, Ws)
+        U0h = np.linalg.solve(A, u0)
+        rows = lambda G, V0: (G + (G * dD[None, :]) @ Wh, V0 + (G * dD[None, :]) @ U0h)
+        Gh, V0h = rows(H["Gs"], H["V0o"])
+        Gch, V0ch = rows(H["Gcs"], H["V0c"])
+        C = self._h1_ctrl
+        r, nreg = len(C), (8 if self._h1_ctrl else 0)
+        pad_c = lambda M: np.pad(M[:, C], ((0, 0), (0, nreg - r))) if nreg else np.zeros((M.shape[0], 0), complex)
+
+        def emaj_aug(rows_cm, ld):                 # [rows, mp + nreg] -> [mp + nreg][ld]
+            out = np.zeros((mp + nreg, ld), complex)
+            out[:, :rows_cm.shape[0]] = rows_cm.T
+            return out
+        W_aug = np.hstack([np.pad(Wh, ((0, 0), (0, mp - m))), pad_c(Wh)])          # [m, mp + nreg]
+        G_aug = np.hstack([np.pad(Gh, ((0, 0), (0, mp - m))), pad_c(Gh)])
+        Gc_aug = np.hstack([np.pad(Gch, ((0, 0), (0, mp - m))), pad_c(Gch)])
+        u0p = np.zeros(mp, complex)
+        u0p[:m] = U0h
+        V0p = np.zeros(ldo, complex)
+        V0p[:no] = V0h
+        V0cp = np.zeros(n_chk, complex)
+        V0cp[:len(V0ch)] = V0ch
+        c = dict(W=dev_c(emaj_aug(np.pad(W_aug, ((0, mp - m), (0, 0))), mp)), U0=dev_c(u0p),
+                 G=dev_c(emaj_aug(G_aug, ldo)), V0=dev_c(V0p), Gc=dev_c(emaj_aug(Gc_aug, n_chk)), V0c=dev_c(V0cp))
+        if nreg:
+            V0r = np.zeros(nreg, complex)
+            V0r[:r] = U0h[C]
+            c.update(Greg=dev_c(emaj(Wh[C, :], nreg)), V0reg=dev_c(V0r),
+                     Wcc=torch.tensor(Wh[np.ix_(C, C)], dtype=torch.complex128, device=self.device),
+                     nph=torch.tensor([float(f.elem_nph[k]) for k in C], dtype=torch.float64, device=self.device),
+                     slot=[self._ctrl_names.index(f.load_names[f.elem_load[k]]) for k in C])
+        if len(self._h1_cache) > 64:
+            self._h1_cache.clear()
+        self._h1_cache[key] = c
+        return c
+
+    def _h1_tables(self, hour, cp, cq):
+        """yprim='step': PFGTables of this solve -- the hour's reduction and the
+        per-env correction K = (I - D W_cc)^-1 D of the controllable elements'
+        Yeq change D (diag, the env's controllable conj(S) per phase: the
+        kernel's own y0' change), its upper triangle in Kreg."""
+        c = self._h1_hour(hour)
+        t = _lib.PFGTables.from_buffer_copy(self.tables)
+        t.W, t.U0, t.G, t.V0 = c["W"].data_ptr(), c["U0"].data_ptr(), c["G"].data_ptr(), c["V0"].data_ptr()
+        t.Gc, t.V0c = c["Gc"].data_ptr(), c["V0c"].data_ptr()
+        keep = [c]
+        if "Greg" in c:
+            n, dev, r = self.num_envs, self.device, len(self._h1_ctrl)
+            z = torch.zeros(n, dtype=torch.float64, device=dev)
+            pk = torch.stack([cp[s] if cp is not None else z for s in c["slot"]])          # [r, n] kW
+            qk = torch.stack([cq[s] if cq is not None else z for s in c["slot"]])
+            d = torch.complex((pk * 1000.0) / c["nph"][:, None], -((qk * 1000.0) / c["nph"][:, None])).t()  # [n, r]
+            if r == 1:
+                K = (d[:, 0] / (1.0 - d[:, 0] * c["Wcc"][0, 0]))[None]                          # [1, n]
+            else:
+                Mx = torch.eye(r, dtype=torch.complex128, device=dev)[None] - d[:, :, None] * c["Wcc"][None]
+                Kf = torch.linalg.solve(Mx, torch.diag_embed(d))                                 # [n, r, r]
+                iu = torch.triu_indices(r, r, device=dev)
+                K = Kf[:, iu[0], iu[1]].t()                                                      # [r(r+1)/2, n]
+            Kreg = torch.view_as_real(K.contiguous()).contiguous()                               # [r(r+1)/2, n, 2]
+            if getattr(self, "_h1_scratch", None) is None or self._h1_scratch[0].shape[1] != n:
+                self._h1_scratch = (torch.zeros((8, n, 2), dtype=torch.float64, device=dev),
+                                    torch.zeros((8, n, 2), dtype=torch.float64, device=dev),
+                                    torch.ones(8, dtype=torch.float64, device=dev))
+            rx, rc, rho = self._h1_scratch
+            t.Greg, t.V0reg, t.Kreg = c["Greg"].data_ptr(), c["V0reg"].data_ptr(), Kreg.data_ptr()
+            t.reg_x, t.reg_c, t.reg_rho = rx.data_ptr(), rc.data_ptr(), rho.data_ptr()
+            keep.append(Kreg)
+        t._keep = keep                             # (the tensors live as long as these tables)
+        return t
 
     def _general_elems(self):
         """pgw_pfg_elem per (padded) element: the load's base kW / kvar, its
@@ -1018,6 +1140,15 @@ class OpenDSSSolver(PowerFlowSolver):
         reg = self.regulators
         if reg is not None:
             p.n_reg, p.r_reg = self._g_nreg, len(reg["nodes"])
+        if self.yprim == "step":
+            f = self.feeder
+            ctrl = [k for k in range(f.m) if f.load_names[f.elem_load[k]] in self._ctrl_names]
+            if len(ctrl) > 8:
+                raise ValueError("yprim='step': at most 8 controllable load phase elements, got %d" % len(ctrl))
+            self._h1_ctrl = ctrl
+            p.mode = _lib.PF_OPENDSS_STEP
+            p.n_reg, p.r_reg = (8, len(ctrl)) if ctrl else (0, 0)
+            self._h1_cache = {}
         self.params = p
         elems = self._general_elems()
         self._g_elem = torch.tensor(np.frombuffer(bytes(elems), np.uint8), device=self.device)
@@ -1192,6 +1323,8 @@ class OpenDSSSolver(PowerFlowSolver):
                 cp = torch.stack([x if x is not None else zeros for x in ps])
                 cq = torch.stack([x if x is not None else zeros for x in qs])
         tables = self.solve_tables(current_time, cp is not None)
+        if self.yprim == "step":
+            tables = self._h1_tables(self.hour_of(current_time), cp, cq)
         fn = _lib.lib().pgw_pf_solve_general if self.general else _lib.lib().pgw_pf_solve
         if self.regulators is not None:
             self._solve_regulated(fn, p, tables, cp, cq)

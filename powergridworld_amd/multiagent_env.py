@@ -388,6 +388,8 @@ class MultiAgentEnv(Env):
             return "RegControl (the control loop runs in OpenDSSSolver.calculate_power_flow)"
         if getattr(self.pf_solver, "snap_start", "direct") != "direct":
             return "snap_start='previous' (each env's solve starts from its own previous solution)"
+        if getattr(self.pf_solver, "yprim", "dss_file") != "dss_file":
+            return "yprim='step' (every solve's Y holds its own loads' admittances)"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)
@@ -660,6 +662,8 @@ class MultiAgentEnv(Env):
             return "RegControl (the control loop runs in OpenDSSSolver.calculate_power_flow)"
         if getattr(self.pf_solver, "snap_start", "direct") != "direct":
             return "snap_start='previous' (each env's solve starts from its own previous solution)"
+        if getattr(self.pf_solver, "yprim", "dss_file") != "dss_file":
+            return "yprim='step' (every solve's Y holds its own loads' admittances)"
         if len(self.agents) > _lib.MAX_AGENTS:
             return "more than %d agents" % _lib.MAX_AGENTS
         cls = type(self)

@@ -60,6 +60,8 @@ def _run(solver, oracle, times, ctrl, lo, hi, K, rng, semantics):
         kw, kvar = oracle.loads(t, {ctrl: p}, {ctrl: q}, K=K)
         if semantics == "opendss":
             V, it = f.snap_opendss(kw, kvar, f.base_kw, f.base_kvar)
+        elif semantics == "opendss_h1":                     # every solve's own Yeq in Y
+            V, it = f.snap_opendss(kw, kvar)
         else:
             V, it = f.solve(kw, kvar, tol=1e-12)
         o_v.append(f.pu(V))
@@ -140,6 +142,52 @@ def test_opendss_snap_start_previous_vs_oracle():
         V_prev = V
         gaps.append(np.abs(g - gd).max())
     assert gaps[0] < 1e-10 and max(gaps[1:]) > 1e-7, gaps      # the first solve starts direct in both
+
+
+@pytest.mark.parametrize("ctrl", ["675c", "671"])
+def test_opendss_yprim_step_vs_oracle(ctrl):
+    """OpenDSSSolver(yprim="step"): every snap solve's Y holds its own loads'
+    Yeq (the hour's base loads and each env's controllable power -- the reading
+    in which the Loads.kW / kvar setters re-stamp Yprim, H1) -- against the
+    oracle's snap_opendss with yprim_kw=None over four hours: the same
+    iteration count for every env, every node within 1e-9 rel.  675c: one
+    controllable phase element (a scalar correction per env); 671: three
+    (delta) elements, a 3 x 3 correction per env.  And measurably not the
+    default reading (yprim="dss_file", H2)."""
+    K = 2048
+    s = _solver(IEEE13, system_load_rescale_factor=1.2, num_envs=K, convergence="opendss", yprim="step")
+    assert s.general and not s.od_table and s.yprim == "step"
+    g, o, git, oit = _run(s, _oracle(IEEE13, 1.2), TIMES, ctrl, -400.0, 900.0, K,
+                          np.random.default_rng(5), "opendss_h1")
+    assert s.params.r_reg == (1 if ctrl == "675c" else 3)
+    np.testing.assert_array_equal(git, oit)
+    np.testing.assert_allclose(g, o, rtol=1e-9, atol=0)
+    d = _solver(IEEE13, system_load_rescale_factor=1.2, num_envs=K, convergence="opendss", general=True)
+    gd, _, _, _ = _run(d, _oracle(IEEE13, 1.2), TIMES, ctrl, -400.0, 900.0, K,
+                       np.random.default_rng(5), "opendss")
+    assert np.abs(g - gd).max() > 1e-7
+
+
+def test_het_yprim_step_runs_the_generic_path():
+    """The heterogeneous scenario with yprim="step": the fused step refuses it
+    (its kernels hold the DSS file's Yeq), the generic path runs it -- the PV
+    farm's min-voltage observation and the rewards finite, every env's solve
+    within OpenDSS's iteration limits."""
+    from powergridworld_amd.multiagent_env import MultiAgentEnv
+    from powergridworld_amd.scenarios.heterogeneous import make_env_config
+    cfg = make_env_config()
+    cfg["pf_config"]["config"]["yprim"] = "step"
+    env = MultiAgentEnv(**cfg, num_envs=256, device=DEV)
+    assert env._ma is None and env.pf_solver.yprim == "step"
+    rng = np.random.default_rng(8)
+    env.reset()
+    for _ in range(12):
+        a = torch.tensor(rng.uniform(-1, 1, (256, 10)), device=DEV)
+        o, r, d, m = env.step({"building": {"building": a[:, :6], "pv": a[:, 6:7], "storage": a[:, 7:8]},
+                               "pv": a[:, 8:9], "ev-charging": a[:, 9:10]})
+        it = env.pf_solver.iterations
+        assert bool(((it >= 2) & (it <= 15)).all())
+        assert all(bool(torch.isfinite(v).all()) for v in r.values())
 
 
 def test_large_feeder_exact_and_opendss_vs_oracle():
