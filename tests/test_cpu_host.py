@@ -646,3 +646,17 @@ def test_checkpoint_walk_restores_in_place():
     assert env.time_index == 3 and env.tables_version == 8          # (version counters untouched)
     assert torch.equal(torch.rand(2, generator=env.gen), r1)
     assert "step_cache" not in " ".join(sd)
+
+
+def test_opendss_solver_reading_options_refused():
+    """The two readings of the snap solve this build cannot confirm without
+    OpenDSS are options with their own constraints:
+    yprim='step' (H1) and snap_start='previous' are OpenDSS-rule readings, and
+    H1 starts from the direct solution; unknown values are refused."""
+    from powergridworld_amd.distribution_system.opendss import OpenDSSSolver
+    feeder, shape = "ieee_13_dss/IEEE13Nodeckt.dss", "ieee_13_dss/annual_hourly_load_profile.csv"
+    for kw in (dict(yprim="nope"), dict(yprim="step", convergence="exact"),
+               dict(yprim="step", snap_start="previous"), dict(snap_start="later"),
+               dict(snap_start="previous", convergence="exact")):
+        with pytest.raises(ValueError):
+            OpenDSSSolver(feeder, shape, **kw)
