@@ -3,10 +3,10 @@ with the IEEE-13 power flow (BASELINE.json config C4), batch 65,536 per GPU.
 
 One "step" = one MultiAgentEnv.step of the whole batch through the public API
 (fused path: one pgw_coord_step call.  By default, OpenDSS's snap-solve rule
-as the reference runs it with the hour's certified response table:
-k_coord_step_od -- 5 x [building, PV, storage] per env and the power flow's
-table lookup with the coordinated reward, one launch -- then
-k_coord_pf_od_list, the snap solve of the envs the table did not serve;
+as the reference runs it with the hour's certified response table, in ONE
+launch: k_coord_step_od -- 5 x [building, PV, storage] per env, the power
+flow's table lookup with the coordinated reward, and the snap solve of the rare
+envs the table does not serve by the lookup wave (od_wave_solve);
 --pf-split off: k_coord_agents_std + k_coord_pf_od (bit-identical);
 --pf-convergence exact: k_coord_agents_std + k_coord_pf, the exact fixed point
 with its predictor tables), actions already resident in HBM.  Episodes (286 steps) end with done["__all__"]; the following env.reset()
@@ -114,6 +114,21 @@ def pf_roofline(conv, avg_us, mean_it, n, table=False, split=False):
 KERNELS = ("k_coord_agents_std", PF_KERNEL, "k_pf_solve", "(unused)", "k_ma_step", "k_pf_general")
 
 
+def table_stats(env):
+    """The hour tables' response-table statistics for the bench line."""
+    st = dict(env.pf_solver.od_resp_stats)
+    out = {k: st.get(k) for k in ("hours", "segments_with_breakpoints", "brackets", "unresolved_brackets",
+                                  "pieces", "pieces_left_to_solve", "max_fit_err", "certified",
+                                  "certified_pieces", "pieces_cut_by_certificate", "uncertified_kw",
+                                  "certify_s", "build_s")}
+    out["note"] = ("built on the device by the snap solve itself (pgw_pf_od_probe) about once per 24 "
+                   "simulated hours, every piece certified (od_certify: Taylor-model bounds prove every band and "
+                   "stopping decision constant over what its record serves; cut pieces leave a guard zone "
+                   "to the solve), cached across episodes (every episode repeats the hours); build_s is the "
+                   "whole build time of this run (in episode_cold), outside the timed region")
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,9 +151,10 @@ def parse():
                     help="the headline's power-flow stopping rule: OpenDSS's snap solve (the "
                          "reference's: loads' Yeq in Y, node-magnitude test 1e-4, 2..15 iterations) "
                          "or the exact fixed point; the other runs as variants.*_pf")
-    ap.add_argument("--pf-split", choices=("on", "off"), default="off",
-                    help="OpenDSS rule with node records: agents + table lookup in one launch and the "
-                         "listed envs' snap solve (on), or the two-kernel step (off); bit-identical")
+    ap.add_argument("--pf-split", choices=("on", "off"), default="on",
+                    help="OpenDSS rule with node records: the one-launch step -- agents, table lookup "
+                         "and the snap solve of the envs the table leaves (on) -- or the two-kernel "
+                         "step (off); bit-identical")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the fp32-storage variant line (N=1 only; never the headline)")
     return ap.parse_args()
@@ -235,6 +251,7 @@ def pf_variant(conv, n, steps, warmup, pool, dev, od_table=True):
     env = CoordinatedMultiBuildingControlEnv(**make_c4_config(pf_convergence=conv), num_envs=n,
                                              device=dev, fused=True)
     env.pf_solver.od_table = bool(od_table)
+    env.set_pf_list(env._one_launch_ok())           # (the one-launch step needs the table)
     P = pool.shape[0]
     env.reset()
     k = [0]
@@ -592,9 +609,14 @@ def main():
                            "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": a_bytes,
                            "traffic": traffic.get(ak), "traffic_run": traffic_runs.get(ak)}
             if split:
-                kernels[ak]["note"] = ("the 5 agents' steps and the power flow's response-table lookup (node "
-                                       "records) in one launch: %d B per env (agents 5 x %d + V675.3, violation, "
-                                       "iteration count)" % (STEP_OD_ENV_BYTES, AGENT_BYTES))
+                kernels[ak]["note"] = ("the whole step in one launch: the 5 agents' steps, the power flow's "
+                                       "response-table lookup (node records) and the snap solve of the envs the "
+                                       "table leaves (the lookup wave, od_wave_solve): %d B per env (agents 5 x %d "
+                                       "+ V675.3, violation, iteration count)" % (STEP_OD_ENV_BYTES, AGENT_BYTES))
+                kernels[ak]["solved_inline_last_step"] = int(
+                    env._fused["od_count"][env._fused["bufs"].od_parity & 1])
+        if split and table and a_us:
+            kernels[ak]["response_table"] = table_stats(env)
         if p_us:
             pk = "k_coord_pf_od_list<14>" if split else PF_KERNEL_NAME[conv]
             kernels[pk] = {"avg_us": p_us, "timed_launches": cnt[1],
@@ -607,18 +629,7 @@ def main():
                 kernels[pk]["hbm_gbs"] = PF_BYTES * n / (p_us * 1e-6) / 1e9
             kernels[pk].update(pf_roofline(conv, p_us, mean_it, n, table, split))
             if table:
-                st = dict(env.pf_solver.od_resp_stats)
-                kernels[pk]["response_table"] = {
-                    k: st.get(k) for k in ("hours", "segments_with_breakpoints", "brackets", "unresolved_brackets",
-                                           "pieces", "pieces_left_to_solve", "max_fit_err", "certified",
-                                           "certified_pieces", "pieces_cut_by_certificate", "uncertified_kw",
-                                           "certify_s", "build_s")}
-                kernels[pk]["response_table"]["note"] = (
-                    "built on the device by the snap solve itself (pgw_pf_od_probe) about once per 24 "
-                    "simulated hours, every piece certified (od_certify: Taylor-model bounds prove every band and "
-                    "stopping decision constant over what its record serves; cut pieces leave a guard zone "
-                    "to the solve), cached across episodes (every episode repeats the hours); build_s is the "
-                    "whole build time of this run (in episode_cold), outside the timed region")
+                kernels[pk]["response_table"] = table_stats(env)
         if avg_us[KERNELS[2]]:
             kernels[KERNELS[2]] = {"avg_us": avg_us[KERNELS[2]], "timed_launches": cnt[2],
                                    "note": "reset power flow + predictor tables (24 h x 3201 grid points "

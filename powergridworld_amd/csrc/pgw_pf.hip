@@ -1381,7 +1381,8 @@ __device__ __forceinline__ void od_rows_sparse(const ODShared<M>& sh, const doub
 // The env's test after an iteration: lo = the exact changes (element nodes
 // and the evaluated rows), hi = lo plus the bounds of the unevaluated rows.
 // Returns 1 converged, 0 not, -1 undecided (the bounds straddle tol).
-__device__ __forceinline__ int od_decide(const ODArgs& o, bool full, int it, double lo, double amin,
+template <class OA>
+__device__ __forceinline__ int od_decide(const OA& o, bool full, int it, double lo, double amin,
                                          double dsum, double jsum) {
   if (it < o.min_iter || lo > o.tol || lo != lo) return 0;
   if (full) return lo <= o.tol ? 1 : 0;
@@ -1945,6 +1946,244 @@ struct ODVLook {
   int32_t timing_only;      // PGW_STEP_NOLOOKUP (A/B timing only): no lookup, no list -- results wrong
 };
 
+// ---- the snap solve of one env by a whole wave --------------------------------
+// The one-launch C4 step (k_coord_step_od<.., true>) solves the rare envs the
+// node records leave (P in a guard zone or a bracket, off the grid) itself,
+// one env at a time with the lookup wave, instead of listing them for a second
+// launch: any launch after the 100-MB agents step costs ~4.6 us here
+// (profiles/r06/c4_step_boundary_experiments.txt), the step without one 23.1
+// against 25.3 us (ab_nolist.txt).  The lane-per-env solve (od_solve) keeps 256
+// envs' currents in 148 KB of LDS at 1 wave per SIMD; this form needs ~15 KB
+// and few registers, so the step kernel keeps its occupancy.
+//   lane i < m      element i: its voltage u_i, its current I'_i and row i of
+//                   the matvec (W'' staged in LDS, s_w[c][k][i]);
+//   lane r (r + 32) check row r from the previous (new) currents (s_rows).
+// Every value is formed with od_solve's operations in its order -- the
+// current law of current_od, the matvec column by column from k = 0 as
+// pf_column (A += Wr I, B += Wi I', C += (Wr+Wi)(I+I')), the rows as
+// od_rows_sparse, dsum / jsum summed in k order; only maxima and minima (order
+// free, od_max propagating NaN) are reduced across lanes -- so the count, the
+// currents and the node-0 voltage equal the lane-per-env solve's bit for bit
+// (tests/test_gpu_pf_od.py::test_od_split_step_bit_identical, every env forced
+// to the solve).
+struct ODWaveArgs {
+  double sr0[PGW_PF_MAX_M], si0[PGW_PF_MAX_M], fr[PGW_PF_MAX_M], fi[PGW_PF_MAX_M];   // PFArgs's
+  double y0r[PGW_PF_MAX_M], y0i[PGW_PF_MAX_M], esc[PGW_PF_MAX_M];                    // ODArgs's
+  double lo2, mn2, mx2;                            // uniform bands (PFSolver<M, true, ..>)
+  double tol, gamma, eps, gmax, gsrc;              // od_decide's
+  const double* block;                             // the resident block (pgw_pf_tables.block)
+  const double* start;                             // pgw_pf_od.start: u_1 and I'(u_0) affine in P, Q
+  const double* rows_V0;
+  const double* rows_G;
+  int32_t m, min_iter, n_rep, n_rows, max_iter, node_mask;
+};
+constexpr int kWaveRowStride = 2 + 2 * PGW_PF_MAX_M + 1;   // odd: 32 rows on distinct banks
+struct ODWaveShared {
+  double w[3][PGW_PF_MAX_M][PGW_PF_MAX_M];         // [c][k][i] = part c of W''_ik
+  double rows[kOdRows * kWaveRowStride];           // V0 re, im, G re (k), G im (k) per check row
+};
+
+__device__ __forceinline__ double wave_bcast(double x, int k) {   // lane k's value (k uniform)
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), k);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double wave_uni(double x) {     // a wave-uniform value, made scalar
+  return wave_bcast(x, 0);
+}
+// (the partner lane's address from an opaque lane id: formed at use, not
+// hoisted into registers held through the solve)
+__device__ __forceinline__ double wave_xor(double x, int d) {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return __shfl(x, l ^ d);
+}
+__device__ __forceinline__ double wave_max(double x) {     // od_max over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) x = od_max(x, wave_xor(x, d));
+  return x;
+}
+__device__ __forceinline__ double wave_min(double x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) x = fmin(x, wave_xor(x, d));
+  return x;
+}
+
+// W'' and the check rows into the wave's LDS (the calling wave only).
+__device__ __forceinline__ void od_wave_stage(const ODWaveArgs& z_, ODWaveShared& sh_) {
+  const ODWaveArgs* zp = &z_;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+s"(zp), "+v"(lane));       // (opaque: see od_wave_solve)
+  const ODWaveArgs& z = *zp;
+  ODWaveShared& sh = sh_;
+  const int M = z.m, T = M * (M + 1) / 2;
+  for (int x = lane; x < 3 * PGW_PF_MAX_M * PGW_PF_MAX_M; x += 64) {
+    const int c = x / (PGW_PF_MAX_M * PGW_PF_MAX_M), k = (x / PGW_PF_MAX_M) % PGW_PF_MAX_M,
+              i = x % PGW_PF_MAX_M;
+    const int a = min(i, k), b = max(i, k);
+    (&sh.w[0][0][0])[x] = (i < M && k < M) ? z.block[c * T + a * M - a * (a - 1) / 2 + (b - a)] : 0.0;
+  }
+  const int S = 2 + 2 * M;
+  for (int x = lane; x < z.n_rows * S; x += 64) {
+    const int r = x / S, j = x - r * S;
+    const double v = j < 2 ? z.rows_V0[2 * r + j]
+                           : z.rows_G[2 * M * r + (j < 2 + M ? 2 * (j - 2) : 2 * (j - 2 - M) + 1)];
+    sh.rows[r * kWaveRowStride + j] = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Rows [r0, r1) of the exact test (lane r: previous magnitude, lane r + 32:
+// new), folded into (err, amin) of lanes < 32 (wave-reduced by the caller).
+__device__ __forceinline__ void od_wave_rows(const ODWaveShared& sh, int M, int r0, int r1, double pjr,
+                                             double pji, double cjr, double cji, double& err, double& amin) {
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));                   // (opaque: addresses formed here)
+  const bool newer = lane >= 32;
+  const int r = min(r0 + (lane & 31), max(r1 - 1, 0));
+  const bool on = r0 + (lane & 31) < r1;
+  const double* R = sh.rows + r * kWaveRowStride;
+  double vr = R[0], vi = R[1];
+#pragma unroll 1
+  for (int k = 0; k < M; ++k) {                      // (uniform) od_rows_sparse's order
+    const double gr = R[2 + k], gi = R[2 + M + k];
+    const double pr = wave_bcast(pjr, k), pi = wave_bcast(pji, k);
+    const double cr = wave_bcast(cjr, k), ci = wave_bcast(cji, k);
+    const double jx = newer ? cr : pr, jy = newer ? ci : pi;
+    vr = fma(gr, jx, vr);
+    vi = fma(gr, jy, vi);
+    vr = fma(-gi, jy, vr);
+    vi = fma(gi, jx, vi);
+  }
+  const double mg = od_mag(fma(vi, vi, vr * vr));
+  const double mn = wave_xor(mg, 32);                // lanes < 32: the new magnitude
+  const bool prev_lane = on && !newer;
+  err = od_max(err, prev_lane ? fabs(mn - mg) : 0.0);
+  amin = fmin(amin, prev_lane ? mg : __builtin_huge_val());
+}
+
+// The snap solve of the env with controllable powers (pc, qc) (uniform), by
+// the whole wave (full EXEC); sh staged.  Returns the count (negative when
+// stopped by max_iter) and leaves node 0's voltage (pf_node0's operations) in
+// (v0r, v0i) of every lane.
+__device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, double pc, double qc, double& v0r,
+                             double& v0i) {
+  // (opaque: nothing of the solve is hoisted into the step's common path,
+  // where its addresses would hold registers through the agents' step)
+  const ODWaveArgs* zp = &z_;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+s"(zp), "+v"(lane));
+  const ODWaveArgs& z = *zp;
+  const ODWaveShared& sh = sh_;
+  const int M = z.m, T = M * (M + 1) / 2;
+  const int i = min(lane, M - 1);
+  // (z lives in the kernarg segment, read in place: per-lane indices are
+  // vector loads from it, no private copy)
+  const double sr0 = z.sr0[i], si0 = z.si0[i], fr = z.fr[i], fi = z.fi[i];
+  const double y0r = z.y0r[i], y0i = z.y0i[i], esc = z.esc[i];
+  const bool node = lane < M && ((z.node_mask >> i) & 1);
+  const double s_r = fma(fr, pc, sr0), s_i = fma(fi, qc, si0);   // pf_power's
+  const double* st = z.start;
+  const double u0re = z.block[3 * T + i], u0sum = z.block[3 * T + 2 * M + i];
+  // u_1 and the table currents I'(u_0) (od_solve's affine / currents_1)
+  double ur = fma(qc, st[2 * (2 * M + i)], fma(pc, st[2 * (M + i)], st[2 * i]));
+  double ui = fma(qc, st[2 * (2 * M + i) + 1], fma(pc, st[2 * (M + i) + 1], st[2 * i + 1]));
+  const int c1 = 3 * M + i;
+  double pjr = fma(qc, st[2 * (2 * M + c1)], fma(pc, st[2 * (M + c1)], st[2 * c1]));
+  double pji = fma(qc, st[2 * (2 * M + c1) + 1], fma(pc, st[2 * (M + c1) + 1], st[2 * c1 + 1]));
+  const double tol_lo = z.tol * (1.0 + 0x1p-30);
+  const bool bounded = z.n_rep < z.n_rows;
+  int it = 1, my_it = 1;
+  bool conv_ok = false, done = z.max_iter <= 1;
+  while (!done) {                                    // (uniform)
+    ++it;
+    // element i's current from u_{it-1} (current_od's operations)
+    const double m2 = fma(ui, ui, ur * ur);
+    double mc = fmin(fmax(m2, z.mn2), z.mx2);
+    mc = (m2 <= z.lo2) ? 1.0 : mc;
+    const double g = fast_rcp(mc);
+    const double cr = fma(s_r, g, -y0r), ci = fma(s_i, g, -y0i);
+    const double cjr = fma(cr, ur, -(ci * ui)), cji = fma(cr, ui, ci * ur);
+    const double cjs = cjr + cji;
+    // row i of the matvec, column by column (pf_acc_init, pf_column)
+    double A = u0re, Bs = 0.0, C = u0sum;
+    int ie = i;
+    asm volatile("" : "+v"(ie));                     // (opaque: see od_wave_rows)
+    const double* wk = &sh.w[0][0][0] + ie;
+#pragma unroll 2
+    for (int k = 0; k < M; ++k) {                    // (uniform)
+      A = fma(wk[k * PGW_PF_MAX_M], wave_bcast(cjr, k), A);
+      Bs = fma(wk[(PGW_PF_MAX_M + k) * PGW_PF_MAX_M], wave_bcast(cji, k), Bs);
+      C = fma(wk[(2 * PGW_PF_MAX_M + k) * PGW_PF_MAX_M], wave_bcast(cjs, k), C);
+    }
+    const double nr = A - Bs, ni = (C - A) - Bs;
+    // the square-root-free lower bound over the element nodes
+    bool hit = false;
+    double err = 0.0, amin = __builtin_huge_val();
+    {
+      const double e2 = esc * esc;
+      const double a2 = fma(ni, ni, nr * nr) * e2, b2 = fma(ui, ui, ur * ur) * e2;
+      hit = node && fabs(a2 - b2) > tol_lo * fma(0.5, a2 + b2, 1.0);
+    }
+    const bool need = it >= z.min_iter && __ballot(hit) == 0ull;   // (uniform)
+    if (need) {
+      const double mo = od_mag(fma(ui, ui, ur * ur)) * esc;
+      const double mn = od_mag(fma(ni, ni, nr * nr)) * esc;
+      err = node ? fabs(mn - mo) : 0.0;
+      amin = node ? mo : __builtin_huge_val();
+    }
+    ur = nr;
+    ui = ni;
+    int d = 0;
+    if (need) {
+      double dsum = 0.0, jsum = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < M; ++k) {                  // (uniform) in k order
+        const double cx = wave_bcast(cjr, k), cy = wave_bcast(cji, k);
+        const double px = wave_bcast(pjr, k), py = wave_bcast(pji, k);
+        dsum += fabs(cx - px) + fabs(cy - py);
+        jsum += fabs(px) + fabs(py);
+      }
+      dsum = wave_uni(fma(0x1p-40, jsum + dsum, dsum));
+      jsum = wave_uni(fma(0x1p-40, jsum, jsum));
+      for (int r0 = 0; r0 < z.n_rep; r0 += 32)
+        od_wave_rows(sh, M, r0, min(r0 + 32, z.n_rep), pjr, pji, cjr, cji, err, amin);
+      double lo = wave_uni(wave_max(err)), am = wave_uni(wave_min(amin));
+      d = __builtin_amdgcn_readfirstlane(od_decide(z, !bounded, it, lo, am, dsum, jsum));
+      if (d < 0) {                                   // (uniform) the bounded rows decide
+        for (int r0 = z.n_rep; r0 < z.n_rows; r0 += 32)
+          od_wave_rows(sh, M, r0, min(r0 + 32, z.n_rows), pjr, pji, cjr, cji, err, amin);
+        lo = wave_uni(wave_max(err));
+        am = wave_uni(wave_min(amin));
+        d = __builtin_amdgcn_readfirstlane(od_decide(z, true, it, lo, am, dsum, jsum));
+      }
+    }
+    pjr = cjr;                                       // this iteration's currents: the next one's
+    pji = cji;                                       // previous, and the outputs' when it stops
+    my_it = it;
+    conv_ok = d > 0;
+    done = d > 0 || it >= z.max_iter;
+  }
+  // node 0 from the accepted currents (pf_node0's operations)
+  const double* B = z.block + 3 * T + 6 * M;         // g0re[M], g0im[M], v0re, v0im
+  double vr = B[2 * M], vi = B[2 * M + 1];
+#pragma unroll 1
+  for (int k = 0; k < M; ++k) {                      // (uniform)
+    const double gr = B[k], gi = B[M + k];
+    const double jr = wave_bcast(pjr, k), ji = wave_bcast(pji, k);
+    vr = fma(gr, jr, vr);
+    vi = fma(gr, ji, vi);
+    vr = fma(-gi, ji, vr);
+    vi = fma(gi, jr, vi);
+  }
+  v0r = vr;
+  v0i = vi;
+  return conv_ok ? my_it : -my_it;
+}
+
 // Fused C4 step, OpenDSS rule with the hour's node records (pgw_pf_od.resp_v,
 // output row 0 the coordinated bus, no other row): the agents AND the power
 // flow's table lookup in one launch.  A block is n_agents waves over 64 envs;
@@ -1960,15 +2199,26 @@ struct ODVLook {
 // (the next step's list).  Bit-identical to k_coord_agents_std + k_coord_pf_od.
 // WT: every store write-through (st_wt), so the step leaves no dirty L2 lines
 // for the next launch's boundary to write back.
-template <bool WT>
-__global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) k_coord_step_od(pgw_coord_params p_, pgw_coord_step_info s,
+// INL (the default one-launch step): the lookup wave solves the envs the table
+// leaves itself (od_wave_solve), one at a time, and nothing is listed -- the
+// step is this launch alone.
+// (the step's parameters and the wave solve's constants: one first argument,
+// read in place from the kernarg segment)
+struct StepOdArgs {
+  pgw_coord_params p;
+  ODWaveArgs z;
+};
+template <bool WT, bool INL>
+__global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) k_coord_step_od(StepOdArgs A_, pgw_coord_step_info s,
                                                                        int64_t n, pgw_coord_buffers b, double pv_ob,
                                                                        StdDerived dv, CoordPFArgs c, ODVLook o) {
   auto put = [](auto* q, auto v) {
     if constexpr (WT) st_wt(q, v);
     else *q = v;
   };
-  const pgw_coord_params& p = PGW_KERNARG0(pgw_coord_params);   // (no private copy)
+  const StepOdArgs& A = PGW_KERNARG0(StepOdArgs);               // (no private copy)
+  const pgw_coord_params& p = A.p;
+  const ODWaveArgs& z = A.z;
   const int a = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
   const bool valid = e < n;
@@ -2017,7 +2267,29 @@ __global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) k_coord_step_od(pgw_coord
     // (a local copy: a reference to the by-value kernel argument would put it
     // in a private-memory frame)
     const ODVLook ol = {o.resp_v, o.resp_x0, o.resp_inv_h, o.resp_nseg, 0};
-    const bool served = valid && !o.timing_only && od_resp_lookup_v(ol, pc, 0.0, vf, it);
+    bool served = valid && !o.timing_only && od_resp_lookup_v(ol, pc, 0.0, vf, it);
+    if constexpr (INL) {
+      // the envs the table left: the wave's snap solve, one env at a time
+      // (the usual wave has none); their node-0 voltage then takes the served
+      // path's place (the same operations as k_coord_pf_od's epilogue)
+      __shared__ ODWaveShared s_solve;
+      uint64_t left = __ballot(valid && !served && !o.timing_only);
+      if (left) {                                    // (uniform) counted as the list form counts them
+        if (lane == 0) atomicAdd(b.od_count + (b.od_parity & 1), __popcll(left));
+        od_wave_stage(z, s_solve);
+      }
+      while (left) {                                 // (uniform)
+        const int L = __builtin_ctzll(left);
+        left &= left - 1;
+        double v0r, v0i;
+        const int its = od_wave_solve(z, s_solve, wave_bcast(pc, L), 0.0, v0r, v0i);
+        if (lane == L) {
+          vf = make_double2(v0r, v0i);
+          it = its;
+          served = true;
+        }
+      }
+    }
     double share = 0.0;
     if (served) {
       const double v0 = sqrt(fma(vf.y, vf.y, vf.x * vf.x));
@@ -2030,7 +2302,8 @@ __global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) k_coord_step_od(pgw_coord
       }
     }
     // the envs left to the solve: one list slot each, one atomic per wave
-    const bool need = valid && !served && !o.timing_only;
+    // (INL: none -- every valid env was served or solved above)
+    const bool need = !INL && valid && !served && !o.timing_only;
     const uint64_t m = __ballot(need);
     if (m) {
       const int first = __builtin_ctzll(m);
@@ -2542,6 +2815,45 @@ static const bool g_step_wt = initial_step_wt();
 static const bool g_step_nolookup = getenv("PGW_STEP_NOLOOKUP") && getenv("PGW_STEP_NOLOOKUP")[0] == '1';
 // PGW_STEP_NOP=1 (diagnostics): an empty one-wave kernel between the step's two launches, to time the boundary
 static const bool g_step_nop = getenv("PGW_STEP_NOP") && getenv("PGW_STEP_NOP")[0] == '1';
+// PGW_STEP_LIST=1 (A/Bs): the two-launch form of the fused step -- the envs
+// the table left listed by k_coord_step_od and solved by k_coord_pf_od_list --
+// instead of the inline wave solve.  PGW_STEP_NOLIST=1 (diagnostics, with
+// PGW_STEP_LIST=1): no list launch -- the listed envs keep their raw rewards
+// and unsolved voltages (timing only).
+static const bool g_step_list = getenv("PGW_STEP_LIST") && getenv("PGW_STEP_LIST")[0] == '1';
+static const bool g_step_nolist = getenv("PGW_STEP_NOLIST") && getenv("PGW_STEP_NOLIST")[0] == '1';
+static ODWaveArgs make_wave_args(const PFArgs& a, const ODArgs& o, const pgw_pf_params& pf,
+                                 const pgw_pf_tables& t) {
+  ODWaveArgs z = {};
+  for (int k = 0; k < PGW_PF_MAX_M; ++k) {
+    z.sr0[k] = a.sr0[k];
+    z.si0[k] = a.si0[k];
+    z.fr[k] = a.fr[k];
+    z.fi[k] = a.fi[k];
+    z.y0r[k] = o.y0r[k];
+    z.y0i[k] = o.y0i[k];
+    z.esc[k] = o.esc[k];
+  }
+  z.lo2 = a.lo2;
+  z.mn2 = a.mn2;
+  z.mx2 = a.mx2;
+  z.tol = o.tol;
+  z.gamma = o.gamma;
+  z.eps = o.eps;
+  z.gmax = o.gmax;
+  z.gsrc = o.gsrc;
+  z.block = t.block;
+  z.start = o.start;
+  z.rows_V0 = o.rows_V0;
+  z.rows_G = o.rows_G;
+  z.m = pf.m;
+  z.min_iter = o.min_iter;
+  z.n_rep = o.n_rep;
+  z.n_rows = o.n_rows;
+  z.max_iter = o.max_iter;
+  z.node_mask = o.node_mask;
+  return z;
+}
 __global__ void k_step_nop(int* p) {
   if (p && threadIdx.x == 1000) *p = 0;
 }
@@ -2619,15 +2931,27 @@ static int32_t coord_step(const pgw_coord_params* p, const pgw_pf_params* pf, co
       const ODArgs o = make_od_args(*pft->od, pf->max_iter);
       if (std_layout && o.resp_v && o.resp_v_row == 0 && pf->n_out == 1 && p->vv_row == 0) {
         const ODVLook lk = {o.resp_v, o.resp_x0, o.resp_inv_h, o.resp_nseg, g_step_nolookup ? 1 : 0};
+        const StepOdArgs sa = {*p, make_wave_args(a, o, *pf, *pft)};
+        const dim3 grid((unsigned)((n + 63) / 64)), block(64 * p->n_agents);
+        if (!g_step_list) {                         // the one-launch step
+          if (g_step_wt)
+            launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<true, true>, grid, block, st, sa, *s, n, b, pv_ob,
+                         make_std_derived(*p), c, lk);
+          else
+            launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<false, true>, grid, block, st, sa, *s, n, b, pv_ob,
+                         make_std_derived(*p), c, lk);
+          return check_launch("k_coord_step_od");
+        }
         if (g_step_wt)
-          launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<true>, dim3((unsigned)((n + 63) / 64)),
-                       dim3(64 * p->n_agents), st, *p, *s, n, b, pv_ob, make_std_derived(*p), c, lk);
+          launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<true, false>, grid, block, st, sa, *s, n, b, pv_ob,
+                       make_std_derived(*p), c, lk);
         else
-          launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<false>, dim3((unsigned)((n + 63) / 64)),
-                       dim3(64 * p->n_agents), st, *p, *s, n, b, pv_ob, make_std_derived(*p), c, lk);
+          launch_timed(PGW_T_COORD_AGENTS, k_coord_step_od<false, false>, grid, block, st, sa, *s, n, b, pv_ob,
+                       make_std_derived(*p), c, lk);
         int32_t rc = check_launch("k_coord_step_od");
         if (rc) return rc;
         if (g_step_nop) hipLaunchKernelGGL(k_step_nop, dim3(1), dim3(64), 0, st, (int*)nullptr);
+        if (g_step_nolist) return PGW_OK;
         if (g_od_list_grid >= grid_for(n))
           launch_timed(PGW_T_COORD_PF, k_coord_pf_od_list<14, false>, dim3((unsigned)grid_for(n)),
                        dim3(kBlock), st, c, a, o, *pft, n, b);

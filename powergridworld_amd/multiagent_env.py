@@ -646,6 +646,8 @@ class MultiAgentEnv(Env):
             F["meta"]["voltage_violation"] = F["vv"]
         F["meta"]["oob_actions"] = self.oob_count
         self._fused = F
+        if self._one_launch_ok():
+            self.set_pf_list(True)
 
     # ================================================================ fused multi-agent path
     def _ma_fusable(self):
@@ -851,13 +853,27 @@ class MultiAgentEnv(Env):
         meta["oob_actions"] = self.oob_count
         return obs, rew, done, meta
 
+    def _one_launch_ok(self):
+        """The fused C4 step can run as one launch (k_coord_step_od): fp64, the
+        OpenDSS rule on the fast kernel with the hour's response table and node
+        records, the coordinated bus the only output row, the standard agent."""
+        s = self.pf_solver
+        return (self.dtype == torch.float64 and getattr(s, "convergence", None) == "opendss" and
+                bool(getattr(s, "od_table", False)) and bool(getattr(s, "od_node_records", False)) and
+                not getattr(s, "general", True) and len(s.output_names) == 1 and
+                self.fused_reward_transform == "coordinated" and self._f32_fusable() is None)
+
     def set_pf_list(self, enabled=True):
         """Fused C4 step under the OpenDSS rule with node records (fp64): True
-        runs the agents and the table lookup in one launch (k_coord_step_od)
-        plus the snap solve of the envs it lists (k_coord_pf_od_list); False
-        (the default) the two-kernel step (k_coord_agents_std, then
-        k_coord_pf_od over every env).  Bit-identical; the split measured no
-        faster, so it is opt-in."""
+        (the default where _one_launch_ok) runs it as ONE launch,
+        k_coord_step_od -- the agents, the table lookup and, for the rare envs
+        the table leaves, the snap solve by the lookup wave (od_wave_solve);
+        False the two-kernel step (k_coord_agents_std, then k_coord_pf_od over
+        every env).  Bit-identical (tests/test_gpu_pf_od.py); one launch saves
+        the second launch's ~4.6 us boundary.
+        od_count[od_parity] counts the envs the step left to the solve.  (The
+        library's PGW_STEP_LIST=1 runs the older list form instead: those envs
+        listed and solved by k_coord_pf_od_list in a second launch.)"""
         F = self._fused
         if F is None or self.dtype != torch.float64:
             return

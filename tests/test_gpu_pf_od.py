@@ -369,17 +369,22 @@ def _unfit(solver, every):
 
 @pytest.mark.parametrize("n,every,steps", [(4133, 0, 40), (4133, 3, 20), (4133, 1, 12), (66000, 1, 3)])
 def test_od_split_step_bit_identical(n, every, steps):
-    """The fused C4 step with the agents and the table lookup in one launch
-    (k_coord_step_od) and the listed envs' snap solve (k_coord_pf_od_list)
-    against the two-kernel step (k_coord_agents_std + k_coord_pf_od): every
-    output bit for bit -- with the table serving (every = 0), with a third of
-    the records forced unfit and with all of them (every env in the list; at
-    66 000 envs the list kernel's grid-stride loop takes two passes) -- and the
-    all-unfit case equal to the step without a table (od_table=False)."""
+    """The fused C4 step with the agents, the table lookup and the snap solve
+    of the envs the table leaves in one launch (k_coord_step_od: the lookup
+    wave's od_wave_solve, one env at a time; with PGW_STEP_LIST=1 the list form,
+    those envs listed for k_coord_pf_od_list) against the two-kernel step
+    (k_coord_agents_std + k_coord_pf_od): every output bit for bit -- with the
+    table serving (every = 0), with a third of the records forced unfit and with
+    all of them (every env solved by the wave solve; at 66 000 envs, 1 032
+    blocks of 64 solves each) -- and the all-unfit case equal to the step
+    without a table (od_table=False).  od_count counts the envs left to the
+    solve in both forms."""
     from powergridworld_amd.scenarios.coordinated import CoordinatedMultiBuildingControlEnv, make_c4_config
     envs = [CoordinatedMultiBuildingControlEnv(**make_c4_config(), num_envs=n, device=DEV, fused=True)
             for _ in range(3)]
     envs[0].set_pf_list(True)
+    envs[1].set_pf_list(False)
+    envs[2].set_pf_list(False)
     envs[2].pf_solver.od_table = False
     rng = np.random.default_rng(17)
     init = torch.tensor(rng.uniform(5.0, 45.0, size=(5, n)), device=DEV)

@@ -13,6 +13,7 @@ NAMES = {"k_coord_agents_std": "k_coord_agents_std",
          "k_coord_pf_od<14": "k_coord_pf_od<14>",
          "k_coord_pf<14, true, false, false": "k_coord_pf<14,true,false,false>",
          "k_coord_pf_split": "k_coord_pf_split",
+         "k_coord_step_od": "k_coord_step_od",
          "k_pf_solve<14, true, false, false>": "k_pf_solve<14,true,false,false>"}
 
 
