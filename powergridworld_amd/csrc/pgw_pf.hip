@@ -2018,18 +2018,41 @@ __device__ __forceinline__ void od_wave_stage(const ODWaveArgs& z_, ODWaveShared
   const ODWaveArgs& z = *zp;
   ODWaveShared& sh = sh_;
   const int M = z.m, T = M * (M + 1) / 2;
-  for (int x = lane; x < 3 * PGW_PF_MAX_M * PGW_PF_MAX_M; x += 64) {
-    const int c = x / (PGW_PF_MAX_M * PGW_PF_MAX_M), k = (x / PGW_PF_MAX_M) % PGW_PF_MAX_M,
-              i = x % PGW_PF_MAX_M;
-    const int a = min(i, k), b = max(i, k);
-    (&sh.w[0][0][0])[x] = (i < M && k < M) ? z.block[c * T + a * M - a * (a - 1) / 2 + (b - a)] : 0.0;
+  // every load of a batch in flight before its LDS stores (a load-store loop
+  // waited one L2 round trip per entry: ~20 us per staged solve); the
+  // addresses are clamped in bounds and the values selected after the load
+  constexpr int kWq = 3 * PGW_PF_MAX_M * PGW_PF_MAX_M / 64;
+  {
+    double v[kWq];
+#pragma unroll
+    for (int q = 0; q < kWq; ++q) {
+      const int x = lane + 64 * q;
+      const int c = x / (PGW_PF_MAX_M * PGW_PF_MAX_M), k = (x / PGW_PF_MAX_M) % PGW_PF_MAX_M,
+                i = x % PGW_PF_MAX_M;
+      const int ic = min(i, M - 1), kc = min(k, M - 1);
+      const int a = min(ic, kc), b = max(ic, kc);
+      const double t = z.block[c * T + a * M - a * (a - 1) / 2 + (b - a)];
+      v[q] = (i < M && k < M) ? t : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kWq; ++q) (&sh.w[0][0][0])[lane + 64 * q] = v[q];
   }
-  const int S = 2 + 2 * M;
-  for (int x = lane; x < z.n_rows * S; x += 64) {
-    const int r = x / S, j = x - r * S;
-    const double v = j < 2 ? z.rows_V0[2 * r + j]
-                           : z.rows_G[2 * M * r + (j < 2 + M ? 2 * (j - 2) : 2 * (j - 2 - M) + 1)];
-    sh.rows[r * kWaveRowStride + j] = v;
+  const int S = 2 + 2 * M, nr = max(z.n_rows, 1);
+  constexpr int kRq = 9;                             // entries per lane per batch
+  for (int x0 = 0; x0 < z.n_rows * S; x0 += 64 * kRq) {   // (uniform: two batches at most)
+    double v[kRq];
+#pragma unroll
+    for (int q = 0; q < kRq; ++q) {
+      const int x = x0 + lane + 64 * q;
+      const int r = min(x / S, nr - 1), j = x - (x / S) * S;
+      v[q] = j < 2 ? z.rows_V0[2 * r + j]
+                   : z.rows_G[2 * M * r + (j < 2 + M ? 2 * (j - 2) : 2 * (j - 2 - M) + 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < kRq; ++q) {
+      const int x = x0 + lane + 64 * q;
+      if (x < z.n_rows * S) sh.rows[(x / S) * kWaveRowStride + (x - (x / S) * S)] = v[q];
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
