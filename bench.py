@@ -146,7 +146,7 @@ def parse():
                          "child process so the oracle's imports stay out of the timed process")
     ap.add_argument("--time-steps", type=int, default=286,
                     help="steps of the kernel-timing pass after the timed region (every launch "
-                         "HIP-event-timed; at least 8, at most --steps)")
+                         "HIP-event-timed; at least 8; a whole episode by default, whatever --steps)")
     ap.add_argument("--pf-convergence", choices=("opendss", "exact"), default="opendss",
                     help="the headline's power-flow stopping rule: OpenDSS's snap solve (the "
                          "reference's: loads' Yeq in Y, node-magnitude test 1e-4, 2..15 iterations) "
@@ -553,7 +553,10 @@ def main():
     # bracketed by HIP events on its own stream.  Kept out of `value`'s region:
     # an event-bracketed launch costs ~10 us of extra step time (measured: the
     # driver-shaped 20-step run went 36 -> 44 us/step with every 2nd launch timed).
-    time_steps = max(8, min(args.steps, args.time_steps))
+    # (a whole episode by default, whatever --steps: the one-launch step's
+    # duration varies with the envs its table leaves to the inline solve --
+    # rocprof 18.8-42.9 us per launch, r06k -- so a 20-launch mean is noise)
+    time_steps = max(8, args.time_steps)
     tot, cnt = timed_pass(run, time_steps)
     # the PF iteration counts of the last timed-pass step (before the episode
     # pass below, which ends with a reset whose cold solve would overwrite them)
