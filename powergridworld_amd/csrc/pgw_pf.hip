@@ -1981,6 +1981,8 @@ constexpr int kWaveRowStride = 2 + 2 * PGW_PF_MAX_M + 1;   // odd: 32 rows on di
 struct ODWaveShared {
   double w[3][PGW_PF_MAX_M][PGW_PF_MAX_M];         // [c][k][i] = part c of W''_ik
   double rows[kOdRows * kWaveRowStride];           // V0 re, im, G re (k), G im (k) per check row
+  double el[9][PGW_PF_MAX_M];                      // per element: sr0 si0 fr fi y0r y0i esc u0re u0sum
+  double st[12 * PGW_PF_MAX_M];                    // pgw_pf_od.start
 };
 
 __device__ __forceinline__ double wave_bcast(double x, int k) {   // lane k's value (k uniform)
@@ -1999,23 +2001,42 @@ __device__ __forceinline__ double wave_xor(double x, int d) {
   asm volatile("" : "+v"(l));
   return __shfl(x, l ^ d);
 }
-__device__ __forceinline__ double wave_max(double x) {     // od_max over the wave
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) x = od_max(x, wave_xor(x, d));
-  return x;
+// x from the lane CTRL names within its 16-lane row (DPP row_ror: no lane is
+// without a source, so idempotent reductions need no identity)
+template <int CTRL>
+__device__ __forceinline__ double row_dpp(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+constexpr int kRowRor1 = 0x121, kRowRor2 = 0x122, kRowRor4 = 0x124, kRowRor8 = 0x128;
+__device__ __forceinline__ double wave_max(double x) {     // od_max over the wave (uniform result)
+  x = od_max(x, row_dpp<kRowRor1>(x));
+  x = od_max(x, row_dpp<kRowRor2>(x));
+  x = od_max(x, row_dpp<kRowRor4>(x));
+  x = od_max(x, row_dpp<kRowRor8>(x));
+  double r = wave_bcast(x, 0);
+#pragma unroll 1
+  for (int l = 16; l < 64; l += 16) r = od_max(r, wave_bcast(x, l));
+  return r;
 }
 __device__ __forceinline__ double wave_min(double x) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) x = fmin(x, wave_xor(x, d));
-  return x;
+  x = fmin(x, row_dpp<kRowRor1>(x));
+  x = fmin(x, row_dpp<kRowRor2>(x));
+  x = fmin(x, row_dpp<kRowRor4>(x));
+  x = fmin(x, row_dpp<kRowRor8>(x));
+  double r = wave_bcast(x, 0);
+#pragma unroll 1
+  for (int l = 16; l < 64; l += 16) r = fmin(r, wave_bcast(x, l));
+  return r;
 }
 
 // W'' and the check rows into the wave's LDS (the calling wave only).
 __device__ __forceinline__ void od_wave_stage(const ODWaveArgs& z_, ODWaveShared& sh_) {
-  const ODWaveArgs* zp = &z_;
   int lane = threadIdx.x & 63;
-  asm volatile("" : "+s"(zp), "+v"(lane));       // (opaque: see od_wave_solve)
-  const ODWaveArgs& z = *zp;
+  asm volatile("" : "+v"(lane));                   // (opaque: see od_wave_solve)
+  const ODWaveArgs& z = z_;                        // (kernarg: scalar loads)
   ODWaveShared& sh = sh_;
   const int M = z.m, T = M * (M + 1) / 2;
   // every load of a batch in flight before its LDS stores (a load-store loop
@@ -2036,6 +2057,30 @@ __device__ __forceinline__ void od_wave_stage(const ODWaveArgs& z_, ODWaveShared
     }
 #pragma unroll
     for (int q = 0; q < kWq; ++q) (&sh.w[0][0][0])[lane + 64 * q] = v[q];
+  }
+  {
+    // the per-element constants (kernarg, L2) and the start table, once per
+    // wave instead of once per solve
+    const int k = lane & 15, kc = min(k, M - 1);
+    double v[12];
+    v[0] = z.sr0[k];
+    v[1] = z.si0[k];
+    v[2] = z.fr[k];
+    v[3] = z.fi[k];
+    v[4] = z.y0r[k];
+    v[5] = z.y0i[k];
+    v[6] = z.esc[k];
+    v[7] = z.block[3 * T + kc];
+    v[8] = z.block[3 * T + 2 * M + kc];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) v[9 + q] = z.start[min(lane + 64 * q, 12 * M - 1)];
+    if (lane < PGW_PF_MAX_M) {
+#pragma unroll
+      for (int j = 0; j < 9; ++j) sh.el[j][lane] = v[j];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (lane + 64 * q < 12 * M) sh.st[lane + 64 * q] = v[9 + q];
   }
   const int S = 2 + 2 * M, nr = max(z.n_rows, 1);
   constexpr int kRq = 9;                             // entries per lane per batch
@@ -2070,8 +2115,9 @@ __device__ __forceinline__ void od_wave_rows(const ODWaveShared& sh, int M, int 
   const bool on = r0 + (lane & 31) < r1;
   const double* R = sh.rows + r * kWaveRowStride;
   double vr = R[0], vi = R[1];
-#pragma unroll 1
-  for (int k = 0; k < M; ++k) {                      // (uniform) od_rows_sparse's order
+#pragma unroll
+  for (int k = 0; k < PGW_PF_MAX_M; ++k) {           // (uniform) od_rows_sparse's order
+    if (k >= M) break;
     const double gr = R[2 + k], gi = R[2 + M + k];
     const double pr = wave_bcast(pjr, k), pi = wave_bcast(pji, k);
     const double cr = wave_bcast(cjr, k), ci = wave_bcast(cji, k);
@@ -2096,21 +2142,19 @@ __device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, doub
                              double& v0i) {
   // (opaque: nothing of the solve is hoisted into the step's common path,
   // where its addresses would hold registers through the agents' step)
-  const ODWaveArgs* zp = &z_;
   int lane = threadIdx.x & 63;
-  asm volatile("" : "+s"(zp), "+v"(lane));
-  const ODWaveArgs& z = *zp;
+  asm volatile("" : "+v"(lane));
+  const ODWaveArgs& z = z_;                        // (kernarg: scalar loads)
   const ODWaveShared& sh = sh_;
   const int M = z.m, T = M * (M + 1) / 2;
   const int i = min(lane, M - 1);
-  // (z lives in the kernarg segment, read in place: per-lane indices are
-  // vector loads from it, no private copy)
-  const double sr0 = z.sr0[i], si0 = z.si0[i], fr = z.fr[i], fi = z.fi[i];
-  const double y0r = z.y0r[i], y0i = z.y0i[i], esc = z.esc[i];
+  // (the per-element constants and the start table staged in LDS)
+  const double sr0 = sh.el[0][i], si0 = sh.el[1][i], fr = sh.el[2][i], fi = sh.el[3][i];
+  const double y0r = sh.el[4][i], y0i = sh.el[5][i], esc = sh.el[6][i];
   const bool node = lane < M && ((z.node_mask >> i) & 1);
   const double s_r = fma(fr, pc, sr0), s_i = fma(fi, qc, si0);   // pf_power's
-  const double* st = z.start;
-  const double u0re = z.block[3 * T + i], u0sum = z.block[3 * T + 2 * M + i];
+  const double* st = sh.st;
+  const double u0re = sh.el[7][i], u0sum = sh.el[8][i];
   // u_1 and the table currents I'(u_0) (od_solve's affine / currents_1)
   double ur = fma(qc, st[2 * (2 * M + i)], fma(pc, st[2 * (M + i)], st[2 * i]));
   double ui = fma(qc, st[2 * (2 * M + i) + 1], fma(pc, st[2 * (M + i) + 1], st[2 * i + 1]));
@@ -2136,11 +2180,13 @@ __device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, doub
     int ie = i;
     asm volatile("" : "+v"(ie));                     // (opaque: see od_wave_rows)
     const double* wk = &sh.w[0][0][0] + ie;
-#pragma unroll 2
-    for (int k = 0; k < M; ++k) {                    // (uniform)
-      A = fma(wk[k * PGW_PF_MAX_M], wave_bcast(cjr, k), A);
-      Bs = fma(wk[(PGW_PF_MAX_M + k) * PGW_PF_MAX_M], wave_bcast(cji, k), Bs);
-      C = fma(wk[(2 * PGW_PF_MAX_M + k) * PGW_PF_MAX_M], wave_bcast(cjs, k), C);
+#pragma unroll
+    for (int k = 0; k < PGW_PF_MAX_M; ++k) {         // (compile-time trip count, uniform guard)
+      if (k < M) {
+        A = fma(wk[k * PGW_PF_MAX_M], wave_bcast(cjr, k), A);
+        Bs = fma(wk[(PGW_PF_MAX_M + k) * PGW_PF_MAX_M], wave_bcast(cji, k), Bs);
+        C = fma(wk[(2 * PGW_PF_MAX_M + k) * PGW_PF_MAX_M], wave_bcast(cjs, k), C);
+      }
     }
     const double nr = A - Bs, ni = (C - A) - Bs;
     // the square-root-free lower bound over the element nodes
@@ -2163,8 +2209,9 @@ __device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, doub
     int d = 0;
     if (need) {
       double dsum = 0.0, jsum = 0.0;
-#pragma unroll 1
-      for (int k = 0; k < M; ++k) {                  // (uniform) in k order
+#pragma unroll
+      for (int k = 0; k < PGW_PF_MAX_M; ++k) {       // (uniform) in k order
+        if (k >= M) break;
         const double cx = wave_bcast(cjr, k), cy = wave_bcast(cji, k);
         const double px = wave_bcast(pjr, k), py = wave_bcast(pji, k);
         dsum += fabs(cx - px) + fabs(cy - py);
@@ -2193,7 +2240,7 @@ __device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, doub
   // node 0 from the accepted currents (pf_node0's operations)
   const double* B = z.block + 3 * T + 6 * M;         // g0re[M], g0im[M], v0re, v0im
   double vr = B[2 * M], vi = B[2 * M + 1];
-#pragma unroll 1
+#pragma unroll 4
   for (int k = 0; k < M; ++k) {                      // (uniform)
     const double gr = B[k], gi = B[M + k];
     const double jr = wave_bcast(pjr, k), ji = wave_bcast(pji, k);
