@@ -2140,8 +2140,11 @@ __device__ __forceinline__ void od_wave_rows(const ODWaveShared& sh, int M, int 
 // (v0r, v0i) of every lane.
 __device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, double pc, double qc, double& v0r,
                              double& v0i) {
-  // (opaque: nothing of the solve is hoisted into the step's common path,
-  // where its addresses would hold registers through the agents' step)
+  // (an opaque lane id: the solve's per-lane addresses are formed here, not
+  // hoisted where they would hold registers through the agents' step; z stays
+  // a kernarg reference -- laundering it made every z.* a per-iteration flat
+  // load; the k loops have compile-time trip counts because readlane is
+  // convergent and a runtime-count loop around it is not unrolled)
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const ODWaveArgs& z = z_;                        // (kernarg: scalar loads)
