@@ -2274,7 +2274,8 @@ __device__ int od_wave_solve(const ODWaveArgs& z_, const ODWaveShared& sh_, doub
 // for the next launch's boundary to write back.
 // INL (the default one-launch step): the lookup wave solves the envs the table
 // leaves itself (od_wave_solve), one at a time, and nothing is listed -- the
-// step is this launch alone.
+// step is this launch alone.  (7 waves per SIMD: 71 VGPRs, 5 blocks per CU;
+// at 6 the kernel ran 0.3 us slower, profiles/r06/ab_one_launch_step.txt.)
 // (the step's parameters and the wave solve's constants: one first argument,
 // read in place from the kernarg segment)
 struct StepOdArgs {
@@ -2282,7 +2283,7 @@ struct StepOdArgs {
   ODWaveArgs z;
 };
 template <bool WT, bool INL>
-__global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) k_coord_step_od(StepOdArgs A_, pgw_coord_step_info s,
+__global__ void __launch_bounds__(64 * PGW_MAX_AGENTS) __attribute__((amdgpu_waves_per_eu(7))) k_coord_step_od(StepOdArgs A_, pgw_coord_step_info s,
                                                                        int64_t n, pgw_coord_buffers b, double pv_ob,
                                                                        StdDerived dv, CoordPFArgs c, ODVLook o) {
   auto put = [](auto* q, auto v) {
